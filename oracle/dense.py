@@ -48,6 +48,7 @@ SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658,
          -0.5900435899266435]
 
 BLOCK = 16  # tile edge (A.1)
+NEAR_F32 = 0.20000000298023224  # float32(0.2): the near-plane cull constant
 
 
 def eval_sh(deg: int, sh: torch.Tensor, dirs: torch.Tensor) -> torch.Tensor:
@@ -154,14 +155,21 @@ def rasterize_dense(means3D, means2D, opacities, shs, colors_precomp, scales, ro
         Sigma = R @ torch.diag_embed(s * s) @ R.transpose(1, 2)
     fx = W / (2.0 * tanfovx)
     fy = H / (2.0 * tanfovy)
-    t = p_view[:, :3]
     limx = 1.3 * tanfovx
     limy = 1.3 * tanfovy
+    # V8: the EWA Jacobian sees the frustum-clamped mean t_c; its pose
+    # derivative is rho + theta x t_c (upstream: -skew(t) of the clamped t).
+    t0 = (xh @ W2C.T)[:, :3]
+    with torch.no_grad():
+        txtz = t0[:, 0] / t0[:, 2]
+        tytz = t0[:, 1] / t0[:, 2]
+        clx = (txtz < -limx) | (txtz > limx)
+        cly = (tytz < -limy) | (tytz > limy)
+        tc_val = torch.stack([txtz.clamp(-limx, limx) * t0[:, 2],
+                              tytz.clamp(-limy, limy) * t0[:, 2], t0[:, 2]], dim=1)
+        tc_val = torch.where(torch.stack([clx, cly, torch.zeros_like(clx)], 1), tc_val, t0)
+    t = t0 + (torch.cat([tc_val, torch.ones(P, 1, dtype=dt)], 1) @ dT.T)[:, :3]
     tz = t[:, 2]
-    txtz = (t[:, 0] / tz).detach()
-    tytz = (t[:, 1] / tz).detach()
-    clx = (txtz < -limx) | (txtz > limx)
-    cly = (tytz < -limy) | (tytz > limy)
     tx = torch.where(clx, (txtz.clamp(-limx, limx) * tz).detach(), t[:, 0])
     ty = torch.where(cly, (tytz.clamp(-limy, limy) * tz).detach(), t[:, 1])
     zero = torch.zeros_like(tz)
@@ -183,7 +191,7 @@ def rasterize_dense(means3D, means2D, opacities, shs, colors_precomp, scales, ro
 
     # ---- integer decisions (no grad)
     with torch.no_grad():
-        visible = p_view[:, 2] > 0.2
+        visible = p_view[:, 2] > NEAR_F32  # upstream compares in float: z <= 0.2f
         visible &= det != 0
         mid = 0.5 * (a + c)
         disc = torch.clamp(mid * mid - det, min=0.1).sqrt()
@@ -311,7 +319,8 @@ def dense_forward_backward(scene: dict, settings: dict, grad_color, grad_depth):
     out = rasterize_dense(means3D, means2D, opac, shs, colors, scales, rots, cov, tau,
                           **settings)
     loss = (out["color"] * grad_color.to(dt)).sum() + (out["depth"] * grad_depth.to(dt)).sum()
-    loss.backward()
+    if loss.requires_grad:  # nothing visible -> every gradient is zero
+        loss.backward()
 
     def g(x, shape):
         if x is None:
@@ -326,6 +335,6 @@ def dense_forward_backward(scene: dict, settings: dict, grad_color, grad_depth):
         dL_dscales=g(scales, (P, 3)) if scales is not None else None,
         dL_drotations=g(rots, (P, 4)) if rots is not None else None,
         dL_dcov3D=g(cov, (P, 6)) if cov is not None else None,
-        dL_dtau=tau.grad.detach().clone(),
+        dL_dtau=tau.grad.detach().clone() if tau.grad is not None else torch.zeros(6, dtype=dt),
     )
     return res
