@@ -1,0 +1,126 @@
+/*
+ * wgsr.h -- C ABI of the MI355X-native WildGS Gaussian-splatting hot path.
+ *
+ * This is the drop-in boundary for the two native extensions WildGS-SLAM
+ * loads on its mapping path:
+ *
+ *   diff_gaussian_rasterization._C  (empty submodule in the reference,
+ *       .gitmodules:7-9; bound by the Python layer that
+ *       thirdparty/gaussian_splatting/gaussian_renderer/__init__.py:15-18,
+ *       58-74 and 130-141 imports)
+ *   simple_knn._C.distCUDA2          (.gitmodules:10-12; called at
+ *       thirdparty/gaussian_splatting/scene/gaussian_model.py:18,201-207)
+ *
+ * Each entry point below names the upstream `_C` function it replaces.  All
+ * pointers are DEVICE pointers (HIP, gfx950) unless stated, all arrays are
+ * contiguous fp32 (int32 where noted), and every launch goes on `stream`
+ * (a hipStream_t; NULL = the null stream).  Scratch memory is obtained through
+ * caller-supplied allocation callbacks -- the C analogue of upstream's
+ * `std::function<char*(size_t)>` resize functors -- so the caller's allocator
+ * (e.g. the torch caching allocator) owns every byte and the library keeps no
+ * global device state.
+ *
+ * Return value: 0 on success, a WGSR_E* code otherwise; wgsr_last_error()
+ * returns a thread-local message for the last failure.
+ */
+#ifndef WGSR_H
+#define WGSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WGSR_OK 0
+#define WGSR_EINVAL 1   /* argument misuse (upstream: AT_ERROR / Exception) */
+#define WGSR_EHIP 2     /* HIP runtime / launch failure                     */
+#define WGSR_EALLOC 3   /* an allocation callback returned NULL             */
+
+/* Returns a device pointer to at least `bytes` bytes, 256-byte aligned, that
+ * stays valid until the caller releases it.  `bytes` may be 0. */
+typedef void* (*wgsr_alloc_fn)(void* ctx, size_t bytes);
+
+/* The rasterisation inputs shared by forward and backward: the tensors and
+ * scalars of upstream's rasterize_gaussians / rasterize_gaussians_backward
+ * argument lists (GaussianRasterizationSettings + per-Gaussian tensors). */
+typedef struct wgsr_raster_args {
+  int P;                        /* number of Gaussians                        */
+  int D;                        /* active SH degree (sh_degree)               */
+  int M;                        /* stored SH coefficients per Gaussian        */
+  int W, H;                     /* image_width, image_height                  */
+  const float* bg;              /* [3]                                        */
+  const float* means3D;         /* [P,3]                                      */
+  const float* colors;          /* [P,3] colors_precomp, or NULL             */
+  const float* opacities;       /* [P,1]                                      */
+  const float* scales;          /* [P,3] or NULL (then cov3D_precomp)         */
+  const float* rotations;       /* [P,4] (w,x,y,z) or NULL                    */
+  const float* cov3D_precomp;   /* [P,6] or NULL                              */
+  const float* shs;             /* [P,M,3] or NULL (then colors)              */
+  const float* viewmatrix;      /* [4,4] world_view_transform (row-vector)    */
+  const float* projmatrix;      /* [4,4] full_proj_transform                  */
+  const float* projmatrix_raw;  /* [4,4] projection_matrix                    */
+  const float* campos;          /* [3]  camera_center                         */
+  float scale_modifier;
+  float tan_fovx, tan_fovy;
+  int prefiltered;              /* upstream: trap if a prefiltered point is culled */
+  int debug;                    /* synchronise + check after every kernel     */
+} wgsr_raster_args;
+
+/* Replaces _C.rasterize_gaussians (forward).
+ * Outputs (caller-allocated, fully written): out_color [3,H,W],
+ * out_depth [1,H,W], out_opacity [1,H,W] (= 1 - T), radii [P] int32,
+ * n_touched [P] int32.  Three state buffers are requested through the
+ * callbacks (geometry ~ P, binning ~ num_rendered, image ~ H*W); the caller
+ * must keep them for wgsr_rasterize_backward.  *num_rendered receives the
+ * number of (Gaussian, tile) pairs.  One device->host read (num_rendered)
+ * synchronises `stream`, as upstream does. */
+int wgsr_rasterize_forward(const wgsr_raster_args* args,
+                           wgsr_alloc_fn geom_alloc, wgsr_alloc_fn binning_alloc,
+                           wgsr_alloc_fn image_alloc, void* alloc_ctx,
+                           float* out_color, float* out_depth, float* out_opacity,
+                           int32_t* radii, int32_t* n_touched, int64_t* num_rendered,
+                           void* stream);
+
+/* Replaces _C.rasterize_gaussians_backward.
+ * Inputs: the forward's radii, state buffers and num_rendered; upstream
+ * gradients dL_dcolor [3,H,W] and dL_ddepth [1,H,W].
+ * Outputs (caller-allocated, fully written, zeros for culled Gaussians):
+ * dL_dmeans2D [P,3] (w.r.t. NDC xy; z = 0), dL_dcolors [P,3],
+ * dL_dopacity [P,1], dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3]
+ * (NULL when M == 0), dL_dscales [P,3], dL_drotations [P,4],
+ * dL_dtau [P,6] (per-Gaussian pose gradient, rho then theta).
+ * A scratch buffer of 48 bytes per rendered pair is requested through
+ * `scratch_alloc`. */
+int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii,
+                            const void* geom_buffer, const void* binning_buffer,
+                            const void* image_buffer, int64_t num_rendered,
+                            const float* dL_dcolor, const float* dL_ddepth,
+                            wgsr_alloc_fn scratch_alloc, void* alloc_ctx,
+                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                            float* dL_dscales, float* dL_drotations, float* dL_dtau,
+                            void* stream);
+
+/* Replaces _C.mark_visible: present[i] = (view-space z of point i > 0.2). */
+int wgsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                      const float* projmatrix, uint8_t* present, void* stream);
+
+/* Replaces simple_knn._C.distCUDA2: out[i] = mean of the squared distances
+ * to the 3 nearest other points of `points` [P,3] (exact). */
+int wgsr_dist_cuda2(int P, const float* points, float* out,
+                    wgsr_alloc_fn scratch_alloc, void* alloc_ctx, void* stream);
+
+/* Byte sizes of the forward state buffers (for callers that pre-allocate). */
+size_t wgsr_geometry_bytes(int P);
+size_t wgsr_binning_bytes(int64_t num_rendered, int W, int H);
+size_t wgsr_image_bytes(int W, int H);
+
+const char* wgsr_last_error(void);
+const char* wgsr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WGSR_H */

@@ -1,0 +1,229 @@
+// C ABI of libwgsr (include/wgsr.h): host orchestration of the gfx950 stages.
+//
+// Mirrors upstream CudaRasterizer::Rasterizer::{forward, backward, markVisible}
+// and SimpleKNN::knn with plain pointers: the caller owns all
+// memory (allocation callbacks), every launch goes on the caller's stream, and
+// the only host synchronisation is the num_rendered read in the forward.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "wgsr.h"
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+thread_local char g_err[1024] = "";
+}
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int num_bits(uint32_t n) {
+  int b = 0;
+  while (b < 32 && (1ull << b) < n) ++b;
+  return b;
+}
+
+namespace {
+
+struct Grid {
+  int gx, gy, nt;
+  explicit Grid(const wgsr_raster_args& a)
+      : gx((a.W + kTile - 1) / kTile), gy((a.H + kTile - 1) / kTile), nt(gx * gy) {}
+};
+
+int tile_sort_bits(const Grid& g) { return num_bits((uint32_t)g.nt) > 0 ? num_bits((uint32_t)g.nt) : 1; }
+// the LSD sort alternates buffers every 8-bit pass
+bool tile_sort_in_alt(const Grid& g) { return ((tile_sort_bits(g) + 7) / 8) % 2 == 1; }
+constexpr int kDepthBits = 32;
+constexpr bool kDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;
+
+int validate(const wgsr_raster_args* a) {
+  if (!a) return set_error(WGSR_EINVAL, "null args");
+  if (a->P < 0) return set_error(WGSR_EINVAL, "means3D must have dimensions (num_points, 3)");
+  if (a->W <= 0 || a->H <= 0) return set_error(WGSR_EINVAL, "image size must be positive (got %dx%d)", a->W, a->H);
+  if (a->P == 0) return WGSR_OK;
+  if (!a->means3D || !a->opacities || !a->bg || !a->viewmatrix || !a->projmatrix || !a->campos)
+    return set_error(WGSR_EINVAL, "missing required tensor");
+  if ((a->shs == nullptr) == (a->colors == nullptr))
+    return set_error(WGSR_EINVAL, "Please provide excatly one of either SHs or precomputed colors!");
+  const bool sr = a->scales && a->rotations;
+  if (sr == (a->cov3D_precomp != nullptr))
+    return set_error(WGSR_EINVAL,
+                     "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  if (a->shs && (a->M <= 0 || a->D < 0 || a->D > 3 || (a->D + 1) * (a->D + 1) > a->M))
+    return set_error(WGSR_EINVAL, "invalid SH configuration (degree %d, %d coefficients)", a->D, a->M);
+  const Grid g(*a);
+  if (g.gx > 65535 || g.gy > 65535) return set_error(WGSR_EINVAL, "image too large");
+  return WGSR_OK;
+}
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) return set_error(WGSR_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+#define STAGE(a, s, expr)                   \
+  do {                                      \
+    HIPCHK(expr);                           \
+    if ((a).debug) {                        \
+      HIPCHK(hipStreamSynchronize(s));      \
+      HIPCHK(hipGetLastError());            \
+    }                                       \
+  } while (0)
+
+void* call_alloc(wgsr_alloc_fn fn, void* ctx, size_t bytes) { return fn ? fn(ctx, bytes) : nullptr; }
+
+}  // namespace
+}  // namespace wgsr
+
+using namespace wgsr;
+
+extern "C" {
+
+const char* wgsr_last_error(void) { return g_err; }
+const char* wgsr_version(void) { return "wgsr 0.1 gfx950"; }
+
+size_t wgsr_geometry_bytes(int P) { return GeomLayout((size_t)(P > 0 ? P : 0)).total; }
+size_t wgsr_binning_bytes(int64_t N, int W, int H) {
+  (void)W; (void)H;
+  return BinLayout((size_t)(N > 0 ? N : 0)).total;
+}
+size_t wgsr_image_bytes(int W, int H) { return ImageLayout(W, H).total; }
+
+int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_alloc, wgsr_alloc_fn binning_alloc,
+                           wgsr_alloc_fn image_alloc, void* ctx, float* out_color, float* out_depth,
+                           float* out_opacity, int32_t* radii, int32_t* n_touched, int64_t* num_rendered,
+                           void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  const wgsr_raster_args& a = *args;
+  hipStream_t s = (hipStream_t)stream;
+  *num_rendered = 0;
+  const size_t HW = (size_t)a.W * a.H;
+  if (a.P == 0) {
+    // upstream returns zero images when there is nothing to rasterise
+    call_alloc(geom_alloc, ctx, 0);
+    call_alloc(binning_alloc, ctx, 0);
+    call_alloc(image_alloc, ctx, 0);
+    HIPCHK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(out_opacity, 0, HW * sizeof(float), s));
+    return WGSR_OK;
+  }
+  const Grid grid(a);
+  const GeomLayout GL((size_t)a.P);
+  const ImageLayout IL(a.W, a.H);
+  void* geom = call_alloc(geom_alloc, ctx, GL.total);
+  if (!geom) return set_error(WGSR_EALLOC, "geometry buffer allocation failed");
+  void* image = call_alloc(image_alloc, ctx, IL.total);
+  if (!image) return set_error(WGSR_EALLOC, "image buffer allocation failed");
+
+  uint32_t* counter = at<uint32_t>(geom, GL.counter);  // [0] num_rendered, [1] error flags
+  HIPCHK(hipMemsetAsync(counter, 0, 16, s));
+  STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1, s));
+
+  // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
+  bool in_alt = false;
+  STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
+                               at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
+                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt));
+  const uint32_t* sorted_g = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
+  // duplicate-slot offsets in depth order; Gaussian -> first slot
+  STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), sorted_g, (size_t)a.P, at<uint32_t>(geom, GL.offs),
+                                    at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
+  uint32_t host_counter[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(host_counter, counter, sizeof(host_counter), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (host_counter[1] && a.prefiltered)
+    return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
+  const size_t N = host_counter[0];
+
+  const BinLayout BL(N);
+  void* binning = call_alloc(binning_alloc, ctx, BL.total);
+  if (!binning && BL.total) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  const uint32_t* sorted_keys = nullptr;
+  const uint32_t* sorted_k = nullptr;
+  if (N > 0) {
+    STAGE(a, s, launch_duplicate(a, geom, sorted_g, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
+                                 at<uint32_t>(binning, BL.slot_g), s));
+    bool talt = false;
+    STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
+                                 at<uint32_t>(binning, BL.val), at<uint32_t>(binning, BL.val_alt), true, N, 0,
+                                 tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
+                                 at<uint32_t>(binning, BL.totals), s, &talt));
+    if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
+    sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
+    sorted_k = at<uint32_t>(binning, talt ? BL.val_alt : BL.val);
+  }
+  uint2* ranges = at<uint2>(image, IL.ranges);
+  if (N > 0) {
+    STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)N, grid.nt, ranges, s));
+  } else {
+    HIPCHK(hipMemsetAsync(ranges, 0, 8 * (size_t)grid.nt, s));
+  }
+  STAGE(a, s, launch_render_fwd(a, ranges, sorted_k, binning ? at<uint32_t>(binning, BL.slot_g) : nullptr, geom,
+                                out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
+                                at<uint32_t>(image, IL.n_contrib), n_touched, s));
+  *num_rendered = (int64_t)N;
+  return WGSR_OK;
+}
+
+int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
+                            const void* binning, const void* image, int64_t num_rendered, const float* dL_dcolor,
+                            const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                            float* dL_dsh, float* dL_dscales, float* dL_drotations, float* dL_dtau, void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  const wgsr_raster_args& a = *args;
+  if (a.P == 0) return WGSR_OK;
+  if (!geom || !image || (num_rendered > 0 && !binning))
+    return set_error(WGSR_EINVAL, "missing forward state buffers");
+  hipStream_t s = (hipStream_t)stream;
+  const Grid grid(a);
+  const ImageLayout IL(a.W, a.H);
+  const size_t N = (size_t)num_rendered;
+  float4* partial = nullptr;
+  if (N > 0) {
+    partial = static_cast<float4*>(call_alloc(scratch_alloc, ctx, 48 * N));
+    if (!partial) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
+    const BinLayout BL(N);
+    const bool talt = tile_sort_in_alt(grid);
+    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
+                                  at<uint32_t>(binning, BL.slot_g), geom, at<float>(image, IL.final_T),
+                                  at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, s));
+  }
+  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                               dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
+  return WGSR_OK;
+}
+
+int wgsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                      uint8_t* present, void* stream) {
+  g_err[0] = 0;
+  if (P < 0) return set_error(WGSR_EINVAL, "negative point count");
+  HIPCHK(launch_mark_visible(P, means3D, viewmatrix, projmatrix, present, (hipStream_t)stream));
+  return WGSR_OK;
+}
+
+int wgsr_dist_cuda2(int P, const float* points, float* out, wgsr_alloc_fn scratch_alloc, void* ctx, void* stream) {
+  g_err[0] = 0;
+  if (P < 0) return set_error(WGSR_EINVAL, "negative point count");
+  if (P == 0) return WGSR_OK;
+  void* scratch = call_alloc(scratch_alloc, ctx, knn_scratch_bytes(P));
+  if (!scratch) return set_error(WGSR_EALLOC, "distCUDA2 scratch allocation failed");
+  HIPCHK(launch_dist_cuda2(P, points, out, scratch, (hipStream_t)stream));
+  return WGSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+// simple_knn._C.distCUDA2 for gfx950.
+//
+// out[i] = mean of the squared distances from point i to its 3 nearest other
+// points -- exact, like upstream's box-pruned search.  Pipeline:
+//   bbox (min/max, seeded with 0 as upstream's cub::DeviceReduce init)
+//   -> 30-bit Morton codes -> radix sort (sort.hip) -> points gathered into
+//   Morton order -> bounds of 256-point boxes and of 64-box super-boxes
+//   -> per point: seed a reject bound from the +-3 Morton neighbours, then
+//      scan every box whose distance to the point is within the current
+//      3rd-best distance.  A wave scans a box when ANY of its lanes needs it;
+//      the box's points are then wave-uniform loads (scalar path), and
+//      scanning a box a lane did not need cannot change its exact answer.
+// Distances are evaluated unfused (dx*dx + dy*dy + dz*dz) so results are
+// bitwise identical to the CPU restatement (oracle/cpu_raster.cpp).
+#include <cfloat>
+
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+constexpr int kBox = 256;
+constexpr int kSuper = 64;  // boxes per super-box
+
+struct KnnLayout {
+  size_t part, bbox, codes, codes_alt, idx, idx_alt, spts, boxes, supers, hist, totals, total;
+  KnnLayout(size_t P) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
+    const size_t nbox = (P + kBox - 1) / kBox, nsup = (nbox + kSuper - 1) / kSuper;
+    part = take(6 * 4 * 1024);
+    bbox = take(6 * 4);
+    codes = take(4 * P);
+    codes_alt = take(4 * P);
+    idx = take(4 * P);
+    idx_alt = take(4 * P);
+    spts = take(16 * P);
+    boxes = take(32 * nbox);
+    supers = take(32 * nsup);
+    hist = take(4 * 256 * (size_t)sort_blocks(P));
+    totals = take(4 * 256);
+    total = o;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_bbox_partial(int P, const float* __restrict__ pts, float* __restrict__ part) {
+  __shared__ float s[6][256];
+  const int t = threadIdx.x;
+  float mn[3] = {0.f, 0.f, 0.f}, mx[3] = {0.f, 0.f, 0.f};  // upstream reduce init {0,0,0}
+  for (int i = blockIdx.x * 256 + t; i < P; i += gridDim.x * 256)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float v = pts[3 * (size_t)i + k];
+      mn[k] = fminf(mn[k], v);
+      mx[k] = fmaxf(mx[k], v);
+    }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { s[k][t] = mn[k]; s[3 + k][t] = mx[k]; }
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        s[k][t] = fminf(s[k][t], s[k][t + off]);
+        s[3 + k][t] = fmaxf(s[3 + k][t], s[3 + k][t + off]);
+      }
+    __syncthreads();
+  }
+  if (t < 6) part[6 * blockIdx.x + t] = s[t][0];
+}
+
+__global__ __launch_bounds__(64) void k_bbox_final(int nparts, const float* __restrict__ part, float* __restrict__ bbox) {
+  const int t = threadIdx.x;
+  if (t >= 6) return;
+  float v = part[t];
+  for (int b = 1; b < nparts; ++b) v = (t < 3) ? fminf(v, part[6 * b + t]) : fmaxf(v, part[6 * b + t]);
+  bbox[t] = v;
+}
+
+__device__ __forceinline__ uint32_t prep_morton(uint32_t x) {
+  x = (x | (x << 16)) & 0x030000FF;
+  x = (x | (x << 8)) & 0x0300F00F;
+  x = (x | (x << 4)) & 0x030C30C3;
+  x = (x | (x << 2)) & 0x09249249;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void k_morton(int P, const float* __restrict__ pts, const float* __restrict__ bbox,
+                                                uint32_t* __restrict__ codes) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  uint32_t c[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float v = ((pts[3 * (size_t)i + k] - bbox[k]) / (bbox[3 + k] - bbox[k])) * ((1 << 10) - 1);
+    c[k] = prep_morton(v == v ? (uint32_t)fmaxf(v, 0.f) : 0u);
+  }
+  codes[i] = c[0] | (c[1] << 1) | (c[2] << 2);
+}
+
+__global__ __launch_bounds__(256) void k_gather_sorted(int P, const float* __restrict__ pts,
+                                                       const uint32_t* __restrict__ idx, float4* __restrict__ spts) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= P) return;
+  const uint32_t i = idx[s];
+  spts[s] = make_float4(pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2], 0.f);
+}
+
+// bounds of `per` consecutive items (float4 points, or (min,max) float4 pairs)
+__global__ __launch_bounds__(256) void k_bounds(int n, int per, const float4* __restrict__ src, int src_is_box,
+                                                float4* __restrict__ dst) {
+  __shared__ float s[6][256];
+  const int t = threadIdx.x;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int j = t; j < per; j += 256) {
+    const int i = blockIdx.x * per + j;
+    if (i >= n) break;
+    const float4 lo = src_is_box ? src[2 * (size_t)i] : src[i];
+    const float4 hi = src_is_box ? src[2 * (size_t)i + 1] : lo;
+    mn[0] = fminf(mn[0], lo.x); mn[1] = fminf(mn[1], lo.y); mn[2] = fminf(mn[2], lo.z);
+    mx[0] = fmaxf(mx[0], hi.x); mx[1] = fmaxf(mx[1], hi.y); mx[2] = fmaxf(mx[2], hi.z);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { s[k][t] = mn[k]; s[3 + k][t] = mx[k]; }
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        s[k][t] = fminf(s[k][t], s[k][t + off]);
+        s[3 + k][t] = fmaxf(s[3 + k][t], s[3 + k][t + off]);
+      }
+    __syncthreads();
+  }
+  if (t == 0) {
+    dst[2 * (size_t)blockIdx.x] = make_float4(s[0][0], s[1][0], s[2][0], 0.f);
+    dst[2 * (size_t)blockIdx.x + 1] = make_float4(s[3][0], s[4][0], s[5][0], 0.f);
+  }
+}
+
+__device__ __forceinline__ float sqdist(float4 a, float4 b) {
+#pragma clang fp contract(off)
+  const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+  return dx * dx + dy * dy + dz * dz;
+}
+
+__device__ __forceinline__ float box_dist(float4 lo, float4 hi, float4 p) {
+#pragma clang fp contract(off)
+  float dx = 0.f, dy = 0.f, dz = 0.f;
+  if (p.x < lo.x || p.x > hi.x) dx = fminf(fabsf(p.x - lo.x), fabsf(p.x - hi.x));
+  if (p.y < lo.y || p.y > hi.y) dy = fminf(fabsf(p.y - lo.y), fabsf(p.y - hi.y));
+  if (p.z < lo.z || p.z > hi.z) dz = fminf(fabsf(p.z - lo.z), fabsf(p.z - hi.z));
+  return dx * dx + dy * dy + dz * dz;
+}
+
+__device__ __forceinline__ void update3(float d, float& b0, float& b1, float& b2) {
+  if (b0 > d) { const float t = b0; b0 = d; d = t; }
+  if (b1 > d) { const float t = b1; b1 = d; d = t; }
+  if (b2 > d) { b2 = d; }
+}
+
+__global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ spts,
+                                             const uint32_t* __restrict__ idx, const float4* __restrict__ boxes,
+                                             int nbox, const float4* __restrict__ supers, int nsup,
+                                             float* __restrict__ out) {
+  const int s0 = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = s0 < P;
+  const int s = valid ? s0 : P - 1;
+  const float4 p = spts[s];
+  float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
+  for (int i = max(0, s - 3); i <= min(P - 1, s + 3); ++i)
+    if (i != s) update3(sqdist(p, spts[i]), b0, b1, b2);
+  const float reject = b2;
+  b0 = b1 = b2 = FLT_MAX;
+  for (int sb = 0; sb < nsup; ++sb) {
+    const bool need_s = box_dist(supers[2 * sb], supers[2 * sb + 1], p) <= fminf(reject, b2);
+    if (!__any(need_s)) continue;
+    const int bend = min(nbox, (sb + 1) * kSuper);
+    for (int b = sb * kSuper; b < bend; ++b) {
+      const bool need_b = box_dist(boxes[2 * b], boxes[2 * b + 1], p) <= fminf(reject, b2);
+      if (!__any(need_b)) continue;
+      const int iend = min(P, (b + 1) * kBox);
+      for (int i = b * kBox; i < iend; ++i) {
+        const float d = sqdist(p, spts[i]);
+        if (i != s) update3(d, b0, b1, b2);
+      }
+    }
+  }
+  if (valid) out[idx[s]] = (b0 + b1 + b2) / 3.0f;
+}
+
+}  // namespace
+
+size_t knn_scratch_bytes(int P) { return KnnLayout((size_t)P).total; }
+
+hipError_t launch_dist_cuda2(int P, const float* points, float* out, void* scratch, hipStream_t s) {
+  if (P <= 0) return hipSuccess;
+  const KnnLayout L((size_t)P);
+  const int nparts = min(1024, (P + 255) / 256);
+  hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, P, points, at<float>(scratch, L.part));
+  hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, nparts, at<float>(scratch, L.part),
+                     at<float>(scratch, L.bbox));
+  hipLaunchKernelGGL(k_morton, dim3((P + 255) / 256), dim3(256), 0, s, P, points, at<float>(scratch, L.bbox),
+                     at<uint32_t>(scratch, L.codes));
+  bool in_alt = false;
+  hipError_t e = radix_sort_pairs(at<uint32_t>(scratch, L.codes), at<uint32_t>(scratch, L.codes_alt),
+                                  at<uint32_t>(scratch, L.idx), at<uint32_t>(scratch, L.idx_alt), true, (size_t)P, 0,
+                                  30, at<uint32_t>(scratch, L.hist), at<uint32_t>(scratch, L.totals), s, &in_alt);
+  if (e != hipSuccess) return e;
+  const uint32_t* sidx = at<uint32_t>(scratch, in_alt ? L.idx_alt : L.idx);
+  float4* spts = at<float4>(scratch, L.spts);
+  hipLaunchKernelGGL(k_gather_sorted, dim3((P + 255) / 256), dim3(256), 0, s, P, points, sidx, spts);
+  const int nbox = (P + kBox - 1) / kBox, nsup = (nbox + kSuper - 1) / kSuper;
+  float4* boxes = at<float4>(scratch, L.boxes);
+  float4* supers = at<float4>(scratch, L.supers);
+  hipLaunchKernelGGL(k_bounds, dim3(nbox), dim3(256), 0, s, P, kBox, spts, 0, boxes);
+  hipLaunchKernelGGL(k_bounds, dim3(nsup), dim3(256), 0, s, nbox, kSuper, boxes, 1, supers);
+  hipLaunchKernelGGL(k_knn, dim3((P + 255) / 256), dim3(256), 0, s, P, spts, sidx, boxes, nbox, supers, nsup, out);
+  return hipGetLastError();
+}
+
+}  // namespace wgsr

@@ -1,0 +1,466 @@
+// Backward rasteriser stages for gfx950.
+//
+//   render_bwd  one 256-thread workgroup per tile walks the tile's list back
+//               to front (upstream BACKWARD::renderCUDA math).  Instead of one
+//               float atomic per (pixel, Gaussian, quantity) -- scattered
+//               single-lane atomics run ~17x under the chip's atomic rate on
+//               MI355X -- each wave reduces its 64 pixels' contributions in
+//               registers, the four waves combine through LDS, and the tile
+//               writes ONE 48-byte partial record per (Gaussian, tile) pair
+//               into that pair's duplicate slot.  No atomics, deterministic.
+//   gauss_bwd   one lane per Gaussian: sums its contiguous slot range of
+//               partial records (fixed order -> bitwise reproducible), then
+//               runs cov2D -> cov3D -> (scale, rotation), SH, projection,
+//               depth and pose (w-pose dL/dtau) backward in registers and
+//               writes every output of _C.rasterize_gaussians_backward once.
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+__constant__ float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+__global__ __launch_bounds__(256) void k_render_bwd(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ slot_g,
+    const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
+    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
+    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial) {
+  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
+  __shared__ uint32_t sK[kBatch];
+  __shared__ float sP[4][kBatch][10];
+  __shared__ uint32_t s_max[4];
+  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int px = (int)(tile % gx) * kTile + (w & 1) * 8 + (lane & 7);
+  const int py = (int)(tile / gx) * kTile + (w >> 1) * 8 + (lane >> 3);
+  const bool inside = px < W && py < H;
+  const size_t pid = (size_t)py * W + px;
+  const size_t HW = (size_t)H * W;
+  const uint2 range = ranges[tile];
+
+  const float T_final = inside ? final_Ts[pid] : 0.f;
+  const uint32_t last = inside ? n_contrib[pid] : 0u;
+  // entries behind every pixel's last contributor cannot receive gradient
+  uint32_t m = last;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  if (lane == 0) s_max[w] = m;
+  __syncthreads();
+  const uint32_t maxlast = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+  const uint32_t end = range.x + maxlast;
+  for (uint32_t i = end + t; i < range.y; i += 256) {
+    const uint32_t k = sorted_k[i];
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    partial[3 * (size_t)k] = z;
+    partial[3 * (size_t)k + 1] = z;
+    partial[3 * (size_t)k + 2] = z;
+  }
+
+  float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f, dpd = 0.f;
+  if (inside) {
+    dpix0 = dL_dpix[pid];
+    dpix1 = dL_dpix[HW + pid];
+    dpix2 = dL_dpix[2 * HW + pid];
+    dpd = dL_ddep[pid];
+  }
+  const float bg_dot = bg[0] * dpix0 + bg[1] * dpix1 + bg[2] * dpix2;
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const float fpx = (float)px, fpy = (float)py;
+
+  float T = T_final;
+  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc_d = 0.f;
+  float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, ld = 0.f;
+  uint32_t contributor = maxlast;
+
+  for (uint32_t b_end = end; b_end > range.x;) {
+    const uint32_t b_start = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x;
+    const int cnt = (int)(b_end - b_start);
+    __syncthreads();
+    if (t < cnt) {
+      const uint32_t k = sorted_k[b_end - 1 - t];
+      const uint32_t g = slot_g[k];
+      sA[t] = splat[3 * (size_t)g];
+      sB[t] = splat[3 * (size_t)g + 1];
+      sC[t] = splat[3 * (size_t)g + 2];
+      sK[t] = k;
+    }
+    __syncthreads();
+    for (int j = 0; j < cnt; ++j) {
+      --contributor;
+      float gv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) gv[q] = 0.f;
+      bool contrib = false;
+      if (contributor < last) {
+        const float4 A = sA[j];
+        const float4 B = sB[j];
+        const float dx = A.x - fpx, dy = A.y - fpy;
+        const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+        if (power <= 0.0f) {
+          const float G = __expf(power);
+          const float alpha = fminf(kMaxAlpha, B.y * G);
+          if (alpha >= kMinAlpha) {
+            contrib = true;
+            const float4 Cc = sC[j];
+            T = T / (1.f - alpha);
+            const float dchannel_dcolor = alpha * T;
+            float dL_dalpha = 0.f;
+            acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+            acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+            acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+            lc0 = Cc.x; lc1 = Cc.y; lc2 = Cc.z;
+            dL_dalpha += (Cc.x - acc0) * dpix0;
+            dL_dalpha += (Cc.y - acc1) * dpix1;
+            dL_dalpha += (Cc.z - acc2) * dpix2;
+            gv[6] = dchannel_dcolor * dpix0;
+            gv[7] = dchannel_dcolor * dpix1;
+            gv[8] = dchannel_dcolor * dpix2;
+            acc_d = last_alpha * ld + (1.f - last_alpha) * acc_d;
+            ld = B.z;
+            dL_dalpha += (B.z - acc_d) * dpd;
+            gv[9] = dchannel_dcolor * dpd;
+            dL_dalpha *= T;
+            last_alpha = alpha;
+            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+            const float dL_dG = B.y * dL_dalpha;
+            const float gdx = G * dx, gdy = G * dy;
+            const float dG_ddelx = -gdx * A.z - gdy * A.w;
+            const float dG_ddely = -gdy * B.x - gdx * A.w;
+            gv[0] = dL_dG * dG_ddelx * ddelx_dx;
+            gv[1] = dL_dG * dG_ddely * ddely_dy;
+            gv[2] = -0.5f * gdx * dx * dL_dG;
+            gv[3] = -0.5f * gdx * dy * dL_dG;
+            gv[4] = -0.5f * gdy * dy * dL_dG;
+            gv[5] = G * dL_dalpha;
+          }
+        }
+      }
+      if (__ballot(contrib) != 0) {
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+          const float s = wave_sum(gv[q]);
+          if (lane == 0) sP[w][j][q] = s;
+        }
+      } else if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 10; ++q) sP[w][j][q] = 0.f;
+      }
+    }
+    __syncthreads();
+    if (t < cnt) {
+      float s[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) s[q] = sP[0][t][q] + sP[1][t][q] + sP[2][t][q] + sP[3][t][q];
+      const size_t k = sK[t];
+      partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
+      partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
+      partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
+    }
+    b_end = b_start;
+  }
+}
+
+__device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]); }
+
+// upstream computeColorFromSH backward: writes dL/dsh[0..K), returns dL/dmean
+__device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
+  const f3 dir_orig = sub3(pos, campos);
+  const float len = sqrtf(dot3(dir_orig, dir_orig));
+  const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+  dRGB.x *= (cbits & 1u) ? 0.f : 1.f;
+  dRGB.y *= (cbits & 2u) ? 0.f : 1.f;
+  dRGB.z *= (cbits & 4u) ? 0.f : 1.f;
+  auto put = [&](int k, float wgt) {
+    dsh[3 * k] = wgt * dRGB.x;
+    dsh[3 * k + 1] = wgt * dRGB.y;
+    dsh[3 * k + 2] = wgt * dRGB.z;
+  };
+  f3 dx = mk3(0.f, 0.f, 0.f), dy = dx, dz = dx;
+  const float x = dir.x, y = dir.y, z = dir.z;
+  put(0, SH_C0);
+  if (deg > 0) {
+    put(1, -SH_C1 * y);
+    put(2, SH_C1 * z);
+    put(3, -SH_C1 * x);
+    dx = scl3(-SH_C1, ldc(sh, 3));
+    dy = scl3(-SH_C1, ldc(sh, 1));
+    dz = scl3(SH_C1, ldc(sh, 2));
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+      put(4, SH_C2[0] * xy);
+      put(5, SH_C2[1] * yz);
+      put(6, SH_C2[2] * (2.f * zz - xx - yy));
+      put(7, SH_C2[3] * xz);
+      put(8, SH_C2[4] * (xx - yy));
+      dx = add3(dx, add3(add3(scl3(SH_C2[0] * y, ldc(sh, 4)), scl3(SH_C2[2] * 2.f * -x, ldc(sh, 6))),
+                         add3(scl3(SH_C2[3] * z, ldc(sh, 7)), scl3(SH_C2[4] * 2.f * x, ldc(sh, 8)))));
+      dy = add3(dy, add3(add3(scl3(SH_C2[0] * x, ldc(sh, 4)), scl3(SH_C2[1] * z, ldc(sh, 5))),
+                         add3(scl3(SH_C2[2] * 2.f * -y, ldc(sh, 6)), scl3(SH_C2[4] * 2.f * -y, ldc(sh, 8)))));
+      dz = add3(dz, add3(add3(scl3(SH_C2[1] * y, ldc(sh, 5)), scl3(SH_C2[2] * 2.f * 2.f * z, ldc(sh, 6))),
+                         scl3(SH_C2[3] * x, ldc(sh, 7))));
+      if (deg > 2) {
+        put(9, SH_C3[0] * y * (3.f * xx - yy));
+        put(10, SH_C3[1] * xy * z);
+        put(11, SH_C3[2] * y * (4.f * zz - xx - yy));
+        put(12, SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy));
+        put(13, SH_C3[4] * x * (4.f * zz - xx - yy));
+        put(14, SH_C3[5] * z * (xx - yy));
+        put(15, SH_C3[6] * x * (xx - 3.f * yy));
+        dx = add3(dx, scl3(SH_C3[0] * 3.f * 2.f * xy, ldc(sh, 9)));
+        dx = add3(dx, scl3(SH_C3[1] * yz, ldc(sh, 10)));
+        dx = add3(dx, scl3(SH_C3[2] * -2.f * xy, ldc(sh, 11)));
+        dx = add3(dx, scl3(SH_C3[3] * -3.f * 2.f * xz, ldc(sh, 12)));
+        dx = add3(dx, scl3(SH_C3[4] * (-3.f * xx + 4.f * zz - yy), ldc(sh, 13)));
+        dx = add3(dx, scl3(SH_C3[5] * 2.f * xz, ldc(sh, 14)));
+        dx = add3(dx, scl3(SH_C3[6] * 3.f * (xx - yy), ldc(sh, 15)));
+        dy = add3(dy, scl3(SH_C3[0] * 3.f * (xx - yy), ldc(sh, 9)));
+        dy = add3(dy, scl3(SH_C3[1] * xz, ldc(sh, 10)));
+        dy = add3(dy, scl3(SH_C3[2] * (-3.f * yy + 4.f * zz - xx), ldc(sh, 11)));
+        dy = add3(dy, scl3(SH_C3[3] * -3.f * 2.f * yz, ldc(sh, 12)));
+        dy = add3(dy, scl3(SH_C3[4] * -2.f * xy, ldc(sh, 13)));
+        dy = add3(dy, scl3(SH_C3[5] * -2.f * yz, ldc(sh, 14)));
+        dy = add3(dy, scl3(SH_C3[6] * -3.f * 2.f * xy, ldc(sh, 15)));
+        dz = add3(dz, scl3(SH_C3[1] * xy, ldc(sh, 10)));
+        dz = add3(dz, scl3(SH_C3[2] * 4.f * 2.f * yz, ldc(sh, 11)));
+        dz = add3(dz, scl3(SH_C3[3] * 3.f * (2.f * zz - xx - yy), ldc(sh, 12)));
+        dz = add3(dz, scl3(SH_C3[4] * 4.f * 2.f * xz, ldc(sh, 13)));
+        dz = add3(dz, scl3(SH_C3[5] * (xx - yy), ldc(sh, 14)));
+      }
+    }
+  }
+  const f3 dL_ddir = mk3(dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB));
+  const f3 v = dir_orig;
+  const float sum2 = dot3(v, v);
+  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+  return mk3(((sum2 - v.x * v.x) * dL_ddir.x - v.y * v.x * dL_ddir.y - v.z * v.x * dL_ddir.z) * invsum32,
+             (-v.x * v.y * dL_ddir.x + (sum2 - v.y * v.y) * dL_ddir.y - v.z * v.y * dL_ddir.z) * invsum32,
+             (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32);
+}
+
+__global__ __launch_bounds__(256) void k_gauss_bwd(
+    int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
+    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
+    const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
+    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
+    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
+    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const size_t i3 = 3 * (size_t)i, i4 = 4 * (size_t)i, i6 = 6 * (size_t)i;
+  float* osh = o_sh ? o_sh + 3 * (size_t)M * i : nullptr;
+  if (!(radii[i] > 0)) {
+    for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
+    for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
+    for (int k = 0; k < 4; ++k) o_rot[i4 + k] = 0.f;
+    if (osh) for (int k = 0; k < 3 * M; ++k) osh[k] = 0.f;
+    o_opac[i] = 0.f;
+    return;
+  }
+  // ---- sum this Gaussian's per-tile partial records (fixed slot order)
+  float g[10];
+#pragma unroll
+  for (int q = 0; q < 10; ++q) g[q] = 0.f;
+  {
+    const size_t s0 = slot_start[i], n = tiles[i];
+    for (size_t k = s0; k < s0 + n; ++k) {
+      const float4 a = partial[3 * k], b = partial[3 * k + 1], c = partial[3 * k + 2];
+      g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
+      g[4] += b.x; g[5] += b.y; g[6] += b.z; g[7] += b.w;
+      g[8] += c.x; g[9] += c.y;
+    }
+  }
+  o_m2d[i3] = g[0]; o_m2d[i3 + 1] = g[1]; o_m2d[i3 + 2] = 0.f;
+  o_opac[i] = g[5];
+  o_col[i3] = g[6]; o_col[i3 + 1] = g[7]; o_col[i3 + 2] = g[8];
+  const float dcx = g[2], dcy = g[3], dcw = g[4], ddepth = g[9];
+
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  // ---- cov2D backward (upstream computeCov2DCUDA)
+  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+  const f3 t = xform43(c.view, mean);
+  float cv[6];
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  f3 sv = mk3(0.f, 0.f, 0.f);
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
+  } else {
+    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
+    q = reinterpret_cast<const float4*>(rots)[i];
+    cov3d_from(sv, scale_mod, q, cv);
+  }
+  float S[3][3];
+  sym3(cv, S);
+  float T[2][3];
+  f3 tc;
+  float xm, ym;
+  ewa_T(c, t, T, tc, xm, ym);
+  float a, b, cc;
+  cov2d(T, S, a, b, cc);
+  const float denom = a * cc - b * b;
+  float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+  float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (denom2inv != 0) {
+    dL_da = denom2inv * (-cc * cc * dcx + 2 * b * cc * dcy + (denom - a * cc) * dcw);
+    dL_dc = denom2inv * (-a * a * dcw + 2 * a * b * dcy + (denom - a * cc) * dcx);
+    dL_db = denom2inv * 2 * (b * cc * dcx - (denom + 2 * b * b) * dcy + a * b * dcw);
+    ocov[0] = T[0][0] * T[0][0] * dL_da + T[0][0] * T[1][0] * dL_db + T[1][0] * T[1][0] * dL_dc;
+    ocov[3] = T[0][1] * T[0][1] * dL_da + T[0][1] * T[1][1] * dL_db + T[1][1] * T[1][1] * dL_dc;
+    ocov[5] = T[0][2] * T[0][2] * dL_da + T[0][2] * T[1][2] * dL_db + T[1][2] * T[1][2] * dL_dc;
+    ocov[1] = 2 * T[0][0] * T[0][1] * dL_da + (T[0][0] * T[1][1] + T[0][1] * T[1][0]) * dL_db +
+              2 * T[1][0] * T[1][1] * dL_dc;
+    ocov[2] = 2 * T[0][0] * T[0][2] * dL_da + (T[0][0] * T[1][2] + T[0][2] * T[1][0]) * dL_db +
+              2 * T[1][0] * T[1][2] * dL_dc;
+    ocov[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db +
+              2 * T[1][1] * T[1][2] * dL_dc;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o_cov[i6 + k] = ocov[k];
+  float dT[2][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float s0 = T[0][0] * S[k][0] + T[0][1] * S[k][1] + T[0][2] * S[k][2];
+    const float s1 = T[1][0] * S[k][0] + T[1][1] * S[k][1] + T[1][2] * S[k][2];
+    dT[0][k] = 2 * s0 * dL_da + s1 * dL_db;
+    dT[1][k] = 2 * s1 * dL_dc + s0 * dL_db;
+  }
+  const float dJ00 = c.Rw[0][0] * dT[0][0] + c.Rw[0][1] * dT[0][1] + c.Rw[0][2] * dT[0][2];
+  const float dJ02 = c.Rw[2][0] * dT[0][0] + c.Rw[2][1] * dT[0][1] + c.Rw[2][2] * dT[0][2];
+  const float dJ11 = c.Rw[1][0] * dT[1][0] + c.Rw[1][1] * dT[1][1] + c.Rw[1][2] * dT[1][2];
+  const float dJ12 = c.Rw[2][0] * dT[1][0] + c.Rw[2][1] * dT[1][1] + c.Rw[2][2] * dT[1][2];
+  const float tz = 1.f / tc.z, tz2 = tz * tz, tz3 = tz2 * tz;
+  const f3 dL_dt = mk3(xm * -c.fx * tz2 * dJ02, ym * -c.fy * tz2 * dJ12,
+                       -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2 * c.fx * tc.x) * tz3 * dJ02 +
+                           (2 * c.fy * tc.y) * tz3 * dJ12);
+  f3 dm = mk3(c.Rw[0][0] * dL_dt.x + c.Rw[1][0] * dL_dt.y + c.Rw[2][0] * dL_dt.z,
+              c.Rw[0][1] * dL_dt.x + c.Rw[1][1] * dL_dt.y + c.Rw[2][1] * dL_dt.z,
+              c.Rw[0][2] * dL_dt.x + c.Rw[1][2] * dL_dt.y + c.Rw[2][2] * dL_dt.z);
+  // pose (w-pose): left perturbation of the camera point (clamped, V8) and of W
+  f3 tau_rho = dL_dt;
+  f3 tau_theta = cross3(tc, dL_dt);
+  {
+    const float J00 = c.fx / tc.z, J02 = -(c.fx * tc.x) / (tc.z * tc.z);
+    const float J11 = c.fy / tc.z, J12 = -(c.fy * tc.y) / (tc.z * tc.z);
+#pragma unroll
+    for (int col = 0; col < 3; ++col) {
+      const f3 rc = mk3(c.Rw[0][col], c.Rw[1][col], c.Rw[2][col]);
+      const f3 gc = mk3(J00 * dT[0][col], J11 * dT[1][col], J02 * dT[0][col] + J12 * dT[1][col]);
+      tau_theta = add3(tau_theta, cross3(rc, gc));
+    }
+  }
+  // ---- preprocess backward: NDC means2D -> mean (through projmatrix)
+  const float* pm = c.proj;
+  const float4 hom = xform44(pm, mean);
+  const float m_w = 1.0f / (hom.w + 0.0000001f);
+  const float mul1 = (pm[0] * mean.x + pm[4] * mean.y + pm[8] * mean.z + pm[12]) * m_w * m_w;
+  const float mul2 = (pm[1] * mean.x + pm[5] * mean.y + pm[9] * mean.z + pm[13]) * m_w * m_w;
+  const float g2x = g[0], g2y = g[1];
+  dm.x += (pm[0] * m_w - pm[3] * mul1) * g2x + (pm[1] * m_w - pm[3] * mul2) * g2y;
+  dm.y += (pm[4] * m_w - pm[7] * mul1) * g2x + (pm[5] * m_w - pm[7] * mul2) * g2y;
+  dm.z += (pm[8] * m_w - pm[11] * mul1) * g2x + (pm[9] * m_w - pm[11] * mul2) * g2y;
+  // pose through the projection (projmatrix_raw a, b, e terms: V5) and depth
+  {
+    const float alpha_ = m_w, beta_ = -hom.x * m_w * m_w, gamma_ = -hom.y * m_w * m_w;
+    const float pa = praw[0], pb = praw[5], pe = praw[11];
+    f3 gp = add3(scl3(g2x, mk3(alpha_ * pa, 0.f, beta_ * pe)), scl3(g2y, mk3(0.f, alpha_ * pb, gamma_ * pe)));
+    gp.z += ddepth;
+    tau_rho = add3(tau_rho, gp);
+    tau_theta = add3(tau_theta, cross3(t, gp));
+  }
+  dm.x += ddepth * c.view[2];
+  dm.y += ddepth * c.view[6];
+  dm.z += ddepth * c.view[10];
+  if (osh) {
+    const f3 dmsh = sh_backward(D, shs + 3 * (size_t)M * i, mean, mk3(campos_p[0], campos_p[1], campos_p[2]),
+                                clamped[i], mk3(g[6], g[7], g[8]), osh);
+    dm = add3(dm, dmsh);
+    const int K = (D + 1) * (D + 1);
+    for (int k = 3 * K; k < 3 * M; ++k) osh[k] = 0.f;
+  }
+  // ---- cov3D -> scale / rotation (upstream computeCov3D backward)
+  if (!cov_pre) {
+    float R[3][3];
+    quat_rot(q, R);
+    const float s3[3] = {scale_mod * sv.x, scale_mod * sv.y, scale_mod * sv.z};
+    const float dS[3][3] = {{ocov[0], 0.5f * ocov[1], 0.5f * ocov[2]},
+                            {0.5f * ocov[1], ocov[3], 0.5f * ocov[4]},
+                            {0.5f * ocov[2], 0.5f * ocov[4], ocov[5]}};
+    float Mm[3][3], dM[3][3];
+#pragma unroll
+    for (int r0 = 0; r0 < 3; ++r0)
+#pragma unroll
+      for (int c0 = 0; c0 < 3; ++c0) Mm[r0][c0] = s3[r0] * R[c0][r0];
+#pragma unroll
+    for (int r0 = 0; r0 < 3; ++r0)
+#pragma unroll
+      for (int c0 = 0; c0 < 3; ++c0)
+        dM[r0][c0] = 2.f * (Mm[r0][0] * dS[0][c0] + Mm[r0][1] * dS[1][c0] + Mm[r0][2] * dS[2][c0]);
+    // w.r.t. the modified scale, as upstream (V9)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o_sc[i3 + k] = R[0][k] * dM[k][0] + R[1][k] * dM[k][1] + R[2][k] * dM[k][2];
+    float G[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) G[j][k] = s3[k] * dM[k][j];
+    const float rr = q.x, x = q.y, y = q.z, z = q.w;
+    o_rot[i4 + 0] = 2 * z * (G[1][0] - G[0][1]) + 2 * y * (G[0][2] - G[2][0]) + 2 * x * (G[2][1] - G[1][2]);
+    o_rot[i4 + 1] = 2 * y * (G[1][0] + G[0][1]) + 2 * z * (G[2][0] + G[0][2]) + 2 * rr * (G[2][1] - G[1][2]) -
+                    4 * x * (G[2][2] + G[1][1]);
+    o_rot[i4 + 2] = 2 * x * (G[1][0] + G[0][1]) + 2 * rr * (G[0][2] - G[2][0]) + 2 * z * (G[2][1] + G[1][2]) -
+                    4 * y * (G[2][2] + G[0][0]);
+    o_rot[i4 + 3] = 2 * rr * (G[1][0] - G[0][1]) + 2 * x * (G[2][0] + G[0][2]) + 2 * y * (G[2][1] + G[1][2]) -
+                    4 * z * (G[1][1] + G[0][0]);
+  } else {
+    for (int k = 0; k < 3; ++k) o_sc[i3 + k] = 0.f;
+    for (int k = 0; k < 4; ++k) o_rot[i4 + k] = 0.f;
+  }
+  o_m3d[i3] = dm.x; o_m3d[i3 + 1] = dm.y; o_m3d[i3 + 2] = dm.z;
+  o_tau[i6 + 0] = tau_rho.x; o_tau[i6 + 1] = tau_rho.y; o_tau[i6 + 2] = tau_rho.z;
+  o_tau[i6 + 3] = tau_theta.x; o_tau[i6 + 4] = tau_theta.y; o_tau[i6 + 5] = tau_theta.z;
+}
+
+}  // namespace
+
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
+                             const uint32_t* slot_g, const void* geom, const float* final_T,
+                             const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
+                             float4* partial, hipStream_t s) {
+  const GeomLayout L(a.P);
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  const int nt = gx * gy;
+  hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(256), 0, s, ranges, sorted_k, slot_g, at<float4>(geom, L.splat),
+                     a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
+                            const float4* partial, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                            float* dL_drot, float* dL_dtau, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  const GeomLayout L(a.P);
+  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, a.D, a.M, radii,
+                     at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
+                     partial, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
+                     a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
+                     dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
+                     dL_dscales, dL_drot, dL_dtau);
+  return hipGetLastError();
+}
+
+}  // namespace wgsr

@@ -1,0 +1,344 @@
+// Forward rasteriser stages for gfx950.
+//
+//   preprocess   one lane per Gaussian: cull, cov3D -> EWA cov2D -> conic,
+//                radius + tile rectangle, SH -> RGB; writes a 48-byte splat
+//                record per Gaussian (the only thing the tile loops read).
+//   [depth sort] visible Gaussians by depth (stable by id)      -- sort.hip
+//   [scan]       duplicate-slot offsets in depth order           -- sort.hip
+//   duplicate    wave-cooperative expansion of every Gaussian's tile
+//                rectangle into (tile, slot) pairs: each lane writes one pair,
+//                so the writes of a wave are contiguous.
+//   [tile sort]  stable sort of the pairs by tile id             -- sort.hip
+//   ranges       per-tile [start, end) by binary search.
+//   render       one 256-thread workgroup per 16x16 tile, splat records staged
+//                in LDS 256 at a time, front-to-back alpha blending.
+//
+// Sorting by depth first and then stably by tile yields exactly upstream's
+// (tile << 32 | depth) order (ties broken by Gaussian index) while the
+// N-sized sort only moves tile ids.
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+__constant__ float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+__device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]); }
+
+// SH -> RGB (upstream computeColorFromSH forward), clamp flags in bits 0..2
+__device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32_t& clamp_bits) {
+  f3 r = scl3(SH_C0, ldc(sh, 0));
+  if (deg > 0) {
+    const float x = dir.x, y = dir.y, z = dir.z;
+    r = sub3(add3(sub3(r, scl3(SH_C1 * y, ldc(sh, 1))), scl3(SH_C1 * z, ldc(sh, 2))), scl3(SH_C1 * x, ldc(sh, 3)));
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+      r = add3(r, scl3(SH_C2[0] * xy, ldc(sh, 4)));
+      r = add3(r, scl3(SH_C2[1] * yz, ldc(sh, 5)));
+      r = add3(r, scl3(SH_C2[2] * (2.f * zz - xx - yy), ldc(sh, 6)));
+      r = add3(r, scl3(SH_C2[3] * xz, ldc(sh, 7)));
+      r = add3(r, scl3(SH_C2[4] * (xx - yy), ldc(sh, 8)));
+      if (deg > 2) {
+        r = add3(r, scl3(SH_C3[0] * y * (3.f * xx - yy), ldc(sh, 9)));
+        r = add3(r, scl3(SH_C3[1] * xy * z, ldc(sh, 10)));
+        r = add3(r, scl3(SH_C3[2] * y * (4.f * zz - xx - yy), ldc(sh, 11)));
+        r = add3(r, scl3(SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), ldc(sh, 12)));
+        r = add3(r, scl3(SH_C3[4] * x * (4.f * zz - xx - yy), ldc(sh, 13)));
+        r = add3(r, scl3(SH_C3[5] * z * (xx - yy), ldc(sh, 14)));
+        r = add3(r, scl3(SH_C3[6] * x * (xx - 3.f * yy), ldc(sh, 15)));
+      }
+    }
+  }
+  r = add3(r, mk3(0.5f, 0.5f, 0.5f));
+  clamp_bits = (r.x < 0 ? 1u : 0u) | (r.y < 0 ? 2u : 0u) | (r.z < 0 ? 4u : 0u);
+  return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ushort4* __restrict__ rect, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ err_flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  radii[i] = 0;
+  n_touched[i] = 0;
+  tiles[i] = 0;
+  dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort last
+
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  const f3 p = mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+  const float4 hom = xform44(c.proj, p);
+  const float pw = 1.0f / (hom.w + 0.0000001f);
+  const f3 pproj = mk3(hom.x * pw, hom.y * pw, hom.z * pw);
+  const f3 pv = xform43(c.view, p);
+  if (pv.z <= kNearZ) {
+    if (prefiltered) atomicOr(err_flag, 1u);
+    return;
+  }
+  float cv[6];
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[6 * (size_t)i + k];
+  } else {
+    const f3 s = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+    const float4 q = reinterpret_cast<const float4*>(rots)[i];
+    cov3d_from(s, scale_mod, q, cv);
+  }
+  float S[3][3];
+  sym3(cv, S);
+  float T[2][3];
+  f3 tc;
+  float xm, ym;
+  ewa_T(c, pv, T, tc, xm, ym);
+  float a, b, cc;
+  cov2d(T, S, a, b, cc);
+  const float det = a * cc - b * b;
+  if (det == 0.0f) return;
+  const float det_inv = 1.f / det;
+  const float mid = 0.5f * (a + cc);
+  const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+  const float px = ndc2pix(pproj.x, W), py = ndc2pix(pproj.y, H);
+  const int r = (int)my_radius;
+  const int x0 = min(gx, max(0, (int)((px - r) / kTile)));
+  const int y0 = min(gy, max(0, (int)((py - r) / kTile)));
+  const int x1 = min(gx, max(0, (int)((px + r + kTile - 1) / kTile)));
+  const int y1 = min(gy, max(0, (int)((py + r + kTile - 1) / kTile)));
+  if ((x1 - x0) * (y1 - y0) == 0) return;
+
+  f3 rgb;
+  uint32_t cbits = 0;
+  if (colors) {
+    rgb = mk3(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2]);
+  } else {
+    f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+    const float len = sqrtf(dot3(dir, dir));
+    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+    rgb = sh_to_rgb(D, shs + 3 * (size_t)M * i, dir, cbits);
+  }
+  const float o = opac[i];
+  splat[3 * (size_t)i + 0] = make_float4(px, py, cc * det_inv, -b * det_inv);
+  splat[3 * (size_t)i + 1] = make_float4(a * det_inv, o, pv.z, 0.f);
+  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+  rect[i] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
+  tiles[i] = (uint32_t)((x1 - x0) * (y1 - y0));
+  clamped[i] = cbits;
+  dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
+  radii[i] = r;
+}
+
+// Expand the tile rectangles of ranks [r0, r0 + 64) (one wave) into pairs.
+__global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uint32_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ sorted_g,
+                                                   const ushort4* __restrict__ rect, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ slot_g) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) - lane;
+  if (r0 >= P) return;
+  const uint32_t r = r0 + lane;
+  const uint32_t my_off = offs[min(r, P)];
+  const uint32_t start = offs[r0];
+  const uint32_t end = offs[min(r0 + 64, P)];
+  uint32_t g = 0, rlo = 0, rhi = 0;
+  if (r < P) {
+    g = sorted_g[r];
+    if (offs[r + 1] > my_off) {
+      const ushort4 rc = rect[g];
+      rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
+      rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);
+    }
+  }
+  for (uint32_t base = start; base < end; base += 64) {
+    const uint32_t k = base + lane;
+    const uint32_t kk = min(k, end - 1);
+    int lo = 0, hi = 64;
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const int mid = (lo + hi) >> 1;
+      const uint32_t v = __shfl(my_off, mid, 64);
+      if (v <= kk) lo = mid; else hi = mid;
+    }
+    const uint32_t local = kk - __shfl(my_off, lo, 64);
+    const uint32_t gg = __shfl(g, lo, 64);
+    const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
+    const uint32_t x0 = a & 0xFFFF, y0 = a >> 16, x1 = b & 0xFFFF;
+    const uint32_t w = x1 - x0;
+    const uint32_t ty = y0 + local / w, tx = x0 + local % w;
+    if (k < end) {
+      keys[k] = ty * (uint32_t)gx + tx;
+      slot_g[k] = gg;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ keys, uint32_t N, int ntiles,
+                                                uint2* __restrict__ ranges) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  auto lower = [&](uint32_t v) {
+    uint32_t lo = 0, hi = N;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (keys[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  ranges[t] = make_uint2(lower((uint32_t)t), lower((uint32_t)t + 1));
+}
+
+// One workgroup = one 16x16 tile; wave w owns the 8x8 quadrant (w & 1, w >> 1).
+__global__ __launch_bounds__(256) void k_render_fwd(const uint2* __restrict__ ranges,
+                                                    const uint32_t* __restrict__ sorted_k,
+                                                    const uint32_t* __restrict__ slot_g,
+                                                    const float4* __restrict__ splat, int W, int H, int gx,
+                                                    int ntiles, const float* __restrict__ bg,
+                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
+                                                    float* __restrict__ out_opac, float* __restrict__ final_T,
+                                                    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+  __shared__ float4 sA[256], sB[256], sC[256];
+  __shared__ uint32_t sG[256];
+  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int px = (int)(tile % gx) * kTile + (w & 1) * 8 + (lane & 7);
+  const int py = (int)(tile / gx) * kTile + (w >> 1) * 8 + (lane >> 3);
+  const bool inside = px < W && py < H;
+  const float fpx = (float)px, fpy = (float)py;
+  const uint2 range = ranges[tile];
+
+  bool done = !inside;
+  float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+  uint32_t contributor = 0, last = 0;
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += 256) {
+    if (__syncthreads_count(done) == 256) break;
+    const uint32_t idx = b0 + t;
+    if (idx < range.y) {
+      const uint32_t g = slot_g[sorted_k[idx]];
+      sA[t] = splat[3 * (size_t)g];
+      sB[t] = splat[3 * (size_t)g + 1];
+      sC[t] = splat[3 * (size_t)g + 2];
+      sG[t] = g;
+    }
+    __syncthreads();
+    const int cnt = (int)min(256u, range.y - b0);
+    for (int j = 0; j < cnt; ++j) {
+      bool touched = false;
+      if (!done) {
+        ++contributor;
+        const float4 A = sA[j];
+        const float4 B = sB[j];
+        const float dx = A.x - fpx, dy = A.y - fpy;
+        const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+        if (power <= 0.0f) {
+          const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
+          if (alpha >= kMinAlpha) {
+            const float test_T = T * (1.f - alpha);
+            if (test_T < kMinT) {
+              done = true;
+            } else {
+              const float4 Cc = sC[j];
+              const float wgt = alpha * T;
+              C0 += Cc.x * wgt;
+              C1 += Cc.y * wgt;
+              C2 += Cc.z * wgt;
+              Dp += B.z * wgt;
+              touched = test_T > 0.5f;
+              T = test_T;
+              last = contributor;
+            }
+          }
+        }
+      }
+      const uint64_t tm = __ballot(touched);
+      if (tm != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)__popcll(tm));
+      if (__all(done)) break;
+    }
+  }
+  if (inside) {
+    const size_t pid = (size_t)py * W + px;
+    const size_t HW = (size_t)H * W;
+    final_T[pid] = T;
+    n_contrib[pid] = last;
+    out_color[pid] = C0 + T * bg[0];
+    out_color[HW + pid] = C1 + T * bg[1];
+    out_color[2 * HW + pid] = C2 + T * bg[2];
+    out_depth[pid] = Dp;
+    out_opac[pid] = 1.f - T;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means,
+                                                      const float* __restrict__ viewm, uint8_t* __restrict__ present) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const f3 p = mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+  const f3 pv = xform43(viewm, p);
+  present[i] = pv.z > kNearZ ? 1 : 0;
+}
+
+}  // namespace
+
+hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
+                             uint32_t* err_flag, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  const GeomLayout L(a.P);
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, a.D, a.M, a.means3D, a.scales,
+                     a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
+                     a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
+                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.tiles),
+                     at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
+                            uint32_t* keys, uint32_t* slot_g, hipStream_t s) {
+  if (P == 0) return hipSuccess;
+  const GeomLayout L(P);
+  const int gx = (a.W + kTile - 1) / kTile;
+  hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, s, P, gx, at<uint32_t>(geom, L.offs),
+                     sorted_g, at<ushort4>(geom, L.rect), keys, slot_g);
+  return hipGetLastError();
+}
+
+hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s) {
+  hipLaunchKernelGGL(k_ranges, dim3((ntiles + 255) / 256), dim3(256), 0, s, sorted_keys, N, ntiles, ranges);
+  return hipGetLastError();
+}
+
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
+                             const uint32_t* slot_g, const void* geom, float* out_color, float* out_depth,
+                             float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
+                             hipStream_t s) {
+  const GeomLayout L(a.P);
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  const int nt = gx * gy;
+  hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(256), 0, s, ranges, sorted_k, slot_g,
+                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,
+                     final_T, n_contrib, n_touched);
+  return hipGetLastError();
+}
+
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
+                               hipStream_t s) {
+  (void)proj;
+  if (P == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
+  return hipGetLastError();
+}
+
+}  // namespace wgsr

@@ -1,0 +1,272 @@
+// LSD radix sort of (u32 key, u32 value) pairs and exclusive scans, gfx950.
+//
+// Replaces the CUB primitives upstream's rasteriser and simple-knn lean on
+// (cub::DeviceRadixSort::SortPairs, cub::DeviceScan::InclusiveSum: SURVEY.md
+// 2 "Kernel inventory").  Design for wave64:
+//  * a pass = histogram -> per-digit row scan -> stable scatter;
+//  * block-local stable ranking uses 64-bit ballots to find the lanes that
+//    share a digit (one LDS counter update per peer group, no LDS atomics);
+//  * the scatter stages the block's keys in LDS in digit order so that runs of
+//    one digit leave as contiguous (coalesced) stores.
+// A workgroup owns 4096 keys (256 threads x 16); each wave owns a contiguous
+// run of 1024 keys that it walks 64 at a time, so ranks follow input order.
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+// exclusive scan of one value per thread over a 256-thread block
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_tmp4, uint32_t* total) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) s_tmp4[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t x = s_tmp4[i];
+    base += (i < w) ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                    int bits, uint32_t nb, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_hist[256];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  s_hist[t] = 0;
+  __syncthreads();
+  const uint32_t mask = (1u << bits) - 1u;
+  const size_t base = (size_t)blockIdx.x * kSortTile + (size_t)w * (64 * kSortItems);
+#pragma unroll 4
+  for (int j = 0; j < kSortItems; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    const uint32_t d = valid ? (keys[e] >> shift) & mask : 0u;
+    const uint64_t active = __ballot(valid);
+    if (active == 0) break;
+    const uint64_t peers = match_digit(d, bits, active);
+    if (valid && lanes_below(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  hist[(size_t)t * nb + blockIdx.x] = s_hist[t];
+}
+
+// exclusive scan of hist row d (over blocks) in place; totals[d] = row sum
+__global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
+                                                       uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_tmp[4];
+  uint32_t* row = hist + (size_t)blockIdx.x * nb;
+  const int t = threadIdx.x;
+  const uint32_t per = (nb + 255) / 256;
+  const uint32_t b0 = t * per, b1 = min(nb, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t b = b0; b < b1; ++b) s += row[b];
+  uint32_t tot;
+  uint32_t run = block_excl_scan256(s, s_tmp, &tot);
+  for (uint32_t b = b0; b < b1; ++b) {
+    uint32_t x = row[b];
+    row[b] = run;
+    run += x;
+  }
+  if (t == 0) totals[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ kin,
+                                                       const uint32_t* __restrict__ vin, int iota, uint32_t n,
+                                                       int shift, int bits, uint32_t nb,
+                                                       const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ totals,
+                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  __shared__ uint32_t s_k[kSortTile];
+  __shared__ uint32_t s_v[kSortTile];
+  __shared__ uint32_t s_wcnt[4][256];
+  __shared__ uint32_t s_lbase[256];
+  __shared__ uint32_t s_gbase[256];
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
+  // global base of digit t for this block: scan of the digit totals + row prefix
+  {
+    const uint32_t tot = totals[t];
+    const uint32_t ex = block_excl_scan256(tot, s_tmp, nullptr);
+    s_gbase[t] = ex + hist[(size_t)t * nb + blockIdx.x];
+  }
+  __syncthreads();
+
+  uint32_t key[kSortItems];
+  uint32_t rank[kSortItems];
+  const size_t blk0 = (size_t)blockIdx.x * kSortTile;
+  const size_t base = blk0 + (size_t)w * (64 * kSortItems);
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    key[j] = valid ? kin[e] : 0u;
+    const uint32_t d = (key[j] >> shift) & mask;
+    const uint64_t active = __ballot(valid);
+    rank[j] = 0;
+    if (active != 0) {
+      const uint64_t peers = match_digit(d, bits, active);
+      const uint32_t below = lanes_below(peers);
+      uint32_t old = 0;
+      if (valid) old = s_wcnt[w][d];
+      if (valid && below == 0) s_wcnt[w][d] = old + (uint32_t)__popcll(peers);
+      rank[j] = old + below;
+    }
+  }
+  __syncthreads();
+  {
+    // per-digit: exclusive prefix over waves, then over digits (block-local)
+    const uint32_t c0 = s_wcnt[0][t], c1 = s_wcnt[1][t], c2 = s_wcnt[2][t], c3 = s_wcnt[3][t];
+    s_wcnt[0][t] = 0;
+    s_wcnt[1][t] = c0;
+    s_wcnt[2][t] = c0 + c1;
+    s_wcnt[3][t] = c0 + c1 + c2;
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    s_lbase[t] = block_excl_scan256(tot, s_tmp, nullptr);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    if (e < n) {
+      const uint32_t d = (key[j] >> shift) & mask;
+      const uint32_t loc = s_lbase[d] + s_wcnt[w][d] + rank[j];
+      s_k[loc] = key[j];
+      s_v[loc] = iota ? (uint32_t)e : vin[e];
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = (uint32_t)min((size_t)kSortTile, (size_t)n - blk0);
+  for (uint32_t i = t; i < cnt; i += 256) {
+    const uint32_t k = s_k[i];
+    const uint32_t d = (k >> shift) & mask;
+    const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
+    kout[dst] = k;
+    vout[dst] = s_v[i];
+  }
+}
+
+// ---- exclusive scan of u32 values gathered as vals[idx[i]] (idx may be null)
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ vals,
+                                                     const uint32_t* __restrict__ idx, uint32_t n,
+                                                     uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * (kScanTile / 256);
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanTile / 256; ++j) {
+    const size_t i = b0 + j;
+    if (i < n) s += vals[idx ? idx[i] : i];
+  }
+  uint32_t tot;
+  block_excl_scan256(s, s_tmp, &tot);
+  if (t == 0) bsum[blockIdx.x] = tot;
+}
+
+// single workgroup: exclusive scan of nbs block sums in place, total -> bsum[nbs], *total_out
+__global__ __launch_bounds__(256) void k_scan_bsum(uint32_t* __restrict__ bsum, uint32_t nbs,
+                                                   uint32_t* __restrict__ total_out) {
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x;
+  const uint32_t per = (nbs + 255) / 256;
+  const uint32_t b0 = t * per, b1 = min(nbs, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t b = b0; b < b1; ++b) s += bsum[b];
+  uint32_t tot;
+  uint32_t run = block_excl_scan256(s, s_tmp, &tot);
+  for (uint32_t b = b0; b < b1; ++b) {
+    uint32_t x = bsum[b];
+    bsum[b] = run;
+    run += x;
+  }
+  if (t == 0) {
+    bsum[nbs] = tot;
+    if (total_out) *total_out = tot;
+  }
+}
+
+// out[i] = exclusive prefix; if scatter_out: scatter_out[idx[i]] = prefix
+__global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ vals,
+                                                   const uint32_t* __restrict__ idx, uint32_t n,
+                                                   const uint32_t* __restrict__ bsum, uint32_t* __restrict__ out,
+                                                   uint32_t* __restrict__ scatter_out) {
+  __shared__ uint32_t s_tmp[4];
+  constexpr int PER = kScanTile / 256;
+  const int t = threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * PER;
+  uint32_t v[PER];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const size_t i = b0 + j;
+    v[j] = (i < n) ? vals[idx ? idx[i] : i] : 0u;
+    s += v[j];
+  }
+  uint32_t run = block_excl_scan256(s, s_tmp, nullptr) + bsum[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const size_t i = b0 + j;
+    if (i < n) {
+      out[i] = run;
+      if (scatter_out) scatter_out[idx[i]] = run;
+    }
+    run += v[j];
+  }
+  if (blockIdx.x == gridDim.x - 1 && t == 255) out[n] = run;  // grand total at out[n]
+}
+
+}  // namespace
+
+hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
+                            size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
+                            hipStream_t stream, bool* result_in_alt) {
+  *result_in_alt = false;
+  if (n == 0 || end_bit <= begin_bit) {
+    if (vals_iota && n > 0) {
+      // a zero-pass sort still has to materialise the identity permutation
+      return hipErrorInvalidValue;
+    }
+    return hipSuccess;
+  }
+  const uint32_t nb = sort_blocks(n);
+  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
+  bool iota = vals_iota;
+  for (int shift = begin_bit; shift < end_bit; shift += 8) {
+    const int bits = min(8, end_bit - shift);
+    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, hist);
+    hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, hist, nb, totals);
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
+                       bits, nb, hist, totals, ko, vo);
+    iota = false;
+    uint32_t* tk = ki; ki = ko; ko = tk;
+    uint32_t* tv = vi; vi = vo; vo = tv;
+    *result_in_alt = !*result_in_alt;
+  }
+  return hipGetLastError();
+}
+
+hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
+                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream) {
+  const uint32_t nbs = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  if (n == 0) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint32_t), stream);
+    if (e == hipSuccess && total_out) e = hipMemsetAsync(total_out, 0, sizeof(uint32_t), stream);
+    return e;
+  }
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum);
+  hipLaunchKernelGGL(k_scan_bsum, dim3(1), dim3(256), 0, stream, bsum, nbs, total_out);
+  hipLaunchKernelGGL(k_scan_down, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum, out, scatter_out);
+  return hipGetLastError();
+}
+
+}  // namespace wgsr

@@ -1,0 +1,258 @@
+// Shared device helpers and buffer layouts for the gfx950 rasteriser.
+//
+// Everything here is CDNA4-first: 64-lane wavefronts (ballots are 64-bit),
+// 256-thread workgroups (= one 16x16 pixel tile, four waves), and buffer
+// regions aligned to 256 bytes so every array starts on its own cache lines.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wgsr {
+
+constexpr int kTile = 16;             // tile edge in pixels (SURVEY A.1 BLOCK_X/Y)
+constexpr int kTilePix = kTile * kTile;
+constexpr int kWave = 64;
+constexpr float kNearZ = 0.2f;        // near-plane cull
+constexpr float kMinAlpha = 1.0f / 255.0f;
+constexpr float kMaxAlpha = 0.99f;
+constexpr float kMinT = 0.0001f;      // early termination
+
+// ---------------------------------------------------------------------------
+// Wave-level primitives (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// number of set bits of `mask` strictly below this lane
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// inclusive prefix sum across the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    uint32_t o = __shfl_up(v, off, kWave);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+// Lanes (among `active`) whose low `bits` bits of d equal this lane's.
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t active) {
+  uint64_t peers = active;
+  for (int b = 0; b < bits; ++b) {
+    uint64_t on = __ballot((d >> b) & 1u);
+    peers &= ((d >> b) & 1u) ? on : ~on;
+  }
+  return peers;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md 5.5 T1): blocks
+// b and b+8 run on one XCD, so give each XCD a contiguous run of work ids.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
+  const uint32_t q = nblocks / 8, r = nblocks % 8, xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// ---------------------------------------------------------------------------
+// Small fp32 math (upstream operation order where it matters)
+// ---------------------------------------------------------------------------
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk3(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ f3 add3(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 sub3(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 scl3(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// The caller's matrices are the row-vector (transposed) forms, read as
+// column-major 4x4: m[4*c + r] = M[r][c] of the column-vector matrix.
+struct Mat16 { float m[16]; };
+
+__device__ __forceinline__ f3 xform43(const float* m, f3 p) {
+  return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+          m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
+}
+__device__ __forceinline__ float4 xform44(const float* m, f3 p) {
+  return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                     m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+// upstream ndc2Pix evaluates in double: ((v + 1.0) * S - 1.0) * 0.5
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
+
+__device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
+  const float r = q.x, x = q.y, y = q.z, z = q.w;
+  R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+  R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+  R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+
+// Sigma = R diag((mod s)^2) R^T, upper triangle (xx, xy, xz, yy, yz, zz)
+__device__ __forceinline__ void cov3d_from(f3 s, float mod, float4 q, float c[6]) {
+  float R[3][3];
+  quat_rot(q, R);
+  const float sx = mod * s.x, sy = mod * s.y, sz = mod * s.z;
+  const float s2[3] = {sx * sx, sy * sy, sz * sz};
+  int idx = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc += R[i][k] * s2[k] * R[j][k];
+      c[idx++] = acc;
+    }
+}
+
+// Camera constants every kernel needs, loaded once per thread from the
+// device matrices (wave-uniform addresses -> scalar loads).
+struct Cam {
+  float view[16];
+  float proj[16];
+  float Rw[3][3];  // world->camera rotation, Rw[r][c] = view[4c + r]
+  float fx, fy, tanx, tany;
+  int W, H;
+};
+
+__device__ __forceinline__ void load_cam(Cam& c, const float* view, const float* proj, int W, int H,
+                                         float tanx, float tany) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { c.view[i] = view[i]; c.proj[i] = proj[i]; }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c.Rw[r][k] = c.view[4 * k + r];
+  c.W = W; c.H = H; c.tanx = tanx; c.tany = tany;
+  c.fx = W / (2.0f * tanx);
+  c.fy = H / (2.0f * tany);
+}
+
+// EWA: T = J Rw (2x3) for camera-space mean t (clamped to 1.3 x the fov).
+__device__ __forceinline__ void ewa_T(const Cam& c, f3 t, float T[2][3], f3& tc, float& xmul, float& ymul) {
+  const float limx = 1.3f * c.tanx, limy = 1.3f * c.tany;
+  const float txtz = t.x / t.z, tytz = t.y / t.z;
+  tc = {fminf(limx, fmaxf(-limx, txtz)) * t.z, fminf(limy, fmaxf(-limy, tytz)) * t.z, t.z};
+  xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+  ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+  const float J00 = c.fx / tc.z, J02 = -(c.fx * tc.x) / (tc.z * tc.z);
+  const float J11 = c.fy / tc.z, J12 = -(c.fy * tc.y) / (tc.z * tc.z);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    T[0][k] = J00 * c.Rw[0][k] + J02 * c.Rw[2][k];
+    T[1][k] = J11 * c.Rw[1][k] + J12 * c.Rw[2][k];
+  }
+}
+
+__device__ __forceinline__ void sym3(const float c6[6], float S[3][3]) {
+  S[0][0] = c6[0]; S[0][1] = c6[1]; S[0][2] = c6[2];
+  S[1][0] = c6[1]; S[1][1] = c6[3]; S[1][2] = c6[4];
+  S[2][0] = c6[2]; S[2][1] = c6[4]; S[2][2] = c6[5];
+}
+
+__device__ __forceinline__ void cov2d(const float T[2][3], const float S[3][3], float& a, float& b, float& c) {
+  float ST0[3], ST1[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    ST0[i] = S[i][0] * T[0][0] + S[i][1] * T[0][1] + S[i][2] * T[0][2];
+    ST1[i] = S[i][0] * T[1][0] + S[i][1] * T[1][1] + S[i][2] * T[1][2];
+  }
+  a = T[0][0] * ST0[0] + T[0][1] * ST0[1] + T[0][2] * ST0[2] + 0.3f;
+  b = T[0][0] * ST1[0] + T[0][1] * ST1[1] + T[0][2] * ST1[2];
+  c = T[1][0] * ST1[0] + T[1][1] * ST1[1] + T[1][2] * ST1[2] + 0.3f;
+}
+
+// ---------------------------------------------------------------------------
+// State-buffer layouts (byte offsets inside the caller-owned uint8 buffers)
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+constexpr int kSortItems = 16;                      // keys per thread in radix passes
+constexpr int kSortTile = 256 * kSortItems;          // keys per radix workgroup
+constexpr int kScanTile = 4096;                      // elements per scan workgroup
+
+__host__ __device__ inline uint32_t sort_blocks(size_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+
+// Per-Gaussian state (geometry buffer).
+struct GeomLayout {
+  size_t splat, rect, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, hist, totals,
+      bsum, counter, total;
+  __host__ __device__ explicit GeomLayout(size_t P) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
+    const size_t nb = sort_blocks(P);
+    splat = take(48 * P);          // float4 x3: (x, y, conic.x, conic.y) (conic.z, opacity, depth, -) (r, g, b, -)
+    rect = take(8 * P);            // ushort4 tile rectangle [x0, y0, x1, y1)
+    tiles = take(4 * P);           // tiles touched
+    clamped = take(4 * P);         // SH clamp flags (3 bits)
+    dkey = take(4 * P);            // depth sort keys / sorted keys
+    dkey_alt = take(4 * P);
+    dval = take(4 * P);            // depth order: rank -> Gaussian id
+    dval_alt = take(4 * P);
+    offs = take(4 * (P + 1));      // rank -> first duplicate slot
+    slot_start = take(4 * P);      // Gaussian -> first duplicate slot
+    hist = take(4 * 256 * (size_t)nb);
+    totals = take(4 * 256);
+    bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
+    counter = take(16);
+    total = o;
+  }
+};
+
+// Per-pair state (binning buffer).
+struct BinLayout {
+  size_t key, key_alt, val, val_alt, slot_g, hist, totals, total;
+  __host__ __device__ BinLayout(size_t N) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
+    const size_t nb = sort_blocks(N);
+    key = take(4 * N);       // tile id per pair (sorted in place of key/key_alt)
+    key_alt = take(4 * N);
+    val = take(4 * N);       // duplicate slot k per sorted pair
+    val_alt = take(4 * N);
+    slot_g = take(4 * N);    // duplicate slot -> Gaussian id
+    hist = take(4 * 256 * (size_t)nb);
+    totals = take(4 * 256);
+    total = o;
+  }
+};
+
+// Per-pixel state (image buffer).
+struct ImageLayout {
+  size_t ranges, final_T, n_contrib, total;
+  __host__ __device__ ImageLayout(int W, int H) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
+    const size_t nt = (size_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    ranges = take(8 * nt);
+    final_T = take(4 * (size_t)W * H);
+    n_contrib = take(4 * (size_t)W * H);
+    total = o;
+  }
+};
+
+template <typename T>
+__host__ __device__ inline T* at(void* base, size_t off) { return reinterpret_cast<T*>(static_cast<char*>(base) + off); }
+template <typename T>
+__host__ __device__ inline const T* at(const void* base, size_t off) {
+  return reinterpret_cast<const T*>(static_cast<const char*>(base) + off);
+}
+
+}  // namespace wgsr

@@ -1,0 +1,59 @@
+// Host-side launchers shared between the translation units of libwgsr.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wgsr.h"
+
+namespace wgsr {
+
+// LSD radix sort on bits [begin_bit, end_bit) (8-bit digits).  Input in
+// keys/vals (vals ignored if vals_iota: value = input position); the result
+// lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
+hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
+                            size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
+                            hipStream_t stream, bool* result_in_alt);
+
+// out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
+// entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
+hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
+                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream);
+
+int num_bits(uint32_t n);  // bits needed to represent values in [0, n)
+
+// thread-local error message plumbing for the C ABI
+int set_error(int code, const char* fmt, ...);
+
+struct RasterGrid {
+  int gx, gy, ntiles;
+};
+
+// forward stages (raster_fwd.hip)
+hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
+                             uint32_t* err_flag, hipStream_t s);
+hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
+                            uint32_t* keys, uint32_t* slot_g, hipStream_t s);
+hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s);
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
+                             const uint32_t* slot_g, const void* geom, float* out_color, float* out_depth,
+                             float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
+                             hipStream_t s);
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
+                               hipStream_t s);
+
+// backward stages (raster_bwd.hip)
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
+                             const uint32_t* slot_g, const void* geom, const float* final_T,
+                             const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
+                             float4* partial, hipStream_t s);
+hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
+                            const float4* partial, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                            float* dL_drot, float* dL_dtau, hipStream_t s);
+
+// distCUDA2 (knn.hip)
+size_t knn_scratch_bytes(int P);
+hipError_t launch_dist_cuda2(int P, const float* points, float* out, void* scratch, hipStream_t s);
+
+}  // namespace wgsr

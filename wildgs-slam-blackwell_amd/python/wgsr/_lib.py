@@ -1,0 +1,149 @@
+"""ctypes binding of libwgsr.so (include/wgsr.h).
+
+The library is the MI355X (gfx950) implementation of the two native
+extensions WildGS-SLAM loads on its mapping path; this module is the only
+place Python touches it.  There is deliberately no fallback: if the shared
+library is missing or fails to load, every entry point raises.
+
+Device memory comes from the torch caching allocator through the C ABI's
+allocation callbacks (``wgsr_alloc_fn``), and launches go on torch's current
+HIP stream, so the kernels compose with the rest of a PyTorch-ROCm program.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_PKG_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+LIB_PATH = os.environ.get("WGSR_LIB", os.path.join(_PKG_ROOT, "lib", "libwgsr.so"))
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_fp = ctypes.c_void_p  # device pointers travel as raw addresses
+
+
+class RasterArgs(ctypes.Structure):
+    """Mirror of ``wgsr_raster_args``."""
+
+    _fields_ = [
+        ("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int),
+        ("W", ctypes.c_int), ("H", ctypes.c_int),
+        ("bg", _fp), ("means3D", _fp), ("colors", _fp), ("opacities", _fp),
+        ("scales", _fp), ("rotations", _fp), ("cov3D_precomp", _fp), ("shs", _fp),
+        ("viewmatrix", _fp), ("projmatrix", _fp), ("projmatrix_raw", _fp), ("campos", _fp),
+        ("scale_modifier", ctypes.c_float), ("tan_fovx", ctypes.c_float),
+        ("tan_fovy", ctypes.c_float), ("prefiltered", ctypes.c_int), ("debug", ctypes.c_int),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load libwgsr.so (after torch, so the HIP runtime is torch's)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(
+                f"libwgsr.so not found at {LIB_PATH}; build it with "
+                f"`make -C wildgs-slam-blackwell_amd` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        c_int, c_i64, c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
+        P_ARGS = ctypes.POINTER(RasterArgs)
+        L.wgsr_rasterize_forward.restype = c_int
+        L.wgsr_rasterize_forward.argtypes = [P_ARGS, ALLOC_FN, ALLOC_FN, ALLOC_FN, ctypes.c_void_p,
+                                             _fp, _fp, _fp, _fp, _fp, ctypes.POINTER(c_i64), _fp]
+        L.wgsr_rasterize_backward.restype = c_int
+        L.wgsr_rasterize_backward.argtypes = [P_ARGS, _fp, _fp, _fp, _fp, c_i64, _fp, _fp, ALLOC_FN,
+                                              ctypes.c_void_p] + [_fp] * 9 + [_fp]
+        L.wgsr_mark_visible.restype = c_int
+        L.wgsr_mark_visible.argtypes = [c_int, _fp, _fp, _fp, _fp, _fp]
+        L.wgsr_dist_cuda2.restype = c_int
+        L.wgsr_dist_cuda2.argtypes = [c_int, _fp, _fp, ALLOC_FN, ctypes.c_void_p, _fp]
+        for name in ("wgsr_geometry_bytes",):
+            getattr(L, name).restype = c_sz
+            getattr(L, name).argtypes = [c_int]
+        L.wgsr_binning_bytes.restype = c_sz
+        L.wgsr_binning_bytes.argtypes = [c_i64, c_int, c_int]
+        L.wgsr_image_bytes.restype = c_sz
+        L.wgsr_image_bytes.argtypes = [c_int, c_int]
+        L.wgsr_last_error.restype = ctypes.c_char_p
+        L.wgsr_last_error.argtypes = []
+        L.wgsr_version.restype = ctypes.c_char_p
+        L.wgsr_version.argtypes = []
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = (
+    "wgsr_rasterize_forward", "wgsr_rasterize_backward", "wgsr_mark_visible", "wgsr_dist_cuda2",
+    "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
+    "wgsr_version",
+)
+
+
+def check(code: int):
+    if code != 0:
+        msg = load().wgsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"wgsr error {code}: {msg}")
+
+
+# ---------------------------------------------------------------------------
+# Allocation callbacks: each call records a torch uint8 tensor in the active
+# request's slot so Python owns (and later frees) every byte.
+# ---------------------------------------------------------------------------
+_tls = threading.local()
+
+
+class AllocRequest:
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.buffers = {}
+
+    def __enter__(self):
+        self._prev = getattr(_tls, "req", None)
+        _tls.req = self
+        return self
+
+    def __exit__(self, *exc):
+        _tls.req = self._prev
+        return False
+
+
+def _make_alloc(slot: str):
+    def _alloc(_ctx, nbytes):
+        req = _tls.req
+        n = int(nbytes)
+        base = torch.empty(max(n, 1), dtype=torch.uint8, device=req.device)
+        req.buffers[slot] = base[:n]
+        req.buffers[slot + "_base"] = base
+        return base.data_ptr()
+    return ALLOC_FN(_alloc)
+
+
+ALLOC_GEOM = _make_alloc("geom")
+ALLOC_BINNING = _make_alloc("binning")
+ALLOC_IMAGE = _make_alloc("image")
+ALLOC_SCRATCH = _make_alloc("scratch")
+
+
+def ptr(t):
+    """Device address of a tensor, or None for an absent (empty) one."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
