@@ -1,0 +1,252 @@
+#!/usr/bin/env python
+"""bench.py -- rasterised Gaussians/s, forward + backward, 1M Gaussians @ 1080p.
+
+BASELINE.json metric: "rasterised Gaussians/s fwd+bwd @1M pts 1080p; PSNR vs ref".
+
+One step = one pass of the hot path over one view: ``_C.rasterize_gaussians``
+followed by ``_C.rasterize_gaussians_backward`` for 1M
+synthetic Gaussians (BASELINE.md distribution, SH degree 3, pose gradient
+always computed) at 1920x1080, all inputs resident in HBM before timing.
+
+* N = 1 (default): BASELINE.json configs[2].  value = P * K / t.
+* N > 1 (torchrun, one rank per GPU): configs[3] -- keyframe-view data
+  parallelism: rank r renders view r of the same replicated 1M Gaussians and
+  the per-Gaussian parameter gradients (59 floats each) are SUM-all-reduced
+  over RCCL every step.  Weak scaling; value = P * N * K / max_rank(t).
+
+Extra fields: ``roofline`` for the dominant kernel (stage times from HIP
+events recorded on the launch stream inside the timed region; algorithmic
+bytes from SURVEY.md 8(d)), ``cpu_baseline`` (the fp32 CPU restatement,
+oracle/cpu_raster.cpp, on the host cores; rank 0 at N = 1 only) and
+``psnr_vs_cpu_db`` (GPU render vs the CPU restatement's render).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "wildgs-slam-blackwell_amd", "python"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "rasterised Gaussians/s fwd+bwd @1M pts 1080p; PSNR vs ref"
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 157.3    # fp32 vector peak (MI355X_MICROARCH.md)
+TILE = 16
+
+
+def byte_model(P, N, W, H, K, M):
+    """Algorithmic bytes per stage (SURVEY.md 8(d) per-unit figures)."""
+    npix = W * H
+    ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
+    return {
+        "preprocess": P * (44 + 12 * K) + 76 * P,
+        "depth_sort": 16 * P,
+        "offsets_scan": 8 * P,
+        "duplicate": 12 * N,
+        "tile_sort": 24 * N,
+        "ranges": 8 * N + 8 * ntile,
+        "render_fwd": 44 * N + 28 * npix + 4 * P,
+        "render_bwd": 48 * N + 24 * npix + 40 * P,
+        "gauss_bwd": P * (44 + 12 * K + 24 + 40) + P * (12 + 12 + 12 * M + 4 + 12 + 16 + 24),
+    }
+
+
+def n_contrib_sum(img_buffer, W, H):
+    """Sum over pixels of n_contrib (pairs walked), from the image state buffer."""
+    def a256(x):
+        return (x + 255) & ~255
+    ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
+    off = a256(8 * ntile) + a256(4 * W * H)
+    nc = img_buffer[off: off + 4 * W * H].view(torch.int32)
+    return int(nc.sum().item())
+
+
+def load_pmc_traffic(stage):
+    """HBM bytes per launch of ``stage`` from the committed PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        rec = d.get("stages", {}).get(stage)
+        if rec:
+            return float(rec["hbm_bytes_per_launch"]), d.get("source")
+    except Exception:
+        pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--sh", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the stage timers")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from diff_gaussian_rasterization import _C
+    from wgsr import _lib
+    from wgsr.camera import synthetic_camera
+    from wgsr.dp import GradBuffer, allreduce_grads
+    from wgsr.scene import make_scene, make_upstream_grads
+
+    P, W, H, deg = args.P, args.width, args.height, args.sh
+    M = (deg + 1) ** 2
+    scene = make_scene(P, W, H, deg, seed=0)
+    gc_cpu, gd_cpu = make_upstream_grads(W, H, seed=1)
+    cam = synthetic_camera(W, H, view=rank)  # configs[3]: view k per rank
+    f = cam.raster_fields()
+    bg_cpu = torch.zeros(3)
+    d = lambda x: x.to(dev).contiguous()  # noqa: E731
+    means, opac, scales, rots, shs = (d(scene.means3D), d(scene.opacities), d(scene.scales),
+                                      d(scene.rotations), d(scene.shs))
+    bg, view, proj, praw, campos = (d(bg_cpu), d(f["viewmatrix"]), d(f["projmatrix"]),
+                                    d(f["projmatrix_raw"]), d(f["campos"]))
+    gc, gd = d(gc_cpu), d(gd_cpu)
+    e = torch.empty(0, device=dev)
+    tanx, tany = f["tanfovx"], f["tanfovy"]
+    gbuf = GradBuffer.allocate(P, M, dev)
+    state = {}
+
+    def step():
+        nr, color, radii, geom, binning, img, depth, opacity, nt = _C.rasterize_gaussians(
+            bg, means, e, opac, scales, rots, 1.0, e, view, proj, praw, tanx, tany, H, W, shs, deg,
+            campos, False, False)
+        _C.rasterize_gaussians_backward(
+            bg, means, radii, e, scales, rots, 1.0, e, view, proj, praw, tanx, tany, gc, gd, shs,
+            deg, campos, geom, nr, binning, img, False, out=gbuf.views)
+        if world > 1:
+            allreduce_grads(gbuf)
+        state.update(nr=nr, color=color, img=img)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    prof = _lib.StageProfile() if not args.no_profile else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if prof:
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    if prof:
+        prof.__exit__(None, None, None)
+    dt = t1 - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    value = P * world * args.steps / dt
+    ms_per_step = 1e3 * dt / args.steps
+    N = state["nr"]
+    out = {
+        "metric": METRIC, "value": value, "unit": "Gaussians/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": ("configs[2]: 1M Gaussians, 1920x1080, SH3, single-view fwd+bwd, pose grad on"
+                         if world == 1 else
+                         f"configs[3]: 1M Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
+                         "+ RCCL SUM all-reduce of the per-Gaussian gradients"),
+            "gaussians": P, "image": f"{W}x{H}", "sh_degree": deg, "num_rendered": N,
+            "views_per_step": world, "parallelism": f"dp{world} (keyframe views)",
+            "allreduce_bytes_per_step": (gbuf.flat.numel() * 4 if world > 1 else 0),
+        },
+    }
+
+    if prof:
+        stages = prof.stages
+        model = byte_model(P, N, W, H, M, M)
+        out["stages_ms_per_step"] = {k: v[0] / max(1, args.steps) for k, v in stages.items() if v[1]}
+        timed = {k: v for k, v in stages.items() if v[1] and k in model}
+        dom = max(timed, key=lambda k: timed[k][0])
+        ms_avg = timed[dom][0] / timed[dom][1]
+        achieved = model[dom] / (ms_avg * 1e-3) / 1e9
+        traffic, src = load_pmc_traffic(dom)
+        out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": achieved,
+                           "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                           "traffic": traffic, "algorithmic_bytes": model[dom],
+                           "avg_launch_ms": ms_avg}
+        if traffic is not None:
+            out["roofline"]["traffic_source"] = src
+        # whole fwd+bwd pass against HBM (the north-star roofline) and the
+        # render kernels' pair arithmetic against the fp32 VALU peak
+        kernel_ms = sum(v[0] for k, v in timed.items()) / max(1, args.steps)
+        total_bytes = sum(model.values())
+        pairs = n_contrib_sum(state["img"], W, H)
+        out["pass_roofline"] = {
+            "algorithmic_bytes": total_bytes, "kernel_ms": kernel_ms,
+            "achieved_GBps_kernels": total_bytes / (kernel_ms * 1e-3) / 1e9,
+            "achieved_GBps_step": total_bytes / (ms_per_step * 1e-3) / 1e9,
+            "frac_step": total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        rf = timed.get("render_fwd", (0, 1))
+        rb = timed.get("render_bwd", (0, 1))
+        out["render_valu"] = {
+            "pairs_walked": pairs,
+            "fwd_TFLOPs": 20 * pairs / (rf[0] / rf[1] * 1e-3) / 1e12 if rf[0] else None,
+            "bwd_TFLOPs": 60 * pairs / (rb[0] / rb[1] * 1e-3) / 1e12 if rb[0] else None,
+            "peak_TFLOPs": VALU_PEAK_TFLOPS}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        t0 = time.perf_counter()
+        cr = cpu_oracle.CpuRaster(means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
+                                  scales=scene.scales, rotations=scene.rotations, H=H, W=W,
+                                  tanfovx=tanx, tanfovy=tany, bg=bg_cpu, scale_modifier=1.0,
+                                  viewmatrix=f["viewmatrix"], projmatrix=f["projmatrix"],
+                                  projmatrix_raw=f["projmatrix_raw"], sh_degree=deg,
+                                  campos=f["campos"])
+        cr.backward(gc_cpu, gd_cpu)
+        tc = time.perf_counter() - t0
+        out["cpu_baseline"] = {
+            "value": P / tc, "unit": "Gaussians/s", "cores": threads, "kind": "port",
+            "sample": f"1 full fwd+bwd step of the same workload ({P} Gaussians, {W}x{H}, SH{deg}) "
+                      f"on oracle/cpu_raster.cpp, {tc:.2f} s"}
+        ref = torch.from_numpy(cr.color)
+        mine = state["color"].detach().cpu()
+        mse = float(((mine - ref) ** 2).mean())
+        out["psnr_vs_cpu_db"] = (20 * math.log10(1.0 / math.sqrt(mse))) if mse > 0 else float("inf")
+        out["rel_l1_vs_cpu"] = float((mine - ref).abs().sum() / ref.abs().sum())
+
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

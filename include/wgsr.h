@@ -117,6 +117,17 @@ size_t wgsr_geometry_bytes(int P);
 size_t wgsr_binning_bytes(int64_t num_rendered, int W, int H);
 size_t wgsr_image_bytes(int W, int H);
 
+/* Optional per-stage timing: HIP events recorded on the caller's stream
+ * around each stage (preprocess, depth_sort, offsets_scan, duplicate,
+ * tile_sort, ranges, render_fwd, render_bwd, gauss_bwd, dist_cuda2).
+ * wgsr_profile_read synchronises on the recorded events and returns the
+ * accumulated milliseconds and launch counts per stage (returns the number
+ * of stages).  Not thread-safe; meant for benchmarks. */
+#define WGSR_NUM_STAGES 10
+void wgsr_profile_enable(int on);
+int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset);
+const char* wgsr_profile_stage_name(int i);
+
 const char* wgsr_last_error(void);
 const char* wgsr_version(void);
 

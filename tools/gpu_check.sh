@@ -1,0 +1,33 @@
+#!/bin/bash
+# GPU-box validation run: parity tests, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; after a crash / fault / timeout the
+# script stops (no further GPU work in the same call).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+
+STEPS="${STEPS:-tests bench prof}"
+for s in $STEPS; do
+  case $s in
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$? ;;
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1; rc=$?
+      if [ $rc -ge 2 ] && [ $rc -le 5 ]; then rc=0; fi ;;  # pytest usage/collection codes are not GPU faults
+    bench)
+      timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err; rc=$? ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile > $GRAFT_REPO_ROOT/$OUT/prof_bench.json 2> $GRAFT_REPO_ROOT/$OUT/prof.err); rc=$? ;;
+    pmc_fetch)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_fetch -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_fetch.err); rc=$? ;;
+    pmc_write)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_write -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_write.err); rc=$? ;;
+    *) echo "unknown step $s"; rc=0 ;;
+  esac
+  echo "$s rc=$rc" | tee -a $OUT/steps.log
+  if fatal $rc; then echo "stopping after fatal rc=$rc in $s"; exit $rc; fi
+done
+exit 0

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "wgsr.h"
 #include "wgsr_common.h"
@@ -33,6 +34,53 @@ int num_bits(uint32_t n) {
 }
 
 namespace {
+
+// ---- optional per-stage timing with HIP events on the caller's stream -----
+const char* const kStageNames[WGSR_NUM_STAGES] = {"preprocess", "depth_sort", "offsets_scan", "duplicate",
+                                                  "tile_sort", "ranges", "render_fwd", "render_bwd",
+                                                  "gauss_bwd", "dist_cuda2"};
+struct Prof {
+  bool on = false;
+  struct Rec { int stage; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  double ms[WGSR_NUM_STAGES] = {};
+  int64_t count[WGSR_NUM_STAGES] = {};
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  void flush() {
+    for (auto& r : recs) {
+      float t = 0.f;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+        ms[r.stage] += t;
+        count[r.stage] += 1;
+      }
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    recs.clear();
+  }
+};
+Prof g_prof;  // process-wide; the bench is single-threaded per rank
+
+struct StageTimer {
+  int stage;
+  hipStream_t s;
+  hipEvent_t a = nullptr;
+  StageTimer(int st, hipStream_t str) : stage(st), s(str) {
+    if (g_prof.on && (a = g_prof.get()) && hipEventRecord(a, s) != hipSuccess) a = nullptr;
+  }
+  ~StageTimer() {
+    if (!a) return;
+    hipEvent_t b = g_prof.get();
+    if (b && hipEventRecord(b, s) == hipSuccess) g_prof.recs.push_back({stage, a, b});
+    else g_prof.pool.push_back(a);
+  }
+};
 
 struct Grid {
   int gx, gy, nt;
@@ -91,6 +139,25 @@ using namespace wgsr;
 extern "C" {
 
 const char* wgsr_last_error(void) { return g_err; }
+
+void wgsr_profile_enable(int on) {
+  g_prof.flush();
+  g_prof.on = on != 0;
+}
+
+int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset) {
+  g_prof.flush();
+  const int m = n < WGSR_NUM_STAGES ? n : WGSR_NUM_STAGES;
+  for (int i = 0; i < m; ++i) {
+    if (ms) ms[i] = g_prof.ms[i];
+    if (counts) counts[i] = g_prof.count[i];
+  }
+  if (reset)
+    for (int i = 0; i < WGSR_NUM_STAGES; ++i) { g_prof.ms[i] = 0; g_prof.count[i] = 0; }
+  return WGSR_NUM_STAGES;
+}
+
+const char* wgsr_profile_stage_name(int i) { return (i >= 0 && i < WGSR_NUM_STAGES) ? kStageNames[i] : ""; }
 const char* wgsr_version(void) { return "wgsr 0.1 gfx950"; }
 
 size_t wgsr_geometry_bytes(int P) { return GeomLayout((size_t)(P > 0 ? P : 0)).total; }
@@ -130,17 +197,20 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
 
   uint32_t* counter = at<uint32_t>(geom, GL.counter);  // [0] num_rendered, [1] error flags
   HIPCHK(hipMemsetAsync(counter, 0, 16, s));
-  STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1, s));
+  { StageTimer T(0, s); STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1, s)); }
 
   // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
   bool in_alt = false;
+  { StageTimer T(1, s);
   STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
                                at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
-                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt));
+                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt)); }
   const uint32_t* sorted_g = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
   // duplicate-slot offsets in depth order; Gaussian -> first slot
+  StageTimer* scan_timer = new StageTimer(2, s);
   STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), sorted_g, (size_t)a.P, at<uint32_t>(geom, GL.offs),
                                     at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
+  delete scan_timer;
   uint32_t host_counter[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(host_counter, counter, sizeof(host_counter), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -154,26 +224,30 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   const uint32_t* sorted_keys = nullptr;
   const uint32_t* sorted_k = nullptr;
   if (N > 0) {
+    { StageTimer T(3, s);
     STAGE(a, s, launch_duplicate(a, geom, sorted_g, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
-                                 at<uint32_t>(binning, BL.slot_g), s));
+                                 at<uint32_t>(binning, BL.slot_g), s)); }
     bool talt = false;
+    { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
                                  at<uint32_t>(binning, BL.val), at<uint32_t>(binning, BL.val_alt), true, N, 0,
                                  tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
-                                 at<uint32_t>(binning, BL.totals), s, &talt));
+                                 at<uint32_t>(binning, BL.totals), s, &talt)); }
     if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
     sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
     sorted_k = at<uint32_t>(binning, talt ? BL.val_alt : BL.val);
   }
   uint2* ranges = at<uint2>(image, IL.ranges);
   if (N > 0) {
+    StageTimer T(5, s);
     STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)N, grid.nt, ranges, s));
   } else {
     HIPCHK(hipMemsetAsync(ranges, 0, 8 * (size_t)grid.nt, s));
   }
+  { StageTimer T(6, s);
   STAGE(a, s, launch_render_fwd(a, ranges, sorted_k, binning ? at<uint32_t>(binning, BL.slot_g) : nullptr, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
-                                at<uint32_t>(image, IL.n_contrib), n_touched, s));
+                                at<uint32_t>(image, IL.n_contrib), n_touched, s)); }
   *num_rendered = (int64_t)N;
   return WGSR_OK;
 }
@@ -199,10 +273,12 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
     if (!partial) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
     const BinLayout BL(N);
     const bool talt = tile_sort_in_alt(grid);
+    StageTimer T(7, s);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
                                   at<uint32_t>(binning, BL.slot_g), geom, at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, s));
   }
+  StageTimer T(8, s);
   STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
                                dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
   return WGSR_OK;
@@ -222,6 +298,7 @@ int wgsr_dist_cuda2(int P, const float* points, float* out, wgsr_alloc_fn scratc
   if (P == 0) return WGSR_OK;
   void* scratch = call_alloc(scratch_alloc, ctx, knn_scratch_bytes(P));
   if (!scratch) return set_error(WGSR_EALLOC, "distCUDA2 scratch allocation failed");
+  StageTimer T(9, (hipStream_t)stream);
   HIPCHK(launch_dist_cuda2(P, points, out, scratch, (hipStream_t)stream));
   return WGSR_OK;
 }

@@ -35,6 +35,7 @@ __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k]
 
 // SH -> RGB (upstream computeColorFromSH forward), clamp flags in bits 0..2
 __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32_t& clamp_bits) {
+#pragma clang fp contract(off)
   f3 r = scl3(SH_C0, ldc(sh, 0));
   if (deg > 0) {
     const float x = dir.x, y = dir.y, z = dir.z;
@@ -71,6 +72,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     ushort4* __restrict__ rect, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag) {
+#pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
   radii[i] = 0;

@@ -70,14 +70,20 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
 }
 
 // ---------------------------------------------------------------------------
-// Small fp32 math (upstream operation order where it matters)
+// Small fp32 math (upstream operation order where it matters).  The geometry
+// helpers below are evaluated without FMA contraction so that the per-Gaussian
+// integer decisions (radius, tile rectangle) are bit-identical to the CPU
+// restatement (oracle/cpu_raster.cpp, built with -ffp-contract=off).
 // ---------------------------------------------------------------------------
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk3(float x, float y, float z) { return {x, y, z}; }
 __device__ __forceinline__ f3 add3(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ f3 sub3(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 scl3(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) {
+#pragma clang fp contract(off)
+  return a.x * b.x + a.y * b.y + a.z * b.z;
+}
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
@@ -87,10 +93,12 @@ __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
 struct Mat16 { float m[16]; };
 
 __device__ __forceinline__ f3 xform43(const float* m, f3 p) {
+#pragma clang fp contract(off)
   return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
           m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
 }
 __device__ __forceinline__ float4 xform44(const float* m, f3 p) {
+#pragma clang fp contract(off)
   return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
                      m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
 }
@@ -98,6 +106,7 @@ __device__ __forceinline__ float4 xform44(const float* m, f3 p) {
 __device__ __forceinline__ float ndc2pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
 
 __device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
+#pragma clang fp contract(off)
   const float r = q.x, x = q.y, y = q.z, z = q.w;
   R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
   R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
@@ -106,6 +115,7 @@ __device__ __forceinline__ void quat_rot(float4 q, float R[3][3]) {
 
 // Sigma = R diag((mod s)^2) R^T, upper triangle (xx, xy, xz, yy, yz, zz)
 __device__ __forceinline__ void cov3d_from(f3 s, float mod, float4 q, float c[6]) {
+#pragma clang fp contract(off)
   float R[3][3];
   quat_rot(q, R);
   const float sx = mod * s.x, sy = mod * s.y, sz = mod * s.z;
@@ -147,6 +157,7 @@ __device__ __forceinline__ void load_cam(Cam& c, const float* view, const float*
 
 // EWA: T = J Rw (2x3) for camera-space mean t (clamped to 1.3 x the fov).
 __device__ __forceinline__ void ewa_T(const Cam& c, f3 t, float T[2][3], f3& tc, float& xmul, float& ymul) {
+#pragma clang fp contract(off)
   const float limx = 1.3f * c.tanx, limy = 1.3f * c.tany;
   const float txtz = t.x / t.z, tytz = t.y / t.z;
   tc = {fminf(limx, fmaxf(-limx, txtz)) * t.z, fminf(limy, fmaxf(-limy, tytz)) * t.z, t.z};
@@ -168,6 +179,7 @@ __device__ __forceinline__ void sym3(const float c6[6], float S[3][3]) {
 }
 
 __device__ __forceinline__ void cov2d(const float T[2][3], const float S[3][3], float& a, float& b, float& c) {
+#pragma clang fp contract(off)
   float ST0[3], ST1[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {

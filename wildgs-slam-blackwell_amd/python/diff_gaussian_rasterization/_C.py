@@ -81,9 +81,13 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
                                  projmatrix_raw, tan_fovx, tan_fovy, dL_dout_color, dL_dout_depth,
                                  sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                 debug):
+                                 debug, *, out=None):
     """-> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh,
-    dL_dscales, dL_drotations, dL_dtau[P,6])."""
+    dL_dscales, dL_drotations, dL_dtau[P,6]).
+
+    ``out`` (extension, keyword-only): dict of preallocated contiguous float32
+    tensors for "means3D", "shs", "opacities", "scales", "rotations" (e.g. the
+    views of a wgsr.dp.GradBuffer) that the kernels write directly."""
     L = _lib.load()
     dev = means3D.device
     P = means3D.size(0)
@@ -99,6 +103,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dL_dsh = torch.zeros(P, M, 3, **fopts) if M == 0 else torch.empty(P, M, 3, **fopts)
     dL_dscales = torch.empty(P, 3, **fopts)
     dL_drotations = torch.empty(P, 4, **fopts)
+    if out is not None:
+        def take(name, default):
+            t = out.get(name)
+            if t is None:
+                return default
+            if t.shape != default.shape or t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError(f"out[{name!r}] must be a contiguous float32 {tuple(default.shape)}")
+            return t
+        dL_dmeans3D = take("means3D", dL_dmeans3D)
+        dL_dsh = take("shs", dL_dsh)
+        dL_dopacity = take("opacities", dL_dopacity)
+        dL_dscales = take("scales", dL_dscales)
+        dL_drotations = take("rotations", dL_drotations)
     dL_dtau = torch.empty(P, 6, **fopts)
     if P == 0:
         return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,

@@ -82,6 +82,12 @@ def load():
         L.wgsr_last_error.argtypes = []
         L.wgsr_version.restype = ctypes.c_char_p
         L.wgsr_version.argtypes = []
+        L.wgsr_profile_enable.restype = None
+        L.wgsr_profile_enable.argtypes = [c_int]
+        L.wgsr_profile_read.restype = c_int
+        L.wgsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64), c_int, c_int]
+        L.wgsr_profile_stage_name.restype = ctypes.c_char_p
+        L.wgsr_profile_stage_name.argtypes = [c_int]
         _lib = L
     return _lib
 
@@ -89,8 +95,28 @@ def load():
 EXPORTED_SYMBOLS = (
     "wgsr_rasterize_forward", "wgsr_rasterize_backward", "wgsr_mark_visible", "wgsr_dist_cuda2",
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
-    "wgsr_version",
+    "wgsr_version", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
 )
+
+
+class StageProfile:
+    """Per-stage device time (HIP events on the launch stream) inside a block."""
+
+    def __enter__(self):
+        L = load()
+        L.wgsr_profile_read(None, None, 0, 1)
+        L.wgsr_profile_enable(1)
+        return self
+
+    def __exit__(self, *exc):
+        L = load()
+        n = 16
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        k = L.wgsr_profile_read(ms, cnt, n, 1)
+        L.wgsr_profile_enable(0)
+        self.stages = {L.wgsr_profile_stage_name(i).decode(): (ms[i], int(cnt[i])) for i in range(k)}
+        return False
 
 
 def check(code: int):
