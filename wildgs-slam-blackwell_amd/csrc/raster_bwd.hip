@@ -146,11 +146,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         }
       }
       if (__ballot(contrib) != 0) {
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-          const float s = wave_sum(gv[q]);
-          if (lane == 0) sP[w][j][q] = s;
-        }
+        wave_sum10_store(gv, &sP[w][j][0]);
       } else if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < 10; ++q) sP[w][j][q] = 0.f;

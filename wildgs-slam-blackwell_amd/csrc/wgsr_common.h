@@ -41,6 +41,56 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   return v;
 }
 
+// Sum of x over each 16-lane row; lane 15 of every row ends with the row sum.
+// Quad butterfly (quad_perm [1,0,3,2], [2,3,0,1]) then row_shr:4 and
+// row_shr:8 with bound_ctrl (shifted-in lanes read 0): VALU-only DPP adds.
+__device__ __forceinline__ float dpp_row_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xf, 0xf, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xf, 0xf, true));
+  return x;
+}
+
+__device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Wave-wide sums of 10 per-lane values, stored to dst[0..9] by 4 lanes.
+// Packed butterfly for gfx950 (must be called with all 64 lanes active):
+//   v_permlane32_swap pairs values (lanes 0-31 keep value 2k, 32-63 value
+//   2k+1): 5 swaps + 5 adds; v_permlane16_swap pairs those by rows: 3 swaps
+//   + 3 adds; then 3 x 4 DPP row adds.  ~30 VALU ops instead of 60 shuffles.
+__device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
+  float R[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * k]), __float_as_uint(v[2 * k + 1]), false,
+                                              false);
+    R[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  float S[3];
+  {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[0]), __float_as_uint(R[1]), false, false);
+    S[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v0 v2 v1 v3
+    r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[2]), __float_as_uint(R[3]), false, false);
+    S[1] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v4 v6 v5 v7
+    r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), 0u, false, false);
+    S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 0 v9 0
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) S[i] = dpp_row_sum16(S[i]);
+  const int lane = __lane_id();
+  if ((lane & 15) == 15) {
+    const int row = lane >> 4;
+    const int m = (row & 1) * 2 + (row >> 1);
+    dst[m] = S[0];
+    dst[4 + m] = S[1];
+    if (!(row & 1)) dst[8 + (row >> 1)] = S[2];
+  }
+}
+
 // inclusive prefix sum across the wave
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = lane_id();
