@@ -232,7 +232,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
                                  at<uint32_t>(binning, BL.val), at<uint32_t>(binning, BL.val_alt), true, N, 0,
                                  tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
-                                 at<uint32_t>(binning, BL.totals), s, &talt)); }
+                                 at<uint32_t>(binning, BL.totals), s, &talt, at<uint32_t>(binning, BL.slot_g),
+                                 at<uint32_t>(binning, BL.point_g))); }
     if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
     sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
     sorted_k = at<uint32_t>(binning, talt ? BL.val_alt : BL.val);
@@ -245,7 +246,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     HIPCHK(hipMemsetAsync(ranges, 0, 8 * (size_t)grid.nt, s));
   }
   { StageTimer T(6, s);
-  STAGE(a, s, launch_render_fwd(a, ranges, sorted_k, binning ? at<uint32_t>(binning, BL.slot_g) : nullptr, geom,
+  (void)sorted_k;
+  STAGE(a, s, launch_render_fwd(a, ranges, binning ? at<uint32_t>(binning, BL.point_g) : nullptr, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, s)); }
   *num_rendered = (int64_t)N;
@@ -275,7 +277,7 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
-                                  at<uint32_t>(binning, BL.slot_g), geom, at<float>(image, IL.final_T),
+                                  at<uint32_t>(binning, BL.point_g), geom, at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, s));
   }
   StageTimer T(8, s);

@@ -1,11 +1,11 @@
 // Backward rasteriser stages for gfx950.
 //
-//   render_bwd  one 256-thread workgroup per tile walks the tile's list back
-//               to front (upstream BACKWARD::renderCUDA math).  Instead of one
+//   render_bwd  one wave64 per tile (4 pixels per lane) walks the tile's list
+//               back to front (upstream BACKWARD::renderCUDA math).  Instead of one
 //               float atomic per (pixel, Gaussian, quantity) -- scattered
 //               single-lane atomics run ~17x under the chip's atomic rate on
-//               MI355X -- each wave reduces its 64 pixels' contributions in
-//               registers, the four waves combine through LDS, and the tile
+//               MI355X -- each lane sums its four pixels in registers, one
+//               packed wave reduction covers the whole tile, and the tile
 //               writes ONE 48-byte partial record per (Gaussian, tile) pair
 //               into that pair's duplicate slot.  No atomics, deterministic.
 //   gauss_bwd   one lane per Gaussian: sums its contiguous slot range of
@@ -30,35 +30,55 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
-__global__ __launch_bounds__(256) void k_render_bwd(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ slot_g,
+// One wave64 per tile, lane l owns the 2x2 pixel quad (l & 7, l >> 3).  Per
+// entry a lane sums its (up to) four pixels' contributions in registers, one
+// packed wave reduction (wave_sum10_store) yields the tile's 10 partial sums,
+// and lane j of the batch writes entry j's 48-byte record.
+__global__ __launch_bounds__(64) void k_render_bwd(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ point_g,
     const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial) {
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sK[kBatch];
-  __shared__ float sP[4][kBatch][10];
-  __shared__ uint32_t s_max[4];
+  __shared__ float sP[kBatch][11];
   const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int px = (int)(tile % gx) * kTile + (w & 1) * 8 + (lane & 7);
-  const int py = (int)(tile / gx) * kTile + (w >> 1) * 8 + (lane >> 3);
-  const bool inside = px < W && py < H;
-  const size_t pid = (size_t)py * W + px;
+  const int lane = threadIdx.x;
+  const int x0 = (int)(tile % gx) * kTile + 2 * (lane & 7);
+  const int y0 = (int)(tile / gx) * kTile + 2 * (lane >> 3);
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
-  const float T_final = inside ? final_Ts[pid] : 0.f;
-  const uint32_t last = inside ? n_contrib[pid] : 0u;
+  float fx[4], fy[4], Tf[4], T[4], dp0[4], dp1[4], dp2[4], dpd[4], bgd[4];
+  float acc0[4], acc1[4], acc2[4], accd[4], la[4], lc0[4], lc1[4], lc2[4], ld[4];
+  uint32_t last[4];
+  uint32_t m = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+    const bool inside = px < W && py < H;
+    const size_t pid = (size_t)py * W + px;
+    fx[p] = (float)px;
+    fy[p] = (float)py;
+    Tf[p] = inside ? final_Ts[pid] : 0.f;
+    last[p] = inside ? n_contrib[pid] : 0u;
+    dp0[p] = inside ? dL_dpix[pid] : 0.f;
+    dp1[p] = inside ? dL_dpix[HW + pid] : 0.f;
+    dp2[p] = inside ? dL_dpix[2 * HW + pid] : 0.f;
+    dpd[p] = inside ? dL_ddep[pid] : 0.f;
+    bgd[p] = bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p];
+    T[p] = Tf[p];
+    acc0[p] = acc1[p] = acc2[p] = accd[p] = 0.f;
+    la[p] = lc0[p] = lc1[p] = lc2[p] = ld[p] = 0.f;
+    m = max(m, last[p]);
+  }
   // entries behind every pixel's last contributor cannot receive gradient
-  uint32_t m = last;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-  if (lane == 0) s_max[w] = m;
-  __syncthreads();
-  const uint32_t maxlast = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
-  const uint32_t end = range.x + maxlast;
-  for (uint32_t i = end + t; i < range.y; i += 256) {
+  const uint32_t end = range.x + m;
+  for (uint32_t i = end + lane; i < range.y; i += 64) {
     const uint32_t k = sorted_k[i];
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     partial[3 * (size_t)k] = z;
@@ -66,103 +86,106 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     partial[3 * (size_t)k + 2] = z;
   }
 
-  float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f, dpd = 0.f;
-  if (inside) {
-    dpix0 = dL_dpix[pid];
-    dpix1 = dL_dpix[HW + pid];
-    dpix2 = dL_dpix[2 * HW + pid];
-    dpd = dL_ddep[pid];
+  // prefetch pipeline (back to front): records of the next batch in registers
+  uint32_t kcur = 0, gcur = 0, knext = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (end >= range.x + 1 + lane) {
+    const uint32_t idx = end - 1 - lane;
+    kcur = sorted_k[idx];
+    gcur = point_g[idx];
+    nA = splat[3 * (size_t)gcur];
+    nB = splat[3 * (size_t)gcur + 1];
+    nC = splat[3 * (size_t)gcur + 2];
   }
-  const float bg_dot = bg[0] * dpix0 + bg[1] * dpix1 + bg[2] * dpix2;
-  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-  const float fpx = (float)px, fpy = (float)py;
+  if (end >= range.x + 1 + kBatch + lane) {
+    knext = sorted_k[end - 1 - kBatch - lane];
+    gnext = point_g[end - 1 - kBatch - lane];
+  }
 
-  float T = T_final;
-  float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc_d = 0.f;
-  float last_alpha = 0.f, lc0 = 0.f, lc1 = 0.f, lc2 = 0.f, ld = 0.f;
-  uint32_t contributor = maxlast;
-
-  for (uint32_t b_end = end; b_end > range.x;) {
-    const uint32_t b_start = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x;
-    const int cnt = (int)(b_end - b_start);
+  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
+    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
     __syncthreads();
-    if (t < cnt) {
-      const uint32_t k = sorted_k[b_end - 1 - t];
-      const uint32_t g = slot_g[k];
-      sA[t] = splat[3 * (size_t)g];
-      sB[t] = splat[3 * (size_t)g + 1];
-      sC[t] = splat[3 * (size_t)g + 2];
-      sK[t] = k;
+    sA[lane] = nA;
+    sB[lane] = nB;
+    sC[lane] = nC;
+    sK[lane] = kcur;
+    __syncthreads();
+    kcur = knext;
+    gcur = gnext;
+    if (b_end >= range.x + 1 + kBatch + lane) {
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
     }
-    __syncthreads();
+    if (b_end >= range.x + 1 + 2 * kBatch + lane) {
+      knext = sorted_k[b_end - 1 - 2 * kBatch - lane];
+      gnext = point_g[b_end - 1 - 2 * kBatch - lane];
+    }
+    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
     for (int j = 0; j < cnt; ++j) {
-      --contributor;
+      const uint32_t cidx = cfirst - j;
+      const float4 A = sA[j];
+      const float4 B = sB[j];
       float gv[10];
 #pragma unroll
       for (int q = 0; q < 10; ++q) gv[q] = 0.f;
       bool contrib = false;
-      if (contributor < last) {
-        const float4 A = sA[j];
-        const float4 B = sB[j];
-        const float dx = A.x - fpx, dy = A.y - fpy;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (cidx >= last[p]) continue;
+        const float dx = A.x - fx[p], dy = A.y - fy[p];
         const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-        if (power <= 0.0f) {
-          const float G = __expf(power);
-          const float alpha = fminf(kMaxAlpha, B.y * G);
-          if (alpha >= kMinAlpha) {
-            contrib = true;
-            const float4 Cc = sC[j];
-            T = T / (1.f - alpha);
-            const float dchannel_dcolor = alpha * T;
-            float dL_dalpha = 0.f;
-            acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-            acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-            acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-            lc0 = Cc.x; lc1 = Cc.y; lc2 = Cc.z;
-            dL_dalpha += (Cc.x - acc0) * dpix0;
-            dL_dalpha += (Cc.y - acc1) * dpix1;
-            dL_dalpha += (Cc.z - acc2) * dpix2;
-            gv[6] = dchannel_dcolor * dpix0;
-            gv[7] = dchannel_dcolor * dpix1;
-            gv[8] = dchannel_dcolor * dpix2;
-            acc_d = last_alpha * ld + (1.f - last_alpha) * acc_d;
-            ld = B.z;
-            dL_dalpha += (B.z - acc_d) * dpd;
-            gv[9] = dchannel_dcolor * dpd;
-            dL_dalpha *= T;
-            last_alpha = alpha;
-            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-            const float dL_dG = B.y * dL_dalpha;
-            const float gdx = G * dx, gdy = G * dy;
-            const float dG_ddelx = -gdx * A.z - gdy * A.w;
-            const float dG_ddely = -gdy * B.x - gdx * A.w;
-            gv[0] = dL_dG * dG_ddelx * ddelx_dx;
-            gv[1] = dL_dG * dG_ddely * ddely_dy;
-            gv[2] = -0.5f * gdx * dx * dL_dG;
-            gv[3] = -0.5f * gdx * dy * dL_dG;
-            gv[4] = -0.5f * gdy * dy * dL_dG;
-            gv[5] = G * dL_dalpha;
-          }
-        }
+        if (power > 0.0f) continue;
+        const float G = __expf(power);
+        const float alpha = fminf(kMaxAlpha, B.y * G);
+        if (alpha < kMinAlpha) continue;
+        contrib = true;
+        const float4 Cc = sC[j];
+        T[p] = T[p] / (1.f - alpha);
+        const float dchannel_dcolor = alpha * T[p];
+        acc0[p] = la[p] * lc0[p] + (1.f - la[p]) * acc0[p];
+        acc1[p] = la[p] * lc1[p] + (1.f - la[p]) * acc1[p];
+        acc2[p] = la[p] * lc2[p] + (1.f - la[p]) * acc2[p];
+        lc0[p] = Cc.x; lc1[p] = Cc.y; lc2[p] = Cc.z;
+        float dL_dalpha = (Cc.x - acc0[p]) * dp0[p];
+        dL_dalpha += (Cc.y - acc1[p]) * dp1[p];
+        dL_dalpha += (Cc.z - acc2[p]) * dp2[p];
+        gv[6] += dchannel_dcolor * dp0[p];
+        gv[7] += dchannel_dcolor * dp1[p];
+        gv[8] += dchannel_dcolor * dp2[p];
+        accd[p] = la[p] * ld[p] + (1.f - la[p]) * accd[p];
+        ld[p] = B.z;
+        dL_dalpha += (B.z - accd[p]) * dpd[p];
+        gv[9] += dchannel_dcolor * dpd[p];
+        dL_dalpha *= T[p];
+        la[p] = alpha;
+        dL_dalpha += (-Tf[p] / (1.f - alpha)) * bgd[p];
+        const float dL_dG = B.y * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * A.z - gdy * A.w;
+        const float dG_ddely = -gdy * B.x - gdx * A.w;
+        gv[0] += dL_dG * dG_ddelx * ddelx_dx;
+        gv[1] += dL_dG * dG_ddely * ddely_dy;
+        gv[2] += -0.5f * gdx * dx * dL_dG;
+        gv[3] += -0.5f * gdx * dy * dL_dG;
+        gv[4] += -0.5f * gdy * dy * dL_dG;
+        gv[5] += G * dL_dalpha;
       }
       if (__ballot(contrib) != 0) {
-        wave_sum10_store(gv, &sP[w][j][0]);
+        wave_sum10_store(gv, &sP[j][0]);
       } else if (lane == 0) {
 #pragma unroll
-        for (int q = 0; q < 10; ++q) sP[w][j][q] = 0.f;
+        for (int q = 0; q < 10; ++q) sP[j][q] = 0.f;
       }
     }
     __syncthreads();
-    if (t < cnt) {
-      float s[10];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) s[q] = sP[0][t][q] + sP[1][t][q] + sP[2][t][q] + sP[3][t][q];
-      const size_t k = sK[t];
+    if (lane < cnt) {
+      const float* s = sP[lane];
+      const size_t k = sK[lane];
       partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
       partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
       partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
     }
-    b_end = b_start;
   }
 }
 
@@ -433,13 +456,13 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 }  // namespace
 
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* slot_g, const void* geom, const float* final_T,
+                             const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(256), 0, s, ranges, sorted_k, slot_g, at<float4>(geom, L.splat),
+  hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(kBatch), 0, s, ranges, sorted_k, point_g, at<float4>(geom, L.splat),
                      a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial);
   return hipGetLastError();
 }

@@ -10,8 +10,9 @@
 //                so the writes of a wave are contiguous.
 //   [tile sort]  stable sort of the pairs by tile id             -- sort.hip
 //   ranges       per-tile [start, end) by binary search.
-//   render       one 256-thread workgroup per 16x16 tile, splat records staged
-//                in LDS 256 at a time, front-to-back alpha blending.
+//   render       one wave64 per 16x16 tile (4 pixels per lane), splat records
+//                staged in LDS 64 at a time and prefetched one batch ahead,
+//                front-to-back alpha blending.
 //
 // Sorting by depth first and then stably by tile yields exactly upstream's
 // (tile << 32 | depth) order (ties broken by Gaussian index) while the
@@ -203,83 +204,117 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ key
   ranges[t] = make_uint2(lower((uint32_t)t), lower((uint32_t)t + 1));
 }
 
-// One workgroup = one 16x16 tile; wave w owns the 8x8 quadrant (w & 1, w >> 1).
-__global__ __launch_bounds__(256) void k_render_fwd(const uint2* __restrict__ ranges,
-                                                    const uint32_t* __restrict__ sorted_k,
-                                                    const uint32_t* __restrict__ slot_g,
-                                                    const float4* __restrict__ splat, int W, int H, int gx,
-                                                    int ntiles, const float* __restrict__ bg,
-                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
-                                                    float* __restrict__ out_opac, float* __restrict__ final_T,
-                                                    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
-  __shared__ float4 sA[256], sB[256], sC[256];
-  __shared__ uint32_t sG[256];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int px = (int)(tile % gx) * kTile + (w & 1) * 8 + (lane & 7);
-  const int py = (int)(tile / gx) * kTile + (w >> 1) * 8 + (lane >> 3);
-  const bool inside = px < W && py < H;
-  const float fpx = (float)px, fpy = (float)py;
-  const uint2 range = ranges[tile];
+// One wave64 = one 16x16 tile; lane l owns the 2x2 pixel quad (l & 7, l >> 3),
+// i.e. four independent front-to-back blends per lane (4-way ILP, and every
+// LDS broadcast of a splat record serves 256 pixels).  Splat records arrive
+// 64 at a time through LDS; the next batch's records are loaded into
+// registers while the current batch is blended (ids two batches ahead).
+constexpr int kFwdBatch = 64;
 
-  bool done = !inside;
-  float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
-  uint32_t contributor = 0, last = 0;
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += 256) {
-    if (__syncthreads_count(done) == 256) break;
-    const uint32_t idx = b0 + t;
-    if (idx < range.y) {
-      const uint32_t g = slot_g[sorted_k[idx]];
-      sA[t] = splat[3 * (size_t)g];
-      sB[t] = splat[3 * (size_t)g + 1];
-      sC[t] = splat[3 * (size_t)g + 2];
-      sG[t] = g;
-    }
+__global__ __launch_bounds__(64) void k_render_fwd(const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ point_g,
+                                                   const float4* __restrict__ splat, int W, int H, int gx,
+                                                   int ntiles, const float* __restrict__ bg,
+                                                   float* __restrict__ out_color, float* __restrict__ out_depth,
+                                                   float* __restrict__ out_opac, float* __restrict__ final_T,
+                                                   uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+  __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
+  __shared__ uint32_t sG[kFwdBatch];
+  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const int lane = threadIdx.x;
+  const int x0 = (int)(tile % gx) * kTile + 2 * (lane & 7);
+  const int y0 = (int)(tile / gx) * kTile + 2 * (lane >> 3);
+  float fx[4], fy[4];
+  uint32_t done = 0;  // bit p: pixel p finished (or outside the image)
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+    fx[p] = (float)px;
+    fy[p] = (float)py;
+    if (!(px < W && py < H)) done |= 1u << p;
+  }
+  const uint2 range = ranges[tile];
+  float T[4] = {1.f, 1.f, 1.f, 1.f}, C0[4] = {0, 0, 0, 0}, C1[4] = {0, 0, 0, 0}, C2[4] = {0, 0, 0, 0},
+        Dp[4] = {0, 0, 0, 0};
+  uint32_t last[4] = {0, 0, 0, 0};
+
+  // prefetch pipeline: records of batch b+1 in registers, ids of batch b+2
+  uint32_t gcur = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (range.x + lane < range.y) {
+    gcur = point_g[range.x + lane];
+    nA = splat[3 * (size_t)gcur];
+    nB = splat[3 * (size_t)gcur + 1];
+    nC = splat[3 * (size_t)gcur + 2];
+  }
+  if (range.x + kFwdBatch + lane < range.y) gnext = point_g[range.x + kFwdBatch + lane];
+
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
+    if (__all(done == 0xFu)) break;
     __syncthreads();
-    const int cnt = (int)min(256u, range.y - b0);
+    sA[lane] = nA;
+    sB[lane] = nB;
+    sC[lane] = nC;
+    sG[lane] = gcur;
+    __syncthreads();
+    gcur = gnext;
+    if (b0 + kFwdBatch + lane < range.y) {
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+    }
+    if (b0 + 2 * kFwdBatch + lane < range.y) gnext = point_g[b0 + 2 * kFwdBatch + lane];
+
+    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+    const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
     for (int j = 0; j < cnt; ++j) {
-      bool touched = false;
-      if (!done) {
-        ++contributor;
-        const float4 A = sA[j];
-        const float4 B = sB[j];
-        const float dx = A.x - fpx, dy = A.y - fpy;
+      const float4 A = sA[j];
+      const float4 B = sB[j];
+      uint32_t touched = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (done & (1u << p)) continue;
+        const float dx = A.x - fx[p], dy = A.y - fy[p];
         const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-        if (power <= 0.0f) {
-          const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
-          if (alpha >= kMinAlpha) {
-            const float test_T = T * (1.f - alpha);
-            if (test_T < kMinT) {
-              done = true;
-            } else {
-              const float4 Cc = sC[j];
-              const float wgt = alpha * T;
-              C0 += Cc.x * wgt;
-              C1 += Cc.y * wgt;
-              C2 += Cc.z * wgt;
-              Dp += B.z * wgt;
-              touched = test_T > 0.5f;
-              T = test_T;
-              last = contributor;
-            }
-          }
+        if (power > 0.0f) continue;
+        const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
+        if (alpha < kMinAlpha) continue;
+        const float test_T = T[p] * (1.f - alpha);
+        if (test_T < kMinT) {
+          done |= 1u << p;
+          continue;
         }
+        const float4 Cc = sC[j];
+        const float wgt = alpha * T[p];
+        C0[p] += Cc.x * wgt;
+        C1[p] += Cc.y * wgt;
+        C2[p] += Cc.z * wgt;
+        Dp[p] += B.z * wgt;
+        touched += test_T > 0.5f ? 1u : 0u;
+        T[p] = test_T;
+        last[p] = cbase + j;
       }
-      const uint64_t tm = __ballot(touched);
-      if (tm != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)__popcll(tm));
-      if (__all(done)) break;
+      // pixels of this wave whose T stays above 0.5 (upstream n_touched)
+      const uint32_t tot = (uint32_t)__popcll(__ballot(touched & 1u)) +
+                           2u * (uint32_t)__popcll(__ballot(touched & 2u)) +
+                           4u * (uint32_t)__popcll(__ballot(touched & 4u));
+      if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
+      if (__all(done == 0xFu)) break;
     }
   }
-  if (inside) {
+  const size_t HW = (size_t)H * W;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+    if (!(px < W && py < H)) continue;
     const size_t pid = (size_t)py * W + px;
-    const size_t HW = (size_t)H * W;
-    final_T[pid] = T;
-    n_contrib[pid] = last;
-    out_color[pid] = C0 + T * bg[0];
-    out_color[HW + pid] = C1 + T * bg[1];
-    out_color[2 * HW + pid] = C2 + T * bg[2];
-    out_depth[pid] = Dp;
-    out_opac[pid] = 1.f - T;
+    final_T[pid] = T[p];
+    n_contrib[pid] = last[p];
+    out_color[pid] = C0[p] + T[p] * bg[0];
+    out_color[HW + pid] = C1[p] + T[p] * bg[1];
+    out_color[2 * HW + pid] = C2[p] + T[p] * bg[2];
+    out_depth[pid] = Dp[p];
+    out_opac[pid] = 1.f - T[p];
   }
 }
 
@@ -322,14 +357,14 @@ hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, ui
   return hipGetLastError();
 }
 
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* slot_g, const void* geom, float* out_color, float* out_depth,
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
+                             const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
                              hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(256), 0, s, ranges, sorted_k, slot_g,
+  hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(kFwdBatch), 0, s, ranges, point_g,
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,
                      final_T, n_contrib, n_touched);
   return hipGetLastError();

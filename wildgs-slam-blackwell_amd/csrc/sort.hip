@@ -82,7 +82,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        int shift, int bits, uint32_t nb,
                                                        const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals,
-                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                       const uint32_t* __restrict__ gtab,
+                                                       uint32_t* __restrict__ gout) {
   __shared__ uint32_t s_k[kSortTile];
   __shared__ uint32_t s_v[kSortTile];
   __shared__ uint32_t s_wcnt[4][256];
@@ -151,7 +153,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     const uint32_t d = (k >> shift) & mask;
     const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
     kout[dst] = k;
-    vout[dst] = s_v[i];
+    const uint32_t v = s_v[i];
+    vout[dst] = v;
+    if (gout) gout[dst] = gtab[v];  // fused gather of a per-value table (last pass)
   }
 }
 
@@ -229,7 +233,8 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt) {
+                            hipStream_t stream, bool* result_in_alt, const uint32_t* gather_table,
+                            uint32_t* gathered_out) {
   *result_in_alt = false;
   if (n == 0 || end_bit <= begin_bit) {
     if (vals_iota && n > 0) {
@@ -245,8 +250,10 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     const int bits = min(8, end_bit - shift);
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, hist);
     hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, hist, nb, totals);
+    const bool last = shift + 8 >= end_bit;
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
-                       bits, nb, hist, totals, ko, vo);
+                       bits, nb, hist, totals, ko, vo, last ? gather_table : nullptr,
+                       last ? gathered_out : nullptr);
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;

@@ -11,9 +11,12 @@ namespace wgsr {
 // LSD radix sort on bits [begin_bit, end_bit) (8-bit digits).  Input in
 // keys/vals (vals ignored if vals_iota: value = input position); the result
 // lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
+// If gather_table is given, the last pass also writes
+// gathered_out[i] = gather_table[sorted value i].
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt);
+                            hipStream_t stream, bool* result_in_alt, const uint32_t* gather_table = nullptr,
+                            uint32_t* gathered_out = nullptr);
 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
@@ -35,8 +38,8 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, hipStream_t s);
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s);
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* slot_g, const void* geom, float* out_color, float* out_depth,
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
+                             const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
                              hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
@@ -44,7 +47,7 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, c
 
 // backward stages (raster_bwd.hip)
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* slot_g, const void* geom, const float* final_T,
+                             const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, hipStream_t s);
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
