@@ -6,6 +6,7 @@
 // the only host synchronisation is the num_rendered read in the forward.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -25,6 +26,13 @@ int set_error(int code, const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
   return code;
+}
+
+int render_ppl(const char* env_name, int dflt) {
+  const char* v = getenv(env_name);
+  if (!v) return dflt;
+  const int x = atoi(v);
+  return (x == 1 || x == 2 || x == 4) ? x : dflt;
 }
 
 int num_bits(uint32_t n) {
@@ -205,10 +213,10 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
                                at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
                                kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt)); }
-  const uint32_t* sorted_g = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
+  const uint32_t* depth_order = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
   // duplicate-slot offsets in depth order; Gaussian -> first slot
   StageTimer* scan_timer = new StageTimer(2, s);
-  STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), sorted_g, (size_t)a.P, at<uint32_t>(geom, GL.offs),
+  STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.offs),
                                     at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
   delete scan_timer;
   uint32_t host_counter[2] = {0, 0};
@@ -223,9 +231,10 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   if (!binning && BL.total) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   const uint32_t* sorted_keys = nullptr;
   const uint32_t* sorted_k = nullptr;
+  const uint32_t* sorted_g = nullptr;  // tile lists (Gaussian ids)
   if (N > 0) {
     { StageTimer T(3, s);
-    STAGE(a, s, launch_duplicate(a, geom, sorted_g, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
+    STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
                                  at<uint32_t>(binning, BL.slot_g), s)); }
     bool talt = false;
     { StageTimer T(4, s);
@@ -234,9 +243,13 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
                                  tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
                                  at<uint32_t>(binning, BL.totals), s, &talt, at<uint32_t>(binning, BL.slot_g),
                                  at<uint32_t>(binning, BL.point_g))); }
+    // the Gaussian ids ride along as a second payload: sorted lists end in
+    // point_g after an odd number of passes, in slot_g after an even one
     if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
     sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
     sorted_k = at<uint32_t>(binning, talt ? BL.val_alt : BL.val);
+    (void)sorted_k;  // slot of each sorted pair: read by the backward
+    sorted_g = at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g);
   }
   uint2* ranges = at<uint2>(image, IL.ranges);
   if (N > 0) {
@@ -246,8 +259,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     HIPCHK(hipMemsetAsync(ranges, 0, 8 * (size_t)grid.nt, s));
   }
   { StageTimer T(6, s);
-  (void)sorted_k;
-  STAGE(a, s, launch_render_fwd(a, ranges, binning ? at<uint32_t>(binning, BL.point_g) : nullptr, geom,
+  STAGE(a, s, launch_render_fwd(a, ranges, sorted_g, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, s)); }
   *num_rendered = (int64_t)N;
@@ -277,7 +289,8 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
-                                  at<uint32_t>(binning, BL.point_g), geom, at<float>(image, IL.final_T),
+                                  at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g), geom,
+                                  at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, s));
   }
   StageTimer T(8, s);

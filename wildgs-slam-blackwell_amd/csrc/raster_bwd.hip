@@ -30,34 +30,40 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
-// One wave64 per tile, lane l owns the 2x2 pixel quad (l & 7, l >> 3).  Per
-// entry a lane sums its (up to) four pixels' contributions in registers, one
-// packed wave reduction (wave_sum10_store) yields the tile's 10 partial sums,
-// and lane j of the batch writes entry j's 48-byte record.
-__global__ __launch_bounds__(64) void k_render_bwd(
+// One tile per workgroup of 4 / PPL waves (tile_pixel<PPL> geometry).  Per
+// entry a lane first checks which of its PPL pixels the splat reaches; a wave
+// none of whose pixels it reaches skips the entry.  Otherwise the lane sums
+// its pixels' contributions in registers, one packed wave reduction
+// (wave_sum10_store) yields the wave's 10 partial sums, the waves' sums are
+// added through LDS, and thread j writes entry j's 48-byte record.
+template <int PPL>
+__global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ point_g,
     const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial) {
+  constexpr int WAVES = 4 / PPL;
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sK[kBatch];
-  __shared__ float sP[kBatch][11];
+  __shared__ float sP[WAVES][kBatch][11];
+  __shared__ uint32_t s_max[WAVES];
   const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int lane = threadIdx.x;
-  const int x0 = (int)(tile % gx) * kTile + 2 * (lane & 7);
-  const int y0 = (int)(tile / gx) * kTile + 2 * (lane >> 3);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
-  float fx[4], fy[4], Tf[4], T[4], dp0[4], dp1[4], dp2[4], dpd[4], bgd[4];
-  float acc0[4], acc1[4], acc2[4], accd[4], la[4], lc0[4], lc1[4], lc2[4], ld[4];
-  uint32_t last[4];
+  float fx[PPL], fy[PPL], Tf[PPL], T[PPL], dp0[PPL], dp1[PPL], dp2[PPL], dpd[PPL], bgd[PPL];
+  float acc0[PPL], acc1[PPL], acc2[PPL], accd[PPL], la[PPL], lc0[PPL], lc1[PPL], lc2[PPL], ld[PPL];
+  uint32_t last[PPL];
   uint32_t m = 0;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+  for (int p = 0; p < PPL; ++p) {
+    int ox, oy;
+    tile_pixel<PPL>(w, lane, p, ox, oy);
+    const int px = tx0 + ox, py = ty0 + oy;
     const bool inside = px < W && py < H;
     const size_t pid = (size_t)py * W + px;
     fx[p] = (float)px;
@@ -77,8 +83,14 @@ __global__ __launch_bounds__(64) void k_render_bwd(
   // entries behind every pixel's last contributor cannot receive gradient
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  if constexpr (WAVES > 1) {
+    if (lane == 0) s_max[w] = m;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) m = max(m, s_max[i]);
+  }
   const uint32_t end = range.x + m;
-  for (uint32_t i = end + lane; i < range.y; i += 64) {
+  for (uint32_t i = end + t; i < range.y; i += 64 * WAVES) {
     const uint32_t k = sorted_k[i];
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     partial[3 * (size_t)k] = z;
@@ -86,102 +98,135 @@ __global__ __launch_bounds__(64) void k_render_bwd(
     partial[3 * (size_t)k + 2] = z;
   }
 
-  // prefetch pipeline (back to front): records of the next batch in registers
+  // prefetch pipeline (wave 0, back to front): records of the next batch in
+  // registers, ids one batch further
   uint32_t kcur = 0, gcur = 0, knext = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (end >= range.x + 1 + lane) {
-    const uint32_t idx = end - 1 - lane;
-    kcur = sorted_k[idx];
-    gcur = point_g[idx];
-    nA = splat[3 * (size_t)gcur];
-    nB = splat[3 * (size_t)gcur + 1];
-    nC = splat[3 * (size_t)gcur + 2];
-  }
-  if (end >= range.x + 1 + kBatch + lane) {
-    knext = sorted_k[end - 1 - kBatch - lane];
-    gnext = point_g[end - 1 - kBatch - lane];
+  if (t < kBatch) {
+    if (end >= range.x + 1 + t) {
+      const uint32_t idx = end - 1 - t;
+      kcur = sorted_k[idx];
+      gcur = point_g[idx];
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+    }
+    if (end >= range.x + 1 + kBatch + t) {
+      knext = sorted_k[end - 1 - kBatch - t];
+      gnext = point_g[end - 1 - kBatch - t];
+    }
   }
 
   for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
     const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
     __syncthreads();
-    sA[lane] = nA;
-    sB[lane] = nB;
-    sC[lane] = nC;
-    sK[lane] = kcur;
-    __syncthreads();
-    kcur = knext;
-    gcur = gnext;
-    if (b_end >= range.x + 1 + kBatch + lane) {
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
+    if (t < kBatch) {
+      sA[t] = nA;
+      sB[t] = nB;
+      sC[t] = nC;
+      sK[t] = kcur;
     }
-    if (b_end >= range.x + 1 + 2 * kBatch + lane) {
-      knext = sorted_k[b_end - 1 - 2 * kBatch - lane];
-      gnext = point_g[b_end - 1 - 2 * kBatch - lane];
+    __syncthreads();
+    if (t < kBatch) {
+      kcur = knext;
+      gcur = gnext;
+      if (b_end >= range.x + 1 + kBatch + t) {
+        nA = splat[3 * (size_t)gcur];
+        nB = splat[3 * (size_t)gcur + 1];
+        nC = splat[3 * (size_t)gcur + 2];
+      }
+      if (b_end >= range.x + 1 + 2 * kBatch + t) {
+        knext = sorted_k[b_end - 1 - 2 * kBatch - t];
+        gnext = point_g[b_end - 1 - 2 * kBatch - t];
+      }
     }
     const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
     for (int j = 0; j < cnt; ++j) {
       const uint32_t cidx = cfirst - j;
       const float4 A = sA[j];
       const float4 B = sB[j];
+      // phase 1: which of this lane's pixels does entry j reach? (cheap)
+      float dxv[PPL], dyv[PPL], Gv[PPL], av[PPL];
+      bool vv[PPL];
+      bool any = false;
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) {
+        dxv[p] = A.x - fx[p];
+        dyv[p] = A.y - fy[p];
+        const float power = -0.5f * (A.z * dxv[p] * dxv[p] + B.x * dyv[p] * dyv[p]) - A.w * dxv[p] * dyv[p];
+        Gv[p] = __expf(power);
+        av[p] = fminf(kMaxAlpha, B.y * Gv[p]);
+        vv[p] = cidx < last[p] && power <= 0.0f && av[p] >= kMinAlpha;
+        any |= vv[p];
+      }
+      if (!__any(any)) {  // no pixel of this wave: zero partial, skip the heavy part
+        if (lane == 0) {
+#pragma unroll
+          for (int q = 0; q < 10; ++q) sP[w][j][q] = 0.f;
+        }
+        continue;
+      }
+      // phase 2: PPL independent, branch-free pixel updates (selects)
+      const float4 Cc = sC[j];
       float gv[10];
 #pragma unroll
       for (int q = 0; q < 10; ++q) gv[q] = 0.f;
-      bool contrib = false;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        if (cidx >= last[p]) continue;
-        const float dx = A.x - fx[p], dy = A.y - fy[p];
-        const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-        if (power > 0.0f) continue;
-        const float G = __expf(power);
-        const float alpha = fminf(kMaxAlpha, B.y * G);
-        if (alpha < kMinAlpha) continue;
-        contrib = true;
-        const float4 Cc = sC[j];
-        T[p] = T[p] / (1.f - alpha);
-        const float dchannel_dcolor = alpha * T[p];
-        acc0[p] = la[p] * lc0[p] + (1.f - la[p]) * acc0[p];
-        acc1[p] = la[p] * lc1[p] + (1.f - la[p]) * acc1[p];
-        acc2[p] = la[p] * lc2[p] + (1.f - la[p]) * acc2[p];
-        lc0[p] = Cc.x; lc1[p] = Cc.y; lc2[p] = Cc.z;
-        float dL_dalpha = (Cc.x - acc0[p]) * dp0[p];
-        dL_dalpha += (Cc.y - acc1[p]) * dp1[p];
-        dL_dalpha += (Cc.z - acc2[p]) * dp2[p];
-        gv[6] += dchannel_dcolor * dp0[p];
-        gv[7] += dchannel_dcolor * dp1[p];
-        gv[8] += dchannel_dcolor * dp2[p];
-        accd[p] = la[p] * ld[p] + (1.f - la[p]) * accd[p];
-        ld[p] = B.z;
-        dL_dalpha += (B.z - accd[p]) * dpd[p];
-        gv[9] += dchannel_dcolor * dpd[p];
-        dL_dalpha *= T[p];
-        la[p] = alpha;
-        dL_dalpha += (-Tf[p] / (1.f - alpha)) * bgd[p];
-        const float dL_dG = B.y * dL_dalpha;
+      for (int p = 0; p < PPL; ++p) {
+        const bool v = vv[p];
+        const float dx = dxv[p], dy = dyv[p], G = Gv[p], alpha = av[p];
+        const float rinv = 1.f / (1.f - alpha);  // one division serves T and the bg term
+        const float Tn = T[p] * rinv;
+        const float dchannel_dcolor = alpha * Tn;
+        const float a0 = la[p] * lc0[p] + (1.f - la[p]) * acc0[p];
+        const float a1 = la[p] * lc1[p] + (1.f - la[p]) * acc1[p];
+        const float a2 = la[p] * lc2[p] + (1.f - la[p]) * acc2[p];
+        const float ad = la[p] * ld[p] + (1.f - la[p]) * accd[p];
+        float dL_dalpha = (Cc.x - a0) * dp0[p];
+        dL_dalpha += (Cc.y - a1) * dp1[p];
+        dL_dalpha += (Cc.z - a2) * dp2[p];
+        dL_dalpha += (B.z - ad) * dpd[p];
+        dL_dalpha *= Tn;
+        dL_dalpha += (-Tf[p] * rinv) * bgd[p];
+        const float wc = v ? dchannel_dcolor : 0.f;
+        const float wa = v ? dL_dalpha : 0.f;
+        const float wg = B.y * wa;  // dL/dG
         const float gdx = G * dx, gdy = G * dy;
         const float dG_ddelx = -gdx * A.z - gdy * A.w;
         const float dG_ddely = -gdy * B.x - gdx * A.w;
-        gv[0] += dL_dG * dG_ddelx * ddelx_dx;
-        gv[1] += dL_dG * dG_ddely * ddely_dy;
-        gv[2] += -0.5f * gdx * dx * dL_dG;
-        gv[3] += -0.5f * gdx * dy * dL_dG;
-        gv[4] += -0.5f * gdy * dy * dL_dG;
-        gv[5] += G * dL_dalpha;
+        gv[0] += wg * dG_ddelx * ddelx_dx;
+        gv[1] += wg * dG_ddely * ddely_dy;
+        gv[2] += -0.5f * gdx * dx * wg;
+        gv[3] += -0.5f * gdx * dy * wg;
+        gv[4] += -0.5f * gdy * dy * wg;
+        gv[5] += G * wa;
+        gv[6] += wc * dp0[p];
+        gv[7] += wc * dp1[p];
+        gv[8] += wc * dp2[p];
+        gv[9] += wc * dpd[p];
+        T[p] = v ? Tn : T[p];
+        acc0[p] = v ? a0 : acc0[p];
+        acc1[p] = v ? a1 : acc1[p];
+        acc2[p] = v ? a2 : acc2[p];
+        accd[p] = v ? ad : accd[p];
+        lc0[p] = v ? Cc.x : lc0[p];
+        lc1[p] = v ? Cc.y : lc1[p];
+        lc2[p] = v ? Cc.z : lc2[p];
+        ld[p] = v ? B.z : ld[p];
+        la[p] = v ? alpha : la[p];
       }
-      if (__ballot(contrib) != 0) {
-        wave_sum10_store(gv, &sP[j][0]);
-      } else if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 10; ++q) sP[j][q] = 0.f;
-      }
+      wave_sum10_store(gv, &sP[w][j][0]);
     }
     __syncthreads();
-    if (lane < cnt) {
-      const float* s = sP[lane];
-      const size_t k = sK[lane];
+    if (t < cnt) {
+      float s[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) {
+        s[q] = sP[0][t][q];
+#pragma unroll
+        for (int i = 1; i < WAVES; ++i) s[q] += sP[i][t][q];
+      }
+      const size_t k = sK[t];
       partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
       partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
       partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
@@ -462,8 +507,13 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(kBatch), 0, s, ranges, sorted_k, point_g, at<float4>(geom, L.splat),
-                     a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial);
+  static const int ppl = render_ppl("WGSR_BWD_PPL", 1);
+#define WGSR_BWD(PPL_)                                                                                        \
+  hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, sorted_k, point_g,    \
+                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
+                     dL_ddepth, partial)
+  if (ppl == 1) WGSR_BWD(1); else if (ppl == 2) WGSR_BWD(2); else WGSR_BWD(4);
+#undef WGSR_BWD
   return hipGetLastError();
 }
 

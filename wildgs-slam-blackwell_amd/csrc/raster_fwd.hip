@@ -204,108 +204,112 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ key
   ranges[t] = make_uint2(lower((uint32_t)t), lower((uint32_t)t + 1));
 }
 
-// One wave64 = one 16x16 tile; lane l owns the 2x2 pixel quad (l & 7, l >> 3),
-// i.e. four independent front-to-back blends per lane (4-way ILP, and every
-// LDS broadcast of a splat record serves 256 pixels).  Splat records arrive
-// 64 at a time through LDS; the next batch's records are loaded into
-// registers while the current batch is blended (ids two batches ahead).
+// One 16x16 tile per workgroup of 4 / PPL waves; each lane blends PPL pixels
+// (PPL-way ILP; every LDS broadcast of a splat record serves 64 x PPL pixels).
+// Splat records arrive 64 at a time through LDS; wave 0 loads the next batch's
+// records into registers while the current batch is blended (ids two ahead).
 constexpr int kFwdBatch = 64;
 
-__global__ __launch_bounds__(64) void k_render_fwd(const uint2* __restrict__ ranges,
-                                                   const uint32_t* __restrict__ point_g,
-                                                   const float4* __restrict__ splat, int W, int H, int gx,
-                                                   int ntiles, const float* __restrict__ bg,
-                                                   float* __restrict__ out_color, float* __restrict__ out_depth,
-                                                   float* __restrict__ out_opac, float* __restrict__ final_T,
-                                                   uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+template <int PPL>
+__global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
+    float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
+    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+  constexpr uint32_t kAll = (1u << PPL) - 1u;
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
   const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int lane = threadIdx.x;
-  const int x0 = (int)(tile % gx) * kTile + 2 * (lane & 7);
-  const int y0 = (int)(tile / gx) * kTile + 2 * (lane >> 3);
-  float fx[4], fy[4];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
+  float fx[PPL], fy[PPL];
   uint32_t done = 0;  // bit p: pixel p finished (or outside the image)
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+  for (int p = 0; p < PPL; ++p) {
+    int ox, oy;
+    tile_pixel<PPL>(w, lane, p, ox, oy);
+    const int px = tx0 + ox, py = ty0 + oy;
     fx[p] = (float)px;
     fy[p] = (float)py;
     if (!(px < W && py < H)) done |= 1u << p;
   }
   const uint2 range = ranges[tile];
-  float T[4] = {1.f, 1.f, 1.f, 1.f}, C0[4] = {0, 0, 0, 0}, C1[4] = {0, 0, 0, 0}, C2[4] = {0, 0, 0, 0},
-        Dp[4] = {0, 0, 0, 0};
-  uint32_t last[4] = {0, 0, 0, 0};
+  float T[PPL], C0[PPL], C1[PPL], C2[PPL], Dp[PPL];
+  uint32_t last[PPL];
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) { T[p] = 1.f; C0[p] = C1[p] = C2[p] = Dp[p] = 0.f; last[p] = 0; }
 
-  // prefetch pipeline: records of batch b+1 in registers, ids of batch b+2
+  // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
   uint32_t gcur = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (range.x + lane < range.y) {
-    gcur = point_g[range.x + lane];
-    nA = splat[3 * (size_t)gcur];
-    nB = splat[3 * (size_t)gcur + 1];
-    nC = splat[3 * (size_t)gcur + 2];
-  }
-  if (range.x + kFwdBatch + lane < range.y) gnext = point_g[range.x + kFwdBatch + lane];
-
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
-    if (__all(done == 0xFu)) break;
-    __syncthreads();
-    sA[lane] = nA;
-    sB[lane] = nB;
-    sC[lane] = nC;
-    sG[lane] = gcur;
-    __syncthreads();
-    gcur = gnext;
-    if (b0 + kFwdBatch + lane < range.y) {
+  if (t < kFwdBatch) {
+    if (range.x + t < range.y) {
+      gcur = point_g[range.x + t];
       nA = splat[3 * (size_t)gcur];
       nB = splat[3 * (size_t)gcur + 1];
       nC = splat[3 * (size_t)gcur + 2];
     }
-    if (b0 + 2 * kFwdBatch + lane < range.y) gnext = point_g[b0 + 2 * kFwdBatch + lane];
+    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
+  }
 
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
+    if (__syncthreads_count(done == kAll) == (int)blockDim.x) break;
+    if (t < kFwdBatch) {
+      sA[t] = nA;
+      sB[t] = nB;
+      sC[t] = nC;
+      sG[t] = gcur;
+    }
+    __syncthreads();
+    if (t < kFwdBatch) {
+      gcur = gnext;
+      if (b0 + kFwdBatch + t < range.y) {
+        nA = splat[3 * (size_t)gcur];
+        nB = splat[3 * (size_t)gcur + 1];
+        nC = splat[3 * (size_t)gcur + 2];
+      }
+      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
+    }
+    if (__all(done == kAll)) continue;  // this wave is finished; keep the barriers
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
     const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
     for (int j = 0; j < cnt; ++j) {
       const float4 A = sA[j];
       const float4 B = sB[j];
+      const float4 Cc = sC[j];
       uint32_t touched = 0;
+      // PPL independent, branch-free pixel updates (the compiler interleaves them)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        if (done & (1u << p)) continue;
+      for (int p = 0; p < PPL; ++p) {
         const float dx = A.x - fx[p], dy = A.y - fy[p];
         const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-        if (power > 0.0f) continue;
         const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
-        if (alpha < kMinAlpha) continue;
         const float test_T = T[p] * (1.f - alpha);
-        if (test_T < kMinT) {
-          done |= 1u << p;
-          continue;
-        }
-        const float4 Cc = sC[j];
-        const float wgt = alpha * T[p];
+        const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;
+        const bool stop = live && test_T < kMinT;
+        const bool blend = live && !(test_T < kMinT);
+        const float wgt = blend ? alpha * T[p] : 0.f;
         C0[p] += Cc.x * wgt;
         C1[p] += Cc.y * wgt;
         C2[p] += Cc.z * wgt;
         Dp[p] += B.z * wgt;
-        touched += test_T > 0.5f ? 1u : 0u;
-        T[p] = test_T;
-        last[p] = cbase + j;
+        touched += (blend && test_T > 0.5f) ? 1u : 0u;
+        T[p] = blend ? test_T : T[p];
+        last[p] = blend ? cbase + j : last[p];
+        done |= stop ? (1u << p) : 0u;
       }
       // pixels of this wave whose T stays above 0.5 (upstream n_touched)
-      const uint32_t tot = (uint32_t)__popcll(__ballot(touched & 1u)) +
-                           2u * (uint32_t)__popcll(__ballot(touched & 2u)) +
-                           4u * (uint32_t)__popcll(__ballot(touched & 4u));
+      uint32_t tot = (uint32_t)__popcll(__ballot(touched & 1u));
+      if constexpr (PPL > 1) tot += 2u * (uint32_t)__popcll(__ballot(touched & 2u));
+      if constexpr (PPL > 2) tot += 4u * (uint32_t)__popcll(__ballot(touched & 4u));
       if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
-      if (__all(done == 0xFu)) break;
+      if (__all(done == kAll)) break;
     }
   }
   const size_t HW = (size_t)H * W;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int px = x0 + (p & 1), py = y0 + (p >> 1);
+  for (int p = 0; p < PPL; ++p) {
+    const int px = (int)fx[p], py = (int)fy[p];
     if (!(px < W && py < H)) continue;
     const size_t pid = (size_t)py * W + px;
     final_T[pid] = T[p];
@@ -364,9 +368,13 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(kFwdBatch), 0, s, ranges, point_g,
-                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,
-                     final_T, n_contrib, n_touched);
+  static const int ppl = render_ppl("WGSR_FWD_PPL", 1);
+#define WGSR_FWD(PPL_)                                                                                       \
+  hipLaunchKernelGGL(k_render_fwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,             \
+                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,  \
+                     final_T, n_contrib, n_touched)
+  if (ppl == 1) WGSR_FWD(1); else if (ppl == 2) WGSR_FWD(2); else WGSR_FWD(4);
+#undef WGSR_FWD
   return hipGetLastError();
 }
 

@@ -83,10 +83,11 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        const uint32_t* __restrict__ hist,
                                                        const uint32_t* __restrict__ totals,
                                                        uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                       const uint32_t* __restrict__ gtab,
-                                                       uint32_t* __restrict__ gout) {
+                                                       const uint32_t* __restrict__ v2in,
+                                                       uint32_t* __restrict__ v2out) {
   __shared__ uint32_t s_k[kSortTile];
   __shared__ uint32_t s_v[kSortTile];
+  __shared__ uint32_t s_v2[kSortTile];
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
@@ -144,6 +145,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
       const uint32_t loc = s_lbase[d] + s_wcnt[w][d] + rank[j];
       s_k[loc] = key[j];
       s_v[loc] = iota ? (uint32_t)e : vin[e];
+      if (v2in) s_v2[loc] = v2in[e];
     }
   }
   __syncthreads();
@@ -153,9 +155,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     const uint32_t d = (k >> shift) & mask;
     const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
     kout[dst] = k;
-    const uint32_t v = s_v[i];
-    vout[dst] = v;
-    if (gout) gout[dst] = gtab[v];  // fused gather of a per-value table (last pass)
+    vout[dst] = s_v[i];
+    if (v2in) v2out[dst] = s_v2[i];
   }
 }
 
@@ -233,8 +234,7 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, const uint32_t* gather_table,
-                            uint32_t* gathered_out) {
+                            hipStream_t stream, bool* result_in_alt, uint32_t* vals2, uint32_t* vals2_alt) {
   *result_in_alt = false;
   if (n == 0 || end_bit <= begin_bit) {
     if (vals_iota && n > 0) {
@@ -244,19 +244,18 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     return hipSuccess;
   }
   const uint32_t nb = sort_blocks(n);
-  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
+  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt, *wi = vals2, *wo = vals2_alt;
   bool iota = vals_iota;
   for (int shift = begin_bit; shift < end_bit; shift += 8) {
     const int bits = min(8, end_bit - shift);
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, hist);
     hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, hist, nb, totals);
-    const bool last = shift + 8 >= end_bit;
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
-                       bits, nb, hist, totals, ko, vo, last ? gather_table : nullptr,
-                       last ? gathered_out : nullptr);
+                       bits, nb, hist, totals, ko, vo, wi, wo);
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;
+    uint32_t* tw = wi; wi = wo; wo = tw;
     *result_in_alt = !*result_in_alt;
   }
   return hipGetLastError();

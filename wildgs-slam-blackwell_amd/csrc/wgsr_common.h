@@ -119,6 +119,28 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+// Tile geometry of the render kernels: PPL pixels per lane, 4 / PPL waves per
+// 16x16 tile.  PPL 1: wave w owns the 8x8 quadrant (w & 1, w >> 1);
+// PPL 2: wave w owns rows 8w..8w+7, lane = 1x2 pixels; PPL 4: one wave, lane =
+// 2x2 quad.  Returns the pixel offset inside the tile.
+template <int PPL>
+__device__ __forceinline__ void tile_pixel(int w, int lane, int p, int& x, int& y) {
+  const int lx = lane & 7, ly = lane >> 3;
+  if constexpr (PPL == 1) {
+    x = (w & 1) * 8 + lx;
+    y = (w >> 1) * 8 + ly;
+  } else if constexpr (PPL == 2) {
+    x = 2 * lx + p;
+    y = w * 8 + ly;
+  } else {
+    x = 2 * lx + (p & 1);
+    y = 2 * ly + (p >> 1);
+  }
+}
+
+// Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
+int render_ppl(const char* env_name, int dflt);
+
 // ---------------------------------------------------------------------------
 // Small fp32 math (upstream operation order where it matters).  The geometry
 // helpers below are evaluated without FMA contraction so that the per-Gaussian

@@ -11,12 +11,11 @@ namespace wgsr {
 // LSD radix sort on bits [begin_bit, end_bit) (8-bit digits).  Input in
 // keys/vals (vals ignored if vals_iota: value = input position); the result
 // lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
-// If gather_table is given, the last pass also writes
-// gathered_out[i] = gather_table[sorted value i].
+// Optional second payload vals2 (ping-pongs with vals2_alt like vals).
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, const uint32_t* gather_table = nullptr,
-                            uint32_t* gathered_out = nullptr);
+                            hipStream_t stream, bool* result_in_alt, uint32_t* vals2 = nullptr,
+                            uint32_t* vals2_alt = nullptr);
 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
