@@ -282,19 +282,25 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   const ImageLayout IL(a.W, a.H);
   const size_t N = (size_t)num_rendered;
   float4* partial = nullptr;
+  uint8_t* pflag = nullptr;
   if (N > 0) {
-    partial = static_cast<float4*>(call_alloc(scratch_alloc, ctx, 48 * N));
-    if (!partial) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
+    // 48-byte partial record per pair + 1-byte "record written" flag
+    const size_t rec_bytes = align256(48 * N);
+    void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + align256(N));
+    if (!scratch) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
+    partial = static_cast<float4*>(scratch);
+    pflag = at<uint8_t>(scratch, rec_bytes);
+    HIPCHK(hipMemsetAsync(pflag, 0, N, s));
     const BinLayout BL(N);
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
                                   at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g), geom,
                                   at<float>(image, IL.final_T),
-                                  at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, s));
+                                  at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
   }
   StageTimer T(8, s);
-  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
                                dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
   return WGSR_OK;
 }

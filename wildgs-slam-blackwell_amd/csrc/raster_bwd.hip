@@ -7,9 +7,10 @@
 //               MI355X -- each lane sums its four pixels in registers, one
 //               packed wave reduction covers the whole tile, and the tile
 //               writes ONE 48-byte partial record per (Gaussian, tile) pair
+//               that actually received gradient (plus a 1-byte slot flag),
 //               into that pair's duplicate slot.  No atomics, deterministic.
-//   gauss_bwd   one lane per Gaussian: sums its contiguous slot range of
-//               partial records (fixed order -> bitwise reproducible), then
+//   gauss_bwd   one lane per Gaussian: sums the flagged records of its
+//               contiguous slot range (fixed order -> bitwise reproducible), then
 //               runs cov2D -> cov3D -> (scale, rotation), SH, projection,
 //               depth and pose (w-pose dL/dtau) backward in registers and
 //               writes every output of _C.rasterize_gaussians_backward once.
@@ -41,11 +42,13 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ point_g,
     const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
-    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial) {
+    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
+    uint8_t* __restrict__ pflag) {
   constexpr int WAVES = 4 / PPL;
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sK[kBatch];
   __shared__ float sP[WAVES][kBatch][11];
+  __shared__ uint32_t sHit[WAVES][kBatch];
   __shared__ uint32_t s_max[WAVES];
   const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -89,14 +92,10 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) m = max(m, s_max[i]);
   }
+  // entries behind every pixel's last contributor get no record: their slot
+  // flags stay 0 (zeroed before the launch), and so does every entry no pixel
+  // of the tile receives gradient from -- typically > 90 % of all pairs
   const uint32_t end = range.x + m;
-  for (uint32_t i = end + t; i < range.y; i += 64 * WAVES) {
-    const uint32_t k = sorted_k[i];
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    partial[3 * (size_t)k] = z;
-    partial[3 * (size_t)k + 1] = z;
-    partial[3 * (size_t)k + 2] = z;
-  }
 
   // prefetch pipeline (wave 0, back to front): records of the next batch in
   // registers, ids one batch further
@@ -159,13 +158,11 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
         vv[p] = cidx < last[p] && power <= 0.0f && av[p] >= kMinAlpha;
         any |= vv[p];
       }
-      if (!__any(any)) {  // no pixel of this wave: zero partial, skip the heavy part
-        if (lane == 0) {
-#pragma unroll
-          for (int q = 0; q < 10; ++q) sP[w][j][q] = 0.f;
-        }
+      if (!__any(any)) {  // no pixel of this wave: no partial, skip the heavy part
+        if (lane == 0) sHit[w][j] = 0;
         continue;
       }
+      if (lane == 0) sHit[w][j] = 1;
       // phase 2: PPL independent, branch-free pixel updates (selects)
       const float4 Cc = sC[j];
       float gv[10];
@@ -219,17 +216,23 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     }
     __syncthreads();
     if (t < cnt) {
-      float s[10];
+      uint32_t hit = 0;
 #pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        s[q] = sP[0][t][q];
+      for (int i = 0; i < WAVES; ++i) hit |= sHit[i][t];
+      if (hit) {
+        float s[10];
 #pragma unroll
-        for (int i = 1; i < WAVES; ++i) s[q] += sP[i][t][q];
+        for (int q = 0; q < 10; ++q) {
+          s[q] = 0.f;
+#pragma unroll
+          for (int i = 0; i < WAVES; ++i) s[q] += sHit[i][t] ? sP[i][t][q] : 0.f;
+        }
+        const size_t k = sK[t];
+        partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
+        partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
+        partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
+        pflag[k] = 1;
       }
-      const size_t k = sK[t];
-      partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
-      partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
-      partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
     }
   }
 }
@@ -314,6 +317,7 @@ __device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t 
 __global__ __launch_bounds__(256) void k_gauss_bwd(
     int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
     const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const uint8_t* __restrict__ pflag,
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
     const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
@@ -332,17 +336,45 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     o_opac[i] = 0.f;
     return;
   }
-  // ---- sum this Gaussian's per-tile partial records (fixed slot order)
+  // parameters first: their loads overlap the partial-record walk below
+  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  f3 sv = mk3(0.f, 0.f, 0.f);
+  float cv[6];
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
+  } else {
+    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
+    q = reinterpret_cast<const float4*>(rots)[i];
+  }
+  // ---- sum this Gaussian's flagged per-tile partial records (fixed slot
+  // order).  Flags are read 4 slots per word, 32 slots per chunk, with
+  // independent loads, so a large Gaussian does not serialise its wave.
   float g[10];
 #pragma unroll
-  for (int q = 0; q < 10; ++q) g[q] = 0.f;
+  for (int qq = 0; qq < 10; ++qq) g[qq] = 0.f;
   {
-    const size_t s0 = slot_start[i], n = tiles[i];
-    for (size_t k = s0; k < s0 + n; ++k) {
-      const float4 a = partial[3 * k], b = partial[3 * k + 1], c = partial[3 * k + 2];
-      g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
-      g[4] += b.x; g[5] += b.y; g[6] += b.z; g[7] += b.w;
-      g[8] += c.x; g[9] += c.y;
+    const uint32_t s0 = slot_start[i], s1 = s0 + tiles[i];
+    const uint32_t* fw = reinterpret_cast<const uint32_t*>(pflag);
+    for (uint32_t base = s0 & ~3u; base < s1; base += 32) {
+      uint32_t wd[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) wd[w] = (base + 4 * w < s1) ? fw[(base >> 2) + w] : 0u;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        uint32_t bits = wd[w];
+        while (bits) {
+          const int b = __builtin_ctz(bits) >> 3;  // byte index with a nonzero flag
+          bits &= ~(0xFFu << (8 * b));
+          const uint32_t k = base + 4 * w + b;
+          if (k < s0 || k >= s1) continue;
+          const float4 a = partial[3 * (size_t)k], bb = partial[3 * (size_t)k + 1], c = partial[3 * (size_t)k + 2];
+          g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
+          g[4] += bb.x; g[5] += bb.y; g[6] += bb.z; g[7] += bb.w;
+          g[8] += c.x; g[9] += c.y;
+        }
+      }
     }
   }
   o_m2d[i3] = g[0]; o_m2d[i3 + 1] = g[1]; o_m2d[i3 + 2] = 0.f;
@@ -353,19 +385,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
   Cam c;
   load_cam(c, viewm, projm, W, H, tanx, tany);
   // ---- cov2D backward (upstream computeCov2DCUDA)
-  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
   const f3 t = xform43(c.view, mean);
-  float cv[6];
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  f3 sv = mk3(0.f, 0.f, 0.f);
-  if (cov_pre) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
-  } else {
-    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
-    q = reinterpret_cast<const float4*>(rots)[i];
-    cov3d_from(sv, scale_mod, q, cv);
-  }
+  if (!cov_pre) cov3d_from(sv, scale_mod, q, cv);
   float S[3][3];
   sym3(cv, S);
   float T[2][3];
@@ -503,7 +524,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
                              const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
-                             float4* partial, hipStream_t s) {
+                             float4* partial, uint8_t* pflag, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
@@ -511,21 +532,21 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
 #define WGSR_BWD(PPL_)                                                                                        \
   hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, sorted_k, point_g,    \
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
-                     dL_ddepth, partial)
+                     dL_ddepth, partial, pflag)
   if (ppl == 1) WGSR_BWD(1); else if (ppl == 2) WGSR_BWD(2); else WGSR_BWD(4);
 #undef WGSR_BWD
   return hipGetLastError();
 }
 
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
-                            const float4* partial, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
-                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                            float* dL_drot, float* dL_dtau, hipStream_t s) {
+                            const float4* partial, const uint8_t* pflag, float* dL_dmeans2D, float* dL_dcolors,
+                            float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                            float* dL_dscales, float* dL_drot, float* dL_dtau, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, a.D, a.M, radii,
                      at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
-                     partial, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
+                     partial, pflag, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
                      dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
                      dL_dscales, dL_drot, dL_dtau);
