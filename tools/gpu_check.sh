@@ -25,6 +25,8 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_fetch -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_fetch.err); rc=$? ;;
     pmc_write)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_write -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_write.err); rc=$? ;;
+    pmc_sq)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq.err); rc=$? ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   echo "$s rc=$rc" | tee -a $OUT/steps.log

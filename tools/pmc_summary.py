@@ -1,0 +1,96 @@
+#!/usr/bin/env python
+"""Summarise rocprofv3 --pmc runs of bench.py per kernel.
+
+HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane)
+coalesced reads, so the corrected read bytes are 2 x FETCH_SIZE (reported
+next to the raw value; other access widths are uncalibrated).  Counters come
+from separate passes (FETCH_SIZE and WRITE_SIZE do not fit one pass).
+
+usage: python tools/pmc_summary.py gpurun_out [out.json]
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+STAGE_OF = {
+    "k_preprocess": "preprocess", "k_duplicate": "duplicate", "k_ranges": "ranges",
+    "k_render_fwd": "render_fwd", "k_render_bwd": "render_bwd", "k_gauss_bwd": "gauss_bwd",
+    "k_scan_reduce": "offsets_scan", "k_scan_bsum": "offsets_scan", "k_scan_down": "offsets_scan",
+}
+
+
+def short(name):
+    name = name.replace("wgsr::(anonymous namespace)::", "")
+    return re.split(r"[(<]", name, maxsplit=1)[0]
+
+
+def load(path):
+    """-> {(kernel, grid): {counter: [values per dispatch]}}"""
+    out = defaultdict(lambda: defaultdict(list))
+    if not os.path.exists(path):
+        return out
+    for r in csv.DictReader(open(path)):
+        key = (short(r["Kernel_Name"]), int(r["Grid_Size"]))
+        out[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def stage_for(kernel, grid, P_grid):
+    if kernel in STAGE_OF:
+        return STAGE_OF[kernel]
+    if kernel.startswith("k_radix"):
+        # depth sort passes run over P keys (grid ~ P/4096 workgroups)
+        return "depth_sort" if grid <= P_grid else "tile_sort"
+    return None
+
+
+def main():
+    root = sys.argv[1]
+    out_path = sys.argv[2] if len(sys.argv) > 2 else None
+    fetch = load(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"))
+    write = load(os.path.join(root, "pmc_write", "run_counter_collection.csv"))
+    sq = load(os.path.join(root, "pmc_sq", "run_counter_collection.csv"))
+    keys = sorted(set(fetch) | set(write) | set(sq))
+    # grid size of the depth-sort radix kernels: the smallest radix scatter grid
+    rg = [g for (k, g) in keys if k == "k_radix_scatter"]
+    P_grid = min(rg) if rg else 0
+    rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_launch": 0.0, "launch_kinds": []})
+    hdr = (f"{'kernel':18s} {'grid':>9s} {'FETCH_KB':>10s} {'WRITE_KB':>10s} {'HBM_MB*':>9s} "
+           f"{'VALU/wave':>9s} {'VMEM/wave':>9s} {'LDS/wave':>8s} {'wait%':>6s}")
+    print(hdr)
+    for key in keys:
+        k, g = key
+        avg = lambda d, c: (sum(d[key][c]) / len(d[key][c])) if d[key].get(c) else None  # noqa: E731
+        f = avg(fetch, "FETCH_SIZE")
+        w = avg(write, "WRITE_SIZE")
+        waves = avg(sq, "SQ_WAVES")
+        valu = avg(sq, "SQ_INSTS_VALU")
+        vrd, vwr = avg(sq, "SQ_INSTS_VMEM_RD"), avg(sq, "SQ_INSTS_VMEM_WR")
+        lds = avg(sq, "SQ_INSTS_LDS")
+        cyc, wait = avg(sq, "SQ_WAVE_CYCLES"), avg(sq, "SQ_WAIT_ANY")
+        hbm = ((2 * f if f is not None else 0) + (w or 0)) * 1024
+        per = lambda x: (x / waves) if (x is not None and waves) else float("nan")  # noqa: E731
+        print(f"{k:18s} {g:9d} {f if f is not None else float('nan'):10.0f} "
+              f"{w if w is not None else float('nan'):10.0f} {hbm / 1e6:9.1f} {per(valu):9.0f} "
+              f"{per((vrd or 0) + (vwr or 0)):9.1f} {per(lds):8.1f} "
+              f"{100 * wait / cyc if (wait and cyc) else float('nan'):6.1f}")
+        rows.append(dict(kernel=k, grid=g, fetch_kib=f, write_kib=w, hbm_bytes=hbm, waves=waves,
+                         valu_per_wave=per(valu), vmem_per_wave=per((vrd or 0) + (vwr or 0)),
+                         lds_per_wave=per(lds), wait_frac=(wait / cyc) if (wait and cyc) else None))
+        st = stage_for(k, g, P_grid)
+        if st:
+            stages[st]["hbm_bytes_per_launch"] += hbm
+            stages[st]["launch_kinds"].append(k)
+    print("* HBM_MB = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 FETCH correction)")
+    if out_path:
+        json.dump({"source": "profiles/r01/pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)", "note": "per-dispatch averages; radix stage bytes summed over "
+                   "one pass's kernels (multiply by passes for the stage)",
+                   "kernels": rows, "stages": stages}, open(out_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
