@@ -24,7 +24,7 @@ STAGE_OF = {
 
 
 def short(name):
-    name = name.replace("wgsr::(anonymous namespace)::", "")
+    name = name.replace("wgsr::(anonymous namespace)::", "").replace("void ", "")
     return re.split(r"[(<]", name, maxsplit=1)[0]
 
 

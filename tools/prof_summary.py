@@ -9,7 +9,7 @@ import sys
 
 
 def short(name):
-    name = name.replace("wgsr::(anonymous namespace)::", "")
+    name = name.replace("wgsr::(anonymous namespace)::", "").replace("void ", "")
     return re.split(r"[(<]", name, maxsplit=1)[0]
 
 

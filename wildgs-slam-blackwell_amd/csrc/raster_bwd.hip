@@ -57,6 +57,8 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
   const uint2 range = ranges[tile];
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+  int wx0, wx1, wy0, wy1;
+  wave_box<PPL>(w, tx0, ty0, wx0, wx1, wy0, wy1);
 
   float fx[PPL], fy[PPL], Tf[PPL], T[PPL], dp0[PPL], dp1[PPL], dp2[PPL], dpd[PPL], bgd[PPL];
   float acc0[PPL], acc1[PPL], acc2[PPL], accd[PPL], la[PPL], lc0[PPL], lc1[PPL], lc2[PPL], ld[PPL];
@@ -140,10 +142,17 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
       }
     }
     const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
-    for (int j = 0; j < cnt; ++j) {
+    // lane j tests entry j's reach box against this wave's pixels; the wave
+    // walks only the entries that can touch it, back to front (a scalar bit loop)
+    sHit[w][lane] = 0;
+    uint64_t todo = __ballot(lane < cnt && reach_hits(sB[lane].w, sC[lane].w, wx0, wx1, wy0, wy1));
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
       const uint32_t cidx = cfirst - j;
       const float4 A = sA[j];
       const float4 B = sB[j];
+      const float4 Cc = sC[j];
       // phase 1: which of this lane's pixels does entry j reach? (cheap)
       float dxv[PPL], dyv[PPL], Gv[PPL], av[PPL];
       bool vv[PPL];
@@ -158,13 +167,9 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
         vv[p] = cidx < last[p] && power <= 0.0f && av[p] >= kMinAlpha;
         any |= vv[p];
       }
-      if (!__any(any)) {  // no pixel of this wave: no partial, skip the heavy part
-        if (lane == 0) sHit[w][j] = 0;
-        continue;
-      }
+      if (!__any(any)) continue;  // no pixel of this wave: no partial, skip the heavy part
       if (lane == 0) sHit[w][j] = 1;
       // phase 2: PPL independent, branch-free pixel updates (selects)
-      const float4 Cc = sC[j];
       float gv[10];
 #pragma unroll
       for (int q = 0; q < 10; ++q) gv[q] = 0.f;
@@ -172,7 +177,8 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
       for (int p = 0; p < PPL; ++p) {
         const bool v = vv[p];
         const float dx = dxv[p], dy = dyv[p], G = Gv[p], alpha = av[p];
-        const float rinv = 1.f / (1.f - alpha);  // one division serves T and the bg term
+        // one v_rcp_f32 serves T and the bg term (alpha <= 0.99 keeps 1 - alpha >= 0.01)
+        const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
         const float Tn = T[p] * rinv;
         const float dchannel_dcolor = alpha * Tn;
         const float a0 = la[p] * lc0[p] + (1.f - la[p]) * acc0[p];

@@ -138,6 +138,26 @@ __device__ __forceinline__ void tile_pixel(int w, int lane, int p, int& x, int& 
   }
 }
 
+// Pixel box [x0, x1] x [y0, y1] covered by wave w of a tile (tile_pixel).
+template <int PPL>
+__device__ __forceinline__ void wave_box(int w, int tx0, int ty0, int& x0, int& x1, int& y0, int& y1) {
+  if constexpr (PPL == 1) {
+    x0 = tx0 + (w & 1) * 8; y0 = ty0 + (w >> 1) * 8; x1 = x0 + 7; y1 = y0 + 7;
+  } else if constexpr (PPL == 2) {
+    x0 = tx0; y0 = ty0 + w * 8; x1 = x0 + 15; y1 = y0 + 7;
+  } else {
+    x0 = tx0; y0 = ty0; x1 = x0 + 15; y1 = y0 + 15;
+  }
+}
+
+// Does a splat's reach box (packed x0 | x1 << 16, y0 | y1 << 16 in the spare
+// lanes of its record) meet the pixel box [x0, x1] x [y0, y1]?  Wave-uniform.
+__device__ __forceinline__ bool reach_hits(float bxf, float byf, int x0, int x1, int y0, int y1) {
+  const uint32_t bx = __float_as_uint(bxf), by = __float_as_uint(byf);
+  return (int)(bx & 0xFFFFu) <= x1 && (int)(bx >> 16) >= x0 && (int)(by & 0xFFFFu) <= y1 &&
+         (int)(by >> 16) >= y0;
+}
+
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
 int render_ppl(const char* env_name, int dflt);
 
