@@ -77,6 +77,13 @@ __global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hi
   if (t == 0) totals[blockIdx.x] = tot;
 }
 
+// Stable scatter of one pass.  All of a thread's keys and payloads are loaded
+// up front (in flight while ranking); ranks come from LDS atomics-with-return
+// issued by each peer group's lowest lane (a wave's LDS atomics execute in
+// issue order, so the returned counts are the sequential ones and the 16
+// atomics pipeline instead of forming a read-wait-write chain); keys and
+// payloads are staged through one 16 KB LDS buffer in digit order so that each
+// digit's run leaves as contiguous stores (small LDS -> high occupancy).
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ kin,
                                                        const uint32_t* __restrict__ vin, int iota, uint32_t n,
                                                        int shift, int bits, uint32_t nb,
@@ -85,45 +92,43 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
                                                        uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                        const uint32_t* __restrict__ v2in,
                                                        uint32_t* __restrict__ v2out) {
-  __shared__ uint32_t s_k[kSortTile];
-  __shared__ uint32_t s_v[kSortTile];
-  __shared__ uint32_t s_v2[kSortTile];
+  __shared__ uint32_t s_buf[kSortTile];
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
   __shared__ uint32_t s_tmp[4];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t mask = (1u << bits) - 1u;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
-  // global base of digit t for this block: scan of the digit totals + row prefix
-  {
-    const uint32_t tot = totals[t];
-    const uint32_t ex = block_excl_scan256(tot, s_tmp, nullptr);
-    s_gbase[t] = ex + hist[(size_t)t * nb + blockIdx.x];
-  }
-  __syncthreads();
-
-  uint32_t key[kSortItems];
-  uint32_t rank[kSortItems];
   const size_t blk0 = (size_t)blockIdx.x * kSortTile;
   const size_t base = blk0 + (size_t)w * (64 * kSortItems);
+  uint32_t key[kSortItems], val[kSortItems], val2[kSortItems], rank[kSortItems];
 #pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     key[j] = valid ? kin[e] : 0u;
+    val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
+    val2[j] = (v2in && valid) ? v2in[e] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
+  // global base of digit t for this block: scan of the digit totals + row prefix
+  {
+    const uint32_t tot = totals[t];
+    const uint32_t ex = block_excl_scan256(tot, s_tmp, nullptr);  // (its barriers publish s_wcnt = 0)
+    s_gbase[t] = ex + hist[(size_t)t * nb + blockIdx.x];
+  }
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
     const uint32_t d = (key[j] >> shift) & mask;
-    const uint64_t active = __ballot(valid);
-    rank[j] = 0;
-    if (active != 0) {
-      const uint64_t peers = match_digit(d, bits, active);
-      const uint32_t below = lanes_below(peers);
-      uint32_t old = 0;
-      if (valid) old = s_wcnt[w][d];
-      if (valid && below == 0) s_wcnt[w][d] = old + (uint32_t)__popcll(peers);
-      rank[j] = old + below;
-    }
+    const uint64_t peers = match_digit(d, bits, __ballot(valid));
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    uint32_t old = 0;
+    if (valid && lane == leader) old = atomicAdd(&s_wcnt[w][d], (uint32_t)__popcll(peers));
+    old = (uint32_t)__shfl((int)old, leader & 63, 64);
+    rank[j] = old + lanes_below(peers);
   }
   __syncthreads();
   {
@@ -140,23 +145,44 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
 #pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
-    if (e < n) {
-      const uint32_t d = (key[j] >> shift) & mask;
-      const uint32_t loc = s_lbase[d] + s_wcnt[w][d] + rank[j];
-      s_k[loc] = key[j];
-      s_v[loc] = iota ? (uint32_t)e : vin[e];
-      if (v2in) s_v2[loc] = v2in[e];
-    }
+    const uint32_t d = (key[j] >> shift) & mask;
+    rank[j] = s_lbase[d] + s_wcnt[w][d] + rank[j];  // block-local slot in digit order
+    if (e < n) s_buf[rank[j]] = key[j];
   }
   __syncthreads();
   const uint32_t cnt = (uint32_t)min((size_t)kSortTile, (size_t)n - blk0);
-  for (uint32_t i = t; i < cnt; i += 256) {
-    const uint32_t k = s_k[i];
-    const uint32_t d = (k >> shift) & mask;
-    const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
-    kout[dst] = k;
-    vout[dst] = s_v[i];
-    if (v2in) v2out[dst] = s_v2[i];
+  uint32_t dst[kSortItems];
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint32_t i = (uint32_t)t + 256u * r;
+    if (i < cnt) {
+      const uint32_t k = s_buf[i];
+      const uint32_t d = (k >> shift) & mask;
+      dst[r] = s_gbase[d] + (i - s_lbase[d]);
+      kout[dst[r]] = k;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j)
+    if (base + (size_t)j * 64 + lane < n) s_buf[rank[j]] = val[j];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortItems; ++r) {
+    const uint32_t i = (uint32_t)t + 256u * r;
+    if (i < cnt) vout[dst[r]] = s_buf[i];
+  }
+  if (v2in) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSortItems; ++j)
+      if (base + (size_t)j * 64 + lane < n) s_buf[rank[j]] = val2[j];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortItems; ++r) {
+      const uint32_t i = (uint32_t)t + 256u * r;
+      if (i < cnt) v2out[dst[r]] = s_buf[i];
+    }
   }
 }
 
