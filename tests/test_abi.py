@@ -39,7 +39,7 @@ def test_state_buffer_sizes_scale():
     g1, g2 = L.wgsr_geometry_bytes(1000), L.wgsr_geometry_bytes(2000)
     assert g2 > g1 and g1 >= 48 * 1000
     assert L.wgsr_image_bytes(1920, 1080) >= 8 * 1920 * 1080
-    assert L.wgsr_binning_bytes(10_000, 64, 64) >= 20 * 10_000
+    assert L.wgsr_binning_bytes(10_000, 64, 64) >= 16 * 10_000
 
 
 def test_settings_tuple_is_upstream():

@@ -230,7 +230,6 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   void* binning = call_alloc(binning_alloc, ctx, BL.total);
   if (!binning && BL.total) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   const uint32_t* sorted_keys = nullptr;
-  const uint32_t* sorted_k = nullptr;
   const uint32_t* sorted_g = nullptr;  // tile lists (Gaussian ids)
   if (N > 0) {
     { StageTimer T(3, s);
@@ -239,16 +238,15 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     bool talt = false;
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
-                                 at<uint32_t>(binning, BL.val), at<uint32_t>(binning, BL.val_alt), true, N, 0,
+                                 at<uint32_t>(binning, BL.slot_g), at<uint32_t>(binning, BL.point_g), false, N, 0,
                                  tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
-                                 at<uint32_t>(binning, BL.totals), s, &talt, at<uint32_t>(binning, BL.slot_g),
-                                 at<uint32_t>(binning, BL.point_g))); }
-    // the Gaussian ids ride along as a second payload: sorted lists end in
-    // point_g after an odd number of passes, in slot_g after an even one
+                                 at<uint32_t>(binning, BL.totals), s, &talt)); }
+    // the Gaussian ids are the payload: sorted lists end in point_g after an
+    // odd number of passes, in slot_g after an even one.  The backward
+    // recomputes each pair's duplicate slot from (Gaussian, tile) instead of
+    // carrying it through the sort.
     if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
     sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
-    sorted_k = at<uint32_t>(binning, talt ? BL.val_alt : BL.val);
-    (void)sorted_k;  // slot of each sorted pair: read by the backward
     sorted_g = at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g);
   }
   uint2* ranges = at<uint2>(image, IL.ranges);
@@ -294,8 +292,8 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
     const BinLayout BL(N);
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
-    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.val_alt : BL.val),
-                                  at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g), geom,
+    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g),
+                                  geom,
                                   at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
   }

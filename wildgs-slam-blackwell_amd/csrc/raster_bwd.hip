@@ -39,14 +39,14 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 // added through LDS, and thread j writes entry j's 48-byte record.
 template <int PPL>
 __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ sorted_k, const uint32_t* __restrict__ point_g,
-    const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const ushort4* __restrict__ rect, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
     uint8_t* __restrict__ pflag) {
   constexpr int WAVES = 4 / PPL;
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
-  __shared__ uint32_t sK[kBatch];
+  __shared__ uint32_t sG[kBatch];
   __shared__ float sP[WAVES][kBatch][11];
   __shared__ uint32_t sHit[WAVES][kBatch];
   __shared__ uint32_t s_max[WAVES];
@@ -101,21 +101,16 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 
   // prefetch pipeline (wave 0, back to front): records of the next batch in
   // registers, ids one batch further
-  uint32_t kcur = 0, gcur = 0, knext = 0, gnext = 0;
+  uint32_t gcur = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
   if (t < kBatch) {
     if (end >= range.x + 1 + t) {
-      const uint32_t idx = end - 1 - t;
-      kcur = sorted_k[idx];
-      gcur = point_g[idx];
+      gcur = point_g[end - 1 - t];
       nA = splat[3 * (size_t)gcur];
       nB = splat[3 * (size_t)gcur + 1];
       nC = splat[3 * (size_t)gcur + 2];
     }
-    if (end >= range.x + 1 + kBatch + t) {
-      knext = sorted_k[end - 1 - kBatch - t];
-      gnext = point_g[end - 1 - kBatch - t];
-    }
+    if (end >= range.x + 1 + kBatch + t) gnext = point_g[end - 1 - kBatch - t];
   }
 
   for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
@@ -125,21 +120,17 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
       sA[t] = nA;
       sB[t] = nB;
       sC[t] = nC;
-      sK[t] = kcur;
+      sG[t] = gcur;
     }
     __syncthreads();
     if (t < kBatch) {
-      kcur = knext;
       gcur = gnext;
       if (b_end >= range.x + 1 + kBatch + t) {
         nA = splat[3 * (size_t)gcur];
         nB = splat[3 * (size_t)gcur + 1];
         nC = splat[3 * (size_t)gcur + 2];
       }
-      if (b_end >= range.x + 1 + 2 * kBatch + t) {
-        knext = sorted_k[b_end - 1 - 2 * kBatch - t];
-        gnext = point_g[b_end - 1 - 2 * kBatch - t];
-      }
+      if (b_end >= range.x + 1 + 2 * kBatch + t) gnext = point_g[b_end - 1 - 2 * kBatch - t];
     }
     const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
     // lane j tests entry j's reach box against this wave's pixels; the wave
@@ -233,7 +224,12 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 #pragma unroll
           for (int i = 0; i < WAVES; ++i) s[q] += sHit[i][t] ? sP[i][t][q] : 0.f;
         }
-        const size_t k = sK[t];
+        // duplicate slot of (Gaussian, this tile): its first slot plus the
+        // tile's row-major index in the Gaussian's tile rectangle (k_duplicate)
+        const uint32_t gid = sG[t];
+        const ushort4 rc = rect[gid];
+        const size_t k = slot_start[gid] + (uint32_t)(tile / gx - rc.y) * (uint32_t)(rc.z - rc.x) +
+                         (uint32_t)(tile % gx - rc.x);
         partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
         partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
         partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
@@ -245,36 +241,24 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 
 __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]); }
 
-// upstream computeColorFromSH backward: writes dL/dsh[0..K), returns dL/dmean
-__device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
+// upstream computeColorFromSH backward; returns dL/dmean and writes dL/dsh
+// for all M stored coefficients (zeros past K).  `sh` and `dsh` may be the
+// same row (the LDS-staged coefficients): every read precedes the writes.
+__device__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
   const f3 dir_orig = sub3(pos, campos);
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
   dRGB.x *= (cbits & 1u) ? 0.f : 1.f;
   dRGB.y *= (cbits & 2u) ? 0.f : 1.f;
   dRGB.z *= (cbits & 4u) ? 0.f : 1.f;
-  auto put = [&](int k, float wgt) {
-    dsh[3 * k] = wgt * dRGB.x;
-    dsh[3 * k + 1] = wgt * dRGB.y;
-    dsh[3 * k + 2] = wgt * dRGB.z;
-  };
   f3 dx = mk3(0.f, 0.f, 0.f), dy = dx, dz = dx;
   const float x = dir.x, y = dir.y, z = dir.z;
-  put(0, SH_C0);
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
   if (deg > 0) {
-    put(1, -SH_C1 * y);
-    put(2, SH_C1 * z);
-    put(3, -SH_C1 * x);
     dx = scl3(-SH_C1, ldc(sh, 3));
     dy = scl3(-SH_C1, ldc(sh, 1));
     dz = scl3(SH_C1, ldc(sh, 2));
     if (deg > 1) {
-      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-      put(4, SH_C2[0] * xy);
-      put(5, SH_C2[1] * yz);
-      put(6, SH_C2[2] * (2.f * zz - xx - yy));
-      put(7, SH_C2[3] * xz);
-      put(8, SH_C2[4] * (xx - yy));
       dx = add3(dx, add3(add3(scl3(SH_C2[0] * y, ldc(sh, 4)), scl3(SH_C2[2] * 2.f * -x, ldc(sh, 6))),
                          add3(scl3(SH_C2[3] * z, ldc(sh, 7)), scl3(SH_C2[4] * 2.f * x, ldc(sh, 8)))));
       dy = add3(dy, add3(add3(scl3(SH_C2[0] * x, ldc(sh, 4)), scl3(SH_C2[1] * z, ldc(sh, 5))),
@@ -282,13 +266,6 @@ __device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t 
       dz = add3(dz, add3(add3(scl3(SH_C2[1] * y, ldc(sh, 5)), scl3(SH_C2[2] * 2.f * 2.f * z, ldc(sh, 6))),
                          scl3(SH_C2[3] * x, ldc(sh, 7))));
       if (deg > 2) {
-        put(9, SH_C3[0] * y * (3.f * xx - yy));
-        put(10, SH_C3[1] * xy * z);
-        put(11, SH_C3[2] * y * (4.f * zz - xx - yy));
-        put(12, SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy));
-        put(13, SH_C3[4] * x * (4.f * zz - xx - yy));
-        put(14, SH_C3[5] * z * (xx - yy));
-        put(15, SH_C3[6] * x * (xx - 3.f * yy));
         dx = add3(dx, scl3(SH_C3[0] * 3.f * 2.f * xy, ldc(sh, 9)));
         dx = add3(dx, scl3(SH_C3[1] * yz, ldc(sh, 10)));
         dx = add3(dx, scl3(SH_C3[2] * -2.f * xy, ldc(sh, 11)));
@@ -311,6 +288,34 @@ __device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t 
       }
     }
   }
+  auto put = [&](int k, float wgt) {
+    dsh[3 * k] = wgt * dRGB.x;
+    dsh[3 * k + 1] = wgt * dRGB.y;
+    dsh[3 * k + 2] = wgt * dRGB.z;
+  };
+  put(0, SH_C0);
+  if (deg > 0) {
+    put(1, -SH_C1 * y);
+    put(2, SH_C1 * z);
+    put(3, -SH_C1 * x);
+    if (deg > 1) {
+      put(4, SH_C2[0] * xy);
+      put(5, SH_C2[1] * yz);
+      put(6, SH_C2[2] * (2.f * zz - xx - yy));
+      put(7, SH_C2[3] * xz);
+      put(8, SH_C2[4] * (xx - yy));
+      if (deg > 2) {
+        put(9, SH_C3[0] * y * (3.f * xx - yy));
+        put(10, SH_C3[1] * xy * z);
+        put(11, SH_C3[2] * y * (4.f * zz - xx - yy));
+        put(12, SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy));
+        put(13, SH_C3[4] * x * (4.f * zz - xx - yy));
+        put(14, SH_C3[5] * z * (xx - yy));
+        put(15, SH_C3[6] * x * (xx - 3.f * yy));
+      }
+    }
+  }
+  for (int k = 3 * (deg + 1) * (deg + 1); k < 3 * M; ++k) dsh[k] = 0.f;
   const f3 dL_ddir = mk3(dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB));
   const f3 v = dir_orig;
   const float sum2 = dot3(v, v);
@@ -320,25 +325,66 @@ __device__ f3 sh_backward(int deg, const float* sh, f3 pos, f3 campos, uint32_t 
              (-v.x * v.z * dL_ddir.x - v.y * v.z * dL_ddir.y + (sum2 - v.z * v.z) * dL_ddir.z) * invsum32);
 }
 
-__global__ __launch_bounds__(256) void k_gauss_bwd(
-    int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
-    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
-    const uint8_t* __restrict__ pflag,
+// Sum Gaussian i's flagged per-tile partial records in fixed slot order.
+// Flags are read 32 slots per chunk (8 independent word loads) and packed to a
+// bit mask; records are then fetched four at a time with independent loads, so
+// a Gaussian with many hit tiles costs few round trips, not one per record.
+__device__ __forceinline__ void sum_partials(uint32_t s0, uint32_t s1, const uint8_t* __restrict__ pflag,
+                                             const float4* __restrict__ partial, float g[10]) {
+#pragma unroll
+  for (int q = 0; q < 10; ++q) g[q] = 0.f;
+  const uint32_t* fw = reinterpret_cast<const uint32_t*>(pflag);
+  for (uint32_t base = s0 & ~3u; base < s1; base += 32) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      uint32_t x = (base + 4 * w < s1) ? fw[(base >> 2) + w] : 0u;
+      x &= 0x01010101u;  // flags are 0 / 1 bytes
+      m |= ((x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu) << (4 * w);
+    }
+    if (base < s0) m &= ~0u << (s0 - base);
+    if (s1 - base < 32) m &= (1u << (s1 - base)) - 1u;
+    while (m) {
+      uint32_t kk[4];
+      bool v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = m != 0;
+        kk[u] = base + (v[u] ? (uint32_t)__builtin_ctz(m) : 0u);
+        m &= m - 1u;
+      }
+      float4 r[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int h = 0; h < 3; ++h) r[u][h] = v[u] ? partial[3 * (size_t)kk[u] + h] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!v[u]) continue;
+        g[0] += r[u][0].x; g[1] += r[u][0].y; g[2] += r[u][0].z; g[3] += r[u][0].w;
+        g[4] += r[u][1].x; g[5] += r[u][1].y; g[6] += r[u][1].z; g[7] += r[u][1].w;
+        g[8] += r[u][2].x; g[9] += r[u][2].y;
+      }
+    }
+  }
+}
+
+// Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
+// holds its 3M SH coefficients on entry and its dL/dsh row on exit.
+__device__ __forceinline__ void gauss_bwd_one(
+    int i, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ clamped, const float g[10],
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
-    const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
+    const float* __restrict__ cov_pre, float* shrow, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
     const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
     float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
-  const size_t i3 = 3 * (size_t)i, i4 = 4 * (size_t)i, i6 = 6 * (size_t)i;
-  float* osh = o_sh ? o_sh + 3 * (size_t)M * i : nullptr;
+    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
   if (!(radii[i] > 0)) {
     for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
     for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
-    for (int k = 0; k < 4; ++k) o_rot[i4 + k] = 0.f;
-    if (osh) for (int k = 0; k < 3 * M; ++k) osh[k] = 0.f;
+    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (shrow) for (int k = 0; k < 3 * M; ++k) shrow[k] = 0.f;
     o_opac[i] = 0.f;
     return;
   }
@@ -353,35 +399,6 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
   } else {
     sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
     q = reinterpret_cast<const float4*>(rots)[i];
-  }
-  // ---- sum this Gaussian's flagged per-tile partial records (fixed slot
-  // order).  Flags are read 4 slots per word, 32 slots per chunk, with
-  // independent loads, so a large Gaussian does not serialise its wave.
-  float g[10];
-#pragma unroll
-  for (int qq = 0; qq < 10; ++qq) g[qq] = 0.f;
-  {
-    const uint32_t s0 = slot_start[i], s1 = s0 + tiles[i];
-    const uint32_t* fw = reinterpret_cast<const uint32_t*>(pflag);
-    for (uint32_t base = s0 & ~3u; base < s1; base += 32) {
-      uint32_t wd[8];
-#pragma unroll
-      for (int w = 0; w < 8; ++w) wd[w] = (base + 4 * w < s1) ? fw[(base >> 2) + w] : 0u;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        uint32_t bits = wd[w];
-        while (bits) {
-          const int b = __builtin_ctz(bits) >> 3;  // byte index with a nonzero flag
-          bits &= ~(0xFFu << (8 * b));
-          const uint32_t k = base + 4 * w + b;
-          if (k < s0 || k >= s1) continue;
-          const float4 a = partial[3 * (size_t)k], bb = partial[3 * (size_t)k + 1], c = partial[3 * (size_t)k + 2];
-          g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
-          g[4] += bb.x; g[5] += bb.y; g[6] += bb.z; g[7] += bb.w;
-          g[8] += c.x; g[9] += c.y;
-        }
-      }
-    }
   }
   o_m2d[i3] = g[0]; o_m2d[i3 + 1] = g[1]; o_m2d[i3 + 2] = 0.f;
   o_opac[i] = g[5];
@@ -475,12 +492,10 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
   dm.x += ddepth * c.view[2];
   dm.y += ddepth * c.view[6];
   dm.z += ddepth * c.view[10];
-  if (osh) {
-    const f3 dmsh = sh_backward(D, shs + 3 * (size_t)M * i, mean, mk3(campos_p[0], campos_p[1], campos_p[2]),
-                                clamped[i], mk3(g[6], g[7], g[8]), osh);
+  if (shrow) {
+    const f3 dmsh = sh_backward(D, M, shrow, mean, mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i],
+                                mk3(g[6], g[7], g[8]), shrow);
     dm = add3(dm, dmsh);
-    const int K = (D + 1) * (D + 1);
-    for (int k = 3 * K; k < 3 * M; ++k) osh[k] = 0.f;
   }
   // ---- cov3D -> scale / rotation (upstream computeCov3D backward)
   if (!cov_pre) {
@@ -509,26 +524,83 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 #pragma unroll
       for (int k = 0; k < 3; ++k) G[j][k] = s3[k] * dM[k][j];
     const float rr = q.x, x = q.y, y = q.z, z = q.w;
-    o_rot[i4 + 0] = 2 * z * (G[1][0] - G[0][1]) + 2 * y * (G[0][2] - G[2][0]) + 2 * x * (G[2][1] - G[1][2]);
-    o_rot[i4 + 1] = 2 * y * (G[1][0] + G[0][1]) + 2 * z * (G[2][0] + G[0][2]) + 2 * rr * (G[2][1] - G[1][2]) -
-                    4 * x * (G[2][2] + G[1][1]);
-    o_rot[i4 + 2] = 2 * x * (G[1][0] + G[0][1]) + 2 * rr * (G[0][2] - G[2][0]) + 2 * z * (G[2][1] + G[1][2]) -
-                    4 * y * (G[2][2] + G[0][0]);
-    o_rot[i4 + 3] = 2 * rr * (G[1][0] - G[0][1]) + 2 * x * (G[2][0] + G[0][2]) + 2 * y * (G[2][1] + G[1][2]) -
-                    4 * z * (G[1][1] + G[0][0]);
+    reinterpret_cast<float4*>(o_rot)[i] = make_float4(
+        2 * z * (G[1][0] - G[0][1]) + 2 * y * (G[0][2] - G[2][0]) + 2 * x * (G[2][1] - G[1][2]),
+        2 * y * (G[1][0] + G[0][1]) + 2 * z * (G[2][0] + G[0][2]) + 2 * rr * (G[2][1] - G[1][2]) -
+            4 * x * (G[2][2] + G[1][1]),
+        2 * x * (G[1][0] + G[0][1]) + 2 * rr * (G[0][2] - G[2][0]) + 2 * z * (G[2][1] + G[1][2]) -
+            4 * y * (G[2][2] + G[0][0]),
+        2 * rr * (G[1][0] - G[0][1]) + 2 * x * (G[2][0] + G[0][2]) + 2 * y * (G[2][1] + G[1][2]) -
+            4 * z * (G[1][1] + G[0][0]));
   } else {
     for (int k = 0; k < 3; ++k) o_sc[i3 + k] = 0.f;
-    for (int k = 0; k < 4; ++k) o_rot[i4 + k] = 0.f;
+    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   o_m3d[i3] = dm.x; o_m3d[i3 + 1] = dm.y; o_m3d[i3 + 2] = dm.z;
   o_tau[i6 + 0] = tau_rho.x; o_tau[i6 + 1] = tau_rho.y; o_tau[i6 + 2] = tau_rho.z;
   o_tau[i6 + 3] = tau_theta.x; o_tau[i6 + 4] = tau_theta.y; o_tau[i6 + 5] = tau_theta.z;
 }
 
+// One wave of 64 Gaussians per workgroup.  The wave's SH slab (64 x 3M
+// floats, contiguous in HBM) moves through LDS in both directions, so SH
+// coefficients are read and dL/dsh written as coalesced 256-byte rows instead
+// of 3M-float strided per-thread runs; rows are padded to 3M + 1 floats so
+// each lane's row walk is bank-conflict free.
+constexpr int kGbWave = 64;
+__global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
+    int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
+    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const uint8_t* __restrict__ pflag,
+    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
+    const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
+    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
+    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
+    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  extern __shared__ float s_sh[];  // kGbWave x (3M + 1) floats (dynamic)
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kGbWave, i = i0 + lane;
+  const int ng = min(kGbWave, P - i0);
+  const int S = 3 * M, SP = S + 1;
+  const bool sh = o_sh != nullptr;
+  // partial-record walk first: its loads are in flight before the SH staging
+  float g[10];
+  {
+    const bool live = i < P && radii[i] > 0;
+    const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+    sum_partials(s0, s1, pflag, partial, g);
+  }
+  // slab element e = lane + 64 r belongs to row e / S, column e % S
+  const int g0 = lane / S, c0 = lane - g0 * S, dg = kGbWave / S, dc = kGbWave - dg * S;
+  if (sh) {
+    const float* src = shs + (size_t)i0 * S;
+    int g = g0, c = c0;
+    for (int e = lane; e < ng * S; e += kGbWave) {
+      s_sh[g * SP + c] = src[e];
+      g += dg; c += dc;
+      if (c >= S) { c -= S; ++g; }
+    }
+    __syncthreads();
+  }
+  if (i < P)
+    gauss_bwd_one(i, D, M, radii, clamped, g, means, scales, rots, cov_pre,
+                  sh ? &s_sh[lane * SP] : nullptr, scale_mod, viewm, projm, praw, campos_p, W, H, tanx, tany,
+                  o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
+  if (sh) {
+    __syncthreads();
+    float* dst = o_sh + (size_t)i0 * S;
+    int g = g0, c = c0;
+    for (int e = lane; e < ng * S; e += kGbWave) {
+      dst[e] = s_sh[g * SP + c];
+      g += dg; c += dc;
+      if (c >= S) { c -= S; ++g; }
+    }
+  }
+}
+
 }  // namespace
 
-hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* point_g, const void* geom, const float* final_T,
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s) {
   const GeomLayout L(a.P);
@@ -536,8 +608,8 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int nt = gx * gy;
   static const int ppl = render_ppl("WGSR_BWD_PPL", 1);
 #define WGSR_BWD(PPL_)                                                                                        \
-  hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, sorted_k, point_g,    \
-                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
+  hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,              \
+                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
                      dL_ddepth, partial, pflag)
   if (ppl == 1) WGSR_BWD(1); else if (ppl == 2) WGSR_BWD(2); else WGSR_BWD(4);
 #undef WGSR_BWD
@@ -550,7 +622,8 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                             float* dL_dscales, float* dL_drot, float* dL_dtau, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
-  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, a.D, a.M, radii,
+  const size_t lds = a.shs ? sizeof(float) * kGbWave * (3 * (size_t)a.M + 1) : 0;
+  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M, radii,
                      at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
                      partial, pflag, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,

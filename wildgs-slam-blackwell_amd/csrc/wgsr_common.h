@@ -322,16 +322,14 @@ struct GeomLayout {
 
 // Per-pair state (binning buffer).
 struct BinLayout {
-  size_t key, key_alt, val, val_alt, slot_g, point_g, hist, totals, total;
+  size_t key, key_alt, slot_g, point_g, hist, totals, total;
   __host__ __device__ BinLayout(size_t N) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
     const size_t nb = sort_blocks(N);
     key = take(4 * N);       // tile id per pair (sorted in place of key/key_alt)
     key_alt = take(4 * N);
-    val = take(4 * N);       // duplicate slot k per sorted pair
-    val_alt = take(4 * N);
-    slot_g = take(4 * N);    // duplicate slot -> Gaussian id
+    slot_g = take(4 * N);    // duplicate slot -> Gaussian id (the sort's payload)
     point_g = take(4 * N);   // sorted pair -> Gaussian id (the tile lists)
     hist = take(4 * 256 * (size_t)nb);
     totals = take(4 * 256);

@@ -45,8 +45,8 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, c
                                hipStream_t s);
 
 // backward stages (raster_bwd.hip)
-hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* sorted_k,
-                             const uint32_t* point_g, const void* geom, const float* final_T,
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
+                             const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s);
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
