@@ -136,7 +136,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     // lane j tests entry j's reach box against this wave's pixels; the wave
     // walks only the entries that can touch it, back to front (a scalar bit loop)
     sHit[w][lane] = 0;
-    uint64_t todo = __ballot(lane < cnt && reach_hits(sB[lane].w, sC[lane].w, wx0, wx1, wy0, wy1));
+    uint64_t todo = __ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;

@@ -135,27 +135,14 @@ __global__ __launch_bounds__(256) void k_preprocess(
     rgb = sh_to_rgb(D, shs + 3 * (size_t)M * i, dir, cbits);
   }
   const float o = opac[i];
-  // Pixel box that contains every pixel this splat can reach with alpha >=
-  // 1/255: o G >= 1/255  <=>  d^T conic d <= 2 ln(255 o), an ellipse with
-  // half-extents sqrt(2 ln(255 o) cov_xx|yy) (cov = the 2D covariance above).
-  // Rounded outward with a 1-pixel margin; the tile loops skip an entry for a
-  // wave whose pixels all lie outside (pure culling: results are unchanged).
-  uint32_t bx = 0xFFFFu, by = 0xFFFFu;  // empty box (lo > hi) if unreachable
-  {
-    const float lim = fmaxf(2.f * __logf(255.f * o), 0.f);
-    if (o >= kMinAlpha) {  // else o G < 1/255 everywhere (G <= 1)
-      const float hx = sqrtf(lim * a) + 1.f, hy = sqrtf(lim * cc) + 1.f;
-      const int bx0 = max(0, (int)floorf(px - hx)), bx1 = min(65535, (int)ceilf(px + hx));
-      const int by0 = max(0, (int)floorf(py - hy)), by1 = min(65535, (int)ceilf(py + hy));
-      if (bx0 <= bx1 && by0 <= by1) {
-        bx = (uint32_t)min(bx0, 65535) | ((uint32_t)bx1 << 16);
-        by = (uint32_t)min(by0, 65535) | ((uint32_t)by1 << 16);
-      }
-    }
-  }
+  // Reach of the splat: o G >= 1/255  <=>  d^T conic d <= lim = 2 ln(255 o)
+  // (G = exp(-d^T conic d / 2) <= 1, so lim < 0 means "reaches no pixel").
+  // The render loops test each entry's ellipse against a wave's pixel
+  // rectangle and skip entries that cannot reach it (pure culling).
+  const float lim = (o >= kMinAlpha) ? 2.f * logf(255.f * o) : -1.f;
   splat[3 * (size_t)i + 0] = make_float4(px, py, cc * det_inv, -b * det_inv);
-  splat[3 * (size_t)i + 1] = make_float4(a * det_inv, o, pv.z, __uint_as_float(bx));
-  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(by));
+  splat[3 * (size_t)i + 1] = make_float4(a * det_inv, o, pv.z, lim);
+  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
   rect[i] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
   tiles[i] = (uint32_t)((x1 - x0) * (y1 - y0));
   clamped[i] = cbits;
@@ -295,7 +282,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
     const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
     // lane j tests entry j's reach box against this wave's pixels; the wave
     // then walks only the entries that can touch it (a scalar bit loop)
-    uint64_t todo = __ballot(lane < cnt && reach_hits(sB[lane].w, sC[lane].w, wx0, wx1, wy0, wy1));
+    uint64_t todo = __ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;

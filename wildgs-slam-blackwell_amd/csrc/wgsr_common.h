@@ -150,12 +150,29 @@ __device__ __forceinline__ void wave_box(int w, int tx0, int ty0, int& x0, int& 
   }
 }
 
-// Does a splat's reach box (packed x0 | x1 << 16, y0 | y1 << 16 in the spare
-// lanes of its record) meet the pixel box [x0, x1] x [y0, y1]?  Wave-uniform.
-__device__ __forceinline__ bool reach_hits(float bxf, float byf, int x0, int x1, int y0, int y1) {
-  const uint32_t bx = __float_as_uint(bxf), by = __float_as_uint(byf);
-  return (int)(bx & 0xFFFFu) <= x1 && (int)(bx >> 16) >= x0 && (int)(by & 0xFFFFu) <= y1 &&
-         (int)(by >> 16) >= y0;
+// Can a splat reach alpha >= 1/255 at any pixel centre of the rectangle
+// [x0, x1] x [y0, y1]?  Record lanes: A = (mean x, mean y, conic xx, conic xy),
+// B = (conic yy, opacity, depth, lim) with lim = 2 ln(255 o) (k_preprocess).
+// Exact minimum of q(d) = d^T conic d over the continuous rectangle (d = mean -
+// pixel, the render's convention): 0 if the mean lies inside, else the least of
+// the four edge minima (q is convex; on an edge it is a 1-D parabola whose
+// vertex is clamped to the edge).  The margin keeps the test conservative
+// against the render's own fp32 rounding, so culling never changes a result.
+// Evaluated lane-parallel (lane j tests entry j), then balloted.
+__device__ __forceinline__ bool ellipse_hits(const float4& A, const float4& B, int x0, int x1, int y0, int y1) {
+  const float lim = B.w;
+  if (!(lim >= 0.f)) return false;
+  const float ca = A.z, cb = A.w, cc = B.x;
+  const float dxl = A.x - (float)x1, dxh = A.x - (float)x0;  // dx range over the rectangle
+  const float dyl = A.y - (float)y1, dyh = A.y - (float)y0;
+  if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return true;
+  const float ica = __builtin_amdgcn_rcpf(ca), icc = __builtin_amdgcn_rcpf(cc);
+  auto q = [&](float dx, float dy) { return ca * dx * dx + 2.f * cb * dx * dy + cc * dy * dy; };
+  const float e0 = q(dxl, fminf(fmaxf(-cb * dxl * icc, dyl), dyh));
+  const float e1 = q(dxh, fminf(fmaxf(-cb * dxh * icc, dyl), dyh));
+  const float e2 = q(fminf(fmaxf(-cb * dyl * ica, dxl), dxh), dyl);
+  const float e3 = q(fminf(fmaxf(-cb * dyh * ica, dxl), dxh), dyh);
+  return fminf(fminf(e0, e1), fminf(e2, e3)) <= lim * 1.001f + 1e-2f;
 }
 
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
