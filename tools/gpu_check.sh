@@ -27,6 +27,17 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_write -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_write.err); rc=$? ;;
     pmc_sq)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq.err); rc=$? ;;
+    ab)
+      # AB_LIBS="name ...": bench each lib/variants/<name>.so ("base" = lib/libwgsr.so), twice, interleaved
+      rc=0
+      for rep in 1 2; do for v in ${AB_LIBS}; do
+        if [ "$v" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$v.so; fi
+        WGSR_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${v}_$rep.json 2> $OUT/ab_${v}_$rep.err; rc=$?
+        if [ $rc -ne 0 ]; then break 2; fi
+      done; done ;;
+    pmc_custom)
+      # PMC_COUNTERS="A B C" PMC_NAME=name: one extra counter pass (SQ block: at most 8 counters)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom}.err); rc=$? ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   echo "$s rc=$rc" | tee -a $OUT/steps.log

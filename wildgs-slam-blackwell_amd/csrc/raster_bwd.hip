@@ -55,13 +55,12 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
-  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
   int wx0, wx1, wy0, wy1;
   wave_box<PPL>(w, tx0, ty0, wx0, wx1, wy0, wy1);
 
   float fx[PPL], fy[PPL], Tf[PPL], T[PPL], dp0[PPL], dp1[PPL], dp2[PPL], dpd[PPL], bgd[PPL];
-  float acc0[PPL], acc1[PPL], acc2[PPL], accd[PPL], la[PPL], lc0[PPL], lc1[PPL], lc2[PPL], ld[PPL];
+  float acc0[PPL], acc1[PPL], acc2[PPL], accd[PPL];
   uint32_t last[PPL];
   uint32_t m = 0;
 #pragma unroll
@@ -82,7 +81,6 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     bgd[p] = bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p];
     T[p] = Tf[p];
     acc0[p] = acc1[p] = acc2[p] = accd[p] = 0.f;
-    la[p] = lc0[p] = lc1[p] = lc2[p] = ld[p] = 0.f;
     m = max(m, last[p]);
   }
   // entries behind every pixel's last contributor cannot receive gradient
@@ -136,7 +134,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     // lane j tests entry j's reach box against this wave's pixels; the wave
     // walks only the entries that can touch it, back to front (a scalar bit loop)
     sHit[w][lane] = 0;
-    uint64_t todo = __ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;
@@ -152,62 +150,58 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
       for (int p = 0; p < PPL; ++p) {
         dxv[p] = A.x - fx[p];
         dyv[p] = A.y - fy[p];
-        const float power = -0.5f * (A.z * dxv[p] * dxv[p] + B.x * dyv[p] * dyv[p]) - A.w * dxv[p] * dyv[p];
+        const float power = -0.5f * (A.z * dxv[p] * dxv[p] + A.w * dyv[p] * dyv[p]) - B.x * dxv[p] * dyv[p];
         Gv[p] = __expf(power);
         av[p] = fminf(kMaxAlpha, B.y * Gv[p]);
         vv[p] = cidx < last[p] && power <= 0.0f && av[p] >= kMinAlpha;
         any |= vv[p];
       }
-      if (!__any(any)) continue;  // no pixel of this wave: no partial, skip the heavy part
+      if (!wave_any(any)) continue;  // no pixel of this wave: no partial, skip the heavy part
       if (lane == 0) sHit[w][j] = 1;
-      // phase 2: PPL independent, branch-free pixel updates (selects)
+      // phase 2: branch-free.  A lane whose pixel the entry misses runs the
+      // same code with alpha = 0 (so T and the accumulated colour pass through
+      // unchanged: 1 / (1 - 0) = 1, 0 * c + 1 * acc = acc, and its colour
+      // weight alpha T is 0) and with dL/dalpha zeroed.  Constant factors of
+      // the mean2D (0.5 W, 0.5 H) and conic (-0.5) gradients are applied once
+      // per Gaussian in k_gauss_bwd.
       float gv[10];
 #pragma unroll
       for (int q = 0; q < 10; ++q) gv[q] = 0.f;
 #pragma unroll
       for (int p = 0; p < PPL; ++p) {
         const bool v = vv[p];
-        const float dx = dxv[p], dy = dyv[p], G = Gv[p], alpha = av[p];
+        const float dx = dxv[p], dy = dyv[p], G = Gv[p];
+        const float alpha = v ? av[p] : 0.f;
         // one v_rcp_f32 serves T and the bg term (alpha <= 0.99 keeps 1 - alpha >= 0.01)
         const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
         const float Tn = T[p] * rinv;
+        T[p] = Tn;
         const float dchannel_dcolor = alpha * Tn;
-        const float a0 = la[p] * lc0[p] + (1.f - la[p]) * acc0[p];
-        const float a1 = la[p] * lc1[p] + (1.f - la[p]) * acc1[p];
-        const float a2 = la[p] * lc2[p] + (1.f - la[p]) * acc2[p];
-        const float ad = la[p] * ld[p] + (1.f - la[p]) * accd[p];
-        float dL_dalpha = (Cc.x - a0) * dp0[p];
-        dL_dalpha += (Cc.y - a1) * dp1[p];
-        dL_dalpha += (Cc.z - a2) * dp2[p];
-        dL_dalpha += (B.z - ad) * dpd[p];
+        float dL_dalpha = (Cc.x - acc0[p]) * dp0[p];
+        dL_dalpha += (Cc.y - acc1[p]) * dp1[p];
+        dL_dalpha += (Cc.z - acc2[p]) * dp2[p];
+        dL_dalpha += (Cc.w - accd[p]) * dpd[p];
         dL_dalpha *= Tn;
         dL_dalpha += (-Tf[p] * rinv) * bgd[p];
-        const float wc = v ? dchannel_dcolor : 0.f;
-        const float wa = v ? dL_dalpha : 0.f;
-        const float wg = B.y * wa;  // dL/dG
+        dL_dalpha = v ? dL_dalpha : 0.f;
+        // colour / depth accumulated behind the next contributor (upstream's
+        // accum_rec = last_alpha * last_colour + (1 - last_alpha) * accum_rec)
+        acc0[p] = alpha * Cc.x + (1.f - alpha) * acc0[p];
+        acc1[p] = alpha * Cc.y + (1.f - alpha) * acc1[p];
+        acc2[p] = alpha * Cc.z + (1.f - alpha) * acc2[p];
+        accd[p] = alpha * Cc.w + (1.f - alpha) * accd[p];
+        const float wg = B.y * dL_dalpha;  // dL/dG
         const float gdx = G * dx, gdy = G * dy;
-        const float dG_ddelx = -gdx * A.z - gdy * A.w;
-        const float dG_ddely = -gdy * B.x - gdx * A.w;
-        gv[0] += wg * dG_ddelx * ddelx_dx;
-        gv[1] += wg * dG_ddely * ddely_dy;
-        gv[2] += -0.5f * gdx * dx * wg;
-        gv[3] += -0.5f * gdx * dy * wg;
-        gv[4] += -0.5f * gdy * dy * wg;
-        gv[5] += G * wa;
-        gv[6] += wc * dp0[p];
-        gv[7] += wc * dp1[p];
-        gv[8] += wc * dp2[p];
-        gv[9] += wc * dpd[p];
-        T[p] = v ? Tn : T[p];
-        acc0[p] = v ? a0 : acc0[p];
-        acc1[p] = v ? a1 : acc1[p];
-        acc2[p] = v ? a2 : acc2[p];
-        accd[p] = v ? ad : accd[p];
-        lc0[p] = v ? Cc.x : lc0[p];
-        lc1[p] = v ? Cc.y : lc1[p];
-        lc2[p] = v ? Cc.z : lc2[p];
-        ld[p] = v ? B.z : ld[p];
-        la[p] = v ? alpha : la[p];
+        gv[0] += wg * (-gdx * A.z - gdy * B.x);
+        gv[1] += wg * (-gdy * A.w - gdx * B.x);
+        gv[2] += gdx * dx * wg;
+        gv[3] += gdx * dy * wg;
+        gv[4] += gdy * dy * wg;
+        gv[5] += G * dL_dalpha;
+        gv[6] += dchannel_dcolor * dp0[p];
+        gv[7] += dchannel_dcolor * dp1[p];
+        gv[8] += dchannel_dcolor * dp2[p];
+        gv[9] += dchannel_dcolor * dpd[p];
       }
       wave_sum10_store(gv, &sP[w][j][0]);
     }
@@ -569,6 +563,12 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
     const bool live = i < P && radii[i] > 0;
     const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
     sum_partials(s0, s1, pflag, partial, g);
+    // factors the render kernel leaves out of its per-pixel terms
+    g[0] *= 0.5f * W;  // d(pixel x) / d(NDC x)
+    g[1] *= 0.5f * H;
+    g[2] *= -0.5f;     // dG/dconic
+    g[3] *= -0.5f;
+    g[4] *= -0.5f;
   }
   // slab element e = lane + 64 r belongs to row e / S, column e % S
   const int g0 = lane / S, c0 = lane - g0 * S, dg = kGbWave / S, dc = kGbWave - dg * S;

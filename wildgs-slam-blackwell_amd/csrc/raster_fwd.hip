@@ -140,9 +140,11 @@ __global__ __launch_bounds__(256) void k_preprocess(
   // The render loops test each entry's ellipse against a wave's pixel
   // rectangle and skip entries that cannot reach it (pure culling).
   const float lim = (o >= kMinAlpha) ? 2.f * logf(255.f * o) : -1.f;
-  splat[3 * (size_t)i + 0] = make_float4(px, py, cc * det_inv, -b * det_inv);
-  splat[3 * (size_t)i + 1] = make_float4(a * det_inv, o, pv.z, lim);
-  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+  // record: A = (mean x, mean y, conic xx, conic yy), B = (conic xy, opacity,
+  // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
+  splat[3 * (size_t)i + 0] = make_float4(px, py, cc * det_inv, a * det_inv);
+  splat[3 * (size_t)i + 1] = make_float4(-b * det_inv, o, lim, 0.f);
+  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rect[i] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
   tiles[i] = (uint32_t)((x1 - x0) * (y1 - y0));
   clamped[i] = cbits;
@@ -221,14 +223,13 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
     int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
     float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
     uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
-  constexpr uint32_t kAll = (1u << PPL) - 1u;
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
   const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   float fx[PPL], fy[PPL];
-  uint32_t done = 0;  // bit p: pixel p finished (or outside the image)
+  uint32_t done = 0;
 #pragma unroll
   for (int p = 0; p < PPL; ++p) {
     int ox, oy;
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
   }
 
   for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
-    if (__syncthreads_count(done == kAll) == (int)blockDim.x) break;
+    if (__syncthreads_count(done == ((1u << PPL) - 1u)) == (int)blockDim.x) break;
     if (t < kFwdBatch) {
       sA[t] = nA;
       sB[t] = nB;
@@ -277,24 +278,25 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
       }
       if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
     }
-    if (__all(done == kAll)) continue;  // this wave is finished; keep the barriers
+    if (__all(done == ((1u << PPL) - 1u))) continue;  // this wave is finished; keep the barriers
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
     const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
     // lane j tests entry j's reach box against this wave's pixels; the wave
     // then walks only the entries that can touch it (a scalar bit loop)
-    uint64_t todo = __ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;
       const float4 A = sA[j];
       const float4 B = sB[j];
       const float4 Cc = sC[j];
-      uint32_t touched = 0;
-      // PPL independent, branch-free pixel updates (the compiler interleaves them)
+      uint32_t tot = 0;  // pixels of this wave whose T stays above 0.5 (upstream n_touched)
+      // PPL independent, branch-free pixel updates (the compiler interleaves
+      // them); the predicates stay in SGPR lane masks
 #pragma unroll
       for (int p = 0; p < PPL; ++p) {
         const float dx = A.x - fx[p], dy = A.y - fy[p];
-        const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
+        const float power = -0.5f * (A.z * dx * dx + A.w * dy * dy) - B.x * dx * dy;
         const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
         const float test_T = T[p] * (1.f - alpha);
         const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;
@@ -304,18 +306,14 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
         C0[p] += Cc.x * wgt;
         C1[p] += Cc.y * wgt;
         C2[p] += Cc.z * wgt;
-        Dp[p] += B.z * wgt;
-        touched += (blend && test_T > 0.5f) ? 1u : 0u;
+        Dp[p] += Cc.w * wgt;
+        tot += (uint32_t)__popcll(wave_ballot(blend && test_T > 0.5f));
         T[p] = blend ? test_T : T[p];
         last[p] = blend ? cbase + j : last[p];
         done |= stop ? (1u << p) : 0u;
       }
-      // pixels of this wave whose T stays above 0.5 (upstream n_touched)
-      uint32_t tot = (uint32_t)__popcll(__ballot(touched & 1u));
-      if constexpr (PPL > 1) tot += 2u * (uint32_t)__popcll(__ballot(touched & 2u));
-      if constexpr (PPL > 2) tot += 4u * (uint32_t)__popcll(__ballot(touched & 4u));
       if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
-      if (__all(done == kAll)) break;
+      if (__all(done == ((1u << PPL) - 1u))) break;
     }
   }
   const size_t HW = (size_t)H * W;

@@ -35,23 +35,28 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_t
   return base + inc - v;
 }
 
+// Per-block digit histogram.  All 16 keys of a thread are loaded up front
+// (independent loads in flight together); each peer group of equal digits in
+// a wave adds its size with one LDS atomic from its lowest lane.
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     int bits, uint32_t nb, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_hist[256];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   s_hist[t] = 0;
-  __syncthreads();
   const uint32_t mask = (1u << bits) - 1u;
   const size_t base = (size_t)blockIdx.x * kSortTile + (size_t)w * (64 * kSortItems);
-#pragma unroll 4
+  uint32_t d[kSortItems];
+#pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
-    const bool valid = e < n;
-    const uint32_t d = valid ? (keys[e] >> shift) & mask : 0u;
-    const uint64_t active = __ballot(valid);
-    if (active == 0) break;
-    const uint64_t peers = match_digit(d, bits, active);
-    if (valid && lanes_below(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
+    d[j] = (e < n) ? (keys[e] >> shift) & mask : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const bool valid = d[j] != 0xFFFFFFFFu;
+    const uint64_t peers = match_digit(d[j], bits, __ballot(valid));
+    if (valid && lanes_below(peers) == 0) atomicAdd(&s_hist[d[j]], (uint32_t)__popcll(peers));
   }
   __syncthreads();
   hist[(size_t)t * nb + blockIdx.x] = s_hist[t];

@@ -102,6 +102,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// Wave votes on a lane predicate that stays an SGPR lane mask (HIP's int
+// __ballot / __any / __all materialise the predicate in a VGPR first).
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ bool wave_all(bool p) { return __builtin_amdgcn_ballot_w64(!p) == 0; }
+
 // Lanes (among `active`) whose low `bits` bits of d equal this lane's.
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, int bits, uint64_t active) {
   uint64_t peers = active;
@@ -151,8 +157,8 @@ __device__ __forceinline__ void wave_box(int w, int tx0, int ty0, int& x0, int& 
 }
 
 // Can a splat reach alpha >= 1/255 at any pixel centre of the rectangle
-// [x0, x1] x [y0, y1]?  Record lanes: A = (mean x, mean y, conic xx, conic xy),
-// B = (conic yy, opacity, depth, lim) with lim = 2 ln(255 o) (k_preprocess).
+// [x0, x1] x [y0, y1]?  Record lanes: A = (mean x, mean y, conic xx, conic yy),
+// B = (conic xy, opacity, lim, 0) with lim = 2 ln(255 o) (k_preprocess).
 // Exact minimum of q(d) = d^T conic d over the continuous rectangle (d = mean -
 // pixel, the render's convention): 0 if the mean lies inside, else the least of
 // the four edge minima (q is convex; on an edge it is a 1-D parabola whose
@@ -160,9 +166,9 @@ __device__ __forceinline__ void wave_box(int w, int tx0, int ty0, int& x0, int& 
 // against the render's own fp32 rounding, so culling never changes a result.
 // Evaluated lane-parallel (lane j tests entry j), then balloted.
 __device__ __forceinline__ bool ellipse_hits(const float4& A, const float4& B, int x0, int x1, int y0, int y1) {
-  const float lim = B.w;
+  const float lim = B.z;
   if (!(lim >= 0.f)) return false;
-  const float ca = A.z, cb = A.w, cc = B.x;
+  const float ca = A.z, cb = B.x, cc = A.w;
   const float dxl = A.x - (float)x1, dxh = A.x - (float)x0;  // dx range over the rectangle
   const float dyl = A.y - (float)y1, dyh = A.y - (float)y0;
   if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return true;
@@ -173,6 +179,14 @@ __device__ __forceinline__ bool ellipse_hits(const float4& A, const float4& B, i
   const float e2 = q(fminf(fmaxf(-cb * dyl * ica, dxl), dxh), dyl);
   const float e3 = q(fminf(fmaxf(-cb * dyh * ica, dxl), dxh), dyh);
   return fminf(fminf(e0, e1), fminf(e2, e3)) <= lim * 1.001f + 1e-2f;
+}
+
+template <int PPL>
+__device__ __forceinline__ bool all_done(const bool (&d)[PPL]) {
+  bool r = true;
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) r = r && d[p];
+  return r;
 }
 
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
