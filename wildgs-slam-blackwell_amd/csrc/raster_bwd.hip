@@ -86,6 +86,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
   // entries behind every pixel's last contributor cannot receive gradient
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+  const uint32_t m_wave = m;  // this wave's pixels take gradient from list indices < m_wave only
   if constexpr (WAVES > 1) {
     if (lane == 0) s_max[w] = m;
     __syncthreads();
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     // lane j tests entry j's reach box against this wave's pixels; the wave
     // walks only the entries that can touch it, back to front (a scalar bit loop)
     sHit[w][lane] = 0;
-    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+    uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < m_wave && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;
