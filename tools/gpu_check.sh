@@ -30,9 +30,12 @@ for s in $STEPS; do
     ab)
       # AB_LIBS="name ...": bench each lib/variants/<name>.so ("base" = lib/libwgsr.so), twice, interleaved
       rc=0
+      # an entry may carry one env setting: name:VAR=value (e.g. base:WGSR_SORT=onesweep)
       for rep in 1 2; do for v in ${AB_LIBS}; do
-        if [ "$v" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$v.so; fi
-        WGSR_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${v}_$rep.json 2> $OUT/ab_${v}_$rep.err; rc=$?
+        lname=${v%%:*}; envset=""; tag=$lname
+        if [ "$v" != "$lname" ]; then envset=${v#*:}; tag=${lname}_${envset//=/_}; fi
+        if [ "$lname" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$lname.so; fi
+        env WGSR_LIB=$lib $envset timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${tag}_$rep.json 2> $OUT/ab_${tag}_$rep.err; rc=$?
         if [ $rc -ne 0 ]; then break 2; fi
       done; done ;;
     pmc_custom)

@@ -39,8 +39,8 @@ struct KnnLayout {
     spts = take(16 * P);
     boxes = take(32 * nbox);
     supers = take(32 * nsup);
-    hist = take(4 * 256 * (size_t)sort_blocks(P));
-    totals = take(4 * 256);
+    hist = take(sort_status_bytes(P));
+    totals = take(kSortTotalsBytes);
     total = o;
   }
 };

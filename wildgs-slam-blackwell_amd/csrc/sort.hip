@@ -1,15 +1,22 @@
-// LSD radix sort of (u32 key, u32 value) pairs and exclusive scans, gfx950.
+// Stable LSD radix sort of (u32 key, u32 value) pairs and exclusive scans, gfx950.
 //
 // Replaces the CUB primitives upstream's rasteriser and simple-knn lean on
 // (cub::DeviceRadixSort::SortPairs, cub::DeviceScan::InclusiveSum: SURVEY.md
-// 2 "Kernel inventory").  Design for wave64:
-//  * a pass = histogram -> per-digit row scan -> stable scatter;
-//  * block-local stable ranking uses 64-bit ballots to find the lanes that
-//    share a digit (one LDS counter update per peer group, no LDS atomics);
-//  * the scatter stages the block's keys in LDS in digit order so that runs of
-//    one digit leave as contiguous (coalesced) stores.
-// A workgroup owns 4096 keys (256 threads x 16); each wave owns a contiguous
-// run of 1024 keys that it walks 64 at a time, so ranks follow input order.
+// 2 "Kernel inventory").  8-bit digits; a workgroup owns 4096 keys.  Two
+// schedules share one scatter kernel:
+//  * reduce-then-scan (default): per pass, block histograms -> per-digit row
+//    scan over blocks -> stable scatter;
+//  * onesweep (WGSR_SORT=onesweep): one histogram kernel for all passes, then
+//    one scatter kernel per pass whose blocks find their offsets by decoupled
+//    look-back.
+// Block-local stable ranking uses 64-bit ballots to find the lanes that share
+// a digit; the scatter stages the block's keys in LDS in digit order so that
+// runs of one digit leave as contiguous (coalesced) stores.  Each wave of the
+// scatter owns a contiguous run of 1024 keys that it walks 64 at a time, so
+// ranks follow input order.
+#include <stdlib.h>
+#include <string.h>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -35,34 +42,67 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_t
   return base + inc - v;
 }
 
-// Per-block digit histogram.  All 16 keys of a thread are loaded up front
-// (independent loads in flight together); each peer group of equal digits in
-// a wave adds its size with one LDS atomic from its lowest lane.
-__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                    int bits, uint32_t nb, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t s_hist[256];
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  s_hist[t] = 0;
-  const uint32_t mask = (1u << bits) - 1u;
-  const size_t base = (size_t)blockIdx.x * kSortTile + (size_t)w * (64 * kSortItems);
-  uint32_t d[kSortItems];
+// ---- digit counting ----------------------------------------------------------
+// Histogram kernels give thread t of a block the 16 CONTIGUOUS keys
+// [16 t, 16 t + 16) of the block's 4096 and count them one LDS atomic per run
+// of equal digits: the sort inputs here (depth bits, tile ids in duplicate
+// order, Morton codes) have long runs in their high digits, which would
+// otherwise serialise as same-address LDS atomics.
+
+__device__ __forceinline__ int load_run16(const uint32_t* __restrict__ keys, size_t n, size_t e0,
+                                          uint32_t (&k)[kSortItems]) {
+  static_assert(kSortItems == 16, "load_run16 reads 4 x uint4");
+  if (e0 + kSortItems <= n) {
+    const uint4* p = reinterpret_cast<const uint4*>(keys + e0);
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
-    const size_t e = base + (size_t)j * 64 + lane;
-    d[j] = (e < n) ? (keys[e] >> shift) & mask : 0xFFFFFFFFu;
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = p[q];
+      k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
+    }
+    return kSortItems;
   }
-  __syncthreads();
+  const int nv = e0 < n ? (int)(n - e0) : 0;
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
-    const bool valid = d[j] != 0xFFFFFFFFu;
-    const uint64_t peers = match_digit(d[j], bits, __ballot(valid));
-    if (valid && lanes_below(peers) == 0) atomicAdd(&s_hist[d[j]], (uint32_t)__popcll(peers));
-  }
-  __syncthreads();
-  hist[(size_t)t * nb + blockIdx.x] = s_hist[t];
+  for (int j = 0; j < kSortItems; ++j) k[j] = j < nv ? keys[e0 + j] : 0u;
+  return nv;
 }
 
-// exclusive scan of hist row d (over blocks) in place; totals[d] = row sum
+__device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[kSortItems], int nv, int shift,
+                                         uint32_t mask) {
+  if (nv <= 0) return;
+  uint32_t cur = (k[0] >> shift) & mask, run = 0;
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    if (j < nv) {
+      const uint32_t d = (k[j] >> shift) & mask;
+      if (d != cur) {
+        atomicAdd(&h[cur], run);
+        cur = d;
+        run = 0;
+      }
+      ++run;
+    }
+  }
+  atomicAdd(&h[cur], run);
+}
+
+// Reduce-then-scan mode, step 1: per-block histogram of one pass, stored
+// digit-major: hist[d * nb + block].
+__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                    int bits, uint32_t nb, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_h[256];
+  const int t = threadIdx.x;
+  s_h[t] = 0;
+  uint32_t k[kSortItems];
+  const int nv = load_run16(keys, n, (size_t)blockIdx.x * kSortTile + (size_t)t * kSortItems, k);
+  __syncthreads();
+  add_runs(s_h, k, nv, shift, (1u << bits) - 1u);
+  __syncthreads();
+  hist[(size_t)t * nb + blockIdx.x] = s_h[t];
+}
+
+// Reduce-then-scan mode, step 2: exclusive scan of hist row d (over blocks)
+// in place; totals[d] = row sum.
 __global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t nb,
                                                        uint32_t* __restrict__ totals) {
   __shared__ uint32_t s_tmp[4];
@@ -75,36 +115,72 @@ __global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hi
   uint32_t tot;
   uint32_t run = block_excl_scan256(s, s_tmp, &tot);
   for (uint32_t b = b0; b < b1; ++b) {
-    uint32_t x = row[b];
+    const uint32_t x = row[b];
     row[b] = run;
     run += x;
   }
   if (t == 0) totals[blockIdx.x] = tot;
 }
 
-// Stable scatter of one pass.  All of a thread's keys and payloads are loaded
+// Onesweep mode: global digit histograms of every pass in one read of the keys.
+__global__ __launch_bounds__(256) void k_onesweep_hist(const uint32_t* __restrict__ keys, uint32_t n, int begin_bit,
+                                                       int end_bit, uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s_h[kMaxSortPasses][256];
+  const int t = threadIdx.x;
+  const int passes = (end_bit - begin_bit + 7) / 8;
+#pragma unroll
+  for (int p = 0; p < kMaxSortPasses; ++p) s_h[p][t] = 0;
+  uint32_t k[kSortItems];
+  const int nv = load_run16(keys, n, (size_t)blockIdx.x * kSortTile + (size_t)t * kSortItems, k);
+  __syncthreads();
+  for (int p = 0; p < passes; ++p) {
+    const int shift = begin_bit + 8 * p;
+    add_runs(s_h[p], k, nv, shift, (1u << min(8, end_bit - shift)) - 1u);
+  }
+  __syncthreads();
+  for (int p = 0; p < passes; ++p)
+    if (s_h[p][t]) atomicAdd(&ghist[p * 256 + t], s_h[p][t]);
+}
+
+// ---- scatter -----------------------------------------------------------------
+// Onesweep look-back status words: flag (bits 31..30: 0 not ready, 1 block
+// aggregate, 2 inclusive prefix) | count (bits 29..0).
+constexpr uint32_t kStAgg = 1u << 30, kStPre = 2u << 30, kStCount = (1u << 30) - 1u;
+constexpr int kLookback = 16;  // predecessor status words fetched per look-back round trip
+
+// One stable digit pass over a block of 4096 keys.  Keys/payloads are loaded
 // up front (in flight while ranking); ranks come from LDS atomics-with-return
 // issued by each peer group's lowest lane (a wave's LDS atomics execute in
 // issue order, so the returned counts are the sequential ones and the 16
 // atomics pipeline instead of forming a read-wait-write chain); keys and
 // payloads are staged through one 16 KB LDS buffer in digit order so that each
-// digit's run leaves as contiguous stores (small LDS -> high occupancy).
-__global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ kin,
-                                                       const uint32_t* __restrict__ vin, int iota, uint32_t n,
-                                                       int shift, int bits, uint32_t nb,
-                                                       const uint32_t* __restrict__ hist,
-                                                       const uint32_t* __restrict__ totals,
-                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                       const uint32_t* __restrict__ v2in,
-                                                       uint32_t* __restrict__ v2out) {
+// digit's run leaves as contiguous stores.
+//   kOnesweep = false: the block's digit offsets come from the scanned
+//     per-block histogram (hist: [256][nb], totals: digit totals).
+//   kOnesweep = true: the block takes the next virtual id (so every block it
+//     waits on is already running), publishes its digit counts and looks back
+//     through its predecessors' status words (totals: this pass's global
+//     digit histogram).
+template <bool kOnesweep>
+__global__ __launch_bounds__(256) void k_radix_scatter(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
+    uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
+    uint32_t* __restrict__ vout, const uint32_t* __restrict__ v2in, uint32_t* __restrict__ v2out) {
   __shared__ uint32_t s_buf[kSortTile];
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
   __shared__ uint32_t s_tmp[4];
+  __shared__ uint32_t s_vid;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t mask = (1u << bits) - 1u;
-  const size_t blk0 = (size_t)blockIdx.x * kSortTile;
+  if (kOnesweep && t == 0) s_vid = atomicAdd(vcounter, 1u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
+  if (kOnesweep) __syncthreads();
+  const uint32_t bid = kOnesweep ? s_vid : blockIdx.x;
+  const size_t blk0 = (size_t)bid * kSortTile;
   const size_t base = blk0 + (size_t)w * (64 * kSortItems);
   uint32_t key[kSortItems], val[kSortItems], val2[kSortItems], rank[kSortItems];
 #pragma unroll
@@ -115,20 +191,17 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
     val2[j] = (v2in && valid) ? v2in[e] : 0u;
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
-  // global base of digit t for this block: scan of the digit totals + row prefix
-  {
-    const uint32_t tot = totals[t];
-    const uint32_t ex = block_excl_scan256(tot, s_tmp, nullptr);  // (its barriers publish s_wcnt = 0)
-    s_gbase[t] = ex + hist[(size_t)t * nb + blockIdx.x];
+  uint32_t gdig = 0;  // reduce-then-scan: this block's global base of digit t
+  if (!kOnesweep) {
+    const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);  // (its barriers publish s_wcnt = 0)
+    gdig = ex + hist[(size_t)t * nb + bid];
   }
 #pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     const uint32_t d = (key[j] >> shift) & mask;
-    const uint64_t peers = match_digit(d, bits, __ballot(valid));
+    const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
     const int leader = __ffsll((unsigned long long)peers) - 1;
     uint32_t old = 0;
     if (valid && lane == leader) old = atomicAdd(&s_wcnt[w][d], (uint32_t)__popcll(peers));
@@ -137,14 +210,46 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
   }
   __syncthreads();
   {
-    // per-digit: exclusive prefix over waves, then over digits (block-local)
     const uint32_t c0 = s_wcnt[0][t], c1 = s_wcnt[1][t], c2 = s_wcnt[2][t], c3 = s_wcnt[3][t];
+    const uint32_t cnt_d = c0 + c1 + c2 + c3;
+    uint32_t* st = status + (size_t)bid * 256 + t;
+    if (kOnesweep)  // publish this block's count of digit t (block 0: already its prefix)
+      __hip_atomic_store(st, (bid == 0 ? kStPre : kStAgg) | cnt_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // per-digit: exclusive prefix over waves, then over digits (block-local)
     s_wcnt[0][t] = 0;
     s_wcnt[1][t] = c0;
     s_wcnt[2][t] = c0 + c1;
     s_wcnt[3][t] = c0 + c1 + c2;
-    const uint32_t tot = c0 + c1 + c2 + c3;
-    s_lbase[t] = block_excl_scan256(tot, s_tmp, nullptr);
+    s_lbase[t] = block_excl_scan256(cnt_d, s_tmp, nullptr);
+    if (kOnesweep) {
+      gdig = block_excl_scan256(totals[t], s_tmp, nullptr);  // digit t's start in the output
+      // decoupled look-back: sum predecessors' counts of digit t until one
+      // carries its inclusive prefix
+      uint32_t excl = 0;
+      int64_t v = (int64_t)bid - 1;  // nearest predecessor not yet summed
+      while (v >= 0) {
+        uint32_t sv[kLookback];
+#pragma unroll
+        for (int k = 0; k < kLookback; ++k)
+          sv[k] = (v - k >= 0) ? __hip_atomic_load(status + (size_t)(v - k) * 256 + t, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : kStPre;
+        int k = 0;
+        bool done = false;
+        for (; k < kLookback; ++k) {
+          const uint32_t f = sv[k] & ~kStCount;
+          if (f == 0) break;  // not published yet: re-fetch from here
+          excl += sv[k] & kStCount;
+          if (f == kStPre) { done = true; break; }
+        }
+        if (done) break;
+        v -= k;
+        if (k < kLookback) __builtin_amdgcn_s_sleep(1);
+      }
+      if (bid > 0) __hip_atomic_store(st, kStPre | (excl + cnt_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      gdig += excl;
+    }
+    s_gbase[t] = gdig;
   }
   __syncthreads();
 #pragma unroll
@@ -263,8 +368,17 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 
 }  // namespace
 
+// WGSR_SORT=onesweep | rts (reduce-then-scan, the default)
+bool use_onesweep() {
+  static const bool v = [] {
+    const char* e = getenv("WGSR_SORT");
+    return e && strcmp(e, "onesweep") == 0;
+  }();
+  return v;
+}
+
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
-                            size_t n, int begin_bit, int end_bit, uint32_t* hist, uint32_t* totals,
+                            size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt, uint32_t* vals2, uint32_t* vals2_alt) {
   *result_in_alt = false;
   if (n == 0 || end_bit <= begin_bit) {
@@ -274,15 +388,35 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     }
     return hipSuccess;
   }
+  const int passes = (end_bit - begin_bit + 7) / 8;
+  if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;
   const uint32_t nb = sort_blocks(n);
+  const bool onesweep = use_onesweep();
+  uint32_t* ghist = totals;                          // onesweep: [passes][256]; rts: digit totals
+  uint32_t* vcount = totals + kMaxSortPasses * 256;  // onesweep: virtual block counters [passes]
+  if (onesweep) {
+    hipError_t e = hipMemsetAsync(totals, 0, kSortTotalsBytes, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(status, 0, 4 * 256 * (size_t)nb * passes, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_onesweep_hist, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit, end_bit,
+                       ghist);
+  }
   uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt, *wi = vals2, *wo = vals2_alt;
   bool iota = vals_iota;
-  for (int shift = begin_bit; shift < end_bit; shift += 8) {
+  for (int p = 0; p < passes; ++p) {
+    const int shift = begin_bit + 8 * p;
     const int bits = min(8, end_bit - shift);
-    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, hist);
-    hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, hist, nb, totals);
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
-                       bits, nb, hist, totals, ko, vo, wi, wo);
+    if (onesweep) {
+      hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n,
+                         shift, bits, nb, nullptr, ghist + 256 * p, vcount + p, status + 256 * (size_t)nb * p, ko,
+                         vo, wi, wo);
+    } else {
+      // status doubles as the [256][nb] per-block histogram
+      hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status);
+      hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
+      hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
+                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, wi, wo);
+    }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;

@@ -324,6 +324,13 @@ constexpr int kSortTile = 256 * kSortItems;          // keys per radix workgroup
 constexpr int kScanTile = 4096;                      // elements per scan workgroup
 
 __host__ __device__ inline uint32_t sort_blocks(size_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+// Onesweep radix sort scratch (sort.hip): look-back status words for up to
+// kMaxSortPasses 8-bit passes, and global digit histograms + block counters.
+constexpr int kMaxSortPasses = 4;
+__host__ __device__ inline size_t sort_status_bytes(size_t n) {
+  return 4ull * 256 * sort_blocks(n) * kMaxSortPasses;
+}
+constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
 // Per-Gaussian state (geometry buffer).
 struct GeomLayout {
@@ -332,7 +339,6 @@ struct GeomLayout {
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
-    const size_t nb = sort_blocks(P);
     splat = take(48 * P);          // float4 x3: (x, y, conic.x, conic.y) (conic.z, opacity, depth, -) (r, g, b, -)
     rect = take(8 * P);            // ushort4 tile rectangle [x0, y0, x1, y1)
     tiles = take(4 * P);           // tiles touched
@@ -343,8 +349,8 @@ struct GeomLayout {
     dval_alt = take(4 * P);
     offs = take(4 * (P + 1));      // rank -> first duplicate slot
     slot_start = take(4 * P);      // Gaussian -> first duplicate slot
-    hist = take(4 * 256 * (size_t)nb);
-    totals = take(4 * 256);
+    hist = take(sort_status_bytes(P));    // radix sort look-back status
+    totals = take(kSortTotalsBytes);
     bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
     counter = take(16);
     total = o;
@@ -357,13 +363,12 @@ struct BinLayout {
   __host__ __device__ BinLayout(size_t N) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
-    const size_t nb = sort_blocks(N);
     key = take(4 * N);       // tile id per pair (sorted in place of key/key_alt)
     key_alt = take(4 * N);
     slot_g = take(4 * N);    // duplicate slot -> Gaussian id (the sort's payload)
     point_g = take(4 * N);   // sorted pair -> Gaussian id (the tile lists)
-    hist = take(4 * 256 * (size_t)nb);
-    totals = take(4 * 256);
+    hist = take(sort_status_bytes(N));    // radix sort look-back status
+    totals = take(kSortTotalsBytes);
     total = o;
   }
 };
