@@ -279,15 +279,16 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   const Grid grid(a);
   const ImageLayout IL(a.W, a.H);
   const size_t N = (size_t)num_rendered;
-  float4* partial = nullptr;
-  uint8_t* pflag = nullptr;
+  // scratch: 48-byte partial record per pair + 1-byte "record written" flag
+  // per pair + per-Gaussian partial sums gsum[10][P] (used by the split
+  // per-Gaussian backward)
+  const size_t rec_bytes = align256(48 * N), flag_bytes = align256(N);
+  void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + flag_bytes + align256(40 * (size_t)a.P));
+  if (!scratch) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
+  float4* partial = N > 0 ? static_cast<float4*>(scratch) : nullptr;
+  uint8_t* pflag = N > 0 ? at<uint8_t>(scratch, rec_bytes) : nullptr;
+  float* gsum = at<float>(scratch, rec_bytes + flag_bytes);
   if (N > 0) {
-    // 48-byte partial record per pair + 1-byte "record written" flag
-    const size_t rec_bytes = align256(48 * N);
-    void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + align256(N));
-    if (!scratch) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
-    partial = static_cast<float4*>(scratch);
-    pflag = at<uint8_t>(scratch, rec_bytes);
     HIPCHK(hipMemsetAsync(pflag, 0, N, s));
     const BinLayout BL(N);
     const bool talt = tile_sort_in_alt(grid);
@@ -298,8 +299,8 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
   }
   StageTimer T(8, s);
-  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
-                               dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
+  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, gsum, dL_dmeans2D, dL_dcolors, dL_dopacity,
+                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
   return WGSR_OK;
 }
 

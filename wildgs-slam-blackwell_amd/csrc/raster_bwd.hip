@@ -14,6 +14,8 @@
 //               runs cov2D -> cov3D -> (scale, rotation), SH, projection,
 //               depth and pose (w-pose dL/dtau) backward in registers and
 //               writes every output of _C.rasterize_gaussians_backward once.
+#include <stdlib.h>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -364,6 +366,35 @@ __device__ __forceinline__ void sum_partials(uint32_t s0, uint32_t s1, const uin
   }
 }
 
+// factors the render kernel leaves out of its per-pixel terms
+__device__ __forceinline__ void scale_partial_sums(float g[10], int W, int H) {
+  g[0] *= 0.5f * W;  // d(pixel x) / d(NDC x)
+  g[1] *= 0.5f * H;
+  g[2] *= -0.5f;     // dG/dconic
+  g[3] *= -0.5f;
+  g[4] *= -0.5f;
+}
+
+// Optional first half of the per-Gaussian backward (WGSR_GB_SPLIT=1): a lean,
+// high-occupancy kernel sums each Gaussian's partial records into
+// gsum[10][P] (coalesced SoA), so k_gauss_bwd starts without the record walk.
+__global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __restrict__ radii,
+                                                      const uint32_t* __restrict__ slot_start,
+                                                      const uint32_t* __restrict__ tiles,
+                                                      const uint8_t* __restrict__ pflag,
+                                                      const float4* __restrict__ partial, int W, int H,
+                                                      float* __restrict__ gsum) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  const bool live = radii[i] > 0;
+  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+  float g[10];
+  sum_partials(s0, s1, pflag, partial, g);
+  scale_partial_sums(g, W, H);
+#pragma unroll
+  for (int q = 0; q < 10; ++q) gsum[(size_t)q * P + i] = g[q];
+}
+
 // Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
 // holds its 3M SH coefficients on entry and its dL/dsh row on exit.
 __device__ __forceinline__ void gauss_bwd_one(
@@ -545,7 +576,7 @@ constexpr int kGbWave = 64;
 __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
     int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
     const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
-    const uint8_t* __restrict__ pflag,
+    const uint8_t* __restrict__ pflag, const float* __restrict__ gsum,
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
     const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
@@ -560,27 +591,17 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
   const bool sh = o_sh != nullptr;
   // partial-record walk first: its loads are in flight before the SH staging
   float g[10];
-  {
+  if (gsum) {  // summed by k_sum_partials
+#pragma unroll
+    for (int q = 0; q < 10; ++q) g[q] = i < P ? gsum[(size_t)q * P + i] : 0.f;
+  } else {
     const bool live = i < P && radii[i] > 0;
     const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
     sum_partials(s0, s1, pflag, partial, g);
-    // factors the render kernel leaves out of its per-pixel terms
-    g[0] *= 0.5f * W;  // d(pixel x) / d(NDC x)
-    g[1] *= 0.5f * H;
-    g[2] *= -0.5f;     // dG/dconic
-    g[3] *= -0.5f;
-    g[4] *= -0.5f;
+    scale_partial_sums(g, W, H);
   }
-  // slab element e = lane + 64 r belongs to row e / S, column e % S
-  const int g0 = lane / S, c0 = lane - g0 * S, dg = kGbWave / S, dc = kGbWave - dg * S;
   if (sh) {
-    const float* src = shs + (size_t)i0 * S;
-    int g = g0, c = c0;
-    for (int e = lane; e < ng * S; e += kGbWave) {
-      s_sh[g * SP + c] = src[e];
-      g += dg; c += dc;
-      if (c >= S) { c -= S; ++g; }
-    }
+    slab_to_lds(shs + (size_t)i0 * S, ng, S, s_sh, lane);
     __syncthreads();
   }
   if (i < P)
@@ -589,13 +610,7 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
                   o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   if (sh) {
     __syncthreads();
-    float* dst = o_sh + (size_t)i0 * S;
-    int g = g0, c = c0;
-    for (int e = lane; e < ng * S; e += kGbWave) {
-      dst[e] = s_sh[g * SP + c];
-      g += dg; c += dc;
-      if (c >= S) { c -= S; ++g; }
-    }
+    lds_to_slab(s_sh, ng, S, o_sh + (size_t)i0 * S, lane);
   }
 }
 
@@ -618,15 +633,25 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
 }
 
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
-                            const float4* partial, const uint8_t* pflag, float* dL_dmeans2D, float* dL_dcolors,
-                            float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
-                            float* dL_dscales, float* dL_drot, float* dL_dtau, hipStream_t s) {
+                            const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                            float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
+  static const bool split = [] {
+    const char* e = getenv("WGSR_GB_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  if (split) {
+    hipLaunchKernelGGL(k_sum_partials, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii,
+                       at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), pflag, partial, a.W, a.H, gsum);
+  } else {
+    gsum = nullptr;
+  }
   const size_t lds = a.shs ? sizeof(float) * kGbWave * (3 * (size_t)a.M + 1) : 0;
   hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M, radii,
                      at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
-                     partial, pflag, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
+                     partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
                      dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
                      dL_dscales, dL_drot, dL_dtau);

@@ -64,7 +64,11 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
-__global__ __launch_bounds__(256) void k_preprocess(
+// One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
+// (64 x 3M floats, contiguous in HBM) is first staged through LDS with
+// coalesced loads (slab_to_lds), instead of each lane reading its own 3M-float run.
+constexpr int kPreWave = 64;
+__global__ __launch_bounds__(kPreWave) void k_preprocess(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
@@ -74,7 +78,13 @@ __global__ __launch_bounds__(256) void k_preprocess(
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (shs != nullptr && colors == nullptr) {
+    slab_to_lds(shs + (size_t)i0 * 3 * M, min(kPreWave, P - i0), 3 * M, s_sh, lane);
+    __syncthreads();
+  }
   if (i >= P) return;
   radii[i] = 0;
   n_touched[i] = 0;
@@ -132,7 +142,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
     const float len = sqrtf(dot3(dir, dir));
     dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-    rgb = sh_to_rgb(D, shs + 3 * (size_t)M * i, dir, cbits);
+    rgb = sh_to_rgb(D, &s_sh[lane * (3 * M + 1)], dir, cbits);
   }
   const float o = opac[i];
   // Reach of the splat: o G >= 1/255  <=>  d^T conic d <= lim = 2 ln(255 o)
@@ -348,7 +358,8 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
-  hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, a.D, a.M, a.means3D, a.scales,
+  const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreWave * (3 * (size_t)a.M + 1) : 0;
+  hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.tiles),

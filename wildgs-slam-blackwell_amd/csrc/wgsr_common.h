@@ -189,6 +189,78 @@ __device__ __forceinline__ bool all_done(const bool (&d)[PPL]) {
   return r;
 }
 
+// ---- per-wave SH slabs: rows of S = 3M floats for 64 consecutive Gaussians
+// are contiguous in HBM; they move between HBM and LDS rows padded to S + 1
+// floats (a lane walking its own row is then bank-conflict free).  All loads
+// of a lane are issued before its first LDS write (no load-wait-store chain);
+// SH3 (S = 48) takes a fully unrolled float4 path.
+template <bool kIn>
+__device__ __forceinline__ void slab_move48(float* gmem, int ng, float* lds, int lane) {
+  constexpr int S = 48, SP = 49, kV = 12;  // 64 rows x 48 floats = 768 float4 = 12 per lane
+  const int nv4 = ng * S / 4;
+  float4 v[kV];
+  if (kIn) {
+    const float4* src = reinterpret_cast<const float4*>(gmem);
+#pragma unroll
+    for (int r = 0; r < kV; ++r) {
+      const int f = lane + 64 * r;
+      v[r] = f < nv4 ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kV; ++r) {
+    const int f = lane + 64 * r;
+    const int g = (4 * f) / S, c = 4 * f - g * S;
+    float* row = lds + g * SP + c;
+    if (kIn) {
+      if (f < nv4) { row[0] = v[r].x; row[1] = v[r].y; row[2] = v[r].z; row[3] = v[r].w; }
+    } else {
+      v[r] = make_float4(row[0], row[1], row[2], row[3]);
+    }
+  }
+  if (!kIn) {
+    float4* dst = reinterpret_cast<float4*>(gmem);
+#pragma unroll
+    for (int r = 0; r < kV; ++r)
+      if (lane + 64 * r < nv4) dst[lane + 64 * r] = v[r];
+  }
+}
+
+template <bool kIn>
+__device__ __forceinline__ void slab_move(float* gmem, int ng, int S, float* lds, int lane) {
+  if (S == 48 && (reinterpret_cast<uintptr_t>(gmem) & 15) == 0) {
+    slab_move48<kIn>(gmem, ng, lds, lane);
+    return;
+  }
+  const int SP = S + 1, total = ng * S;
+  for (int e0 = 0; e0 < total; e0 += 8 * 64) {
+    float v[8];
+    if (kIn) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + 64 * u + lane;
+        v[u] = e < total ? gmem[e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 64 * u + lane;
+      if (e < total) {
+        const int g = e / S, c = e - g * S;
+        if (kIn) lds[g * SP + c] = v[u];
+        else gmem[e] = lds[g * SP + c];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void slab_to_lds(const float* src, int ng, int S, float* lds, int lane) {
+  slab_move<true>(const_cast<float*>(src), ng, S, lds, lane);
+}
+__device__ __forceinline__ void lds_to_slab(const float* lds, int ng, int S, float* dst, int lane) {
+  slab_move<false>(dst, ng, S, const_cast<float*>(lds), lane);
+}
+
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
 int render_ppl(const char* env_name, int dflt);
 

@@ -51,8 +51,8 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s);
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
-                            const float4* partial, const uint8_t* pflag, float* dL_dmeans2D, float* dL_dcolors,
-                            float* dL_dopacity,
+                            const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity,
                             float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                             float* dL_drot, float* dL_dtau, hipStream_t s);
 
