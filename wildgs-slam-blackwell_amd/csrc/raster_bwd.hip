@@ -15,6 +15,7 @@
 //               depth and pose (w-pose dL/dtau) backward in registers and
 //               writes every output of _C.rasterize_gaussians_backward once.
 #include <stdlib.h>
+#include <string.h>
 
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
@@ -232,6 +233,178 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
         partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
         pflag[k] = 1;
       }
+    }
+  }
+}
+
+// Quad mode (default): ONE wave per 16x16 tile; lane l owns pixel (l & 7,
+// l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's ellipse
+// against each quadrant (four ballots), so per entry the wave evaluates only
+// the quadrants the splat can reach (wave-uniform branches) -- the culling of
+// the 4-wave layout -- but sums all of them with ONE wave reduction and writes
+// the record without a cross-wave combine.
+__global__ __launch_bounds__(64) void k_render_bwd_quad(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const ushort4* __restrict__ rect, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
+    const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
+    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
+    uint8_t* __restrict__ pflag) {
+  constexpr int Q = 4;
+  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
+  __shared__ uint32_t sG[kBatch];
+  __shared__ float sP[kBatch][11];
+  __shared__ uint32_t sHit[kBatch];
+  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const int lane = threadIdx.x;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
+  const size_t HW = (size_t)H * W;
+  const uint2 range = ranges[tile];
+  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+
+  // per-quadrant pixel state; pairs are packed for v_pk_* math
+  v2f pxy[Q], dp01[Q], dp2d[Q], acc01[Q], acc2d[Q];
+  float T[Q], tb[Q];
+  uint32_t last[Q], mq[Q];
+  uint32_t m = 0;
+#pragma unroll
+  for (int p = 0; p < Q; ++p) {
+    const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
+    const bool inside = px < W && py < H;
+    const size_t pid = (size_t)py * W + px;
+    pxy[p] = v2f{(float)px, (float)py};
+    const float Tf = inside ? final_Ts[pid] : 0.f;
+    last[p] = inside ? n_contrib[pid] : 0u;
+    const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
+    const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
+    dp01[p] = v2f{d0, d1};
+    dp2d[p] = v2f{d2, dd};
+    tb[p] = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);  // background term: dL/dalpha += tb / (1 - alpha)
+    T[p] = Tf;
+    acc01[p] = v2f{0.f, 0.f};
+    acc2d[p] = v2f{0.f, 0.f};
+    // quadrant p takes gradient from list indices < mq[p] only
+    uint32_t x = last[p];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
+    mq[p] = x;
+    m = max(m, x);
+  }
+  // entries behind every pixel's last contributor get no record: their slot
+  // flags stay 0 (zeroed before the launch), and so does every entry no pixel
+  // of the tile receives gradient from -- typically > 90 % of all pairs
+  const uint32_t end = range.x + m;
+
+  // prefetch pipeline (back to front): records of the next batch in
+  // registers, ids one batch further
+  uint32_t gcur = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (end >= range.x + 1 + lane) {
+    gcur = point_g[end - 1 - lane];
+    nA = splat[3 * (size_t)gcur];
+    nB = splat[3 * (size_t)gcur + 1];
+    nC = splat[3 * (size_t)gcur + 2];
+  }
+  if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
+
+  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
+    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
+    __syncthreads();
+    sA[lane] = nA;
+    sB[lane] = nB;
+    sC[lane] = nC;
+    sG[lane] = gcur;
+    sHit[lane] = 0;
+    __syncthreads();
+    gcur = gnext;
+    if (b_end >= range.x + 1 + kBatch + lane) {
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+    }
+    if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
+
+    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
+    // lane j tests entry j against each quadrant (reach ellipse and the
+    // quadrant's last contributor); quadrant p's survivors are bits of qb[p]
+    uint64_t qb[Q];
+    {
+      const uint32_t myidx = cfirst - (uint32_t)lane;
+      const float4 a = sA[lane], b = sB[lane];
+#pragma unroll
+      for (int p = 0; p < Q; ++p) {
+        const int x0 = tx0 + (p & 1) * 8, y0 = ty0 + (p >> 1) * 8;
+        qb[p] = wave_ballot(lane < cnt && myidx < mq[p] && ellipse_hits(a, b, x0, x0 + 7, y0, y0 + 7));
+      }
+    }
+    uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t cidx = cfirst - j;
+      const float4 A = sA[j];
+      const float4 B = sB[j];
+      const float4 Cc = sC[j];
+      const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
+      const float cxy = B.x, op = B.y;
+      v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
+      float g4 = 0.f, g5 = 0.f;
+      bool hit = false;
+#pragma unroll
+      for (int p = 0; p < Q; ++p) {
+        if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
+        // phase 1: does entry j reach this lane's pixel of quadrant p?
+        const v2f d = mxy - pxy[p];  // (dx, dy) = mean - pixel
+        const v2f q2 = cd * d * d;  // (conic_xx dx^2, conic_yy dy^2)
+        const float power = fmaf(-0.5f, q2.x + q2.y, -((cxy * d.x) * d.y));
+        const float G = __expf(power);
+        const float av = fminf(kMaxAlpha, op * G);
+        const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
+        if (!wave_any(v)) continue;
+        hit = true;
+        // phase 2: branch-free; a lane whose pixel the entry misses runs with
+        // alpha = 0 (T and the accumulated colour pass through exactly) and
+        // dL/dalpha = 0.  Constant factors of the mean2D (0.5 W, 0.5 H) and
+        // conic (-0.5) gradients are applied once per Gaussian in k_gauss_bwd.
+        const float alpha = v ? av : 0.f;
+        const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);  // alpha <= 0.99
+        const float Tn = T[p] * rinv;
+        T[p] = Tn;
+        const float dch = alpha * Tn;
+        // colour / depth behind this contributor: upstream's accum_rec
+        const v2f d01 = c01 - acc01[p], d2d = c2d - acc2d[p];
+        const v2f s2 = d01 * dp01[p] + d2d * dp2d[p];
+        float dLda = (s2.x + s2.y) * Tn + tb[p] * rinv;
+        dLda = v ? dLda : 0.f;
+        acc01[p] += alpha * d01;  // = alpha c + (1 - alpha) accum_rec
+        acc2d[p] += alpha * d2d;
+        const float wg = op * dLda;  // dL/dG
+        const v2f gd = G * d;        // (G dx, G dy)
+        g01 += wg * (gd * cd + v2f{gd.y, gd.x} * cxy);  // (-1) x dG/d(dx, dy) x dL/dG
+        const v2f u = wg * gd;
+        g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG
+        g4 += u.y * d.y;
+        g5 += G * dLda;
+        g67 += dch * dp01[p];
+        g89 += dch * dp2d[p];
+      }
+      if (!hit) continue;  // no pixel of the tile: no partial
+      const float gv[10] = {-g01.x, -g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
+      wave_sum10_store(gv, &sP[j][0]);
+      if (lane == 0) sHit[j] = 1;
+    }
+    __syncthreads();
+    if (lane < cnt && sHit[lane]) {
+      // duplicate slot of (Gaussian, this tile): its first slot plus the
+      // tile's row-major index in the Gaussian's tile rectangle (k_duplicate)
+      const uint32_t gid = sG[lane];
+      const ushort4 rc = rect[gid];
+      const size_t k = slot_start[gid] + (uint32_t)(tile / gx - rc.y) * (uint32_t)(rc.z - rc.x) +
+                       (uint32_t)(tile % gx - rc.x);
+      const float* sv = sP[lane];
+      partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+      partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+      partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
+      pflag[k] = 1;
     }
   }
 }
@@ -623,6 +796,16 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
   static const int ppl = render_ppl("WGSR_BWD_PPL", 1);
+  static const bool quad = [] {
+    const char* e = getenv("WGSR_BWD_MODE");
+    return !(e && strcmp(e, "waves") == 0);
+  }();
+  if (quad) {
+    hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat),
+                       at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T,
+                       n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
+    return hipGetLastError();
+  }
 #define WGSR_BWD(PPL_)                                                                                        \
   hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,              \
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \

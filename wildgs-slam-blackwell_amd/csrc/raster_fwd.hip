@@ -305,8 +305,9 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
       // them); the predicates stay in SGPR lane masks
 #pragma unroll
       for (int p = 0; p < PPL; ++p) {
-        const float dx = A.x - fx[p], dy = A.y - fy[p];
-        const float power = -0.5f * (A.z * dx * dx + A.w * dy * dy) - B.x * dx * dy;
+        const v2f d = v2f{A.x, A.y} - v2f{fx[p], fy[p]};  // (dx, dy) = mean - pixel
+        const v2f q2 = v2f{A.z, A.w} * d * d;               // (conic_xx dx^2, conic_yy dy^2)
+        const float power = fmaf(-0.5f, q2.x + q2.y, -((B.x * d.x) * d.y));
         const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
         const float test_T = T[p] * (1.f - alpha);
         const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;

@@ -261,6 +261,9 @@ __device__ __forceinline__ void lds_to_slab(const float* lds, int ng, int S, flo
   slab_move<false>(dst, ng, S, const_cast<float*>(lds), lane);
 }
 
+// Two packed floats: arithmetic on these lowers to v_pk_*_f32 on gfx950.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
 int render_ppl(const char* env_name, int dflt);
 
