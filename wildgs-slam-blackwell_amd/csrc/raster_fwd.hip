@@ -346,9 +346,9 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
   }
 }
 
-// Quad mode (default): ONE wave per 16x16 tile; lane l owns pixel (l & 7,
-// l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's ellipse
-// against every quadrant that still has live pixels (four ballots); per entry
+// Quad mode (WGSR_FWD_MODE=quad): ONE wave per 16x16 tile; lane l owns pixel
+// (l & 7, l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's
+// ellipse against every quadrant that still has live pixels (four ballots); per entry
 // the wave blends only the quadrants the splat can reach (wave-uniform
 // branches), reads the record from LDS once and issues one n_touched atomic.
 // Packed float2 math for the colour / depth sums.
@@ -518,9 +518,12 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
   static const int ppl = render_ppl("WGSR_FWD_PPL", 1);
+  // WGSR_FWD_MODE=quad selects the one-wave-per-tile kernel (measured ~14 %
+  // slower: the forward has no per-entry reduction to amortise, and 4 waves
+  // per tile hide latency better)
   static const bool quad = [] {
     const char* e = getenv("WGSR_FWD_MODE");
-    return !(e && strcmp(e, "waves") == 0);
+    return e && strcmp(e, "quad") == 0;
   }();
   if (quad) {
     hipLaunchKernelGGL(k_render_fwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat), a.W,
