@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 // the quadrants the splat can reach (wave-uniform branches) -- the culling of
 // the 4-wave layout -- but sums all of them with ONE wave reduction and writes
 // the record without a cross-wave combine.
-__global__ __launch_bounds__(64) void k_render_bwd_quad(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
     const ushort4* __restrict__ rect, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
