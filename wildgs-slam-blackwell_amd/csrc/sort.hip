@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout, const uint32_t* __restrict__ v2in, uint32_t* __restrict__ v2out) {
+    uint32_t* __restrict__ vout) {
   __shared__ uint32_t s_buf[kSortTile];
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
@@ -182,14 +182,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   const uint32_t bid = kOnesweep ? s_vid : blockIdx.x;
   const size_t blk0 = (size_t)bid * kSortTile;
   const size_t base = blk0 + (size_t)w * (64 * kSortItems);
-  uint32_t key[kSortItems], val[kSortItems], val2[kSortItems], rank[kSortItems];
+  uint32_t key[kSortItems], val[kSortItems], rank[kSortItems];
 #pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     key[j] = valid ? kin[e] : 0u;
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
-    val2[j] = (v2in && valid) ? v2in[e] : 0u;
   }
   uint32_t gdig = 0;  // reduce-then-scan: this block's global base of digit t
   if (!kOnesweep) {
@@ -282,18 +281,6 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t i = (uint32_t)t + 256u * r;
     if (i < cnt) vout[dst[r]] = s_buf[i];
   }
-  if (v2in) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kSortItems; ++j)
-      if (base + (size_t)j * 64 + lane < n) s_buf[rank[j]] = val2[j];
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kSortItems; ++r) {
-      const uint32_t i = (uint32_t)t + 256u * r;
-      if (i < cnt) v2out[dst[r]] = s_buf[i];
-    }
-  }
 }
 
 // ---- exclusive scan of u32 values gathered as vals[idx[i]] (idx may be null)
@@ -379,7 +366,7 @@ bool use_onesweep() {
 
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, uint32_t* vals2, uint32_t* vals2_alt) {
+                            hipStream_t stream, bool* result_in_alt) {
   *result_in_alt = false;
   if (n == 0 || end_bit <= begin_bit) {
     if (vals_iota && n > 0) {
@@ -401,7 +388,7 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     hipLaunchKernelGGL(k_onesweep_hist, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit, end_bit,
                        ghist);
   }
-  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt, *wi = vals2, *wo = vals2_alt;
+  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
   bool iota = vals_iota;
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + 8 * p;
@@ -409,18 +396,17 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     if (onesweep) {
       hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n,
                          shift, bits, nb, nullptr, ghist + 256 * p, vcount + p, status + 256 * (size_t)nb * p, ko,
-                         vo, wi, wo);
+                         vo);
     } else {
       // status doubles as the [256][nb] per-block histogram
       hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
       hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, wi, wo);
+                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
     }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;
-    uint32_t* tw = wi; wi = wo; wo = tw;
     *result_in_alt = !*result_in_alt;
   }
   return hipGetLastError();

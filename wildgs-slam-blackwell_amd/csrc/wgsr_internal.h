@@ -11,12 +11,10 @@ namespace wgsr {
 // Stable LSD radix sort on bits [begin_bit, end_bit) (8-bit digits, onesweep).
 // Input in keys/vals (vals ignored if vals_iota: value = input position); the
 // result lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
-// Optional second payload vals2 (ping-pongs with vals2_alt like vals).
 // Scratch: status >= sort_status_bytes(n), totals >= kSortTotalsBytes.
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, uint32_t* vals2 = nullptr,
-                            uint32_t* vals2_alt = nullptr);
+                            hipStream_t stream, bool* result_in_alt);
 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
