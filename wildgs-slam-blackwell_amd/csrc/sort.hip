@@ -153,7 +153,7 @@ constexpr int kLookback = 16;  // predecessor status words fetched per look-back
 // issued by each peer group's lowest lane (a wave's LDS atomics execute in
 // issue order, so the returned counts are the sequential ones and the 16
 // atomics pipeline instead of forming a read-wait-write chain); keys and
-// payloads are staged through one 16 KB LDS buffer in digit order so that each
+// payloads are staged as (key, value) pairs through one 32 KB LDS buffer in digit order so that each
 // digit's run leaves as contiguous stores.
 //   kOnesweep = false: the block's digit offsets come from the scanned
 //     per-block histogram (hist: [256][nb], totals: digit totals).
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout) {
-  __shared__ uint32_t s_buf[kSortTile];
+  __shared__ uint2 s_buf[kSortTile];  // (key, value) pairs in digit order (32 KB)
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
@@ -255,31 +255,21 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   for (int j = 0; j < kSortItems; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const uint32_t d = (key[j] >> shift) & mask;
-    rank[j] = s_lbase[d] + s_wcnt[w][d] + rank[j];  // block-local slot in digit order
-    if (e < n) s_buf[rank[j]] = key[j];
+    const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];  // block-local slot in digit order
+    if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
   }
   __syncthreads();
   const uint32_t cnt = (uint32_t)min((size_t)kSortTile, (size_t)n - blk0);
-  uint32_t dst[kSortItems];
 #pragma unroll
   for (int r = 0; r < kSortItems; ++r) {
     const uint32_t i = (uint32_t)t + 256u * r;
     if (i < cnt) {
-      const uint32_t k = s_buf[i];
-      const uint32_t d = (k >> shift) & mask;
-      dst[r] = s_gbase[d] + (i - s_lbase[d]);
-      kout[dst[r]] = k;
+      const uint2 kv = s_buf[i];
+      const uint32_t d = (kv.x >> shift) & mask;
+      const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
+      kout[dst] = kv.x;
+      vout[dst] = kv.y;
     }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kSortItems; ++j)
-    if (base + (size_t)j * 64 + lane < n) s_buf[rank[j]] = val[j];
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kSortItems; ++r) {
-    const uint32_t i = (uint32_t)t + 256u * r;
-    if (i < cnt) vout[dst[r]] = s_buf[i];
   }
 }
 
