@@ -203,9 +203,13 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   void* image = call_alloc(image_alloc, ctx, IL.total);
   if (!image) return set_error(WGSR_EALLOC, "image buffer allocation failed");
 
-  uint32_t* counter = at<uint32_t>(geom, GL.counter);  // [0] num_rendered, [1] error flags
-  HIPCHK(hipMemsetAsync(counter, 0, 16, s));
-  { StageTimer T(0, s); STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1, s)); }
+  // counter: [0] pairs in the exact tile lists, [1] error flags, then
+  // kRectPairLanes u64 partial sums of upstream's num_rendered (getRect areas)
+  uint32_t* counter = at<uint32_t>(geom, GL.counter);
+  HIPCHK(hipMemsetAsync(counter, 0, 16 + 8 * kRectPairLanes, s));
+  { StageTimer T(0, s);
+  STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
+                                reinterpret_cast<unsigned long long*>(counter + 4), s)); }
 
   // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
   bool in_alt = false;
@@ -219,14 +223,20 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.offs),
                                     at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
   delete scan_timer;
-  uint32_t host_counter[2] = {0, 0};
+  uint32_t host_counter[4 + 2 * kRectPairLanes] = {};
   HIPCHK(hipMemcpyAsync(host_counter, counter, sizeof(host_counter), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
-  const size_t N = host_counter[0];
+  const size_t N = host_counter[0];  // pairs actually listed (<= N_rect)
+  size_t N_rect = 0;
+  for (int i = 0; i < kRectPairLanes; ++i)
+    N_rect += (size_t)host_counter[4 + 2 * i] | ((size_t)host_counter[5 + 2 * i] << 32);
+  if (N > N_rect) return set_error(WGSR_EHIP, "internal: exact tile lists exceed the rectangles");
 
-  const BinLayout BL(N);
+  // the binning layout is sized by upstream's num_rendered (returned to the
+  // caller and handed back to the backward), so both sides agree on it
+  const BinLayout BL(N_rect);
   void* binning = call_alloc(binning_alloc, ctx, BL.total);
   if (!binning && BL.total) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   const uint32_t* sorted_keys = nullptr;
@@ -260,7 +270,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   STAGE(a, s, launch_render_fwd(a, ranges, sorted_g, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, s)); }
-  *num_rendered = (int64_t)N;
+  *num_rendered = (int64_t)N_rect;
   return WGSR_OK;
 }
 

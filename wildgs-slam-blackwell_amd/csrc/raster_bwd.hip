@@ -223,11 +223,9 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
           for (int i = 0; i < WAVES; ++i) s[q] += sHit[i][t] ? sP[i][t][q] : 0.f;
         }
         // duplicate slot of (Gaussian, this tile): its first slot plus the
-        // tile's row-major index in the Gaussian's tile rectangle (k_duplicate)
+        // tile's index in the Gaussian's exact tile list (k_duplicate)
         const uint32_t gid = sG[t];
-        const ushort4 rc = rect[gid];
-        const size_t k = slot_start[gid] + (uint32_t)(tile / gx - rc.y) * (uint32_t)(rc.z - rc.x) +
-                         (uint32_t)(tile % gx - rc.x);
+        const size_t k = slot_start[gid] + pair_local(sA[t], sB[t], rect[gid], (int)(tile % gx), (int)(tile / gx));
         partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
         partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
         partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
@@ -395,11 +393,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     __syncthreads();
     if (lane < cnt && sHit[lane]) {
       // duplicate slot of (Gaussian, this tile): its first slot plus the
-      // tile's row-major index in the Gaussian's tile rectangle (k_duplicate)
+      // tile's index in the Gaussian's exact tile list (k_duplicate)
       const uint32_t gid = sG[lane];
-      const ushort4 rc = rect[gid];
-      const size_t k = slot_start[gid] + (uint32_t)(tile / gx - rc.y) * (uint32_t)(rc.z - rc.x) +
-                       (uint32_t)(tile % gx - rc.x);
+      const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], (int)(tile % gx), (int)(tile / gx));
       const float* sv = sP[lane];
       partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
       partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);

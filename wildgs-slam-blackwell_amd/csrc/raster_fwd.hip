@@ -79,7 +79,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
     ushort4* __restrict__ rect, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag) {
+    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs) {
 #pragma clang fp contract(off)
   extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
@@ -155,20 +155,32 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   const float lim = (o >= kMinAlpha) ? 2.f * logf(255.f * o) : -1.f;
   // record: A = (mean x, mean y, conic xx, conic yy), B = (conic xy, opacity,
   // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
-  splat[3 * (size_t)i + 0] = make_float4(px, py, cc * det_inv, a * det_inv);
-  splat[3 * (size_t)i + 1] = make_float4(-b * det_inv, o, lim, 0.f);
+  const float4 A = make_float4(px, py, cc * det_inv, a * det_inv);
+  const float4 B = make_float4(-b * det_inv, o, lim, 0.f);
+  splat[3 * (size_t)i + 0] = A;
+  splat[3 * (size_t)i + 1] = B;
   splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rect[i] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
-  tiles[i] = (uint32_t)((x1 - x0) * (y1 - y0));
+  // exact tile list length (row_span); upstream's num_rendered counts the rect
+  const Reach rr = reach_of(A, B);
+  uint32_t cnt = 0;
+  for (int ty = y0; ty < y1; ++ty) {
+    int xa;
+    cnt += (uint32_t)row_span(rr, ty, x0, x1, xa);
+  }
+  tiles[i] = cnt;
+  atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], (unsigned long long)((x1 - x0) * (y1 - y0)));
   clamped[i] = cbits;
   dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
   radii[i] = r;
 }
 
-// Expand the tile rectangles of ranks [r0, r0 + 64) (one wave) into pairs.
+// Expand the exact tile lists (row_span) of depth ranks [r0, r0 + 64) (one
+// wave) into pairs: lane <-> pair, so the writes are contiguous.
 __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ sorted_g,
-                                                   const ushort4* __restrict__ rect, uint32_t* __restrict__ keys,
+                                                   const ushort4* __restrict__ rect,
+                                                   const float4* __restrict__ splat, uint32_t* __restrict__ keys,
                                                    uint32_t* __restrict__ slot_g) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) - lane;
@@ -178,14 +190,18 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
   const uint32_t start = offs[r0];
   const uint32_t end = offs[min(r0 + 64, P)];
   uint32_t g = 0, rlo = 0, rhi = 0;
+  float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
   if (r < P) {
     g = sorted_g[r];
     if (offs[r + 1] > my_off) {
       const ushort4 rc = rect[g];
       rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
       rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);
+      A = splat[3 * (size_t)g];
+      B = splat[3 * (size_t)g + 1];
     }
   }
+  const Reach rr = reach_of(A, B);  // this lane's Gaussian; shared per pair below
   for (uint32_t base = start; base < end; base += 64) {
     const uint32_t k = base + lane;
     const uint32_t kk = min(k, end - 1);
@@ -199,9 +215,24 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
     const uint32_t local = kk - __shfl(my_off, lo, 64);
     const uint32_t gg = __shfl(g, lo, 64);
     const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
-    const uint32_t x0 = a & 0xFFFF, y0 = a >> 16, x1 = b & 0xFFFF;
-    const uint32_t w = x1 - x0;
-    const uint32_t ty = y0 + local / w, tx = x0 + local % w;
+    const int x0 = (int)(a & 0xFFFF), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFF), y1 = (int)(b >> 16);
+    Reach rg;
+    rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
+    rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
+    rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
+    rg.ok = __shfl(rr.ok, lo, 64);
+    // walk the rect rows to the one holding list entry `local`
+    uint32_t acc = 0, tx = 0, ty = (uint32_t)y0;
+    for (int row = y0; row < y1; ++row) {
+      int xa;
+      const uint32_t len = (uint32_t)row_span(rg, row, x0, x1, xa);
+      if (local < acc + len) {
+        ty = (uint32_t)row;
+        tx = (uint32_t)xa + (local - acc);
+        break;
+      }
+      acc += len;
+    }
     if (k < end) {
       keys[k] = ty * (uint32_t)gx + tx;
       slot_g[k] = gg;
@@ -482,7 +513,7 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 }  // namespace
 
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, hipStream_t s) {
+                             uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
@@ -491,7 +522,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.tiles),
-                     at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag);
+                     at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs);
   return hipGetLastError();
 }
 
@@ -501,7 +532,7 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
   const GeomLayout L(P);
   const int gx = (a.W + kTile - 1) / kTile;
   hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, s, P, gx, at<uint32_t>(geom, L.offs),
-                     sorted_g, at<ushort4>(geom, L.rect), keys, slot_g);
+                     sorted_g, at<ushort4>(geom, L.rect), at<float4>(geom, L.splat), keys, slot_g);
   return hipGetLastError();
 }
 

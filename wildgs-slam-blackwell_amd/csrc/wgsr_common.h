@@ -261,6 +261,71 @@ __device__ __forceinline__ void lds_to_slab(const float* lds, int ng, int S, flo
   slab_move<false>(dst, ng, S, const_cast<float*>(lds), lane);
 }
 
+// ---- exact tile lists -------------------------------------------------------
+// A splat's reach ellipse {d : d^T conic d <= L}, L = lim * 1.001 + 0.01 (the
+// render culling margin; lim = 2 ln(255 o), k_preprocess), with the invariants
+// the per-row spans need.  Record lanes as in k_preprocess: A = (x, y,
+// conic_xx, conic_yy), B.x = conic_xy, B.z = lim.
+struct Reach {
+  float mx, my, ca, cb, L, det, ey, dya, ica;
+  int ok;  // 1: ellipse, 0: reaches nothing, -1: degenerate conic (keep the rect)
+};
+
+// k_preprocess (count), k_duplicate (enumerate) and k_render_bwd (slot of a
+// pair) must agree bit for bit: FMA contraction is off and only single
+// hardware instructions (v_sqrt_f32, v_rcp_f32) are used for sqrt / 1/x.
+__device__ __forceinline__ Reach reach_of(const float4& A, const float4& B) {
+#pragma clang fp contract(off)
+  Reach r;
+  r.mx = A.x; r.my = A.y; r.ca = A.z; r.cb = B.x;
+  const float cc = A.w;
+  r.L = B.z * 1.001f + 1e-2f;
+  r.det = r.ca * cc - r.cb * r.cb;
+  r.ok = !(B.z >= 0.f) ? 0 : (r.det > 0.f ? 1 : -1);
+  const float idet = __builtin_amdgcn_rcpf(r.det);
+  r.ica = __builtin_amdgcn_rcpf(r.ca);
+  r.ey = __builtin_amdgcn_sqrtf(r.ca * r.L * idet);                  // |dy| extent (dy = mean y - y)
+  const float dxe = __builtin_amdgcn_sqrtf(cc * r.L * idet);          // |dx| extent
+  r.dya = -r.cb * __builtin_amdgcn_rcpf(cc) * dxe;                    // dy where dx = +dxe
+  return r;
+}
+
+// Tile columns [xa, xa + n) of tile row ty that the reach ellipse can touch,
+// clipped to the rect columns [x0, x1).  The ellipse cut by the row's band of
+// pixel-centre y's is convex, so the columns it meets form one interval, found
+// in closed form from the band's extreme x (+0.05 px padding for rounding).
+// Pairs outside these spans cannot reach alpha >= 1/255 at any pixel of their
+// tile, so they are never duplicated; upstream's getRect stays the outer bound.
+__device__ __forceinline__ int row_span(const Reach& r, int ty, int x0, int x1, int& xa) {
+#pragma clang fp contract(off)
+  xa = x0;
+  if (r.ok <= 0) return r.ok < 0 ? x1 - x0 : 0;
+  const float Y0 = (float)(ty * kTile), Y1 = Y0 + (float)(kTile - 1);
+  const float dlo = fmaxf(r.my - Y1, -r.ey), dhi = fminf(r.my - Y0, r.ey);
+  if (dlo > dhi) return 0;
+  const float ylo = fminf(fmaxf(r.dya, dlo), dhi), yhi = fminf(fmaxf(-r.dya, dlo), dhi);
+  const float cL = r.ca * r.L;
+  const float dmax = (-r.cb * ylo + __builtin_amdgcn_sqrtf(fmaxf(cL - r.det * ylo * ylo, 0.f))) * r.ica;
+  const float dmin = (-r.cb * yhi - __builtin_amdgcn_sqrtf(fmaxf(cL - r.det * yhi * yhi, 0.f))) * r.ica;
+  const float pad = 0.05f + 1e-4f * fabsf(r.mx);
+  const float xlo = r.mx - dmax - pad, xhi = r.mx - dmin + pad;  // pixel x = mean x - dx
+  const int a = max((int)ceilf((xlo - (float)(kTile - 1)) * (1.f / kTile)), x0);
+  const int b = min((int)floorf(xhi * (1.f / kTile)) + 1, x1);
+  xa = a;
+  return max(b - a, 0);
+}
+
+// Index of tile (tx, ty) in a splat's exact tile list (row-major over the
+// rect rows from y0); the pair's duplicate slot is slot_start + this.
+__device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B, ushort4 rc, int tx, int ty) {
+  const Reach r = reach_of(A, B);
+  uint32_t acc = 0;
+  int xa;
+  for (int row = rc.y; row < ty; ++row) acc += (uint32_t)row_span(r, row, rc.x, rc.z, xa);
+  row_span(r, ty, rc.x, rc.z, xa);
+  return acc + (uint32_t)(tx - xa);
+}
+
 // Two packed floats: arithmetic on these lowers to v_pk_*_f32 on gfx950.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
@@ -399,6 +464,9 @@ constexpr int kSortTile = 256 * kSortItems;          // keys per radix workgroup
 constexpr int kScanTile = 4096;                      // elements per scan workgroup
 
 __host__ __device__ inline uint32_t sort_blocks(size_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+// upstream num_rendered is accumulated in this many u64 partial sums (spread
+// so that the per-wave atomics of k_preprocess do not serialise on one word)
+constexpr int kRectPairLanes = 64;
 // Onesweep radix sort scratch (sort.hip): look-back status words for up to
 // kMaxSortPasses 8-bit passes, and global digit histograms + block counters.
 constexpr int kMaxSortPasses = 4;
@@ -427,7 +495,7 @@ struct GeomLayout {
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
     bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
-    counter = take(16);
+    counter = take(16 + 8 * kRectPairLanes);  // [0] listed pairs, [1] error flags, then u64 rect-pair partials
     total = o;
   }
 };
