@@ -43,7 +43,7 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 template <int PPL>
 __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ushort4* __restrict__ rect, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
+    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
     uint8_t* __restrict__ pflag) {
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
         // duplicate slot of (Gaussian, this tile): its first slot plus the
         // tile's index in the Gaussian's exact tile list (k_duplicate)
         const uint32_t gid = sG[t];
-        const size_t k = slot_start[gid] + pair_local(sA[t], sB[t], rect[gid], (int)(tile % gx), (int)(tile / gx));
+        const size_t k = slot_start[gid] + pair_local(sA[t], sB[t], rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
         partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
         partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
         partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
 // the record without a cross-wave combine.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ushort4* __restrict__ rect, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
+    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
     uint8_t* __restrict__ pflag) {
@@ -395,7 +395,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       // duplicate slot of (Gaussian, this tile): its first slot plus the
       // tile's index in the Gaussian's exact tile list (k_duplicate)
       const uint32_t gid = sG[lane];
-      const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], (int)(tile % gx), (int)(tile / gx));
+      const size_t k =
+          slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
       const float* sv = sP[lane];
       partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
       partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
@@ -798,13 +799,13 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   }();
   if (quad) {
     hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat),
-                       at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T,
+                       at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T,
                        n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
     return hipGetLastError();
   }
 #define WGSR_BWD(PPL_)                                                                                        \
   hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,              \
-                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
+                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
                      dL_ddepth, partial, pflag)
   if (ppl == 1) WGSR_BWD(1); else if (ppl == 2) WGSR_BWD(2); else WGSR_BWD(4);
 #undef WGSR_BWD

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ushort4* __restrict__ rect, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
+    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs) {
 #pragma clang fp contract(off)
@@ -164,11 +164,22 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   // exact tile list length (row_span); upstream's num_rendered counts the rect
   const Reach rr = reach_of(A, B);
   uint32_t cnt = 0;
+  uint4 tab = make_uint4(0u, 0u, 0u, 0u);
   for (int ty = y0; ty < y1; ++ty) {
     int xa;
-    cnt += (uint32_t)row_span(rr, ty, x0, x1, xa);
+    const uint32_t len = (uint32_t)row_span(rr, ty, x0, x1, xa);
+    const int k = ty - y0;
+    if (k < 4) {
+      tab.x |= len << (8 * k);
+      tab.z |= (uint32_t)(xa - x0) << (8 * k);
+    } else if (k < kRowTab) {
+      tab.y |= len << (8 * (k - 4));
+      tab.w |= (uint32_t)(xa - x0) << (8 * (k - 4));
+    }
+    cnt += len;
   }
   tiles[i] = cnt;
+  rowtab[i] = tab;
   atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], (unsigned long long)((x1 - x0) * (y1 - y0)));
   clamped[i] = cbits;
   dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
@@ -180,6 +191,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
 __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ sorted_g,
                                                    const ushort4* __restrict__ rect,
+                                                   const uint4* __restrict__ rowtab,
                                                    const float4* __restrict__ splat, uint32_t* __restrict__ keys,
                                                    uint32_t* __restrict__ slot_g) {
   const uint32_t lane = threadIdx.x & 63;
@@ -190,18 +202,22 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
   const uint32_t start = offs[r0];
   const uint32_t end = offs[min(r0 + 64, P)];
   uint32_t g = 0, rlo = 0, rhi = 0;
-  float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+  uint4 tab = make_uint4(0u, 0u, 0u, 0u);
+  bool tall = false;  // rows beyond the row table (or a rect too wide for it)
   if (r < P) {
     g = sorted_g[r];
     if (offs[r + 1] > my_off) {
       const ushort4 rc = rect[g];
       rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
       rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);
-      A = splat[3 * (size_t)g];
-      B = splat[3 * (size_t)g + 1];
+      tab = rowtab[g];
+      tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
     }
   }
-  const Reach rr = reach_of(A, B);  // this lane's Gaussian; shared per pair below
+  // rare: some Gaussian of the wave needs spans beyond its row table
+  const bool any_tall = wave_any(tall);
+  Reach rr{};
+  if (any_tall && tall) rr = reach_of(splat[3 * (size_t)g], splat[3 * (size_t)g + 1]);
   for (uint32_t base = start; base < end; base += 64) {
     const uint32_t k = base + lane;
     const uint32_t kk = min(k, end - 1);
@@ -216,22 +232,38 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
     const uint32_t gg = __shfl(g, lo, 64);
     const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
     const int x0 = (int)(a & 0xFFFF), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFF), y1 = (int)(b >> 16);
-    Reach rg;
-    rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
-    rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
-    rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
-    rg.ok = __shfl(rr.ok, lo, 64);
-    // walk the rect rows to the one holding list entry `local`
-    uint32_t acc = 0, tx = 0, ty = (uint32_t)y0;
-    for (int row = y0; row < y1; ++row) {
-      int xa;
-      const uint32_t len = (uint32_t)row_span(rg, row, x0, x1, xa);
-      if (local < acc + len) {
-        ty = (uint32_t)row;
-        tx = (uint32_t)xa + (local - acc);
-        break;
+    const uint4 tb = make_uint4(__shfl(tab.x, lo, 64), __shfl(tab.y, lo, 64), __shfl(tab.z, lo, 64),
+                                __shfl(tab.w, lo, 64));
+    // walk the table rows to the one holding list entry `local`
+    const bool use_tab = x1 - x0 <= 255;
+    const int nt = use_tab ? min(y1 - y0, kRowTab) : 0;
+    uint32_t acc = 0, tx = 0, ty = 0;
+    bool found = false;
+    for (int row = 0; row < nt; ++row) {
+      const uint32_t len = rowtab_len(tb, row);
+      if (!found && local < acc + len) {
+        ty = (uint32_t)(y0 + row);
+        tx = (uint32_t)x0 + rowtab_x(tb, row) + (local - acc);
+        found = true;
       }
-      acc += len;
+      if (!found) acc += len;
+    }
+    if (any_tall) {  // wave-uniform: the shuffles need every lane
+      Reach rg;
+      rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
+      rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
+      rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
+      rg.ok = __shfl(rr.ok, lo, 64);
+      for (int row = y0 + nt; !found && row < y1; ++row) {
+        int xa;
+        const uint32_t len = (uint32_t)row_span(rg, row, x0, x1, xa);
+        if (local < acc + len) {
+          ty = (uint32_t)row;
+          tx = (uint32_t)xa + (local - acc);
+          found = true;
+        }
+        acc += len;
+      }
     }
     if (k < end) {
       keys[k] = ty * (uint32_t)gx + tx;
@@ -521,8 +553,8 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
-                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint32_t>(geom, L.tiles),
-                     at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs);
+                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
+                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs);
   return hipGetLastError();
 }
 
@@ -532,7 +564,8 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
   const GeomLayout L(P);
   const int gx = (a.W + kTile - 1) / kTile;
   hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, s, P, gx, at<uint32_t>(geom, L.offs),
-                     sorted_g, at<ushort4>(geom, L.rect), at<float4>(geom, L.splat), keys, slot_g);
+                     sorted_g, at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<float4>(geom, L.splat),
+                     keys, slot_g);
   return hipGetLastError();
 }
 

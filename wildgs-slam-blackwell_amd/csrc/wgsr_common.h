@@ -315,13 +315,34 @@ __device__ __forceinline__ int row_span(const Reach& r, int ty, int x0, int x1, 
   return max(b - a, 0);
 }
 
+// Row table (written by k_preprocess, 16 B per Gaussian): the spans of the
+// first kRowTab rect rows as bytes, x = lengths of rows 0-3, y = rows 4-7,
+// z = start columns - x0 of rows 0-3, w = rows 4-7 (rect widths are < 256
+// tiles).  Rows past kRowTab are recomputed with row_span.
+constexpr int kRowTab = 8;
+__device__ __forceinline__ bool rowtab_ok(ushort4 rc) { return rc.z - rc.x <= 255; }
+__device__ __forceinline__ uint32_t rowtab_len(const uint4& t, int k) {
+  return ((k < 4 ? t.x : t.y) >> (8 * (k & 3))) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t rowtab_x(const uint4& t, int k) {
+  return ((k < 4 ? t.z : t.w) >> (8 * (k & 3))) & 0xFFu;
+}
+
 // Index of tile (tx, ty) in a splat's exact tile list (row-major over the
 // rect rows from y0); the pair's duplicate slot is slot_start + this.
-__device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B, ushort4 rc, int tx, int ty) {
-  const Reach r = reach_of(A, B);
+__device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B, ushort4 rc, const uint4& tab,
+                                               int tx, int ty) {
+  const int k = ty - rc.y;
+  const bool use_tab = rowtab_ok(rc);
   uint32_t acc = 0;
+  if (use_tab) {
+    const int kt = min(k, kRowTab);
+    for (int row = 0; row < kt; ++row) acc += rowtab_len(tab, row);
+    if (k < kRowTab) return acc + (uint32_t)(tx - rc.x - (int)rowtab_x(tab, k));
+  }
+  const Reach r = reach_of(A, B);
   int xa;
-  for (int row = rc.y; row < ty; ++row) acc += (uint32_t)row_span(r, row, rc.x, rc.z, xa);
+  for (int row = rc.y + (use_tab ? kRowTab : 0); row < ty; ++row) acc += (uint32_t)row_span(r, row, rc.x, rc.z, xa);
   row_span(r, ty, rc.x, rc.z, xa);
   return acc + (uint32_t)(tx - xa);
 }
@@ -477,14 +498,15 @@ constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
 // Per-Gaussian state (geometry buffer).
 struct GeomLayout {
-  size_t splat, rect, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, hist, totals,
+  size_t splat, rect, rowtab, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, hist, totals,
       bsum, counter, total;
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
-    splat = take(48 * P);          // float4 x3: (x, y, conic.x, conic.y) (conic.z, opacity, depth, -) (r, g, b, -)
+    splat = take(48 * P);          // float4 x3: (x, y, conic_xx, conic_yy) (conic_xy, opacity, lim, -) (r, g, b, depth)
     rect = take(8 * P);            // ushort4 tile rectangle [x0, y0, x1, y1)
-    tiles = take(4 * P);           // tiles touched
+    rowtab = take(16 * P);         // uint4 row table: spans of the first kRowTab rect rows (RowTable)
+    tiles = take(4 * P);           // exact tile list length
     clamped = take(4 * P);         // SH clamp flags (3 bits)
     dkey = take(4 * P);            // depth sort keys / sorted keys
     dkey_alt = take(4 * P);
