@@ -18,6 +18,23 @@ namespace wgsr {
 
 namespace {
 thread_local char g_err[1024] = "";
+
+// Pinned host landing zone for the forward's pair counts + the event that
+// marks their arrival (one per host thread; never freed).
+struct HostCounters {
+  uint32_t* buf = nullptr;
+  hipEvent_t ev = nullptr;
+};
+HostCounters& host_counters() {
+  thread_local HostCounters hc;
+  if (!hc.buf) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, kCounterBytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    hc.buf = static_cast<uint32_t*>(p);
+    if (hipEventCreateWithFlags(&hc.ev, hipEventDisableTiming) != hipSuccess) hc.ev = nullptr;
+  }
+  return hc;
+}
 }
 
 int set_error(int code, const char* fmt, ...) {
@@ -203,14 +220,22 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   void* image = call_alloc(image_alloc, ctx, IL.total);
   if (!image) return set_error(WGSR_EALLOC, "image buffer allocation failed");
 
-  // counter: [0] pairs in the exact tile lists, [1] error flags, then
-  // kRectPairLanes u64 partial sums of upstream's num_rendered (getRect areas)
+  // counter block (kCounterBytes): error flags and the partial sums of
+  // upstream's num_rendered and of the exact list lengths, all produced by
+  // k_preprocess
   uint32_t* counter = at<uint32_t>(geom, GL.counter);
-  HIPCHK(hipMemsetAsync(counter, 0, 16 + 8 * kRectPairLanes, s));
+  HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
   { StageTimer T(0, s);
   STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
                                 reinterpret_cast<unsigned long long*>(counter + 4), s)); }
 
+  // The pair counts are known once k_preprocess is done: copy them to pinned
+  // host memory behind it and let the depth sort + scan run while the host
+  // waits for them, allocates the binning buffer and queues the rest.
+  HostCounters& hc = host_counters();
+  if (!hc.buf || !hc.ev) return set_error(WGSR_EHIP, "pinned counter buffer / event allocation failed");
+  HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(hc.ev, s));
   // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
   bool in_alt = false;
   { StageTimer T(1, s);
@@ -223,15 +248,16 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.offs),
                                     at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
   delete scan_timer;
-  uint32_t host_counter[4 + 2 * kRectPairLanes] = {};
-  HIPCHK(hipMemcpyAsync(host_counter, counter, sizeof(host_counter), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipEventSynchronize(hc.ev));
+  const uint32_t* host_counter = hc.buf;
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
-  const size_t N = host_counter[0];  // pairs actually listed (<= N_rect)
-  size_t N_rect = 0;
-  for (int i = 0; i < kRectPairLanes; ++i)
-    N_rect += (size_t)host_counter[4 + 2 * i] | ((size_t)host_counter[5 + 2 * i] << 32);
+  const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
+  size_t N_rect = 0, N = 0;  // upstream num_rendered, pairs actually listed (<= N_rect)
+  for (int i = 0; i < kRectPairLanes; ++i) {
+    N_rect += partial[i];
+    N += partial[kRectPairLanes + i];
+  }
   if (N > N_rect) return set_error(WGSR_EHIP, "internal: exact tile lists exceed the rectangles");
 
   // the binning layout is sized by upstream's num_rendered (returned to the

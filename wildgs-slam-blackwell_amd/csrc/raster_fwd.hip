@@ -67,11 +67,8 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
-// One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
-// (64 x 3M floats, contiguous in HBM) is first staged through LDS with
-// coalesced loads (slab_to_lds), instead of each lane reading its own 3M-float run.
-constexpr int kPreWave = 64;
-__global__ __launch_bounds__(kPreWave) void k_preprocess(
+// One Gaussian of k_preprocess; returns (rect area, exact list length), 0 if culled.
+__device__ __forceinline__ uint2 preprocess_one(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
@@ -79,16 +76,9 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
     ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs) {
+    uint32_t* __restrict__ err_flag,
+    int i, int lane, const float* s_sh) {
 #pragma clang fp contract(off)
-  extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (shs != nullptr && colors == nullptr) {
-    slab_to_lds(shs + (size_t)i0 * 3 * M, min(kPreWave, P - i0), 3 * M, s_sh, lane);
-    __syncthreads();
-  }
-  if (i >= P) return;
   radii[i] = 0;
   n_touched[i] = 0;
   tiles[i] = 0;
@@ -103,7 +93,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   const f3 pv = xform43(c.view, p);
   if (pv.z <= kNearZ) {
     if (prefiltered) atomicOr(err_flag, 1u);
-    return;
+    return make_uint2(0u, 0u);
   }
   float cv[6];
   if (cov_pre) {
@@ -123,7 +113,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   float a, b, cc;
   cov2d(T, S, a, b, cc);
   const float det = a * cc - b * b;
-  if (det == 0.0f) return;
+  if (det == 0.0f) return make_uint2(0u, 0u);
   const float det_inv = 1.f / det;
   const float mid = 0.5f * (a + cc);
   const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -135,7 +125,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   const int y0 = min(gy, max(0, (int)((py - r) / kTile)));
   const int x1 = min(gx, max(0, (int)((px + r + kTile - 1) / kTile)));
   const int y1 = min(gy, max(0, (int)((py + r + kTile - 1) / kTile)));
-  if ((x1 - x0) * (y1 - y0) == 0) return;
+  if ((x1 - x0) * (y1 - y0) == 0) return make_uint2(0u, 0u);
 
   f3 rgb;
   uint32_t cbits = 0;
@@ -180,10 +170,51 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   }
   tiles[i] = cnt;
   rowtab[i] = tab;
-  atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], (unsigned long long)((x1 - x0) * (y1 - y0)));
   clamped[i] = cbits;
   dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
   radii[i] = r;
+  return make_uint2((uint32_t)((x1 - x0) * (y1 - y0)), cnt);
+}
+
+// One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
+// (64 x 3M floats, contiguous in HBM) is first staged through LDS with
+// coalesced loads (slab_to_lds), instead of each lane reading its own 3M-float run.
+constexpr int kPreWave = 64;
+__global__ __launch_bounds__(kPreWave) void k_preprocess(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
+    unsigned long long* __restrict__ list_pairs) {
+
+  extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (shs != nullptr && colors == nullptr) {
+    slab_to_lds(shs + (size_t)i0 * 3 * M, min(kPreWave, P - i0), 3 * M, s_sh, lane);
+    __syncthreads();
+  }
+  uint2 ac = make_uint2(0u, 0u);
+  if (i < P)
+    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, tiles, clamped, dkey, radii,
+                        n_touched, err_flag, i, lane, s_sh);
+  // upstream num_rendered and the exact pair count: one atomic per wave each,
+  // spread over kRectPairLanes words
+  unsigned long long area = ac.x, cnt = ac.y;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    area += __shfl_xor(area, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  if (lane == 0) {
+    atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
+    atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
+  }
 }
 
 // Expand the exact tile lists (row_span) of depth ranks [r0, r0 + 64) (one
@@ -546,6 +577,7 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
                              uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s) {
+  unsigned long long* list_pairs = rect_pairs + kRectPairLanes;
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
@@ -554,7 +586,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
-                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs);
+                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs);
   return hipGetLastError();
 }
 

@@ -488,6 +488,9 @@ __host__ __device__ inline uint32_t sort_blocks(size_t n) { return (uint32_t)((n
 // upstream num_rendered is accumulated in this many u64 partial sums (spread
 // so that the per-wave atomics of k_preprocess do not serialise on one word)
 constexpr int kRectPairLanes = 64;
+// geometry counter block: u32 [0] scan total, [1] error flags, [2..3] pad,
+// then u64 rect-pair partials [kRectPairLanes], then u64 listed-pair partials
+constexpr size_t kCounterBytes = 16 + 2 * 8 * kRectPairLanes;
 // Onesweep radix sort scratch (sort.hip): look-back status words for up to
 // kMaxSortPasses 8-bit passes, and global digit histograms + block counters.
 constexpr int kMaxSortPasses = 4;
@@ -517,7 +520,7 @@ struct GeomLayout {
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
     bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
-    counter = take(16 + 8 * kRectPairLanes);  // [0] listed pairs, [1] error flags, then u64 rect-pair partials
+    counter = take(kCounterBytes);  // see kCounterBytes
     total = o;
   }
 };

@@ -31,7 +31,8 @@ struct RasterGrid {
 };
 
 // forward stages (raster_fwd.hip)
-// rect_pairs += upstream's num_rendered contribution (rect areas)
+// rect_pairs[0..kRectPairLanes) += upstream's num_rendered contributions (rect
+// areas); rect_pairs[kRectPairLanes..2 kRectPairLanes) += exact list lengths
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
                              uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
