@@ -41,6 +41,8 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "rasterised Gaussians/s fwd+bwd @1M pts 1080p; PSNR vs ref"
 HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3    # fp32 vector peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4
 TILE = 16
 
 
@@ -69,6 +71,15 @@ def n_contrib_sum(img_buffer, W, H):
     off = a256(8 * ntile) + a256(4 * W * H)
     nc = img_buffer[off: off + 4 * W * H].view(torch.int32)
     return int(nc.sum().item())
+
+
+def load_pmc_stage(stage):
+    """The committed PMC summary's record for ``stage`` (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        return json.load(open(path)).get("stages", {}).get(stage)
+    except Exception:
+        return None
 
 
 def load_pmc_traffic(stage):
@@ -218,6 +229,20 @@ def main():
             "fwd_TFLOPs": 20 * pairs / (rf[0] / rf[1] * 1e-3) / 1e12 if rf[0] else None,
             "bwd_TFLOPs": 60 * pairs / (rb[0] / rb[1] * 1e-3) / 1e12 if rb[0] else None,
             "peak_TFLOPs": VALU_PEAK_TFLOPS}
+        # the render kernels' actual bound: VALU issue.  Wave-level VALU
+        # instructions per launch (rocprofv3 SQ_INSTS_VALU, profiles/) over
+        # the live launch time, against 1 wave-instruction / 4 cycles / SIMD
+        issue = {}
+        for st in ("render_fwd", "render_bwd"):
+            rec = load_pmc_stage(st)
+            t = timed.get(st)
+            if rec and rec.get("valu_insts_per_launch") and t and t[0]:
+                rate = rec["valu_insts_per_launch"] / (t[0] / t[1] * 1e-3)
+                issue[st] = {"valu_wave_insts": rec["valu_insts_per_launch"],
+                             "achieved_Ginst_s": rate / 1e9, "peak_Ginst_s": VALU_ISSUE_PEAK / 1e9,
+                             "frac": rate / VALU_ISSUE_PEAK}
+        if issue:
+            out["render_valu_issue"] = issue
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_oracle

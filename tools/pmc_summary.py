@@ -59,7 +59,8 @@ def main():
     # grid size of the depth-sort radix kernels: the smallest radix scatter grid
     rg = [g for (k, g) in keys if k == "k_radix_scatter"]
     P_grid = min(rg) if rg else 0
-    rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_launch": 0.0, "launch_kinds": []})
+    rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_launch": 0.0, "valu_insts_per_launch": 0.0,
+                                            "launch_kinds": []})
     hdr = (f"{'kernel':18s} {'grid':>9s} {'FETCH_KB':>10s} {'WRITE_KB':>10s} {'HBM_MB*':>9s} "
            f"{'VALU/wave':>9s} {'VMEM/wave':>9s} {'LDS/wave':>8s} {'wait%':>6s}")
     print(hdr)
@@ -85,6 +86,8 @@ def main():
         st = stage_for(k, g, P_grid)
         if st:
             stages[st]["hbm_bytes_per_launch"] += hbm
+            if valu is not None and waves:
+                stages[st]["valu_insts_per_launch"] += valu  # wave-level VALU instructions
             stages[st]["launch_kinds"].append(k)
     print("* HBM_MB = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 FETCH correction)")
     if out_path:

@@ -34,208 +34,7 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
-// One tile per workgroup of 4 / PPL waves (tile_pixel<PPL> geometry).  Per
-// entry a lane first checks which of its PPL pixels the splat reaches; a wave
-// none of whose pixels it reaches skips the entry.  Otherwise the lane sums
-// its pixels' contributions in registers, one packed wave reduction
-// (wave_sum10_store) yields the wave's 10 partial sums, the waves' sums are
-// added through LDS, and thread j writes entry j's 48-byte record.
-template <int PPL>
-__global__ __launch_bounds__(64 * (4 / PPL)) void k_render_bwd(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
-    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
-    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
-    uint8_t* __restrict__ pflag) {
-  constexpr int WAVES = 4 / PPL;
-  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
-  __shared__ uint32_t sG[kBatch];
-  __shared__ float sP[WAVES][kBatch][11];
-  __shared__ uint32_t sHit[WAVES][kBatch];
-  __shared__ uint32_t s_max[WAVES];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
-  const size_t HW = (size_t)H * W;
-  const uint2 range = ranges[tile];
-  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-  int wx0, wx1, wy0, wy1;
-  wave_box<PPL>(w, tx0, ty0, wx0, wx1, wy0, wy1);
-
-  float fx[PPL], fy[PPL], Tf[PPL], T[PPL], dp0[PPL], dp1[PPL], dp2[PPL], dpd[PPL], bgd[PPL];
-  float acc0[PPL], acc1[PPL], acc2[PPL], accd[PPL];
-  uint32_t last[PPL];
-  uint32_t m = 0;
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    int ox, oy;
-    tile_pixel<PPL>(w, lane, p, ox, oy);
-    const int px = tx0 + ox, py = ty0 + oy;
-    const bool inside = px < W && py < H;
-    const size_t pid = (size_t)py * W + px;
-    fx[p] = (float)px;
-    fy[p] = (float)py;
-    Tf[p] = inside ? final_Ts[pid] : 0.f;
-    last[p] = inside ? n_contrib[pid] : 0u;
-    dp0[p] = inside ? dL_dpix[pid] : 0.f;
-    dp1[p] = inside ? dL_dpix[HW + pid] : 0.f;
-    dp2[p] = inside ? dL_dpix[2 * HW + pid] : 0.f;
-    dpd[p] = inside ? dL_ddep[pid] : 0.f;
-    bgd[p] = bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p];
-    T[p] = Tf[p];
-    acc0[p] = acc1[p] = acc2[p] = accd[p] = 0.f;
-    m = max(m, last[p]);
-  }
-  // entries behind every pixel's last contributor cannot receive gradient
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-  const uint32_t m_wave = m;  // this wave's pixels take gradient from list indices < m_wave only
-  if constexpr (WAVES > 1) {
-    if (lane == 0) s_max[w] = m;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < WAVES; ++i) m = max(m, s_max[i]);
-  }
-  // entries behind every pixel's last contributor get no record: their slot
-  // flags stay 0 (zeroed before the launch), and so does every entry no pixel
-  // of the tile receives gradient from -- typically > 90 % of all pairs
-  const uint32_t end = range.x + m;
-
-  // prefetch pipeline (wave 0, back to front): records of the next batch in
-  // registers, ids one batch further
-  uint32_t gcur = 0, gnext = 0;
-  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (t < kBatch) {
-    if (end >= range.x + 1 + t) {
-      gcur = point_g[end - 1 - t];
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
-    }
-    if (end >= range.x + 1 + kBatch + t) gnext = point_g[end - 1 - kBatch - t];
-  }
-
-  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
-    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
-    __syncthreads();
-    if (t < kBatch) {
-      sA[t] = nA;
-      sB[t] = nB;
-      sC[t] = nC;
-      sG[t] = gcur;
-    }
-    __syncthreads();
-    if (t < kBatch) {
-      gcur = gnext;
-      if (b_end >= range.x + 1 + kBatch + t) {
-        nA = splat[3 * (size_t)gcur];
-        nB = splat[3 * (size_t)gcur + 1];
-        nC = splat[3 * (size_t)gcur + 2];
-      }
-      if (b_end >= range.x + 1 + 2 * kBatch + t) gnext = point_g[b_end - 1 - 2 * kBatch - t];
-    }
-    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
-    // lane j tests entry j's reach box against this wave's pixels; the wave
-    // walks only the entries that can touch it, back to front (a scalar bit loop)
-    sHit[w][lane] = 0;
-    uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < m_wave && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint32_t cidx = cfirst - j;
-      const float4 A = sA[j];
-      const float4 B = sB[j];
-      const float4 Cc = sC[j];
-      // phase 1: which of this lane's pixels does entry j reach? (cheap)
-      float dxv[PPL], dyv[PPL], Gv[PPL], av[PPL];
-      bool vv[PPL];
-      bool any = false;
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        dxv[p] = A.x - fx[p];
-        dyv[p] = A.y - fy[p];
-        const float power = -0.5f * (A.z * dxv[p] * dxv[p] + A.w * dyv[p] * dyv[p]) - B.x * dxv[p] * dyv[p];
-        Gv[p] = __expf(power);
-        av[p] = fminf(kMaxAlpha, B.y * Gv[p]);
-        vv[p] = cidx < last[p] && power <= 0.0f && av[p] >= kMinAlpha;
-        any |= vv[p];
-      }
-      if (!wave_any(any)) continue;  // no pixel of this wave: no partial, skip the heavy part
-      if (lane == 0) sHit[w][j] = 1;
-      // phase 2: branch-free.  A lane whose pixel the entry misses runs the
-      // same code with alpha = 0 (so T and the accumulated colour pass through
-      // unchanged: 1 / (1 - 0) = 1, 0 * c + 1 * acc = acc, and its colour
-      // weight alpha T is 0) and with dL/dalpha zeroed.  Constant factors of
-      // the mean2D (0.5 W, 0.5 H) and conic (-0.5) gradients are applied once
-      // per Gaussian in k_gauss_bwd.
-      float gv[10];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) gv[q] = 0.f;
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        const bool v = vv[p];
-        const float dx = dxv[p], dy = dyv[p], G = Gv[p];
-        const float alpha = v ? av[p] : 0.f;
-        // one v_rcp_f32 serves T and the bg term (alpha <= 0.99 keeps 1 - alpha >= 0.01)
-        const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
-        const float Tn = T[p] * rinv;
-        T[p] = Tn;
-        const float dchannel_dcolor = alpha * Tn;
-        float dL_dalpha = (Cc.x - acc0[p]) * dp0[p];
-        dL_dalpha += (Cc.y - acc1[p]) * dp1[p];
-        dL_dalpha += (Cc.z - acc2[p]) * dp2[p];
-        dL_dalpha += (Cc.w - accd[p]) * dpd[p];
-        dL_dalpha *= Tn;
-        dL_dalpha += (-Tf[p] * rinv) * bgd[p];
-        dL_dalpha = v ? dL_dalpha : 0.f;
-        // colour / depth accumulated behind the next contributor (upstream's
-        // accum_rec = last_alpha * last_colour + (1 - last_alpha) * accum_rec)
-        acc0[p] = alpha * Cc.x + (1.f - alpha) * acc0[p];
-        acc1[p] = alpha * Cc.y + (1.f - alpha) * acc1[p];
-        acc2[p] = alpha * Cc.z + (1.f - alpha) * acc2[p];
-        accd[p] = alpha * Cc.w + (1.f - alpha) * accd[p];
-        const float wg = B.y * dL_dalpha;  // dL/dG
-        const float gdx = G * dx, gdy = G * dy;
-        gv[0] += wg * (-gdx * A.z - gdy * B.x);
-        gv[1] += wg * (-gdy * A.w - gdx * B.x);
-        gv[2] += gdx * dx * wg;
-        gv[3] += gdx * dy * wg;
-        gv[4] += gdy * dy * wg;
-        gv[5] += G * dL_dalpha;
-        gv[6] += dchannel_dcolor * dp0[p];
-        gv[7] += dchannel_dcolor * dp1[p];
-        gv[8] += dchannel_dcolor * dp2[p];
-        gv[9] += dchannel_dcolor * dpd[p];
-      }
-      wave_sum10_store(gv, &sP[w][j][0]);
-    }
-    __syncthreads();
-    if (t < cnt) {
-      uint32_t hit = 0;
-#pragma unroll
-      for (int i = 0; i < WAVES; ++i) hit |= sHit[i][t];
-      if (hit) {
-        float s[10];
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-          s[q] = 0.f;
-#pragma unroll
-          for (int i = 0; i < WAVES; ++i) s[q] += sHit[i][t] ? sP[i][t][q] : 0.f;
-        }
-        // duplicate slot of (Gaussian, this tile): its first slot plus the
-        // tile's index in the Gaussian's exact tile list (k_duplicate)
-        const uint32_t gid = sG[t];
-        const size_t k = slot_start[gid] + pair_local(sA[t], sB[t], rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
-        partial[3 * k] = make_float4(s[0], s[1], s[2], s[3]);
-        partial[3 * k + 1] = make_float4(s[4], s[5], s[6], s[7]);
-        partial[3 * k + 2] = make_float4(s[8], s[9], 0.f, 0.f);
-        pflag[k] = 1;
-      }
-    }
-  }
-}
-
-// Quad mode (default): ONE wave per 16x16 tile; lane l owns pixel (l & 7,
+// ONE wave per 16x16 tile; lane l owns pixel (l & 7,
 // l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's ellipse
 // against each quadrant (four ballots), so per entry the wave evaluates only
 // the quadrants the splat can reach (wave-uniform branches) -- the culling of
@@ -344,6 +143,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const float4 Cc = sC[j];
       const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
       const float cxy = B.x, op = B.y;
+      const v2f cd2 = cd + cd;  // (2 A.z, 2 A.w): d(power2)/d(dx, dy) = (2 A.z dx + B.x dy, 2 A.w dy + B.x dx)
       v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
       float g4 = 0.f, g5 = 0.f;
       bool hit = false;
@@ -352,9 +152,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
         // phase 1: does entry j reach this lane's pixel of quadrant p?
         const v2f d = mxy - pxy[p];  // (dx, dy) = mean - pixel
-        const v2f q2 = cd * d * d;  // (conic_xx dx^2, conic_yy dy^2)
-        const float power = fmaf(-0.5f, q2.x + q2.y, -((cxy * d.x) * d.y));
-        const float G = __expf(power);
+        const v2f q2 = cd * d * d;  // log2(e) x (-conic_xx dx^2 / 2, -conic_yy dy^2 / 2)
+        const float power = q2.x + q2.y + (cxy * d.x) * d.y;  // log2(e) x upstream's power
+        const float G = __builtin_amdgcn_exp2f(power);
         const float av = fminf(kMaxAlpha, op * G);
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
         if (!wave_any(v)) continue;
@@ -377,7 +177,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         acc2d[p] += alpha * d2d;
         const float wg = op * dLda;  // dL/dG
         const v2f gd = G * d;        // (G dx, G dy)
-        g01 += wg * (gd * cd + v2f{gd.y, gd.x} * cxy);  // (-1) x dG/d(dx, dy) x dL/dG
+        g01 += wg * (gd * cd2 + v2f{gd.y, gd.x} * cxy);  // log2(e) x dG/d(dx, dy) x dL/dG
         const v2f u = wg * gd;
         g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG
         g4 += u.y * d.y;
@@ -386,7 +186,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         g89 += dch * dp2d[p];
       }
       if (!hit) continue;  // no pixel of the tile: no partial
-      const float gv[10] = {-g01.x, -g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
+      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
       wave_sum10_store(gv, &sP[j][0]);
       if (lane == 0) sHit[j] = 1;
     }
@@ -538,8 +338,8 @@ __device__ __forceinline__ void sum_partials(uint32_t s0, uint32_t s1, const uin
 
 // factors the render kernel leaves out of its per-pixel terms
 __device__ __forceinline__ void scale_partial_sums(float g[10], int W, int H) {
-  g[0] *= 0.5f * W;  // d(pixel x) / d(NDC x)
-  g[1] *= 0.5f * H;
+  g[0] *= 0.5f * W * (1.f / kL2E);  // d(pixel x) / d(NDC x); power2 is log2(e) x power
+  g[1] *= 0.5f * H * (1.f / kL2E);
   g[2] *= -0.5f;     // dG/dconic
   g[3] *= -0.5f;
   g[4] *= -0.5f;
@@ -786,29 +586,16 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
 
 }  // namespace
 
-hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g, const void* geom, const float* final_T,
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
+                             const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  static const int ppl = render_ppl("WGSR_BWD_PPL", 1);
-  static const bool quad = [] {
-    const char* e = getenv("WGSR_BWD_MODE");
-    return !(e && strcmp(e, "waves") == 0);
-  }();
-  if (quad) {
-    hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat),
-                       at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T,
-                       n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
-    return hipGetLastError();
-  }
-#define WGSR_BWD(PPL_)                                                                                        \
-  hipLaunchKernelGGL(k_render_bwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,              \
-                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,        \
-                     dL_ddepth, partial, pflag)
-  if (ppl == 1) WGSR_BWD(1); else if (ppl == 2) WGSR_BWD(2); else WGSR_BWD(4);
-#undef WGSR_BWD
+  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat),
+                     at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
+                     a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
   return hipGetLastError();
 }
 

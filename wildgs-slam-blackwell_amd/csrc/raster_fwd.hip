@@ -145,8 +145,8 @@ __device__ __forceinline__ uint2 preprocess_one(
   const float lim = (o >= kMinAlpha) ? 2.f * logf(255.f * o) : -1.f;
   // record: A = (mean x, mean y, conic xx, conic yy), B = (conic xy, opacity,
   // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
-  const float4 A = make_float4(px, py, cc * det_inv, a * det_inv);
-  const float4 B = make_float4(-b * det_inv, o, lim, 0.f);
+  const float4 A = make_float4(px, py, kConicSq * (cc * det_inv), kConicSq * (a * det_inv));
+  const float4 B = make_float4(kConicXY * (-b * det_inv), o, lim, 0.f);
   splat[3 * (size_t)i + 0] = A;
   splat[3 * (size_t)i + 1] = B;
   splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
@@ -403,10 +403,10 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
 #pragma unroll
       for (int p = 0; p < PPL; ++p) {
         const v2f d = v2f{A.x, A.y} - v2f{fx[p], fy[p]};  // (dx, dy) = mean - pixel
-        const v2f q2 = v2f{A.z, A.w} * d * d;               // (conic_xx dx^2, conic_yy dy^2)
-        const float power = fmaf(-0.5f, q2.x + q2.y, -((B.x * d.x) * d.y));
-        const float alpha = fminf(kMaxAlpha, B.y * __expf(power));
-        const float test_T = T[p] * (1.f - alpha);
+        const v2f q2 = v2f{A.z, A.w} * d * d;  // log2(e) x (-conic_xx dx^2 / 2, -conic_yy dy^2 / 2)
+        const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
+        const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
+        const float test_T = fmaf(-T[p], alpha, T[p]);  // T (1 - alpha) in one op
         const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;
         const bool stop = live && test_T < kMinT;
         const bool blend = live && !(test_T < kMinT);
@@ -436,130 +436,6 @@ __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
     out_color[HW + pid] = C1[p] + T[p] * bg[1];
     out_color[2 * HW + pid] = C2[p] + T[p] * bg[2];
     out_depth[pid] = Dp[p];
-    out_opac[pid] = 1.f - T[p];
-  }
-}
-
-// Quad mode (WGSR_FWD_MODE=quad): ONE wave per 16x16 tile; lane l owns pixel
-// (l & 7, l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's
-// ellipse against every quadrant that still has live pixels (four ballots); per entry
-// the wave blends only the quadrants the splat can reach (wave-uniform
-// branches), reads the record from LDS once and issues one n_touched atomic.
-// Packed float2 math for the colour / depth sums.
-__global__ __launch_bounds__(64) void k_render_fwd_quad(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
-    float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
-    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
-  constexpr int Q = 4;
-  __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
-  __shared__ uint32_t sG[kFwdBatch];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int lane = threadIdx.x;
-  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
-  v2f pxy[Q], c01[Q], c2d[Q];
-  float T[Q];
-  uint32_t last[Q];
-  uint32_t done = 0;  // bit p: this lane's pixel of quadrant p finished (or outside the image)
-#pragma unroll
-  for (int p = 0; p < Q; ++p) {
-    const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
-    pxy[p] = v2f{(float)px, (float)py};
-    if (!(px < W && py < H)) done |= 1u << p;
-    T[p] = 1.f;
-    c01[p] = v2f{0.f, 0.f};
-    c2d[p] = v2f{0.f, 0.f};
-    last[p] = 0;
-  }
-  const uint2 range = ranges[tile];
-
-  // prefetch pipeline: records of batch b+1 in registers, ids of b+2
-  uint32_t gcur = 0, gnext = 0;
-  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (range.x + lane < range.y) {
-    gcur = point_g[range.x + lane];
-    nA = splat[3 * (size_t)gcur];
-    nB = splat[3 * (size_t)gcur + 1];
-    nC = splat[3 * (size_t)gcur + 2];
-  }
-  if (range.x + kFwdBatch + lane < range.y) gnext = point_g[range.x + kFwdBatch + lane];
-
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
-    // quadrant p is live while any of its pixels is (wave-uniform bits)
-    uint32_t qlive = 0;
-#pragma unroll
-    for (int p = 0; p < Q; ++p) qlive |= wave_any(!(done & (1u << p))) ? (1u << p) : 0u;
-    if (qlive == 0) break;
-    __syncthreads();
-    sA[lane] = nA;
-    sB[lane] = nB;
-    sC[lane] = nC;
-    sG[lane] = gcur;
-    __syncthreads();
-    gcur = gnext;
-    if (b0 + kFwdBatch + lane < range.y) {
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
-    }
-    if (b0 + 2 * kFwdBatch + lane < range.y) gnext = point_g[b0 + 2 * kFwdBatch + lane];
-    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-    const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
-    uint64_t qb[Q];
-    {
-      const float4 a = sA[lane], b = sB[lane];
-#pragma unroll
-      for (int p = 0; p < Q; ++p) {
-        const int x0 = tx0 + (p & 1) * 8, y0 = ty0 + (p >> 1) * 8;
-        qb[p] = wave_ballot(lane < cnt && ((qlive >> p) & 1u) && ellipse_hits(a, b, x0, x0 + 7, y0, y0 + 7));
-      }
-    }
-    uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const float4 A = sA[j];
-      const float4 B = sB[j];
-      const float4 Cc = sC[j];
-      const v2f mxy{A.x, A.y}, cd{A.z, A.w}, col01{Cc.x, Cc.y}, col2d{Cc.z, Cc.w};
-      const float cxy = B.x, op = B.y;
-      uint32_t tot = 0;  // pixels whose T stays above 0.5 (upstream n_touched)
-#pragma unroll
-      for (int p = 0; p < Q; ++p) {
-        if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
-        const v2f d = mxy - pxy[p];
-        const v2f q2 = cd * d * d;
-        const float power = fmaf(-0.5f, q2.x + q2.y, -((cxy * d.x) * d.y));
-        const float alpha = fminf(kMaxAlpha, op * __expf(power));
-        const float test_T = T[p] * (1.f - alpha);
-        const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;
-        const bool stop = live && test_T < kMinT;
-        const bool blend = live && !(test_T < kMinT);
-        const float wgt = blend ? alpha * T[p] : 0.f;
-        c01[p] += col01 * wgt;
-        c2d[p] += col2d * wgt;
-        tot += (uint32_t)__popcll(wave_ballot(blend && test_T > 0.5f));
-        T[p] = blend ? test_T : T[p];
-        last[p] = blend ? cbase + j : last[p];
-        done |= stop ? (1u << p) : 0u;
-      }
-      if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
-      if (wave_all(done == (1u << Q) - 1u)) break;
-    }
-  }
-  const size_t HW = (size_t)H * W;
-  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-#pragma unroll
-  for (int p = 0; p < Q; ++p) {
-    const int px = (int)pxy[p].x, py = (int)pxy[p].y;
-    if (!(px < W && py < H)) continue;
-    const size_t pid = (size_t)py * W + px;
-    final_T[pid] = T[p];
-    n_contrib[pid] = last[p];
-    out_color[pid] = c01[p].x + T[p] * bg0;
-    out_color[HW + pid] = c01[p].y + T[p] * bg1;
-    out_color[2 * HW + pid] = c2d[p].x + T[p] * bg2;
-    out_depth[pid] = c2d[p].y;
     out_opac[pid] = 1.f - T[p];
   }
 }
@@ -614,18 +490,6 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
   static const int ppl = render_ppl("WGSR_FWD_PPL", 1);
-  // WGSR_FWD_MODE=quad selects the one-wave-per-tile kernel (measured ~14 %
-  // slower: the forward has no per-entry reduction to amortise, and 4 waves
-  // per tile hide latency better)
-  static const bool quad = [] {
-    const char* e = getenv("WGSR_FWD_MODE");
-    return e && strcmp(e, "quad") == 0;
-  }();
-  if (quad) {
-    hipLaunchKernelGGL(k_render_fwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat), a.W,
-                       a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T, n_contrib, n_touched);
-    return hipGetLastError();
-  }
 #define WGSR_FWD(PPL_)                                                                                       \
   hipLaunchKernelGGL(k_render_fwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,             \
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,  \

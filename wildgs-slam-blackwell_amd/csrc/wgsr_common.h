@@ -17,6 +17,13 @@ constexpr float kNearZ = 0.2f;        // near-plane cull
 constexpr float kMinAlpha = 1.0f / 255.0f;
 constexpr float kMaxAlpha = 0.99f;
 constexpr float kMinT = 0.0001f;      // early termination
+// The splat record stores the conic pre-scaled so that the render kernels get
+// log2 of the Gaussian falloff directly: power2 = A.z dx^2 + A.w dy^2 + B.x dx dy
+// = log2(e) * power, G = exp2(power2) (one v_exp_f32, no multiply).
+constexpr float kL2E = 1.4426950408889634f;
+constexpr float kConicSq = -0.5f * kL2E;  // A.z = kConicSq conic_xx, A.w = kConicSq conic_yy
+constexpr float kConicXY = -kL2E;         // B.x = kConicXY conic_xy
+constexpr float kUnConicSq = -2.0f / kL2E, kUnConicXY = -1.0f / kL2E;
 
 // ---------------------------------------------------------------------------
 // Wave-level primitives (wave64)
@@ -168,7 +175,7 @@ __device__ __forceinline__ void wave_box(int w, int tx0, int ty0, int& x0, int& 
 __device__ __forceinline__ bool ellipse_hits(const float4& A, const float4& B, int x0, int x1, int y0, int y1) {
   const float lim = B.z;
   if (!(lim >= 0.f)) return false;
-  const float ca = A.z, cb = B.x, cc = A.w;
+  const float ca = A.z * kUnConicSq, cb = B.x * kUnConicXY, cc = A.w * kUnConicSq;
   const float dxl = A.x - (float)x1, dxh = A.x - (float)x0;  // dx range over the rectangle
   const float dyl = A.y - (float)y1, dyh = A.y - (float)y0;
   if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return true;
@@ -277,8 +284,8 @@ struct Reach {
 __device__ __forceinline__ Reach reach_of(const float4& A, const float4& B) {
 #pragma clang fp contract(off)
   Reach r;
-  r.mx = A.x; r.my = A.y; r.ca = A.z; r.cb = B.x;
-  const float cc = A.w;
+  r.mx = A.x; r.my = A.y; r.ca = A.z * kUnConicSq; r.cb = B.x * kUnConicXY;
+  const float cc = A.w * kUnConicSq;
   r.L = B.z * 1.001f + 1e-2f;
   r.det = r.ca * cc - r.cb * r.cb;
   r.ok = !(B.z >= 0.f) ? 0 : (r.det > 0.f ? 1 : -1);
