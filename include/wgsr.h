@@ -112,6 +112,49 @@ int wgsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
 int wgsr_dist_cuda2(int P, const float* points, float* out,
                     wgsr_alloc_fn scratch_alloc, void* alloc_ctx, void* stream);
 
+/* ---- what follows the rasteriser each iteration ---- */
+
+/* One Adam parameter tensor (contiguous fp32, `numel` elements).  The host
+ * supplies torch.optim.Adam's per-step scalars: step_size = lr / (1 -
+ * beta1^step), bias_correction2_sqrt = sqrt(1 - beta2^step). */
+typedef struct wgsr_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  float step_size;
+  float bias_correction2_sqrt;
+} wgsr_adam_tensor;
+#define WGSR_ADAM_MAX_TENSORS 16
+
+/* Replaces optimizer.step() of the reference's torch.optim.Adam(param_groups,
+ * lr=0.0, eps=1e-15) (gaussian_model.py:309; no weight decay, no amsgrad)
+ * for up to WGSR_ADAM_MAX_TENSORS tensors in one launch, element arithmetic
+ * in torch's order: exp_avg.lerp_(grad, 1-beta1);
+ * exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1-beta2);
+ * param.addcdiv_(exp_avg, sqrt(exp_avg_sq)/bias_correction2_sqrt + eps,
+ * -step_size).  beta1/beta2/eps are the Python (double) hyper-parameters:
+ * 1-beta is formed in double and rounded once, as torch does. */
+int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
+                   void* stream);
+
+/* One row-major tensor for row compaction: rows of `row_bytes` (a multiple
+ * of 4) from `src` [P rows]; `dst` receives the kept rows in order. */
+typedef struct wgsr_row_tensor {
+  const void* src;
+  void* dst;
+  int64_t row_bytes;
+} wgsr_row_tensor;
+#define WGSR_COMPACT_MAX_TENSORS 32
+
+/* Replaces prune_points / _prune_optimizer's `t[keep]` (gaussian_model.py:
+ * 526-564) over up to WGSR_COMPACT_MAX_TENSORS per-Gaussian tensors at once:
+ * dst_i = src_i[keep] for every tensor (keep: [P] bytes, 0/1).  Each dst must
+ * hold sum(keep) rows. */
+int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,
+                      wgsr_alloc_fn scratch_alloc, void* alloc_ctx, void* stream);
+
 /* Byte sizes of the forward state buffers (for callers that pre-allocate). */
 size_t wgsr_geometry_bytes(int P);
 size_t wgsr_binning_bytes(int64_t num_rendered, int W, int H);

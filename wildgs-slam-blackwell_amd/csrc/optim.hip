@@ -1,0 +1,259 @@
+// Optimizer step and densification compaction for the Gaussian parameters,
+// gfx950 (the work that follows the rasteriser in
+// every mapping iteration, gaussian_model.py:271-320 and 526-644).
+//
+//  * wgsr_adam_step: torch.optim.Adam's update (the reference's optimizer,
+//    gaussian_model.py:309, lr per parameter group, eps = 1e-15, no weight
+//    decay) for all parameter groups in ONE launch.  torch's foreach Adam
+//    makes ~7 elementwise passes over every tensor; here each element's
+//    (param, grad, exp_avg, exp_avg_sq) is read once and (param, exp_avg,
+//    exp_avg_sq) written once: 28 B per element, HBM bound.
+//  * wgsr_compact_rows: prune_points / _prune_optimizer's `t[mask]` over the
+//    ~21 per-Gaussian tensors (6 params, 12 Adam states, densification stats)
+//    in one scan + one gather launch instead of 21 boolean-index kernels.
+#include <algorithm>
+
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+constexpr int kAdamMax = WGSR_ADAM_MAX_TENSORS;
+
+struct AdamBatch {
+  wgsr_adam_tensor t[kAdamMax];
+  int64_t ustart[kAdamMax + 1];  // first 4-element unit of each tensor (each starts on a unit)
+  int n;
+  float beta2, w1, w2, eps;  // w1 = 1 - beta1, w2 = 1 - beta2, rounded from double like torch's scalars
+};
+
+// Same arithmetic, in the same order, as torch's _multi_tensor_adam (fp32
+// opmath): exp_avg.lerp_(grad, 1 - beta1); exp_avg_sq.mul_(beta2)
+// .addcmul_(grad, grad, 1 - beta2); denom = sqrt(exp_avg_sq) / sqrt(bc2) + eps;
+// param.addcdiv_(exp_avg, denom, -lr / bc1).
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float beta2, float w2,
+                                          float eps, float neg_step, float bc2_sqrt) {
+  m = (w1 < 0.5f) ? m + w1 * (g - m) : g - (g - m) * (1.f - w1);  // lerp
+  v = v * beta2;
+  v = v + w2 * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  p = p + neg_step * (m / denom);
+}
+
+__device__ __forceinline__ void adam_scalar(const wgsr_adam_tensor& T, int64_t e0, float w1, float beta2, float w2,
+                                            float eps) {
+  for (int64_t e = e0; e < min(e0 + 4, T.numel); ++e) {
+    float p = T.param[e], m = T.exp_avg[e], v = T.exp_avg_sq[e];
+    adam_elem(p, T.grad[e], m, v, w1, beta2, w2, eps, -T.step_size, T.bias_correction2_sqrt);
+    T.param[e] = p;
+    T.exp_avg[e] = m;
+    T.exp_avg_sq[e] = v;
+  }
+}
+
+// Grid-stride over tiles of kU x 256 four-element units of the concatenated
+// tensors; thread t owns units tile + j*256 + t (coalesced per j).  All kU
+// units' loads are issued before any math so each thread keeps 4 kU
+// 16-byte loads in flight.  A unit never straddles two tensors (each tensor
+// starts on a unit); ragged tails and unaligned tensors take the scalar path.
+constexpr int kAdamU = 2;
+__global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
+  const int64_t units = b.ustart[b.n];
+  const float w1 = b.w1, w2 = b.w2, beta2 = b.beta2, eps = b.eps;
+  for (int64_t tile = (int64_t)blockIdx.x * (256 * kAdamU); tile < units; tile += (int64_t)gridDim.x * (256 * kAdamU)) {
+    float4 p[kAdamU], g[kAdamU], m[kAdamU], v[kAdamU];
+    int ti[kAdamU];
+    int64_t e0[kAdamU];
+    bool vec[kAdamU];
+#pragma unroll
+    for (int j = 0; j < kAdamU; ++j) {
+      const int64_t u = tile + j * 256 + threadIdx.x;
+      int k = 0;
+      while (k + 1 < b.n && u >= b.ustart[k + 1]) ++k;
+      ti[j] = k;
+      const wgsr_adam_tensor& T = b.t[k];
+      e0[j] = 4 * (u - b.ustart[k]);
+      vec[j] = u < units && e0[j] + 4 <= T.numel &&
+               ((reinterpret_cast<uintptr_t>(T.param) | reinterpret_cast<uintptr_t>(T.grad) |
+                 reinterpret_cast<uintptr_t>(T.exp_avg) | reinterpret_cast<uintptr_t>(T.exp_avg_sq)) & 15) == 0;
+      if (vec[j]) {
+        p[j] = *reinterpret_cast<const float4*>(T.param + e0[j]);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v gv = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(T.grad + e0[j]));
+        g[j] = make_float4(gv.x, gv.y, gv.z, gv.w);
+        m[j] = *reinterpret_cast<const float4*>(T.exp_avg + e0[j]);
+        v[j] = *reinterpret_cast<const float4*>(T.exp_avg_sq + e0[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kAdamU; ++j) {
+      const int64_t u = tile + j * 256 + threadIdx.x;
+      if (u >= units) continue;
+      const wgsr_adam_tensor& T = b.t[ti[j]];
+      if (!vec[j]) {
+        adam_scalar(T, e0[j], w1, beta2, w2, eps);
+        continue;
+      }
+      const float ns = -T.step_size, bc2s = T.bias_correction2_sqrt;
+      adam_elem(p[j].x, g[j].x, m[j].x, v[j].x, w1, beta2, w2, eps, ns, bc2s);
+      adam_elem(p[j].y, g[j].y, m[j].y, v[j].y, w1, beta2, w2, eps, ns, bc2s);
+      adam_elem(p[j].z, g[j].z, m[j].z, v[j].z, w1, beta2, w2, eps, ns, bc2s);
+      adam_elem(p[j].w, g[j].w, m[j].w, v[j].w, w1, beta2, w2, eps, ns, bc2s);
+      *reinterpret_cast<float4*>(T.param + e0[j]) = p[j];
+      *reinterpret_cast<float4*>(T.exp_avg + e0[j]) = m[j];
+      *reinterpret_cast<float4*>(T.exp_avg_sq + e0[j]) = v[j];
+    }
+  }
+}
+
+// ---- row compaction ---------------------------------------------------------
+constexpr int kCompactRows = 4096;  // rows per workgroup (256 threads x 16)
+constexpr int kGatherU = 8;
+
+// keep[r0 .. r0+16) as a bit mask (one 16-B load when aligned and in range)
+__device__ __forceinline__ uint32_t keep_flags16(const uint8_t* __restrict__ keep, int64_t P, int64_t r0) {
+  uint32_t f = 0;
+  if (r0 + 16 <= P && (reinterpret_cast<uintptr_t>(keep) & 15) == 0) {
+    const uint4 q = *reinterpret_cast<const uint4*>(keep + r0);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f |= ((w[i] >> (8 * j)) & 0xffu) ? (1u << (4 * i + j)) : 0u;
+  } else {
+    for (int j = 0; j < 16; ++j)
+      if (r0 + j < P && keep[r0 + j]) f |= 1u << j;
+  }
+  return f;
+}
+
+// per-block count of kept rows
+__global__ __launch_bounds__(256) void k_keep_count(const uint8_t* __restrict__ keep, int64_t P,
+                                                    uint32_t* __restrict__ bcount) {
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kCompactRows + (int64_t)t * 16;
+  const uint32_t c = wave_sum_u32((uint32_t)__popc(keep_flags16(keep, P, r0)));
+  if ((t & 63) == 0) s_tmp[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) bcount[blockIdx.x] = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+}
+
+struct RowBatch {
+  wgsr_row_tensor t[WGSR_COMPACT_MAX_TENSORS];
+  int n;
+};
+
+// Block (x, y) lists the kept rows of row block x (in order) in LDS, then
+// copies tensor y's kept rows to the block's contiguous output range word by
+// word (coalesced stores; reads follow the kept rows).
+__global__ __launch_bounds__(256) void k_compact_gather(const uint8_t* __restrict__ keep, int64_t P,
+                                                        const uint32_t* __restrict__ bbase, RowBatch b) {
+  __shared__ uint16_t s_rows[kCompactRows];
+  __shared__ uint32_t s_wsum[4];
+  const int t = threadIdx.x, w = t >> 6;
+  const int64_t blk0 = (int64_t)blockIdx.x * kCompactRows;
+  const int64_t r0 = blk0 + (int64_t)t * 16;
+  const uint32_t flags = keep_flags16(keep, P, r0);
+  const uint32_t c = (uint32_t)__popc(flags);
+  const uint32_t inc = wave_incl_scan(c);
+  if ((t & 63) == 63) s_wsum[w] = inc;
+  __syncthreads();
+  uint32_t off = inc - c;
+  for (int i = 0; i < w; ++i) off += s_wsum[i];
+  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (flags & (1u << j)) s_rows[off++] = (uint16_t)(t * 16 + j);
+  __syncthreads();
+  const int64_t out0 = bbase[blockIdx.x];
+  {  // one tensor per grid row: blocks x tensors workgroups fill the chip
+    const wgsr_row_tensor& T = b.t[blockIdx.y];
+    const uint32_t wpr = (uint32_t)(T.row_bytes / 4);  // 32-bit words per row
+    const uint32_t* src = static_cast<const uint32_t*>(T.src) + blk0 * wpr;
+    uint32_t* dst = static_cast<uint32_t*>(T.dst) + out0 * wpr;
+    const uint32_t words = total * wpr;  // <= 4096 rows x row words: 32-bit index math
+    const float inv_wpr = 1.f / (float)wpr;
+    // kGatherU independent loads in flight per thread before the stores
+    for (uint32_t k0 = t; k0 < words; k0 += 256 * kGatherU) {
+      uint32_t val[kGatherU];
+#pragma unroll
+      for (int j = 0; j < kGatherU; ++j) {
+        const uint32_t k = k0 + 256 * j;
+        if (k < words) {
+          // k < 2^24: the float quotient is within one of k / wpr
+          uint32_t row = (uint32_t)((float)k * inv_wpr);
+          if (row * wpr > k) --row;
+          else if ((row + 1) * wpr <= k) ++row;
+          val[j] = src[(uint32_t)s_rows[row] * wpr + (k - row * wpr)];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kGatherU; ++j)
+        if (k0 + 256 * j < words) dst[k0 + 256 * j] = val[j];
+    }
+  }
+}
+
+}  // namespace
+
+}  // namespace wgsr
+
+using namespace wgsr;
+
+extern "C" {
+
+int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps, void* stream) {
+  if (n < 0 || n > kAdamMax || (n > 0 && !tensors)) return set_error(WGSR_EINVAL, "wgsr_adam_step: 0..%d tensors", kAdamMax);
+  AdamBatch b{};
+  b.n = n;
+  b.beta2 = (float)beta2;
+  b.w1 = (float)(1.0 - beta1);
+  b.w2 = (float)(1.0 - beta2);
+  b.eps = (float)eps;
+  b.ustart[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    b.t[i] = tensors[i];
+    if (b.t[i].numel < 0 || (b.t[i].numel > 0 && (!b.t[i].param || !b.t[i].grad || !b.t[i].exp_avg ||
+                                                   !b.t[i].exp_avg_sq)))
+      return set_error(WGSR_EINVAL, "wgsr_adam_step: tensor %d has null pointers", i);
+    b.ustart[i + 1] = b.ustart[i] + (b.t[i].numel + 3) / 4;
+  }
+  const int64_t units = b.ustart[n];
+  if (units == 0) return WGSR_OK;
+  const int64_t blocks = std::min<int64_t>((units + 256 * kAdamU - 1) / (256 * kAdamU), 256 * 16);
+  hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_adam_step: %s", hipGetErrorString(e));
+}
+
+int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,
+                      wgsr_alloc_fn scratch_alloc, void* ctx, void* stream) {
+  if (P < 0 || n < 0 || n > WGSR_COMPACT_MAX_TENSORS) return set_error(WGSR_EINVAL, "wgsr_compact_rows: bad sizes");
+  if (P == 0 || n == 0) return WGSR_OK;
+  if (!keep) return set_error(WGSR_EINVAL, "wgsr_compact_rows: null keep mask");
+  RowBatch b{};
+  b.n = n;
+  for (int i = 0; i < n; ++i) {
+    b.t[i] = tensors[i];
+    if (b.t[i].row_bytes <= 0 || (b.t[i].row_bytes & 3) || !b.t[i].src || !b.t[i].dst)
+      return set_error(WGSR_EINVAL, "wgsr_compact_rows: tensor %d needs a positive multiple-of-4 row size", i);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nb = (uint32_t)((P + kCompactRows - 1) / kCompactRows);
+  void* scratch = scratch_alloc(ctx, align256(4 * (size_t)(nb + 1)) + 256);
+  if (!scratch) return set_error(WGSR_EALLOC, "wgsr_compact_rows: scratch allocation failed");
+  uint32_t* bcount = static_cast<uint32_t*>(scratch);
+  hipLaunchKernelGGL(k_keep_count, dim3(nb), dim3(256), 0, s, keep, P, bcount);
+  // exclusive scan of the block counts in place (one workgroup)
+  hipError_t e = exclusive_scan_gather(bcount, nullptr, nb, bcount, nullptr,
+                                       at<uint32_t>(scratch, align256(4 * (size_t)(nb + 1))), nullptr, s);
+  if (e != hipSuccess) return set_error(WGSR_EHIP, "wgsr_compact_rows: %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(k_compact_gather, dim3(nb, (unsigned)n), dim3(256), 0, s, keep, P, bcount, b);
+  e = hipGetLastError();
+  return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_compact_rows: %s", hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -38,6 +38,23 @@ class RasterArgs(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    """Mirror of ``wgsr_adam_tensor``."""
+
+    _fields_ = [("param", _fp), ("grad", _fp), ("exp_avg", _fp), ("exp_avg_sq", _fp),
+                ("numel", ctypes.c_int64), ("step_size", ctypes.c_float),
+                ("bias_correction2_sqrt", ctypes.c_float)]
+
+
+class RowTensor(ctypes.Structure):
+    """Mirror of ``wgsr_row_tensor``."""
+
+    _fields_ = [("src", _fp), ("dst", _fp), ("row_bytes", ctypes.c_int64)]
+
+
+ADAM_MAX_TENSORS = 16
+COMPACT_MAX_TENSORS = 32
+
 _lib = None
 _lock = threading.Lock()
 
@@ -78,6 +95,12 @@ def load():
         L.wgsr_binning_bytes.argtypes = [c_i64, c_int, c_int]
         L.wgsr_image_bytes.restype = c_sz
         L.wgsr_image_bytes.argtypes = [c_int, c_int]
+        L.wgsr_adam_step.restype = c_int
+        L.wgsr_adam_step.argtypes = [ctypes.POINTER(AdamTensor), c_int, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, _fp]
+        L.wgsr_compact_rows.restype = c_int
+        L.wgsr_compact_rows.argtypes = [_fp, c_i64, ctypes.POINTER(RowTensor), c_int, ALLOC_FN,
+                                        ctypes.c_void_p, _fp]
         L.wgsr_last_error.restype = ctypes.c_char_p
         L.wgsr_last_error.argtypes = []
         L.wgsr_version.restype = ctypes.c_char_p
@@ -96,6 +119,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_rasterize_forward", "wgsr_rasterize_backward", "wgsr_mark_visible", "wgsr_dist_cuda2",
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
     "wgsr_version", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
+    "wgsr_adam_step", "wgsr_compact_rows",
 )
 
 
