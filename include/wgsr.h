@@ -155,6 +155,33 @@ typedef struct wgsr_row_tensor {
 int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,
                       wgsr_alloc_fn scratch_alloc, void* alloc_ctx, void* stream);
 
+/* ---- SSIM for the mapping loss -------------------
+ * Images are `planes` contiguous H x W fp32 planes (any leading dims
+ * flattened; zero padding at the borders, as F.conv2d(padding=ws//2)).
+ * window_size in {3,5,7,9,11}; Gaussian window, sigma 1.5.
+ *
+ * wgsr_ssim_forward replaces loss_utils.ssim(img1, img2, window_size)
+ * (thirdparty/gaussian_splatting/utils/loss_utils.py:61-101): *mean = mean
+ * SSIM over all pixels (size_average=True), plane_mean[p] (optional) = per
+ * plane mean.  dmap (optional, 3 x planes x H x W floats) receives the
+ * per-pixel derivatives the backward needs (dS/dmu1, dS/dE[x^2], dS/dE[xy]).
+ * Scratch: wgsr_ssim_scratch_bytes(planes, H, W) through scratch_alloc. */
+size_t wgsr_ssim_scratch_bytes(int64_t planes, int H, int W);
+int wgsr_ssim_forward(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
+                      float* dmap, float* plane_mean, float* mean, wgsr_alloc_fn scratch_alloc, void* alloc_ctx,
+                      void* stream);
+/* dL/dimg1 of the forward above given plane_scale[p] = dL/dS for every pixel
+ * of plane p (device array; e.g. dL/dmean / (planes*H*W)).  img2 gets no
+ * gradient (the reference passes the ground-truth image there). */
+int wgsr_ssim_backward(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
+                       const float* dmap, const float* plane_scale, float* grad_img1, void* stream);
+/* compute_ssim_components(img1, img2, window_size) (src/utils/dyn_uncertainty/
+ * mapping_utils.py:99-204) for `images` images of `channels` planes each:
+ * channel means of the clipped luminance, contrast and structure maps
+ * (each images x H x W).  Forward only (the reference detaches them). */
+int wgsr_ssim_components(const float* img1, const float* img2, int64_t images, int channels, int H, int W,
+                         int window_size, float* luminance, float* contrast, float* structure, void* stream);
+
 /* Byte sizes of the forward state buffers (for callers that pre-allocate). */
 size_t wgsr_geometry_bytes(int P);
 size_t wgsr_binning_bytes(int64_t num_rendered, int W, int H);

@@ -23,6 +23,10 @@ for s in $STEPS; do
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile > $GRAFT_REPO_ROOT/$OUT/prof_bench.json 2> $GRAFT_REPO_ROOT/$OUT/prof.err); rc=$? ;;
     f1)
       timeout -k 10 300 python tools/bench_f1.py > $OUT/bench_f1.json 2> $OUT/bench_f1.err; rc=$? ;;
+    f2)
+      timeout -k 10 300 python tools/bench_f2.py > $OUT/bench_f2.json 2> $OUT/bench_f2.err; rc=$? ;;
+    f2prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f2prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f2.py > $GRAFT_REPO_ROOT/$OUT/f2prof.json 2> $GRAFT_REPO_ROOT/$OUT/f2prof.err); rc=$? ;;
     f1prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f1prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f1.py --iters 20 > $GRAFT_REPO_ROOT/$OUT/f1prof.json 2> $GRAFT_REPO_ROOT/$OUT/f1prof.err); rc=$? ;;
     pmc_fetch)

@@ -101,6 +101,15 @@ def load():
         L.wgsr_compact_rows.restype = c_int
         L.wgsr_compact_rows.argtypes = [_fp, c_i64, ctypes.POINTER(RowTensor), c_int, ALLOC_FN,
                                         ctypes.c_void_p, _fp]
+        L.wgsr_ssim_scratch_bytes.restype = ctypes.c_size_t
+        L.wgsr_ssim_scratch_bytes.argtypes = [c_i64, c_int, c_int]
+        L.wgsr_ssim_forward.restype = c_int
+        L.wgsr_ssim_forward.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, _fp, _fp, _fp, ALLOC_FN,
+                                        ctypes.c_void_p, _fp]
+        L.wgsr_ssim_backward.restype = c_int
+        L.wgsr_ssim_backward.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, _fp, _fp, _fp, _fp]
+        L.wgsr_ssim_components.restype = c_int
+        L.wgsr_ssim_components.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, c_int, _fp, _fp, _fp, _fp]
         L.wgsr_last_error.restype = ctypes.c_char_p
         L.wgsr_last_error.argtypes = []
         L.wgsr_version.restype = ctypes.c_char_p
@@ -120,6 +129,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
     "wgsr_version", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_compact_rows",
+    "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
 )
 
 
