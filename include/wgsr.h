@@ -182,6 +182,25 @@ int wgsr_ssim_backward(const float* img1, const float* img2, int64_t planes, int
 int wgsr_ssim_components(const float* img1, const float* img2, int64_t images, int channels, int H, int W,
                          int window_size, float* luminance, float* contrast, float* structure, void* stream);
 
+/* ---- PLY vertex records ------------------------
+ * GaussianModel.save_ply / load_ply (gaussian_model.py:338-493) keep the
+ * Gaussians as P fixed-size records of `ncol` float32 properties.  A column
+ * set names one contiguous device tensor [P, cols] and, for each of its
+ * columns, the record column it maps to.  pack writes records (record
+ * columns no set maps -- the reference's zero normals -- become 0); unpack
+ * reads them.  Both run on the device (LDS transpose, coalesced on both
+ * sides); the host moves only the record block between file and HBM. */
+#define WGSR_PLY_MAX_TENSORS 8
+#define WGSR_PLY_MAX_COLS 128
+typedef struct wgsr_ply_column_set {
+  float* data;              /* [P, cols] contiguous fp32 (device) */
+  int cols;
+  const int* record_col;    /* host array [cols] */
+} wgsr_ply_column_set;
+int wgsr_ply_pack(const wgsr_ply_column_set* sets, int ntens, int64_t P, int ncol, float* records, void* stream);
+int wgsr_ply_unpack(const float* records, int64_t P, int ncol, const wgsr_ply_column_set* sets, int ntens,
+                    void* stream);
+
 /* Byte sizes of the forward state buffers (for callers that pre-allocate). */
 size_t wgsr_geometry_bytes(int P);
 size_t wgsr_binning_bytes(int64_t num_rendered, int W, int H);

@@ -27,6 +27,10 @@ for s in $STEPS; do
       timeout -k 10 300 python tools/bench_f2.py > $OUT/bench_f2.json 2> $OUT/bench_f2.err; rc=$? ;;
     f2prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f2prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f2.py > $GRAFT_REPO_ROOT/$OUT/f2prof.json 2> $GRAFT_REPO_ROOT/$OUT/f2prof.err); rc=$? ;;
+    f3)
+      timeout -k 10 300 python tools/bench_f3.py > $OUT/bench_f3.json 2> $OUT/bench_f3.err; rc=$? ;;
+    f3prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f3prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f3.py > $GRAFT_REPO_ROOT/$OUT/f3prof.json 2> $GRAFT_REPO_ROOT/$OUT/f3prof.err); rc=$? ;;
     f1prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f1prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f1.py --iters 20 > $GRAFT_REPO_ROOT/$OUT/f1prof.json 2> $GRAFT_REPO_ROOT/$OUT/f1prof.err); rc=$? ;;
     pmc_fetch)

@@ -52,6 +52,14 @@ class RowTensor(ctypes.Structure):
     _fields_ = [("src", _fp), ("dst", _fp), ("row_bytes", ctypes.c_int64)]
 
 
+class PlyColumnSet(ctypes.Structure):
+    """Mirror of ``wgsr_ply_column_set``."""
+
+    _fields_ = [("data", _fp), ("cols", ctypes.c_int), ("record_col", ctypes.POINTER(ctypes.c_int))]
+
+
+PLY_MAX_TENSORS = 8
+PLY_MAX_COLS = 128
 ADAM_MAX_TENSORS = 16
 COMPACT_MAX_TENSORS = 32
 
@@ -110,6 +118,10 @@ def load():
         L.wgsr_ssim_backward.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, _fp, _fp, _fp, _fp]
         L.wgsr_ssim_components.restype = c_int
         L.wgsr_ssim_components.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, c_int, _fp, _fp, _fp, _fp]
+        L.wgsr_ply_pack.restype = c_int
+        L.wgsr_ply_pack.argtypes = [ctypes.POINTER(PlyColumnSet), c_int, c_i64, c_int, _fp, _fp]
+        L.wgsr_ply_unpack.restype = c_int
+        L.wgsr_ply_unpack.argtypes = [_fp, c_i64, c_int, ctypes.POINTER(PlyColumnSet), c_int, _fp]
         L.wgsr_last_error.restype = ctypes.c_char_p
         L.wgsr_last_error.argtypes = []
         L.wgsr_version.restype = ctypes.c_char_p
@@ -130,6 +142,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_version", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_compact_rows",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
+    "wgsr_ply_pack", "wgsr_ply_unpack",
 )
 
 
