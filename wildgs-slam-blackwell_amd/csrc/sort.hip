@@ -2,7 +2,8 @@
 //
 // Replaces the CUB primitives upstream's rasteriser and simple-knn lean on
 // (cub::DeviceRadixSort::SortPairs, cub::DeviceScan::InclusiveSum: SURVEY.md
-// 2 "Kernel inventory").  8-bit digits; a workgroup owns 4096 keys.  Two
+// 2 "Kernel inventory").  8-bit digits; a workgroup owns 4096 keys (2048 for
+// sorts of <= 2M keys, so a per-Gaussian pass still fills the chip).  Two
 // schedules share one scatter kernel:
 //  * reduce-then-scan (default): per pass, block histograms -> per-digit row
 //    scan over blocks -> stable scatter;
@@ -12,7 +13,7 @@
 // Block-local stable ranking uses 64-bit ballots to find the lanes that share
 // a digit; the scatter stages the block's keys in LDS in digit order so that
 // runs of one digit leave as contiguous (coalesced) stores.  Each wave of the
-// scatter owns a contiguous run of 1024 keys that it walks 64 at a time, so
+// scatter owns a contiguous run of 64 I keys that it walks 64 at a time, so
 // ranks follow input order.
 #include <stdlib.h>
 #include <string.h>
@@ -43,36 +44,36 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_t
 }
 
 // ---- digit counting ----------------------------------------------------------
-// Histogram kernels give thread t of a block the 16 CONTIGUOUS keys
-// [16 t, 16 t + 16) of the block's 4096 and count them one LDS atomic per run
+// Histogram kernels give thread t of a block the I CONTIGUOUS keys
+// [I t, I t + I) of the block's 256 I and count them one LDS atomic per run
 // of equal digits: the sort inputs here (depth bits, tile ids in duplicate
 // order, Morton codes) have long runs in their high digits, which would
 // otherwise serialise as same-address LDS atomics.
 
-__device__ __forceinline__ int load_run16(const uint32_t* __restrict__ keys, size_t n, size_t e0,
-                                          uint32_t (&k)[kSortItems]) {
-  static_assert(kSortItems == 16, "load_run16 reads 4 x uint4");
-  if (e0 + kSortItems <= n) {
+template <int I>
+__device__ __forceinline__ int load_run(const uint32_t* __restrict__ keys, size_t n, size_t e0, uint32_t (&k)[I]) {
+  static_assert(I % 4 == 0, "load_run reads uint4s");
+  if (e0 + I <= n) {
     const uint4* p = reinterpret_cast<const uint4*>(keys + e0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < I / 4; ++q) {
       const uint4 v = p[q];
       k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
     }
-    return kSortItems;
+    return I;
   }
   const int nv = e0 < n ? (int)(n - e0) : 0;
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) k[j] = j < nv ? keys[e0 + j] : 0u;
+  for (int j = 0; j < I; ++j) k[j] = j < nv ? keys[e0 + j] : 0u;
   return nv;
 }
 
-__device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[kSortItems], int nv, int shift,
-                                         uint32_t mask) {
+template <int I>
+__device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[I], int nv, int shift, uint32_t mask) {
   if (nv <= 0) return;
   uint32_t cur = (k[0] >> shift) & mask, run = 0;
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
+  for (int j = 0; j < I; ++j) {
     if (j < nv) {
       const uint32_t d = (k[j] >> shift) & mask;
       if (d != cur) {
@@ -88,13 +89,14 @@ __device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[kSortI
 
 // Reduce-then-scan mode, step 1: per-block histogram of one pass, stored
 // digit-major: hist[d * nb + block].
+template <int I>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     int bits, uint32_t nb, uint32_t* __restrict__ hist) {
   __shared__ uint32_t s_h[256];
   const int t = threadIdx.x;
   s_h[t] = 0;
-  uint32_t k[kSortItems];
-  const int nv = load_run16(keys, n, (size_t)blockIdx.x * kSortTile + (size_t)t * kSortItems, k);
+  uint32_t k[I];
+  const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, k);
   __syncthreads();
   add_runs(s_h, k, nv, shift, (1u << bits) - 1u);
   __syncthreads();
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hi
 }
 
 // Onesweep mode: global digit histograms of every pass in one read of the keys.
+template <int I>
 __global__ __launch_bounds__(256) void k_onesweep_hist(const uint32_t* __restrict__ keys, uint32_t n, int begin_bit,
                                                        int end_bit, uint32_t* __restrict__ ghist) {
   __shared__ uint32_t s_h[kMaxSortPasses][256];
@@ -130,12 +133,13 @@ __global__ __launch_bounds__(256) void k_onesweep_hist(const uint32_t* __restric
   const int passes = (end_bit - begin_bit + 7) / 8;
 #pragma unroll
   for (int p = 0; p < kMaxSortPasses; ++p) s_h[p][t] = 0;
-  uint32_t k[kSortItems];
-  const int nv = load_run16(keys, n, (size_t)blockIdx.x * kSortTile + (size_t)t * kSortItems, k);
+  uint32_t k[I];
+  const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, k);
   __syncthreads();
+  const int per = (end_bit - begin_bit + passes - 1) / passes;
   for (int p = 0; p < passes; ++p) {
-    const int shift = begin_bit + 8 * p;
-    add_runs(s_h[p], k, nv, shift, (1u << min(8, end_bit - shift)) - 1u);
+    const int shift = begin_bit + per * p;
+    add_runs(s_h[p], k, nv, shift, (1u << min(per, end_bit - shift)) - 1u);
   }
   __syncthreads();
   for (int p = 0; p < passes; ++p)
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(256) void k_onesweep_hist(const uint32_t* __restric
 constexpr uint32_t kStAgg = 1u << 30, kStPre = 2u << 30, kStCount = (1u << 30) - 1u;
 constexpr int kLookback = 16;  // predecessor status words fetched per look-back round trip
 
-// One stable digit pass over a block of 4096 keys.  Keys/payloads are loaded
+// One stable digit pass over a block of 256 I keys.  Keys/payloads are loaded
 // up front (in flight while ranking); ranks come from LDS atomics-with-return
 // issued by each peer group's lowest lane (a wave's LDS atomics execute in
 // issue order, so the returned counts are the sequential ones and the 16
@@ -161,13 +165,14 @@ constexpr int kLookback = 16;  // predecessor status words fetched per look-back
 //     waits on is already running), publishes its digit counts and looks back
 //     through its predecessors' status words (totals: this pass's global
 //     digit histogram).
-template <bool kOnesweep>
+template <bool kOnesweep, int I>
 __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout) {
-  __shared__ uint2 s_buf[kSortTile];  // (key, value) pairs in digit order (32 KB)
+  constexpr int kTile = 256 * I;
+  __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16)
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
@@ -180,11 +185,11 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
   if (kOnesweep) __syncthreads();
   const uint32_t bid = kOnesweep ? s_vid : blockIdx.x;
-  const size_t blk0 = (size_t)bid * kSortTile;
-  const size_t base = blk0 + (size_t)w * (64 * kSortItems);
-  uint32_t key[kSortItems], val[kSortItems], rank[kSortItems];
+  const size_t blk0 = (size_t)bid * kTile;
+  const size_t base = blk0 + (size_t)w * (64 * I);
+  uint32_t key[I], val[I], rank[I];
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
+  for (int j = 0; j < I; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     key[j] = valid ? kin[e] : 0u;
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     gdig = ex + hist[(size_t)t * nb + bid];
   }
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
+  for (int j = 0; j < I; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     const uint32_t d = (key[j] >> shift) & mask;
@@ -252,16 +257,16 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kSortItems; ++j) {
+  for (int j = 0; j < I; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const uint32_t d = (key[j] >> shift) & mask;
     const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];  // block-local slot in digit order
     if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
   }
   __syncthreads();
-  const uint32_t cnt = (uint32_t)min((size_t)kSortTile, (size_t)n - blk0);
+  const uint32_t cnt = (uint32_t)min((size_t)kTile, (size_t)n - blk0);
 #pragma unroll
-  for (int r = 0; r < kSortItems; ++r) {
+  for (int r = 0; r < I; ++r) {
     const uint32_t i = (uint32_t)t + 256u * r;
     if (i < cnt) {
       const uint2 kv = s_buf[i];
@@ -345,11 +350,14 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 
 }  // namespace
 
-// WGSR_SORT=onesweep | rts (reduce-then-scan, the default)
-bool use_onesweep() {
-  static const bool v = [] {
+// WGSR_SORT=onesweep | onesweep_small (only sorts of <= kSmallSortN keys) |
+// rts (reduce-then-scan, the default)
+int sort_mode() {
+  static const int v = [] {
     const char* e = getenv("WGSR_SORT");
-    return e && strcmp(e, "onesweep") == 0;
+    if (e && strcmp(e, "onesweep") == 0) return 1;
+    if (e && strcmp(e, "onesweep_small") == 0) return 2;
+    return 0;
   }();
   return v;
 }
@@ -368,31 +376,53 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
   const int passes = (end_bit - begin_bit + 7) / 8;
   if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;
   const uint32_t nb = sort_blocks(n);
-  const bool onesweep = use_onesweep();
+  const bool small = sort_items(n) == kSmallSortItems;
+  const bool onesweep = sort_mode() == 1 || (sort_mode() == 2 && small);
   uint32_t* ghist = totals;                          // onesweep: [passes][256]; rts: digit totals
   uint32_t* vcount = totals + kMaxSortPasses * 256;  // onesweep: virtual block counters [passes]
   if (onesweep) {
     hipError_t e = hipMemsetAsync(totals, 0, kSortTotalsBytes, stream);
     if (e == hipSuccess) e = hipMemsetAsync(status, 0, 4 * 256 * (size_t)nb * passes, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_onesweep_hist, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit, end_bit,
-                       ghist);
+    if (small)
+      hipLaunchKernelGGL(k_onesweep_hist<kSmallSortItems>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
+                         begin_bit, end_bit, ghist);
+    else
+      hipLaunchKernelGGL(k_onesweep_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
+                         end_bit, ghist);
   }
   uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
   bool iota = vals_iota;
+  // balanced digits (13 tile-id bits -> 7 + 6, not 8 + 5): wider per-block
+  // digit runs leave as longer contiguous stores in every pass
+  const int per = (end_bit - begin_bit + passes - 1) / passes;
   for (int p = 0; p < passes; ++p) {
-    const int shift = begin_bit + 8 * p;
-    const int bits = min(8, end_bit - shift);
+    const int shift = begin_bit + per * p;
+    const int bits = min(per, end_bit - shift);
     if (onesweep) {
-      hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n,
-                         shift, bits, nb, nullptr, ghist + 256 * p, vcount + p, status + 256 * (size_t)nb * p, ko,
-                         vo);
+      if (small)
+        hipLaunchKernelGGL((k_radix_scatter<true, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
+                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
+                           status + 256 * (size_t)nb * p, ko, vo);
+      else
+        hipLaunchKernelGGL((k_radix_scatter<true, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
+                           (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
+                           status + 256 * (size_t)nb * p, ko, vo);
     } else {
       // status doubles as the [256][nb] per-block histogram
-      hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status);
+      if (small)
+        hipLaunchKernelGGL(k_radix_hist<kSmallSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift,
+                           bits, nb, status);
+      else
+        hipLaunchKernelGGL(k_radix_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits,
+                           nb, status);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
-      hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
+      if (small)
+        hipLaunchKernelGGL((k_radix_scatter<false, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
+                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
+      else
+        hipLaunchKernelGGL((k_radix_scatter<false, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
+                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
     }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;

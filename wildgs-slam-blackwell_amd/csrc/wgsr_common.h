@@ -487,11 +487,24 @@ __device__ __forceinline__ void cov2d(const float T[2][3], const float S[3][3], 
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-constexpr int kSortItems = 16;                      // keys per thread in radix passes
-constexpr int kSortTile = 256 * kSortItems;          // keys per radix workgroup
-constexpr int kScanTile = 4096;                      // elements per scan workgroup
+// Radix passes: 256-thread workgroups of kSortItems keys per thread; sorts of
+// up to kSmallSortN keys (the per-Gaussian depth / Morton sorts) use
+// kSmallSortItems so that a 1M-key pass still spreads over ~1000 workgroups
+// (4096-key tiles would leave a 1M-key pass at 245, under one per CU; 2048-key
+// tiles measured faster than 1024).
+#ifndef WGSR_SMALL_SORT_ITEMS
+#define WGSR_SMALL_SORT_ITEMS 8
+#endif
+constexpr int kSortItems = 16;
+constexpr int kSmallSortItems = WGSR_SMALL_SORT_ITEMS;
+constexpr size_t kSmallSortN = size_t(1) << 21;
+constexpr int kScanTile = 1024;                      // elements per scan workgroup
 
-__host__ __device__ inline uint32_t sort_blocks(size_t n) { return (uint32_t)((n + kSortTile - 1) / kSortTile); }
+__host__ __device__ inline int sort_items(size_t n) { return n <= kSmallSortN ? kSmallSortItems : kSortItems; }
+__host__ __device__ inline uint32_t sort_blocks(size_t n) {
+  const size_t tile = 256 * (size_t)sort_items(n);
+  return (uint32_t)((n + tile - 1) / tile);
+}
 // upstream num_rendered is accumulated in this many u64 partial sums (spread
 // so that the per-wave atomics of k_preprocess do not serialise on one word)
 constexpr int kRectPairLanes = 64;
@@ -501,8 +514,13 @@ constexpr size_t kCounterBytes = 16 + 2 * 8 * kRectPairLanes;
 // Onesweep radix sort scratch (sort.hip): look-back status words for up to
 // kMaxSortPasses 8-bit passes, and global digit histograms + block counters.
 constexpr int kMaxSortPasses = 4;
+// Sized so that any sort of n' <= n keys fits (buffers sized for an upper
+// bound, e.g. upstream's rectangle pair count, sort the exact count).
 __host__ __device__ inline size_t sort_status_bytes(size_t n) {
-  return 4ull * 256 * sort_blocks(n) * kMaxSortPasses;
+  const size_t small = n < kSmallSortN ? n : kSmallSortN;
+  const size_t b_small = (small + 256 * kSmallSortItems - 1) / (256 * kSmallSortItems);
+  const size_t b_large = (n + 256 * kSortItems - 1) / (256 * kSortItems);
+  return 4ull * 256 * (b_small > b_large ? b_small : b_large) * kMaxSortPasses;
 }
 constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
