@@ -270,7 +270,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   if (N > 0) {
     { StageTimer T(3, s);
     STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
-                                 at<uint32_t>(binning, BL.slot_g), s)); }
+                                 at<uint32_t>(binning, BL.slot_g), at<uint8_t>(binning, BL.flag), s)); }
     bool talt = false;
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
@@ -301,7 +301,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
 }
 
 int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
-                            const void* binning, const void* image, int64_t num_rendered, const float* dL_dcolor,
+                            void* binning, const void* image, int64_t num_rendered, const float* dL_dcolor,
                             const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, float* dL_dmeans2D,
                             float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
                             float* dL_dsh, float* dL_dscales, float* dL_drotations, float* dL_dtau, void* stream) {
@@ -315,18 +315,19 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   const Grid grid(a);
   const ImageLayout IL(a.W, a.H);
   const size_t N = (size_t)num_rendered;
-  // scratch: 48-byte partial record per pair + 1-byte "record written" flag
-  // per pair + per-Gaussian partial sums gsum[10][P] (used by the split
-  // per-Gaussian backward)
-  const size_t rec_bytes = align256(48 * N), flag_bytes = align256(N);
-  void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + flag_bytes + align256(40 * (size_t)a.P));
+  // scratch: 48-byte partial record per pair + per-Gaussian partial sums
+  // gsum[10][P] (used by the split per-Gaussian backward).  The 1-byte
+  // "record written" flag per pair lives in the binning buffer, zeroed by the
+  // forward's k_duplicate (render_bwd sets it for the same pairs on every
+  // backward call of that forward, so repeated backwards agree).
+  const size_t rec_bytes = align256(48 * N);
+  void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + align256(40 * (size_t)a.P));
   if (!scratch) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
   float4* partial = N > 0 ? static_cast<float4*>(scratch) : nullptr;
-  uint8_t* pflag = N > 0 ? at<uint8_t>(scratch, rec_bytes) : nullptr;
-  float* gsum = at<float>(scratch, rec_bytes + flag_bytes);
+  const BinLayout BL(N);
+  uint8_t* pflag = N > 0 ? at<uint8_t>(binning, BL.flag) : nullptr;
+  float* gsum = at<float>(scratch, rec_bytes);
   if (N > 0) {
-    HIPCHK(hipMemsetAsync(pflag, 0, N, s));
-    const BinLayout BL(N);
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g),

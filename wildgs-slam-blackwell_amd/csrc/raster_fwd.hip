@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
                                                    const ushort4* __restrict__ rect,
                                                    const uint4* __restrict__ rowtab,
                                                    const float4* __restrict__ splat, uint32_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ slot_g) {
+                                                   uint32_t* __restrict__ slot_g, uint8_t* __restrict__ pflag) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) - lane;
   if (r0 >= P) return;
@@ -299,6 +299,7 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
     if (k < end) {
       keys[k] = ty * (uint32_t)gx + tx;
       slot_g[k] = gg;
+      pflag[k] = 0;  // the backward's "record written" flag of this slot
     }
   }
 }
@@ -467,13 +468,13 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 }
 
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
-                            uint32_t* keys, uint32_t* slot_g, hipStream_t s) {
+                            uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s) {
   if (P == 0) return hipSuccess;
   const GeomLayout L(P);
   const int gx = (a.W + kTile - 1) / kTile;
   hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, s, P, gx, at<uint32_t>(geom, L.offs),
                      sorted_g, at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<float4>(geom, L.splat),
-                     keys, slot_g);
+                     keys, slot_g, pflag);
   return hipGetLastError();
 }
 

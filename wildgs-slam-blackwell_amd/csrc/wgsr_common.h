@@ -552,7 +552,7 @@ struct GeomLayout {
 
 // Per-pair state (binning buffer).
 struct BinLayout {
-  size_t key, key_alt, slot_g, point_g, hist, totals, total;
+  size_t key, key_alt, slot_g, point_g, flag, hist, totals, total;
   __host__ __device__ BinLayout(size_t N) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -560,6 +560,7 @@ struct BinLayout {
     key_alt = take(4 * N);
     slot_g = take(4 * N);    // duplicate slot -> Gaussian id (the sort's payload)
     point_g = take(4 * N);   // sorted pair -> Gaussian id (the tile lists)
+    flag = take(N);          // per duplicate slot: backward record written (zeroed by k_duplicate)
     hist = take(sort_status_bytes(N));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
     total = o;

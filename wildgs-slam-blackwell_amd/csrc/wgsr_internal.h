@@ -36,7 +36,7 @@ struct RasterGrid {
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
                              uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
-                            uint32_t* keys, uint32_t* slot_g, hipStream_t s);
+                            uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s);
 hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
                              const void* geom, float* out_color, float* out_depth,
