@@ -325,6 +325,109 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ key
 // records into registers while the current batch is blended (ids two ahead).
 constexpr int kFwdBatch = 64;
 
+// One pixel per lane (the default layout): 4 waves per 16x16 tile, wave w
+// owns the 8x8 quadrant w.  Same arithmetic as k_render_fwd<1>, written so
+// that every per-pixel predicate (done, live, stop, blend) stays an SGPR lane
+// mask: the per-entry update is ~20 VALU instructions (power 6, exp2, alpha
+// 2, two tests, T update, weight, two packed accumulates, two selects).
+__global__ __launch_bounds__(256) void k_render_fwd1(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
+    float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
+    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+  __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
+  __shared__ uint32_t sG[kFwdBatch];
+  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
+  int ox, oy;
+  tile_pixel<1>(w, lane, 0, ox, oy);
+  const int px = tx0 + ox, py = ty0 + oy;
+  const v2f pxy{(float)px, (float)py};
+  // per-pixel predicates live in SGPR lane masks (a ballot of a compound
+  // predicate would be materialised through VGPRs): dm = finished pixels
+  uint64_t dm = wave_ballot(!(px < W && py < H));
+  const uint2 range = ranges[tile];
+  int wx0, wx1, wy0, wy1;
+  wave_box<1>(w, tx0, ty0, wx0, wx1, wy0, wy1);
+  float T = 1.f;
+  v2f c01{0.f, 0.f}, c2d{0.f, 0.f};  // (colour 0, colour 1), (colour 2, depth)
+  uint32_t last = 0;
+
+  // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
+  uint32_t gcur = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (t < kFwdBatch) {
+    if (range.x + t < range.y) {
+      gcur = point_g[range.x + t];
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+    }
+    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
+  }
+
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
+    if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(dm)) == (int)blockDim.x) break;
+    if (t < kFwdBatch) {
+      sA[t] = nA;
+      sB[t] = nB;
+      sC[t] = nC;
+      sG[t] = gcur;
+    }
+    __syncthreads();
+    if (t < kFwdBatch) {
+      gcur = gnext;
+      if (b0 + kFwdBatch + t < range.y) {
+        nA = splat[3 * (size_t)gcur];
+        nB = splat[3 * (size_t)gcur + 1];
+        nC = splat[3 * (size_t)gcur + 2];
+      }
+      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
+    }
+    if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
+    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+    const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
+    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const float4 A = sA[j];
+      const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
+      const float4 Cc = sC[j];
+      const v2f d = v2f{A.x, A.y} - pxy;                     // (dx, dy) = mean - pixel
+      const v2f q2 = v2f{A.z, A.w} * d * d;                  // log2(e) x (-conic_xx dx^2/2, -conic_yy dy^2/2)
+      const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
+      const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
+      const float test_T = fmaf(-T, alpha, T);  // T (1 - alpha)
+      const uint64_t live = wave_ballot(power <= 0.0f) & wave_ballot(alpha >= kMinAlpha) & ~dm;
+      const uint64_t low = wave_ballot(test_T < kMinT);
+      const uint64_t blend = live & ~low;
+      const bool bl = __builtin_amdgcn_inverse_ballot_w64(blend);
+      const float wgt = bl ? alpha * T : 0.f;
+      c01 += wgt * v2f{Cc.x, Cc.y};
+      c2d += wgt * v2f{Cc.z, Cc.w};
+      // upstream n_touched: pixels whose T stays above 0.5 after this blend
+      const uint32_t tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
+      T = bl ? test_T : T;
+      last = bl ? cbase + j : last;
+      dm |= live & low;
+      if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
+      if (dm == ~0ull) break;
+    }
+  }
+  if (!(px < W && py < H)) return;
+  const size_t HW = (size_t)H * W;
+  const size_t pid = (size_t)py * W + px;
+  final_T[pid] = T;
+  n_contrib[pid] = last;
+  out_color[pid] = c01.x + T * bg[0];
+  out_color[HW + pid] = c01.y + T * bg[1];
+  out_color[2 * HW + pid] = c2d.x + T * bg[2];
+  out_depth[pid] = c2d.y;
+  out_opac[pid] = 1.f - T;
+}
+
 template <int PPL>
 __global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
@@ -495,7 +598,11 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   hipLaunchKernelGGL(k_render_fwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,             \
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,  \
                      final_T, n_contrib, n_touched)
-  if (ppl == 1) WGSR_FWD(1); else if (ppl == 2) WGSR_FWD(2); else WGSR_FWD(4);
+  if (ppl == 1)
+    hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, point_g, at<float4>(geom, L.splat), a.W,
+                       a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T, n_contrib, n_touched);
+  else if (ppl == 2) WGSR_FWD(2);
+  else WGSR_FWD(4);
 #undef WGSR_FWD
   return hipGetLastError();
 }
