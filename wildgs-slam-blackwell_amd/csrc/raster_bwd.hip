@@ -58,8 +58,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const uint2 range = ranges[tile];
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
-  // per-quadrant pixel state; pairs are packed for v_pk_* math
-  v2f pxy[Q], dp01[Q], dp2d[Q], acc01[Q], acc2d[Q];
+  // per-quadrant pixel state; pairs are packed for v_pk_* math.  Pixel
+  // positions are not kept per quadrant: quadrant p's pixel is this lane's
+  // quadrant-0 pixel p0 + 8 (p & 1, p >> 1), so (dx, dy) for quadrant p is
+  // (mean - p0) minus an immediate (fewer live VGPRs: no spills)
+  const v2f p0{(float)(tx0 + (lane & 7)), (float)(ty0 + (lane >> 3))};
+  v2f dp01[Q], dp2d[Q], acc01[Q], acc2d[Q];
   float T[Q], tb[Q];
   uint32_t last[Q], mq[Q];
   uint32_t m = 0;
@@ -68,7 +72,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
     const bool inside = px < W && py < H;
     const size_t pid = (size_t)py * W + px;
-    pxy[p] = v2f{(float)px, (float)py};
     const float Tf = inside ? final_Ts[pid] : 0.f;
     last[p] = inside ? n_contrib[pid] : 0u;
     const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
@@ -83,8 +86,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     uint32_t x = last[p];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
-    mq[p] = x;
-    m = max(m, x);
+    mq[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);  // wave-uniform: an SGPR
+    m = max(m, mq[p]);
   }
   // entries behind every pixel's last contributor get no record: their slot
   // flags stay 0 (zeroed before the launch), and so does every entry no pixel
@@ -142,6 +145,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const float4 B = sB[j];
       const float4 Cc = sC[j];
       const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
+      const v2f d0 = mxy - p0;  // (dx, dy) for quadrant 0
       const float cxy = B.x, op = B.y;
       const v2f cd2 = cd + cd;  // (2 A.z, 2 A.w): d(power2)/d(dx, dy) = (2 A.z dx + B.x dy, 2 A.w dy + B.x dx)
       v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       for (int p = 0; p < Q; ++p) {
         if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
         // phase 1: does entry j reach this lane's pixel of quadrant p?
-        const v2f d = mxy - pxy[p];  // (dx, dy) = mean - pixel
+        const v2f d = d0 - v2f{8.f * (p & 1), 8.f * (p >> 1)};  // (dx, dy) = mean - pixel
         const v2f q2 = cd * d * d;  // log2(e) x (-conic_xx dx^2 / 2, -conic_yy dy^2 / 2)
         const float power = q2.x + q2.y + (cxy * d.x) * d.y;  // log2(e) x upstream's power
         const float G = __builtin_amdgcn_exp2f(power);
