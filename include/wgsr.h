@@ -92,11 +92,12 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args,
  * (NULL when M == 0), dL_dscales [P,3], dL_drotations [P,4],
  * dL_dtau [P,6] (per-Gaussian pose gradient, rho then theta).
  * A scratch buffer of ~48 bytes per rendered pair is requested through
- * `scratch_alloc`.  The binning buffer's per-pair flag bytes are written
- * (the same values on every backward of one forward). */
+ * `scratch_alloc`.  The binning buffer's per-pair flag bytes and the image
+ * buffer's backward launch order are written (the same values on every
+ * backward of one forward). */
 int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii,
                             const void* geom_buffer, void* binning_buffer,
-                            const void* image_buffer, int64_t num_rendered,
+                            void* image_buffer, int64_t num_rendered,
                             const float* dL_dcolor, const float* dL_ddepth,
                             wgsr_alloc_fn scratch_alloc, void* alloc_ctx,
                             float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,

@@ -45,13 +45,6 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
-int render_ppl(const char* env_name, int dflt) {
-  const char* v = getenv(env_name);
-  if (!v) return dflt;
-  const int x = atoi(v);
-  return (x == 1 || x == 2 || x == 4) ? x : dflt;
-}
-
 int num_bits(uint32_t n) {
   int b = 0;
   while (b < 32 && (1ull << b) < n) ++b;
@@ -286,22 +279,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     sorted_g = at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g);
   }
   uint2* ranges = at<uint2>(image, IL.ranges);
-  if (N > 0) {
-    StageTimer T(5, s);
-    STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)N, grid.nt, ranges, s));
-  } else {
-    HIPCHK(hipMemsetAsync(ranges, 0, 8 * (size_t)grid.nt, s));
-  }
+  { StageTimer T(5, s);  // (N = 0: every range is empty)
+  STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)N, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
+                            at<uint32_t>(image, IL.order_fwd), s)); }
   { StageTimer T(6, s);
-  STAGE(a, s, launch_render_fwd(a, ranges, sorted_g, geom,
+  STAGE(a, s, launch_render_fwd(a, ranges, at<uint32_t>(image, IL.order_fwd), sorted_g, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
-                                at<uint32_t>(image, IL.n_contrib), n_touched, s)); }
+                                at<uint32_t>(image, IL.n_contrib), n_touched, at<uint32_t>(image, IL.tile_m), s)); }
   *num_rendered = (int64_t)N_rect;
   return WGSR_OK;
 }
 
 int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
-                            void* binning, const void* image, int64_t num_rendered, const float* dL_dcolor,
+                            void* binning, void* image, int64_t num_rendered, const float* dL_dcolor,
                             const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, float* dL_dmeans2D,
                             float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
                             float* dL_dsh, float* dL_dscales, float* dL_drotations, float* dL_dtau, void* stream) {
@@ -330,7 +320,10 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   if (N > 0) {
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
-    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g),
+    uint32_t* order = at<uint32_t>(image, IL.order_bwd);
+    STAGE(a, s, launch_tile_order(at<uint32_t>(image, IL.tile_m), grid.nt, order, s));
+    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order,
+                                  at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g),
                                   geom,
                                   at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));

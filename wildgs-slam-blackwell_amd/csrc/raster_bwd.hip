@@ -41,7 +41,8 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 // the 4-wave layout -- but sums all of them with ONE wave reduction and writes
 // the record without a cross-wave combine.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
+    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
     const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __shared__ uint32_t sG[kBatch];
   __shared__ float sP[kBatch][11];
   __shared__ uint32_t sHit[kBatch];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const int lane = threadIdx.x;
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   const size_t HW = (size_t)H * W;
@@ -590,14 +591,15 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
 
 }  // namespace
 
-hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
-                             const void* geom, const float* final_T,
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
+                             const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, point_g, at<float4>(geom, L.splat),
+  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
+                     at<float4>(geom, L.splat),
                      at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
                      a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
   return hipGetLastError();

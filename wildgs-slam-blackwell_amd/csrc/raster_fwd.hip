@@ -304,8 +304,66 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
   }
 }
 
+// ---- tile ranges and the tiles' launch order ---------------------------------
+// The render kernels take tile order[xcd_remap(blockIdx)]: blocks b with the
+// same b % 8 run on one XCD (round-robin dispatch), and xcd_remap hands each
+// XCD a contiguous chunk of tiles (a band of the image: splat records shared
+// by neighbouring tiles stay in that XCD's L2).  Inside a chunk the tiles are
+// ordered heaviest first (longest-processing-time list scheduling): with ~2
+// waves per SIMD slot over the kernel, launch order decides the makespan
+// (bench scene, backward: 68 % -> 91 % of the ideal in a list-scheduling
+// simulation).  Order only changes scheduling, never a result.
+constexpr int kOrderBuckets = 1024;
+
+__device__ __forceinline__ void tile_chunk(uint32_t x, uint32_t nt, uint32_t& c0, uint32_t& c1) {
+  const uint32_t q = nt / 8, r = nt % 8;
+  c0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  c1 = c0 + (x < r ? q + 1 : q);
+}
+
+// Counting sort of the chunk's tiles by descending work bucket (one
+// 1024-thread workgroup per chunk; positions inside a bucket come from LDS
+// atomics, so ties may land in any order).
+// work of a tile: work[tile], or with quads the max of work[4 tile .. 4 tile + 3]
+__device__ __forceinline__ uint32_t tile_work(const uint32_t* __restrict__ work, bool quads, uint32_t tile) {
+  if (!quads) return work[tile];
+  const uint4 q = reinterpret_cast<const uint4*>(work)[tile];
+  return max(max(q.x, q.y), max(q.z, q.w));
+}
+
+__device__ __forceinline__ void order_chunk(uint32_t c0, uint32_t c1, const uint32_t* __restrict__ work, bool quads,
+                                            uint32_t* __restrict__ order, uint32_t* s_cnt) {
+  const int t = threadIdx.x;
+  s_cnt[t] = 0;
+  __syncthreads();
+  auto bucket = [&](uint32_t tile) {
+    return (uint32_t)(kOrderBuckets - 1) - min((uint32_t)(kOrderBuckets - 1), tile_work(work, quads, tile));
+  };
+  for (uint32_t tile = c0 + t; tile < c1; tile += 1024) atomicAdd(&s_cnt[bucket(tile)], 1u);
+  __syncthreads();
+  // exclusive scan of the 1024 bucket counts (one per thread)
+  __shared__ uint32_t s_w[16];
+  const uint32_t v = s_cnt[t];
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off, 64);
+    if ((t & 63) >= off) inc += o;
+  }
+  if ((t & 63) == 63) s_w[t >> 6] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < (t >> 6); ++i) base += s_w[i];
+  __syncthreads();
+  s_cnt[t] = base + inc - v;
+  __syncthreads();
+  for (uint32_t tile = c0 + t; tile < c1; tile += 1024) order[c0 + atomicAdd(&s_cnt[bucket(tile)], 1u)] = tile;
+}
+
+// ranges[tile] = [first, end) of the tile's run in the sorted pair keys
+// (binary search); len[tile] = its list length.
 __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ keys, uint32_t N, int ntiles,
-                                                uint2* __restrict__ ranges) {
+                                                uint2* __restrict__ ranges, uint32_t* __restrict__ len) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
   auto lower = [&](uint32_t v) {
@@ -316,28 +374,45 @@ __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ key
     }
     return lo;
   };
-  ranges[t] = make_uint2(lower((uint32_t)t), lower((uint32_t)t + 1));
+  const uint2 r = make_uint2(lower((uint32_t)t), lower((uint32_t)t + 1));
+  ranges[t] = r;
+  len[t] = r.y - r.x;
 }
 
-// One 16x16 tile per workgroup of 4 / PPL waves; each lane blends PPL pixels
-// (PPL-way ILP; every LDS broadcast of a splat record serves 64 x PPL pixels).
-// Splat records arrive 64 at a time through LDS; wave 0 loads the next batch's
-// records into registers while the current batch is blended (ids two ahead).
+// The backward's launch order by each tile's deepest contributor (its
+// back-to-front walk length), written by the forward.
+// One workgroup per XCD chunk, or (global) one for all tiles: then the
+// render kernel takes order[blockIdx] and round-robin dispatch deals every
+// 8th tile of the sorted list to each XCD.
+__global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict__ work, bool quads, bool global,
+                                                     uint32_t ntiles, uint32_t* __restrict__ order) {
+  __shared__ uint32_t s_cnt[kOrderBuckets];
+  uint32_t c0 = 0, c1 = ntiles;
+  if (!global) tile_chunk(blockIdx.x, ntiles, c0, c1);
+  order_chunk(c0, c1, work, quads, order, s_cnt);
+}
+
+// Splat records arrive 64 at a time through LDS; wave 0 loads the next
+// batch's records into registers while the current batch is blended (ids two
+// ahead).
 constexpr int kFwdBatch = 64;
 
-// One pixel per lane (the default layout): 4 waves per 16x16 tile, wave w
-// owns the 8x8 quadrant w.  Same arithmetic as k_render_fwd<1>, written so
-// that every per-pixel predicate (done, live, stop, blend) stays an SGPR lane
-// mask: the per-entry update is ~20 VALU instructions (power 6, exp2, alpha
-// 2, two tests, T update, weight, two packed accumulates, two selects).
+// One 16x16 tile per workgroup of 4 waves; wave w owns the 8x8 quadrant w,
+// one pixel per lane.  Every per-pixel predicate (done, live, low, blend) is
+// an explicit SGPR lane mask combined by scalar ops: the per-entry update is
+// ~22 VALU instructions (power 6, exp2, alpha 2, four compares, T update,
+// weight, two packed accumulates, three selects).  Also writes each
+// quadrant's deepest contributor (tile_m4), the backward's per-tile work.
 __global__ __launch_bounds__(256) void k_render_fwd1(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
-    float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
-    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, const uint32_t* __restrict__ point_g,
+    const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
+    float* __restrict__ out_color, float* __restrict__ out_depth, float* __restrict__ out_opac,
+    float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ tile_m4) {
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const uint32_t slot = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const uint32_t tile = order ? order[slot] : slot;  // null: xcd_remap's order as it is
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   int ox, oy;
@@ -416,6 +491,12 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
       if (dm == ~0ull) break;
     }
   }
+  {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
+    uint32_t mx = last;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if (lane == 0) tile_m4[4 * tile + w] = mx;
+  }
   if (!(px < W && py < H)) return;
   const size_t HW = (size_t)H * W;
   const size_t pid = (size_t)py * W + px;
@@ -428,121 +509,6 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
   out_opac[pid] = 1.f - T;
 }
 
-template <int PPL>
-__global__ __launch_bounds__(64 * (4 / PPL)) void k_render_fwd(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    int W, int H, int gx, int ntiles, const float* __restrict__ bg, float* __restrict__ out_color,
-    float* __restrict__ out_depth, float* __restrict__ out_opac, float* __restrict__ final_T,
-    uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched) {
-  __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
-  __shared__ uint32_t sG[kFwdBatch];
-  const uint32_t tile = xcd_remap(blockIdx.x, (uint32_t)ntiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
-  float fx[PPL], fy[PPL];
-  uint32_t done = 0;
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    int ox, oy;
-    tile_pixel<PPL>(w, lane, p, ox, oy);
-    const int px = tx0 + ox, py = ty0 + oy;
-    fx[p] = (float)px;
-    fy[p] = (float)py;
-    if (!(px < W && py < H)) done |= 1u << p;
-  }
-  const uint2 range = ranges[tile];
-  int wx0, wx1, wy0, wy1;
-  wave_box<PPL>(w, tx0, ty0, wx0, wx1, wy0, wy1);
-  float T[PPL], C0[PPL], C1[PPL], C2[PPL], Dp[PPL];
-  uint32_t last[PPL];
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) { T[p] = 1.f; C0[p] = C1[p] = C2[p] = Dp[p] = 0.f; last[p] = 0; }
-
-  // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
-  uint32_t gcur = 0, gnext = 0;
-  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (t < kFwdBatch) {
-    if (range.x + t < range.y) {
-      gcur = point_g[range.x + t];
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
-    }
-    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
-  }
-
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
-    if (__syncthreads_count(done == ((1u << PPL) - 1u)) == (int)blockDim.x) break;
-    if (t < kFwdBatch) {
-      sA[t] = nA;
-      sB[t] = nB;
-      sC[t] = nC;
-      sG[t] = gcur;
-    }
-    __syncthreads();
-    if (t < kFwdBatch) {
-      gcur = gnext;
-      if (b0 + kFwdBatch + t < range.y) {
-        nA = splat[3 * (size_t)gcur];
-        nB = splat[3 * (size_t)gcur + 1];
-        nC = splat[3 * (size_t)gcur + 2];
-      }
-      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
-    }
-    if (__all(done == ((1u << PPL) - 1u))) continue;  // this wave is finished; keep the barriers
-    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-    const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
-    // lane j tests entry j's reach box against this wave's pixels; the wave
-    // then walks only the entries that can touch it (a scalar bit loop)
-    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const float4 A = sA[j];
-      const float4 B = sB[j];
-      const float4 Cc = sC[j];
-      uint32_t tot = 0;  // pixels of this wave whose T stays above 0.5 (upstream n_touched)
-      // PPL independent, branch-free pixel updates (the compiler interleaves
-      // them); the predicates stay in SGPR lane masks
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        const v2f d = v2f{A.x, A.y} - v2f{fx[p], fy[p]};  // (dx, dy) = mean - pixel
-        const v2f q2 = v2f{A.z, A.w} * d * d;  // log2(e) x (-conic_xx dx^2 / 2, -conic_yy dy^2 / 2)
-        const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
-        const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
-        const float test_T = fmaf(-T[p], alpha, T[p]);  // T (1 - alpha) in one op
-        const bool live = !(done & (1u << p)) && power <= 0.0f && alpha >= kMinAlpha;
-        const bool stop = live && test_T < kMinT;
-        const bool blend = live && !(test_T < kMinT);
-        const float wgt = blend ? alpha * T[p] : 0.f;
-        C0[p] += Cc.x * wgt;
-        C1[p] += Cc.y * wgt;
-        C2[p] += Cc.z * wgt;
-        Dp[p] += Cc.w * wgt;
-        tot += (uint32_t)__popcll(wave_ballot(blend && test_T > 0.5f));
-        T[p] = blend ? test_T : T[p];
-        last[p] = blend ? cbase + j : last[p];
-        done |= stop ? (1u << p) : 0u;
-      }
-      if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
-      if (__all(done == ((1u << PPL) - 1u))) break;
-    }
-  }
-  const size_t HW = (size_t)H * W;
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    const int px = (int)fx[p], py = (int)fy[p];
-    if (!(px < W && py < H)) continue;
-    const size_t pid = (size_t)py * W + px;
-    final_T[pid] = T[p];
-    n_contrib[pid] = last[p];
-    out_color[pid] = C0[p] + T[p] * bg[0];
-    out_color[HW + pid] = C1[p] + T[p] * bg[1];
-    out_color[2 * HW + pid] = C2[p] + T[p] * bg[2];
-    out_depth[pid] = Dp[p];
-    out_opac[pid] = 1.f - T[p];
-  }
-}
 
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means,
                                                       const float* __restrict__ viewm, uint8_t* __restrict__ present) {
@@ -581,29 +547,49 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
   return hipGetLastError();
 }
 
-hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s) {
-  hipLaunchKernelGGL(k_ranges, dim3((ntiles + 255) / 256), dim3(256), 0, s, sorted_keys, N, ntiles, ranges);
+// WGSR_FWD_LPT=1: order the forward's tiles by list length too (measured no
+// gain on the bench scene: its per-tile forward work is nearly uniform)
+static bool fwd_lpt() {
+  static const bool v = [] {
+    const char* e = getenv("WGSR_FWD_LPT");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
+hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
+                         uint32_t* order, hipStream_t s) {
+  hipLaunchKernelGGL(k_ranges, dim3((ntiles + 255) / 256), dim3(256), 0, s, sorted_keys, N, ntiles, ranges, len);
+  if (fwd_lpt()) hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, len, false, false, (uint32_t)ntiles, order);
   return hipGetLastError();
 }
 
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
-                             const void* geom, float* out_color, float* out_depth,
+// WGSR_BWD_ORDER=global: one LPT list over all tiles instead of per XCD chunk
+bool bwd_order_global() {
+  static const bool v = [] {
+    const char* e = getenv("WGSR_BWD_ORDER");
+    return e && strcmp(e, "global") == 0;
+  }();
+  return v;
+}
+
+hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* order, hipStream_t s) {
+  const bool global = bwd_order_global();
+  hipLaunchKernelGGL(k_tile_order, dim3(global ? 1 : 8), dim3(1024), 0, s, work_quads, true, global, (uint32_t)ntiles,
+                     order);
+  return hipGetLastError();
+}
+
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
+                             const uint32_t* point_g, const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
-                             hipStream_t s) {
+                             uint32_t* tile_m, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  static const int ppl = render_ppl("WGSR_FWD_PPL", 1);
-#define WGSR_FWD(PPL_)                                                                                       \
-  hipLaunchKernelGGL(k_render_fwd<PPL_>, dim3(nt), dim3(64 * (4 / PPL_)), 0, s, ranges, point_g,             \
-                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity,  \
-                     final_T, n_contrib, n_touched)
-  if (ppl == 1)
-    hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, point_g, at<float4>(geom, L.splat), a.W,
-                       a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T, n_contrib, n_touched);
-  else if (ppl == 2) WGSR_FWD(2);
-  else WGSR_FWD(4);
-#undef WGSR_FWD
+  hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, fwd_lpt() ? order : nullptr, point_g,
+                     at<float4>(geom, L.splat), a.W,
+                     a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T, n_contrib, n_touched, tile_m);
   return hipGetLastError();
 }
 

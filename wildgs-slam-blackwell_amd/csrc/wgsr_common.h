@@ -358,7 +358,6 @@ __device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B,
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
-int render_ppl(const char* env_name, int dflt);
 
 // ---------------------------------------------------------------------------
 // Small fp32 math (upstream operation order where it matters).  The geometry
@@ -569,12 +568,16 @@ struct BinLayout {
 
 // Per-pixel state (image buffer).
 struct ImageLayout {
-  size_t ranges, final_T, n_contrib, total;
+  size_t ranges, tile_len, tile_m, order_fwd, order_bwd, final_T, n_contrib, total;
   __host__ __device__ ImageLayout(int W, int H) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
     const size_t nt = (size_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     ranges = take(8 * nt);
+    tile_len = take(4 * nt);   // list length per tile (forward work)
+    tile_m = take(16 * nt);    // deepest contributor per tile quadrant (backward work)
+    order_fwd = take(4 * nt);  // launch orders (heaviest first per XCD chunk)
+    order_bwd = take(4 * nt);
     final_T = take(4 * (size_t)W * H);
     n_contrib = take(4 * (size_t)W * H);
     total = o;

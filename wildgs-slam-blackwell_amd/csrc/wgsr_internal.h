@@ -37,17 +37,22 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                              uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
-hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, hipStream_t s);
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
-                             const void* geom, float* out_color, float* out_depth,
+// tile ranges + the forward's launch order (tiles by list length, per XCD chunk)
+hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
+                         uint32_t* order, hipStream_t s);
+// the backward's launch order (tiles by deepest contributor, per XCD chunk)
+hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* order, hipStream_t s);
+bool bwd_order_global();
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
+                             const uint32_t* point_g, const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
-                             hipStream_t s);
+                             uint32_t* tile_m4, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                                hipStream_t s);
 
 // backward stages (raster_bwd.hip)
-hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
-                             const void* geom, const float* final_T,
+hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
+                             const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, hipStream_t s);
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
