@@ -411,6 +411,7 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     uint32_t* __restrict__ tile_m4) {
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
+  __shared__ uint32_t sTouch[4][kFwdBatch];  // per wave: n_touched increments of the batch's entries
   const uint32_t slot = xcd_remap(blockIdx.x, (uint32_t)ntiles);
   const uint32_t tile = order ? order[slot] : slot;  // null: xcd_remap's order as it is
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -464,9 +465,10 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
     const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
     uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-    while (todo) {
+    sTouch[w][lane] = 0;
+    while (todo != 0 && dm != ~0ull) {
       const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
+      todo &= ~(1ull << j);
       const float4 A = sA[j];
       const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
       const float4 Cc = sC[j];
@@ -487,9 +489,11 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
       T = bl ? test_T : T;
       last = bl ? cbase + j : last;
       dm |= live & low;
-      if (tot != 0 && lane == 0) atomicAdd(&n_touched[sG[j]], (int)tot);
-      if (dm == ~0ull) break;
+      sTouch[w][j] = tot;  // (every lane stores the same value: no branch)
     }
+    // one atomic per touched entry, all of the batch's in one wave instruction
+    const uint32_t tv = sTouch[w][lane];
+    if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
   }
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
     uint32_t mx = last;
