@@ -20,6 +20,7 @@ STAGE_OF = {
     "k_preprocess": "preprocess", "k_duplicate": "duplicate", "k_ranges": "ranges",
     "k_render_fwd": "render_fwd", "k_render_bwd": "render_bwd", "k_gauss_bwd": "gauss_bwd",
     "k_render_fwd_quad": "render_fwd", "k_render_bwd_quad": "render_bwd", "k_sum_partials": "gauss_bwd",
+    "k_render_fwd1": "render_fwd", "k_tile_order": "render_bwd",
     "k_scan_reduce": "offsets_scan", "k_scan_bsum": "offsets_scan", "k_scan_down": "offsets_scan",
 }
 
