@@ -68,7 +68,11 @@ def n_contrib_sum(img_buffer, W, H):
     def a256(x):
         return (x + 255) & ~255
     ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
-    off = a256(8 * ntile) + a256(4 * W * H)
+    # ImageLayout (csrc/wgsr_common.h): ranges, tile_len, tile_m, order_fwd,
+    # order_bwd, final_T, n_contrib -- each region 256-byte aligned
+    off = 0
+    for nbytes in (8 * ntile, 4 * ntile, 16 * ntile, 4 * ntile, 4 * ntile, 4 * W * H):
+        off += a256(nbytes)
     nc = img_buffer[off: off + 4 * W * H].view(torch.int32)
     return int(nc.sum().item())
 
