@@ -11,8 +11,14 @@ always computed) at 1920x1080, all inputs resident in HBM before timing.
 * N = 1 (default): BASELINE.json configs[2].  value = P * K / t.
 * N > 1 (torchrun, one rank per GPU): configs[3] -- keyframe-view data
   parallelism: rank r renders view r of the same replicated 1M Gaussians and
-  the per-Gaussian parameter gradients (59 floats each) are SUM-all-reduced
-  over RCCL every step.  Weak scaling; value = P * N * K / max_rank(t).
+  every rank ends the step holding the SUM over the N views of the
+  per-Gaussian parameter gradients (59 floats each).  Default exchange
+  (wgsr.dp.ViewShardedBackward): each view's 12-float screen-space record of
+  every Gaussian goes to the Gaussian's owner rank (RCCL all-to-all), owners
+  run the camera-side backward of all N views for their 1/N shard, and the
+  shards are all-gathered -- 71 instead of 118 floats per Gaussian per rank
+  at N = 8 (``--dp-exchange allreduce``: the plain RCCL all-reduce).  Weak
+  scaling; value = P * N * K / max_rank(t).
 
 Extra fields: ``roofline`` for the dominant kernel (stage times from HIP
 events recorded on the launch stream inside the timed region; algorithmic
@@ -112,6 +118,11 @@ def main():
     ap.add_argument("--sh", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the stage timers")
+    ap.add_argument("--dp-exchange", choices=("views", "allreduce"), default=None,
+                    help="N > 1 gradient exchange: 'views' (default: screen-space records to the "
+                         "Gaussians' owners, owner-computed shards all-gathered; wgsr.dp."
+                         "ViewShardedBackward) or 'allreduce' (59-float gradient all-reduce). "
+                         "Giving it at N = 1 runs that path on one GPU.")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,7 +136,7 @@ def main():
     from diff_gaussian_rasterization import _C
     from wgsr import _lib
     from wgsr.camera import synthetic_camera
-    from wgsr.dp import GradBuffer, allreduce_grads
+    from wgsr.dp import GradBuffer, ViewShardedBackward, allreduce_grads
     from wgsr.scene import make_scene, make_upstream_grads
 
     P, W, H, deg = args.P, args.width, args.height, args.sh
@@ -144,12 +155,20 @@ def main():
     e = torch.empty(0, device=dev)
     tanx, tany = f["tanfovx"], f["tanfovy"]
     gbuf = GradBuffer.allocate(P, M, dev)
+    exchange = args.dp_exchange or ("views" if world > 1 else None)
+    vsb = ViewShardedBackward(P, M, dev) if exchange == "views" else None
+    camd = dict(viewmatrix=view, projmatrix=proj, projmatrix_raw=praw, campos=campos, tanfovx=tanx,
+                tanfovy=tany, bg=bg)
     state = {}
 
     def step():
         nr, color, radii, geom, binning, img, depth, opacity, nt = _C.rasterize_gaussians(
             bg, means, e, opac, scales, rots, 1.0, e, view, proj, praw, tanx, tany, H, W, shs, deg,
             campos, False, False)
+        if vsb is not None:
+            vsb.backward((means, scales, rots, shs, deg, camd, nr, radii, geom, binning, img), gc, gd)
+            state.update(nr=nr, color=color, img=img)
+            return
         _C.rasterize_gaussians_backward(
             bg, means, radii, e, scales, rots, 1.0, e, view, proj, praw, tanx, tany, gc, gd, shs,
             deg, campos, geom, nr, binning, img, False, out=gbuf.views)
@@ -194,10 +213,15 @@ def main():
             "workload": ("configs[2]: 1M Gaussians, 1920x1080, SH3, single-view fwd+bwd, pose grad on"
                          if world == 1 else
                          f"configs[3]: 1M Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
-                         "+ RCCL SUM all-reduce of the per-Gaussian gradients"),
+                         "+ the SUM over views of the per-Gaussian gradients on every rank "
+                         f"(RCCL, exchange: {exchange})"),
             "gaussians": P, "image": f"{W}x{H}", "sh_degree": deg, "num_rendered": N,
             "views_per_step": world, "parallelism": f"dp{world} (keyframe views)",
-            "allreduce_bytes_per_step": (gbuf.flat.numel() * 4 if world > 1 else 0),
+            "dp_exchange": exchange or "none",
+            "exchange_bytes_per_rank_per_step": (
+                0 if world == 1 else
+                int(2 * (world - 1) / world * gbuf.flat.numel() * 4) if exchange == "allreduce" else
+                int((world - 1) / world * vsb.P_pad * (12 + gbuf.floats_per_gaussian) * 4)),
         },
     }
 

@@ -105,6 +105,52 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii,
                             float* dL_dscales, float* dL_drotations, float* dL_dtau,
                             void* stream);
 
+/* ---- view-sharded data-parallel backward ----------------
+ * No upstream counterpart (the reference is single-GPU; its mapper renders
+ * one keyframe view per step, src/mapper.py:1089-1170).  Splits
+ * wgsr_rasterize_backward at the per-Gaussian screen-space partial sums so
+ * ranks exchange 48 bytes per Gaussian per view instead of all-reducing the
+ * 59-float parameter gradients (wgsr/dp.py). */
+#define WGSR_VIEW_RECORD_FLOATS 12  /* g[10] (as k_gauss_bwd), radius, SH clamp bits */
+#define WGSR_VIEW_CAMERA_FLOATS 64  /* view[16] proj[16] proj_raw[16] campos[3] tanx tany W H, pad */
+
+/* Packs args' camera (viewmatrix, projmatrix, projmatrix_raw, campos,
+ * tan_fovx/y, W, H) into one device row of WGSR_VIEW_CAMERA_FLOATS floats. */
+int wgsr_pack_view_camera(const wgsr_raster_args* args, float* camera_row, void* stream);
+
+/* First half of wgsr_rasterize_backward for one view: render backward, then
+ * per Gaussian i < P_pad one record of WGSR_VIEW_RECORD_FLOATS floats in
+ * records [P_pad, 12]: dL/dmean2D (NDC x, y), dL/dconic (3), dL/dopacity,
+ * dL/dcolor (3), dL/ddepth, radius (float), SH clamp bits (float).  Rows of
+ * culled Gaussians and rows >= P are zero (radius 0 = not visible). */
+int wgsr_rasterize_backward_records(const wgsr_raster_args* args, const int32_t* radii,
+                                    const void* geom_buffer, void* binning_buffer,
+                                    void* image_buffer, int64_t num_rendered,
+                                    const float* dL_dcolor, const float* dL_ddepth,
+                                    wgsr_alloc_fn scratch_alloc, void* alloc_ctx, int P_pad,
+                                    float* records, void* stream);
+
+/* Number of pose-gradient partial rows wgsr_gauss_backward_views writes. */
+int wgsr_gauss_backward_views_blocks(int lo, int hi);
+
+/* Second half, for Gaussians [lo, hi) over n_views views: view v's camera is
+ * row v of `cameras` [n_views, 64] and its records for the shard start at
+ * records + v * record_view_stride (floats; row i - lo).  Writes rows
+ * [lo, hi) of dL_dmeans3D [P,3], dL_dsh [P,M,3], dL_dopacity [P,1],
+ * dL_dscales [P,3], dL_drotations [P,4] = the SUM over the views of what
+ * wgsr_rasterize_backward returns per view.  tau_partials (or NULL):
+ * [wgsr_gauss_backward_views_blocks(lo, hi)][n_views][6] per-block sums of
+ * the pose gradient (rho, theta) per view.  stats (or NULL): [hi - lo][3] =
+ * sum over views of ||dL/dmean2D[:2]||, number of views with radius > 0,
+ * max radius (the reference's add_densification_stats inputs).  params uses
+ * P, D, M, means3D, scales, rotations, shs, scale_modifier; cov3D_precomp is
+ * not supported. */
+int wgsr_gauss_backward_views(const wgsr_raster_args* params, int lo, int hi, int n_views,
+                              const float* cameras, const float* records,
+                              int64_t record_view_stride, float* dL_dmeans3D, float* dL_dsh,
+                              float* dL_dopacity, float* dL_dscales, float* dL_drotations,
+                              float* tau_partials, float* stats, void* stream);
+
 /* Replaces _C.mark_visible: present[i] = (view-space z of point i > 0.2). */
 int wgsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
                       const float* projmatrix, uint8_t* present, void* stream);

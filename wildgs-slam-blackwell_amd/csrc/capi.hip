@@ -290,18 +290,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   return WGSR_OK;
 }
 
-int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
-                            void* binning, void* image, int64_t num_rendered, const float* dL_dcolor,
-                            const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, float* dL_dmeans2D,
-                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                            float* dL_dsh, float* dL_dscales, float* dL_drotations, float* dL_dtau, void* stream) {
-  g_err[0] = 0;
-  if (int e = validate(args)) return e;
-  const wgsr_raster_args& a = *args;
-  if (a.P == 0) return WGSR_OK;
+}  // extern "C"
+
+namespace wgsr {
+namespace {
+// Backward render of one view: per-pair partial records (scratch) + the
+// "record written" flags in the binning buffer.  Shared by the full backward
+// and the view-sharded records path.
+int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* binning, void* image,
+                          int64_t num_rendered, const float* dL_dcolor, const float* dL_ddepth,
+                          wgsr_alloc_fn scratch_alloc, void* ctx, hipStream_t s, float4** partial_out,
+                          uint8_t** pflag_out) {
   if (!geom || !image || (num_rendered > 0 && !binning))
     return set_error(WGSR_EINVAL, "missing forward state buffers");
-  hipStream_t s = (hipStream_t)stream;
   const Grid grid(a);
   const ImageLayout IL(a.W, a.H);
   const size_t N = (size_t)num_rendered;
@@ -316,7 +317,6 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   float4* partial = N > 0 ? static_cast<float4*>(scratch) : nullptr;
   const BinLayout BL(N);
   uint8_t* pflag = N > 0 ? at<uint8_t>(binning, BL.flag) : nullptr;
-  float* gsum = at<float>(scratch, rec_bytes);
   if (N > 0) {
     const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
@@ -328,9 +328,102 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
                                   at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
   }
+  *partial_out = partial;
+  *pflag_out = pflag;
+  return WGSR_OK;
+}
+}  // namespace
+}  // namespace wgsr
+
+extern "C" {
+
+int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
+                            void* binning, void* image, int64_t num_rendered, const float* dL_dcolor,
+                            const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                            float* dL_dsh, float* dL_dscales, float* dL_drotations, float* dL_dtau, void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  const wgsr_raster_args& a = *args;
+  if (a.P == 0) return WGSR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  float4* partial = nullptr;
+  uint8_t* pflag = nullptr;
+  if (int e = render_backward_pairs(a, geom, binning, image, num_rendered, dL_dcolor, dL_ddepth, scratch_alloc, ctx,
+                                    s, &partial, &pflag))
+    return e;
+  float* gsum = partial ? reinterpret_cast<float*>(reinterpret_cast<char*>(partial) + align256(48 * (size_t)num_rendered))
+                        : nullptr;
   StageTimer T(8, s);
   STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, gsum, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
+  return WGSR_OK;
+}
+
+int wgsr_pack_view_camera(const wgsr_raster_args* args, float* camera_row, void* stream) {
+  g_err[0] = 0;
+  if (!args || !camera_row || !args->viewmatrix || !args->projmatrix || !args->projmatrix_raw || !args->campos)
+    return set_error(WGSR_EINVAL, "wgsr_pack_view_camera: missing camera tensor");
+  HIPCHK(launch_pack_camera(*args, camera_row, (hipStream_t)stream));
+  return WGSR_OK;
+}
+
+int wgsr_rasterize_backward_records(const wgsr_raster_args* args, const int32_t* radii, const void* geom,
+                                    void* binning, void* image, int64_t num_rendered, const float* dL_dcolor,
+                                    const float* dL_ddepth, wgsr_alloc_fn scratch_alloc, void* ctx, int P_pad,
+                                    float* records, void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  const wgsr_raster_args& a = *args;
+  if (P_pad < a.P) return set_error(WGSR_EINVAL, "P_pad (%d) < P (%d)", P_pad, a.P);
+  if (P_pad > 0 && !records) return set_error(WGSR_EINVAL, "missing records buffer");
+  hipStream_t s = (hipStream_t)stream;
+  float4* partial = nullptr;
+  uint8_t* pflag = nullptr;
+  if (a.P > 0) {
+    if (int e = render_backward_pairs(a, geom, binning, image, num_rendered, dL_dcolor, dL_ddepth, scratch_alloc,
+                                      ctx, s, &partial, &pflag))
+      return e;
+  }
+  StageTimer T(8, s);
+  STAGE(a, s, launch_view_records(a, radii, geom, partial, pflag, P_pad, records, s));
+  return WGSR_OK;
+}
+
+int wgsr_gauss_backward_views_blocks(int lo, int hi) { return gauss_bwd_views_blocks(lo, hi); }
+
+int wgsr_gauss_backward_views(const wgsr_raster_args* params, int lo, int hi, int n_views, const float* cameras,
+                              const float* records, int64_t record_view_stride, float* dL_dmeans3D, float* dL_dsh,
+                              float* dL_dopacity, float* dL_dscales, float* dL_drotations, float* tau_partials,
+                              float* stats, void* stream) {
+  g_err[0] = 0;
+  if (!params) return set_error(WGSR_EINVAL, "null args");
+  const wgsr_raster_args& a = *params;
+  if (lo < 0 || hi < lo || hi > a.P) return set_error(WGSR_EINVAL, "shard [%d, %d) outside [0, %d)", lo, hi, a.P);
+  if (n_views < 0) return set_error(WGSR_EINVAL, "negative view count");
+  if (hi == lo || n_views == 0) {
+    if (hi > lo) return set_error(WGSR_EINVAL, "a non-empty shard needs at least one view");
+    return WGSR_OK;
+  }
+  if (!a.means3D || !a.scales || !a.rotations)
+    return set_error(WGSR_EINVAL, "the view-sharded backward needs means3D, scales and rotations "
+                                  "(cov3D_precomp is not supported)");
+  if (a.shs && (a.M <= 0 || a.M > 16 || a.D < 0 || a.D > 3 || (a.D + 1) * (a.D + 1) > a.M))
+    return set_error(WGSR_EINVAL, "invalid SH configuration (degree %d, %d coefficients)", a.D, a.M);
+  if (!cameras || !records) return set_error(WGSR_EINVAL, "missing camera table or records");
+  if (record_view_stride < (int64_t)(hi - lo) * WGSR_VIEW_RECORD_FLOATS || record_view_stride % 4)
+    return set_error(WGSR_EINVAL, "record_view_stride must be a multiple of 4 and >= %d",
+                     (hi - lo) * WGSR_VIEW_RECORD_FLOATS);
+  if (!dL_dmeans3D || !dL_dopacity || !dL_dscales || !dL_drotations || (a.shs && !dL_dsh))
+    return set_error(WGSR_EINVAL, "missing gradient output");
+  hipStream_t s = (hipStream_t)stream;
+  StageTimer T(8, s);
+  HIPCHK(launch_gauss_bwd_views(a, lo, hi, n_views, cameras, records, record_view_stride, dL_dmeans3D, dL_dsh,
+                                dL_dopacity, dL_dscales, dL_drotations, tau_partials, stats, s));
+  if (a.debug) {
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+  }
   return WGSR_OK;
 }
 

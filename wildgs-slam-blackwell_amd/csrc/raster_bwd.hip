@@ -216,6 +216,9 @@ __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k]
 // upstream computeColorFromSH backward; returns dL/dmean and writes dL/dsh
 // for all M stored coefficients (zeros past K).  `sh` and `dsh` may be the
 // same row (the LDS-staged coefficients): every read precedes the writes.
+// kAcc: dsh is a caller register array of 48 floats that receives += (the
+// multi-view backward); otherwise dsh is written, zeros past K.
+template <bool kAcc = false>
 __device__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
   const f3 dir_orig = sub3(pos, campos);
   const float len = sqrtf(dot3(dir_orig, dir_orig));
@@ -261,9 +264,15 @@ __device__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, ui
     }
   }
   auto put = [&](int k, float wgt) {
-    dsh[3 * k] = wgt * dRGB.x;
-    dsh[3 * k + 1] = wgt * dRGB.y;
-    dsh[3 * k + 2] = wgt * dRGB.z;
+    if (kAcc) {
+      dsh[3 * k] += wgt * dRGB.x;
+      dsh[3 * k + 1] += wgt * dRGB.y;
+      dsh[3 * k + 2] += wgt * dRGB.z;
+    } else {
+      dsh[3 * k] = wgt * dRGB.x;
+      dsh[3 * k + 1] = wgt * dRGB.y;
+      dsh[3 * k + 2] = wgt * dRGB.z;
+    }
   };
   put(0, SH_C0);
   if (deg > 0) {
@@ -287,7 +296,8 @@ __device__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, ui
       }
     }
   }
-  for (int k = 3 * (deg + 1) * (deg + 1); k < 3 * M; ++k) dsh[k] = 0.f;
+  if (!kAcc)
+    for (int k = 3 * (deg + 1) * (deg + 1); k < 3 * M; ++k) dsh[k] = 0.f;
   const f3 dL_ddir = mk3(dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB));
   const f3 v = dir_orig;
   const float sum2 = dot3(v, v);
@@ -370,47 +380,22 @@ __global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __re
   for (int q = 0; q < 10; ++q) gsum[(size_t)q * P + i] = g[q];
 }
 
-// Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
-// holds its 3M SH coefficients on entry and its dL/dsh row on exit.
-__device__ __forceinline__ void gauss_bwd_one(
-    int i, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ clamped, const float g[10],
-    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
-    const float* __restrict__ cov_pre, float* shrow, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
-    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
-    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
-  const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
-  if (!(radii[i] > 0)) {
-    for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
-    for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
-    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (shrow) for (int k = 0; k < 3 * M; ++k) shrow[k] = 0.f;
-    o_opac[i] = 0.f;
-    return;
-  }
-  // parameters first: their loads overlap the partial-record walk below
-  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  f3 sv = mk3(0.f, 0.f, 0.f);
-  float cv[6];
-  if (cov_pre) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
-  } else {
-    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
-    q = reinterpret_cast<const float4*>(rots)[i];
-  }
-  o_m2d[i3] = g[0]; o_m2d[i3 + 1] = g[1]; o_m2d[i3 + 2] = 0.f;
-  o_opac[i] = g[5];
-  o_col[i3] = g[6]; o_col[i3 + 1] = g[7]; o_col[i3 + 2] = g[8];
-  const float dcx = g[2], dcy = g[3], dcw = g[4], ddepth = g[9];
+// Camera-side backward of one Gaussian in one view (upstream
+// computeCov2DCUDA + the projection / depth terms of preprocessCUDA backward,
+// plus the w-pose gradient): from its screen-space partial sums g[10] to
+// dL/dmean3D (without the SH term), dL/dcov3D and the pose gradient (rho,
+// theta).  pa, pb, pe: projmatrix_raw[0], [5], [11].
+struct CamBwd {
+  f3 dm;
+  float ocov[6];
+  f3 rho, theta;
+};
 
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
+__device__ __forceinline__ void cam_backward(const Cam& c, float pa, float pb, float pe, f3 mean, const float cv[6],
+                                             const float g[10], CamBwd& o) {
+  const float dcx = g[2], dcy = g[3], dcw = g[4], ddepth = g[9];
   // ---- cov2D backward (upstream computeCov2DCUDA)
   const f3 t = xform43(c.view, mean);
-  if (!cov_pre) cov3d_from(sv, scale_mod, q, cv);
   float S[3][3];
   sym3(cv, S);
   float T[2][3];
@@ -422,7 +407,9 @@ __device__ __forceinline__ void gauss_bwd_one(
   const float denom = a * cc - b * b;
   float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
   const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-  float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float* ocov = o.ocov;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) ocov[k] = 0.f;
   if (denom2inv != 0) {
     dL_da = denom2inv * (-cc * cc * dcx + 2 * b * cc * dcy + (denom - a * cc) * dcw);
     dL_dc = denom2inv * (-a * a * dcw + 2 * a * b * dcy + (denom - a * cc) * dcx);
@@ -437,8 +424,6 @@ __device__ __forceinline__ void gauss_bwd_one(
     ocov[4] = 2 * T[0][2] * T[0][1] * dL_da + (T[0][1] * T[1][2] + T[0][2] * T[1][1]) * dL_db +
               2 * T[1][1] * T[1][2] * dL_dc;
   }
-#pragma unroll
-  for (int k = 0; k < 6; ++k) o_cov[i6 + k] = ocov[k];
   float dT[2][3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -484,7 +469,6 @@ __device__ __forceinline__ void gauss_bwd_one(
   // pose through the projection (projmatrix_raw a, b, e terms: V5) and depth
   {
     const float alpha_ = m_w, beta_ = -hom.x * m_w * m_w, gamma_ = -hom.y * m_w * m_w;
-    const float pa = praw[0], pb = praw[5], pe = praw[11];
     f3 gp = add3(scl3(g2x, mk3(alpha_ * pa, 0.f, beta_ * pe)), scl3(g2y, mk3(0.f, alpha_ * pb, gamma_ * pe)));
     gp.z += ddepth;
     tau_rho = add3(tau_rho, gp);
@@ -493,46 +477,101 @@ __device__ __forceinline__ void gauss_bwd_one(
   dm.x += ddepth * c.view[2];
   dm.y += ddepth * c.view[6];
   dm.z += ddepth * c.view[10];
+  o.dm = dm;
+  o.rho = tau_rho;
+  o.theta = tau_theta;
+}
+
+// Upstream computeCov3D backward: dL/dcov3D -> dL/dscale (w.r.t. the modified
+// scale, V9) and dL/drotation (raw quaternion).  Linear in dL/dcov3D.
+__device__ __forceinline__ void cov_to_scale_rot(float4 q, f3 sv, float scale_mod, const float ocov[6], float* o_sc,
+                                                 float* o_rot) {
+  float R[3][3];
+  quat_rot(q, R);
+  const float s3[3] = {scale_mod * sv.x, scale_mod * sv.y, scale_mod * sv.z};
+  const float dS[3][3] = {{ocov[0], 0.5f * ocov[1], 0.5f * ocov[2]},
+                          {0.5f * ocov[1], ocov[3], 0.5f * ocov[4]},
+                          {0.5f * ocov[2], 0.5f * ocov[4], ocov[5]}};
+  float Mm[3][3], dM[3][3];
+#pragma unroll
+  for (int r0 = 0; r0 < 3; ++r0)
+#pragma unroll
+    for (int c0 = 0; c0 < 3; ++c0) Mm[r0][c0] = s3[r0] * R[c0][r0];
+#pragma unroll
+  for (int r0 = 0; r0 < 3; ++r0)
+#pragma unroll
+    for (int c0 = 0; c0 < 3; ++c0)
+      dM[r0][c0] = 2.f * (Mm[r0][0] * dS[0][c0] + Mm[r0][1] * dS[1][c0] + Mm[r0][2] * dS[2][c0]);
+  // w.r.t. the modified scale, as upstream (V9)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o_sc[k] = R[0][k] * dM[k][0] + R[1][k] * dM[k][1] + R[2][k] * dM[k][2];
+  float G[3][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G[j][k] = s3[k] * dM[k][j];
+  const float rr = q.x, x = q.y, y = q.z, z = q.w;
+  *reinterpret_cast<float4*>(o_rot) = make_float4(
+      2 * z * (G[1][0] - G[0][1]) + 2 * y * (G[0][2] - G[2][0]) + 2 * x * (G[2][1] - G[1][2]),
+      2 * y * (G[1][0] + G[0][1]) + 2 * z * (G[2][0] + G[0][2]) + 2 * rr * (G[2][1] - G[1][2]) -
+          4 * x * (G[2][2] + G[1][1]),
+      2 * x * (G[1][0] + G[0][1]) + 2 * rr * (G[0][2] - G[2][0]) + 2 * z * (G[2][1] + G[1][2]) -
+          4 * y * (G[2][2] + G[0][0]),
+      2 * rr * (G[1][0] - G[0][1]) + 2 * x * (G[2][0] + G[0][2]) + 2 * y * (G[2][1] + G[1][2]) -
+          4 * z * (G[1][1] + G[0][0]));
+}
+
+// Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
+// holds its 3M SH coefficients on entry and its dL/dsh row on exit.
+__device__ __forceinline__ void gauss_bwd_one(
+    int i, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ clamped, const float g[10],
+    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
+    const float* __restrict__ cov_pre, float* shrow, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
+    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
+    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
+    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
+  if (!(radii[i] > 0)) {
+    for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
+    for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
+    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (shrow) for (int k = 0; k < 3 * M; ++k) shrow[k] = 0.f;
+    o_opac[i] = 0.f;
+    return;
+  }
+  // parameters first: their loads overlap the partial-record walk below
+  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  f3 sv = mk3(0.f, 0.f, 0.f);
+  float cv[6];
+  if (cov_pre) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
+  } else {
+    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
+    q = reinterpret_cast<const float4*>(rots)[i];
+  }
+  o_m2d[i3] = g[0]; o_m2d[i3 + 1] = g[1]; o_m2d[i3 + 2] = 0.f;
+  o_opac[i] = g[5];
+  o_col[i3] = g[6]; o_col[i3 + 1] = g[7]; o_col[i3 + 2] = g[8];
+
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  if (!cov_pre) cov3d_from(sv, scale_mod, q, cv);
+  CamBwd cb;
+  cam_backward(c, praw[0], praw[5], praw[11], mean, cv, g, cb);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o_cov[i6 + k] = cb.ocov[k];
+  f3 dm = cb.dm;
+  const f3 tau_rho = cb.rho, tau_theta = cb.theta;
   if (shrow) {
     const f3 dmsh = sh_backward(D, M, shrow, mean, mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i],
                                 mk3(g[6], g[7], g[8]), shrow);
     dm = add3(dm, dmsh);
   }
-  // ---- cov3D -> scale / rotation (upstream computeCov3D backward)
   if (!cov_pre) {
-    float R[3][3];
-    quat_rot(q, R);
-    const float s3[3] = {scale_mod * sv.x, scale_mod * sv.y, scale_mod * sv.z};
-    const float dS[3][3] = {{ocov[0], 0.5f * ocov[1], 0.5f * ocov[2]},
-                            {0.5f * ocov[1], ocov[3], 0.5f * ocov[4]},
-                            {0.5f * ocov[2], 0.5f * ocov[4], ocov[5]}};
-    float Mm[3][3], dM[3][3];
-#pragma unroll
-    for (int r0 = 0; r0 < 3; ++r0)
-#pragma unroll
-      for (int c0 = 0; c0 < 3; ++c0) Mm[r0][c0] = s3[r0] * R[c0][r0];
-#pragma unroll
-    for (int r0 = 0; r0 < 3; ++r0)
-#pragma unroll
-      for (int c0 = 0; c0 < 3; ++c0)
-        dM[r0][c0] = 2.f * (Mm[r0][0] * dS[0][c0] + Mm[r0][1] * dS[1][c0] + Mm[r0][2] * dS[2][c0]);
-    // w.r.t. the modified scale, as upstream (V9)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o_sc[i3 + k] = R[0][k] * dM[k][0] + R[1][k] * dM[k][1] + R[2][k] * dM[k][2];
-    float G[3][3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) G[j][k] = s3[k] * dM[k][j];
-    const float rr = q.x, x = q.y, y = q.z, z = q.w;
-    reinterpret_cast<float4*>(o_rot)[i] = make_float4(
-        2 * z * (G[1][0] - G[0][1]) + 2 * y * (G[0][2] - G[2][0]) + 2 * x * (G[2][1] - G[1][2]),
-        2 * y * (G[1][0] + G[0][1]) + 2 * z * (G[2][0] + G[0][2]) + 2 * rr * (G[2][1] - G[1][2]) -
-            4 * x * (G[2][2] + G[1][1]),
-        2 * x * (G[1][0] + G[0][1]) + 2 * rr * (G[0][2] - G[2][0]) + 2 * z * (G[2][1] + G[1][2]) -
-            4 * y * (G[2][2] + G[0][0]),
-        2 * rr * (G[1][0] - G[0][1]) + 2 * x * (G[2][0] + G[0][2]) + 2 * y * (G[2][1] + G[1][2]) -
-            4 * z * (G[1][1] + G[0][0]));
+    cov_to_scale_rot(q, sv, scale_mod, cb.ocov, &o_sc[i3], &o_rot[4 * (size_t)i]);
   } else {
     for (int k = 0; k < 3; ++k) o_sc[i3 + k] = 0.f;
     reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -548,7 +587,7 @@ __device__ __forceinline__ void gauss_bwd_one(
 // of 3M-float strided per-thread runs; rows are padded to 3M + 1 floats so
 // each lane's row walk is bank-conflict free.
 constexpr int kGbWave = 64;
-__global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
+__global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_gauss_bwd(
     int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
     const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
     const uint8_t* __restrict__ pflag, const float* __restrict__ gsum,
@@ -584,6 +623,158 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd(
                   sh ? &s_sh[lane * SP] : nullptr, scale_mod, viewm, projm, praw, campos_p, W, H, tanx, tany,
                   o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   if (sh) {
+    __syncthreads();
+    lds_to_slab(s_sh, ng, S, o_sh + (size_t)i0 * S, lane);
+  }
+}
+
+
+// ---- view-sharded backward (wgsr/dp.py) ---------------------
+// A view's backward is split at the per-Gaussian screen-space partial sums:
+// k_view_records writes each Gaussian's 12-float record (the ten sums g[10]
+// k_gauss_bwd would start from, its radius and SH clamp bits), so a rank can
+// ship 48 bytes per Gaussian per view to the Gaussian's owner instead of
+// all-reducing 59 floats of parameter gradients; the owner's
+// k_gauss_bwd_views then runs the camera-side backward of every view for its
+// shard and sums the views in registers.
+__global__ __launch_bounds__(256) void k_view_records(int P, int P_pad, const int32_t* __restrict__ radii,
+                                                      const uint32_t* __restrict__ slot_start,
+                                                      const uint32_t* __restrict__ tiles,
+                                                      const uint32_t* __restrict__ clamped,
+                                                      const uint8_t* __restrict__ pflag,
+                                                      const float4* __restrict__ partial, int W, int H,
+                                                      float4* __restrict__ rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P_pad) return;
+  float g[10];
+  const bool live = i < P && radii[i] > 0;
+  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+  sum_partials(s0, s1, pflag, partial, g);
+  scale_partial_sums(g, W, H);
+  const float r = live ? (float)radii[i] : 0.f, cb = live ? (float)clamped[i] : 0.f;
+  rec[3 * (size_t)i] = make_float4(g[0], g[1], g[2], g[3]);
+  rec[3 * (size_t)i + 1] = make_float4(g[4], g[5], g[6], g[7]);
+  rec[3 * (size_t)i + 2] = make_float4(g[8], g[9], r, cb);
+}
+
+// Camera table row (WGSR_VIEW_CAMERA_FLOATS floats): viewmatrix[16],
+// projmatrix[16], projmatrix_raw[16], campos[3], tan_fovx, tan_fovy, W, H.
+__global__ __launch_bounds__(64) void k_pack_camera(const float* __restrict__ viewm, const float* __restrict__ projm,
+                                                    const float* __restrict__ praw, const float* __restrict__ campos,
+                                                    float tanx, float tany, int W, int H, float* __restrict__ row) {
+  const int l = threadIdx.x;
+  float v = 0.f;
+  if (l < 16) v = viewm[l];
+  else if (l < 32) v = projm[l - 16];
+  else if (l < 48) v = praw[l - 32];
+  else if (l < 51) v = campos[l - 48];
+  else if (l == 51) v = tanx;
+  else if (l == 52) v = tany;
+  else if (l == 53) v = (float)W;
+  else if (l == 54) v = (float)H;
+  row[l] = v;
+}
+
+// Owner side: Gaussians [lo, hi), one wave per 64, the SH slab through LDS
+// (as k_gauss_bwd).  For each of the nv views, the view's record (a block of
+// rec_stride float4s per view, row i - lo) drives cam_backward and the SH
+// backward with that view's camera; dL/dmean3D, dL/dsh, dL/dopacity and
+// dL/dcov3D are summed over the views in registers, and the view-independent
+// cov3D -> (scale, rotation) step runs once on the summed dL/dcov3D (it is
+// linear).  Per view, the wave's pose-gradient sum goes to
+// tau_blk[block][view][6] (fixed-order wave reduction: deterministic); stats
+// (optional) receive the densification statistics of the reference's
+// add_densification_stats summed over views: sum ||dL/dmeans2D[:2]||, the
+// number of views that see the Gaussian and its largest screen radius.
+__global__ __launch_bounds__(kGbWave) void k_gauss_bwd_views(
+    int lo, int hi, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ shs, float scale_mod, int nv,
+    const float* __restrict__ cams, const float4* __restrict__ rec, int64_t rec_stride, float* __restrict__ o_m3d,
+    float* __restrict__ o_sh, float* __restrict__ o_opac, float* __restrict__ o_sc, float* __restrict__ o_rot,
+    float* __restrict__ tau_blk, float* __restrict__ stats) {
+  extern __shared__ float s_sh[];  // kGbWave x (3M + 1) floats (dynamic)
+  const int lane = threadIdx.x;
+  const int i0 = lo + blockIdx.x * kGbWave, i = i0 + lane;
+  const int ng = min(kGbWave, hi - i0);
+  const bool live = i < hi;
+  const int S = 3 * M, SP = S + 1;
+  const bool sh = shs != nullptr;
+  const size_t i3 = 3 * (size_t)i;
+  if (sh) {
+    slab_to_lds(shs + (size_t)i0 * S, ng, S, s_sh, lane);
+    __syncthreads();
+  }
+  f3 mean = mk3(0.f, 0.f, 0.f), sv = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  if (live) {
+    mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+    sv = mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
+    q = reinterpret_cast<const float4*>(rots)[i];
+  }
+  float cv[6];
+  cov3d_from(sv, scale_mod, q, cv);  // view independent: once per Gaussian
+  float dsh[48];
+#pragma unroll
+  for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+  f3 dm = mk3(0.f, 0.f, 0.f);
+  float ocov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dop = 0.f, st_norm = 0.f, st_cnt = 0.f, st_rad = 0.f;
+  const float4* my = rec + 3 * (size_t)(i - lo);
+  for (int v = 0; v < nv; ++v) {
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0;
+    if (live) {
+      r0 = my[(size_t)v * rec_stride];
+      r1 = my[(size_t)v * rec_stride + 1];
+      r2 = my[(size_t)v * rec_stride + 2];
+    }
+    const bool vis = r2.z > 0.f;  // this view's radius
+    f3 rho = mk3(0.f, 0.f, 0.f), theta = rho;
+    if (vis) {
+      const float g[10] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y};
+      const float* t = cams + (size_t)v * WGSR_VIEW_CAMERA_FLOATS;
+      Cam c;
+      load_cam(c, t, t + 16, (int)t[53], (int)t[54], t[51], t[52]);
+      CamBwd cb;
+      cam_backward(c, t[32], t[37], t[43], mean, cv, g, cb);
+      f3 dmv = cb.dm;
+      if (sh)
+        dmv = add3(dmv, sh_backward<true>(D, M, &s_sh[lane * SP], mean, mk3(t[48], t[49], t[50]), (uint32_t)r2.w,
+                                          mk3(g[6], g[7], g[8]), dsh));
+      dm = add3(dm, dmv);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) ocov[k] += cb.ocov[k];
+      dop += g[5];
+      rho = cb.rho;
+      theta = cb.theta;
+      st_norm += sqrtf(g[0] * g[0] + g[1] * g[1]);
+      st_cnt += 1.f;
+      st_rad = fmaxf(st_rad, r2.z);
+    }
+    if (tau_blk) {
+      const float tv[6] = {rho.x, rho.y, rho.z, theta.x, theta.y, theta.z};
+      float* dst = tau_blk + ((size_t)blockIdx.x * nv + v) * 6;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const float s = wave_sum(tv[k]);
+        if (lane == 0) dst[k] = s;
+      }
+    }
+  }
+  if (live) {
+    o_m3d[i3] = dm.x; o_m3d[i3 + 1] = dm.y; o_m3d[i3 + 2] = dm.z;
+    o_opac[i] = dop;
+    cov_to_scale_rot(q, sv, scale_mod, ocov, &o_sc[i3], &o_rot[4 * (size_t)i]);
+    if (stats) {
+      const size_t j = 3 * (size_t)(i - lo);
+      stats[j] = st_norm; stats[j + 1] = st_cnt; stats[j + 2] = st_rad;
+    }
+  }
+  if (sh) {
+    // this lane's row only, then the wave moves the slab: all rows written
+    // before lds_to_slab reads across lanes
+#pragma unroll
+    for (int k = 0; k < 48; ++k)
+      if (k < S) s_sh[lane * SP + k] = dsh[k];
     __syncthreads();
     lds_to_slab(s_sh, ng, S, o_sh + (size_t)i0 * S, lane);
   }
@@ -628,6 +819,38 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
                      dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
                      dL_dscales, dL_drot, dL_dtau);
+  return hipGetLastError();
+}
+
+hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, const void* geom, const float4* partial,
+                               const uint8_t* pflag, int P_pad, float* records, hipStream_t s) {
+  if (P_pad == 0) return hipSuccess;
+  const GeomLayout L(a.P);
+  hipLaunchKernelGGL(k_view_records, dim3((P_pad + 255) / 256), dim3(256), 0, s, a.P, P_pad, radii,
+                     at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
+                     pflag, partial, a.W, a.H, reinterpret_cast<float4*>(records));
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_camera(const wgsr_raster_args& a, float* row, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_camera, dim3(1), dim3(WGSR_VIEW_CAMERA_FLOATS), 0, s, a.viewmatrix, a.projmatrix,
+                     a.projmatrix_raw, a.campos, a.tan_fovx, a.tan_fovy, a.W, a.H, row);
+  return hipGetLastError();
+}
+
+int gauss_bwd_views_blocks(int lo, int hi) { return hi > lo ? (hi - lo + kGbWave - 1) / kGbWave : 0; }
+
+hipError_t launch_gauss_bwd_views(const wgsr_raster_args& a, int lo, int hi, int nv, const float* cams,
+                                  const float* records, int64_t rec_stride_floats, float* dL_dmeans3D, float* dL_dsh,
+                                  float* dL_dopacity, float* dL_dscales, float* dL_drot, float* tau_blk, float* stats,
+                                  hipStream_t s) {
+  const int nb = gauss_bwd_views_blocks(lo, hi);
+  if (nb == 0) return hipSuccess;
+  const size_t lds = a.shs ? sizeof(float) * kGbWave * (3 * (size_t)a.M + 1) : 0;
+  hipLaunchKernelGGL(k_gauss_bwd_views, dim3(nb), dim3(kGbWave), lds, s, lo, hi, a.D, a.M, a.means3D, a.scales,
+                     a.rotations, a.shs, a.scale_modifier, nv, cams, reinterpret_cast<const float4*>(records),
+                     rec_stride_floats / 4, dL_dmeans3D, a.shs ? dL_dsh : nullptr, dL_dopacity, dL_dscales, dL_drot,
+                     tau_blk, stats);
   return hipGetLastError();
 }
 

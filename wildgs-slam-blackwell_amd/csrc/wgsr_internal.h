@@ -61,6 +61,16 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                             float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                             float* dL_drot, float* dL_dtau, hipStream_t s);
 
+// view-sharded backward (raster_bwd.hip, wgsr/dp.py)
+hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, const void* geom, const float4* partial,
+                               const uint8_t* pflag, int P_pad, float* records, hipStream_t s);
+hipError_t launch_pack_camera(const wgsr_raster_args& a, float* row, hipStream_t s);
+int gauss_bwd_views_blocks(int lo, int hi);
+hipError_t launch_gauss_bwd_views(const wgsr_raster_args& a, int lo, int hi, int nv, const float* cams,
+                                  const float* records, int64_t rec_stride_floats, float* dL_dmeans3D, float* dL_dsh,
+                                  float* dL_dopacity, float* dL_dscales, float* dL_drot, float* tau_blk, float* stats,
+                                  hipStream_t s);
+
 // distCUDA2 (knn.hip)
 size_t knn_scratch_bytes(int P);
 hipError_t launch_dist_cuda2(int P, const float* points, float* out, void* scratch, hipStream_t s);

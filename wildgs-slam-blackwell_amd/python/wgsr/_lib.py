@@ -92,6 +92,15 @@ def load():
         L.wgsr_rasterize_backward.restype = c_int
         L.wgsr_rasterize_backward.argtypes = [P_ARGS, _fp, _fp, _fp, _fp, c_i64, _fp, _fp, ALLOC_FN,
                                               ctypes.c_void_p] + [_fp] * 9 + [_fp]
+        L.wgsr_pack_view_camera.restype = c_int
+        L.wgsr_pack_view_camera.argtypes = [P_ARGS, _fp, _fp]
+        L.wgsr_rasterize_backward_records.restype = c_int
+        L.wgsr_rasterize_backward_records.argtypes = [P_ARGS, _fp, _fp, _fp, _fp, c_i64, _fp, _fp, ALLOC_FN,
+                                                      ctypes.c_void_p, c_int, _fp, _fp]
+        L.wgsr_gauss_backward_views_blocks.restype = c_int
+        L.wgsr_gauss_backward_views_blocks.argtypes = [c_int, c_int]
+        L.wgsr_gauss_backward_views.restype = c_int
+        L.wgsr_gauss_backward_views.argtypes = [P_ARGS, c_int, c_int, c_int, _fp, _fp, c_i64] + [_fp] * 7 + [_fp]
         L.wgsr_mark_visible.restype = c_int
         L.wgsr_mark_visible.argtypes = [c_int, _fp, _fp, _fp, _fp, _fp]
         L.wgsr_dist_cuda2.restype = c_int
@@ -143,7 +152,12 @@ EXPORTED_SYMBOLS = (
     "wgsr_adam_step", "wgsr_compact_rows",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
+    "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",
+    "wgsr_gauss_backward_views",
 )
+
+VIEW_RECORD_FLOATS = 12   # WGSR_VIEW_RECORD_FLOATS
+VIEW_CAMERA_FLOATS = 64   # WGSR_VIEW_CAMERA_FLOATS
 
 
 class StageProfile:

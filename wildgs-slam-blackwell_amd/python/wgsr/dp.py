@@ -24,6 +24,7 @@ on ROCm (over xGMI on one node); the CPU tests use "gloo".
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
@@ -97,3 +98,222 @@ def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tenso
 def views_for_rank(num_views: int, rank: int, world: int):
     """Round-robin view assignment: rank r renders views r, r + world, ..."""
     return list(range(rank, num_views, world))
+
+
+# ---------------------------------------------------------------------------
+# View-sharded backward: exchange screen-space partials, not gradients.
+# ---------------------------------------------------------------------------
+# The all-reduce above moves 2 (N-1)/N x 59 floats per Gaussian per rank.  A
+# view's parameter gradient is a per-Gaussian function of the camera and of
+# ten screen-space partial sums (dL/dmean2D, dL/dconic, dL/dopacity,
+# dL/dcolour, dL/ddepth) that the render backward produces.  So each rank
+# ships its view's 12-float record of every Gaussian to the Gaussian's OWNER
+# (all-to-all, (N-1)/N x 12 floats per Gaussian), each owner runs the
+# camera-side backward of all N views for its 1/N shard and sums them in
+# registers (one kernel), and the summed shards are all-gathered
+# ((N-1)/N x 59 floats) -- every rank ends with the same SUM over views that
+# allreduce_grads produces, for 71 instead of 118 floats of traffic per
+# Gaussian at N = 8.  The pose gradient of each view is reduced over the
+# owners' shards (N x 6 floats), and the densification statistics of all
+# views come out of the same kernel.
+
+
+class _HipViewKernels:
+    """The three libwgsr entry points of the view-sharded backward."""
+
+    @staticmethod
+    def _raster_args(P, D, M, W, H, means3D, scales, rotations, shs, scale_modifier, cam, keep):
+        from diff_gaussian_rasterization import _C
+        e = None
+        cam = {k: (v.contiguous() if torch.is_tensor(v) else v) for k, v in cam.items()}
+        return _C._args(P, D, M, W, H, cam.get("bg", means3D), means3D, e, means3D, scales, rotations, e,
+                        shs, cam.get("viewmatrix"), cam.get("projmatrix"), cam.get("projmatrix_raw"),
+                        cam.get("campos"), scale_modifier, cam.get("tanfovx", 1.0), cam.get("tanfovy", 1.0),
+                        False, False, keep)
+
+    def pack_camera(self, cam, W, H, out_row):
+        from wgsr import _lib
+        L = _lib.load()
+        keep = []
+        a = self._raster_args(0, 0, 0, W, H, None, None, None, None, 1.0, cam, keep)
+        _lib.check(L.wgsr_pack_view_camera(ctypes.byref(a), out_row.data_ptr(),
+                                           _lib.stream_handle(out_row.device)))
+
+    def records(self, fwd, dL_dcolor, dL_ddepth, P_pad, out):
+        """fwd: the forward's (means3D, scales, rotations, shs, D, cam dict,
+        num_rendered, radii, geom, binning, image).  out: [P_pad, 12]."""
+        from wgsr import _lib
+        L = _lib.load()
+        means3D, scales, rotations, shs, D, cam, nr, radii, geom, binning, image = fwd
+        if shs is None or scales is None or rotations is None:
+            raise RuntimeError("the view-sharded backward needs SHs, scales and rotations "
+                               "(colors_precomp / cov3D_precomp are not supported)")
+        P = means3D.size(0)
+        M = shs.size(1) if shs is not None else 0
+        H, W = dL_dcolor.size(1), dL_dcolor.size(2)
+        keep = []
+        a = self._raster_args(P, int(D), M, W, H, means3D.contiguous(), scales.contiguous(),
+                              rotations.contiguous(), shs.contiguous() if shs is not None else None, 1.0,
+                              cam, keep)
+        gc, gd = dL_dcolor.contiguous(), dL_ddepth.contiguous()
+        p = _lib.ptr
+        dev = means3D.device
+        with torch.cuda.device(dev), _lib.AllocRequest(dev):
+            code = L.wgsr_rasterize_backward_records(
+                ctypes.byref(a), p(radii), p(geom), p(binning), p(image), int(nr), gc.data_ptr(),
+                gd.data_ptr(), _lib.ALLOC_SCRATCH, None, int(P_pad), out.data_ptr(), _lib.stream_handle(dev))
+        _lib.check(code)
+
+    def tau_blocks(self, lo, hi):
+        from wgsr import _lib
+        return int(_lib.load().wgsr_gauss_backward_views_blocks(int(lo), int(hi)))
+
+    def gauss_views(self, params, lo, hi, cams, recs, grads, tau_out, stats_out):
+        """params: (means3D, scales, rotations, shs, D, scale_modifier);
+        cams [V, 64]; recs [V, S, 12]; grads: GradBuffer views (rows [lo, hi)
+        written); tau_out [blocks, V, 6] or None; stats_out [hi-lo, 3] or None."""
+        from wgsr import _lib
+        L = _lib.load()
+        means3D, scales, rotations, shs, D, scale_modifier = params
+        P = means3D.size(0)
+        M = shs.size(1) if shs is not None else 0
+        keep = []
+        a = self._raster_args(P, int(D), M, 1, 1, means3D, scales, rotations, shs, scale_modifier, {}, keep)
+        V = cams.size(0)
+        dev = means3D.device
+        p = _lib.ptr
+        code = L.wgsr_gauss_backward_views(
+            ctypes.byref(a), int(lo), int(hi), int(V), cams.data_ptr(), recs.data_ptr(),
+            int(recs.stride(0)), grads["means3D"].data_ptr(), p(grads["shs"]), grads["opacities"].data_ptr(),
+            grads["scales"].data_ptr(), grads["rotations"].data_ptr(), p(tau_out), p(stats_out),
+            _lib.stream_handle(dev))
+        _lib.check(code)
+
+
+def _gloo_cuda(group):
+    """gloo has no device collectives for every op: stage device tensors
+    through host memory (test rigs only -- RCCL is the product backend)."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _all_to_all_equal(out, inp, group):
+    if _gloo_cuda(group) and inp.is_cuda:
+        o = torch.empty_like(out, device="cpu")
+        dist.all_to_all_single(o, inp.cpu(), group=group)
+        out.copy_(o)
+        return None
+    return dist.all_to_all_single(out, inp, group=group, async_op=True)
+
+
+def _all_gather_into(out_flat, inp, group):
+    if _gloo_cuda(group) and inp.is_cuda:
+        h = torch.empty(out_flat.shape, dtype=out_flat.dtype)
+        dist.all_gather_into_tensor(h, inp.cpu(), group=group)
+        out_flat.copy_(h)
+        return None
+    return dist.all_gather_into_tensor(out_flat, inp, group=group, async_op=True)
+
+
+def _all_gather_inplace(full, rank, group):
+    """full [world * S, ...]: rank's block holds its shard; gather the rest."""
+    world = dist.get_world_size(group)
+    S = full.size(0) // world
+    if _gloo_cuda(group) and full.is_cuda:
+        h = full.cpu()
+        dist.all_gather_into_tensor(h.view(-1), h[rank * S:(rank + 1) * S].reshape(-1).clone(), group=group)
+        full.copy_(h)
+        return None
+    return dist.all_gather_into_tensor(full.view(-1), full[rank * S:(rank + 1) * S].view(-1), group=group,
+                                       async_op=True)
+
+
+def _all_reduce(t, group):
+    if _gloo_cuda(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+        return None
+    return dist.all_reduce(t, group=group, async_op=True)
+
+
+class ViewShardedBackward:
+    """Keyframe-view data-parallel backward with owner-computes sharding.
+
+    Rank r renders view r (its own forward) and calls ``backward`` with that
+    forward's state; every rank returns the SUM over all ranks' views of the
+    parameter gradients (``grads``, the same [P, ...] tensors allreduce_grads
+    produces), its own view's pose gradient (rho, theta) and, with
+    ``stats=True``, the densification statistics summed over the views
+    (sum ||dL/dmeans2D[:2]||, visibility count, max radius per Gaussian).
+
+    Gaussians are sharded by index: rank s owns [s S, (s+1) S), S = ceil(P/N).
+    """
+
+    def __init__(self, P: int, M: int, device, group=None, stats: bool = False, kernels=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.P, self.M = P, M
+        self.S = max(1, -(-P // self.world))
+        self.P_pad = self.S * self.world
+        self.lo = min(P, self.rank * self.S)
+        self.hi = min(P, self.lo + self.S)
+        self.k = kernels or _HipViewKernels()
+        dev = torch.device(device)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.buf = GradBuffer.allocate(self.P_pad, M, dev)
+        self.buf.flat.zero_()  # padding rows are gathered, never read
+        self.grads = {k: v[:P] for k, v in self.buf.views.items()}
+        self.send = torch.zeros(self.P_pad, 12, **f32)
+        self.recv = torch.empty(self.world, self.S, 12, **f32)
+        self.cam_row = torch.zeros(64, **f32)
+        self.cams = torch.empty(self.world, 64, **f32)
+        nb = self.k.tau_blocks(self.lo, self.hi)
+        self.tau_blk = torch.zeros(max(nb, 1), self.world, 6, **f32)
+        self.tau = torch.zeros(self.world, 6, **f32)
+        self.stats = torch.zeros(self.P_pad, 3, **f32) if stats else None
+
+    def backward(self, fwd, dL_dcolor, dL_ddepth, scale_modifier: float = 1.0):
+        """fwd = (means3D, scales, rotations, shs, D, cam, num_rendered, radii,
+        geom, binning, image) of this rank's forward; cam is the dict of
+        camera tensors/scalars (viewmatrix, projmatrix, projmatrix_raw,
+        campos, tanfovx, tanfovy, bg).  -> (grads dict, tau [6] of this
+        rank's view, stats [P, 3] or None)."""
+        means3D, scales, rotations, shs, D, cam = fwd[:6]
+        H, W = dL_dcolor.size(1), dL_dcolor.size(2)
+        g = self.group
+        # this view's camera row -> every owner (tiny; overlaps the records)
+        self.k.pack_camera(cam, W, H, self.cam_row)
+        if self.world > 1:
+            w_cam = _all_gather_into(self.cams.view(-1), self.cam_row, g)
+        else:
+            self.cams.copy_(self.cam_row[None])
+            w_cam = None
+        # this view's screen-space records of every Gaussian -> owners
+        self.k.records(fwd, dL_dcolor, dL_ddepth, self.P_pad, self.send)
+        if self.world > 1:
+            w = _all_to_all_equal(self.recv.view(self.P_pad, 12), self.send, g)
+            if w is not None:
+                w.wait()
+        else:
+            self.recv.view(self.P_pad, 12).copy_(self.send)
+        if w_cam is not None:
+            w_cam.wait()
+        # owner: all views of the shard, summed
+        st = self.stats[self.lo:self.hi] if self.stats is not None else None
+        self.k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
+                           self.recv, self.buf.views, self.tau_blk if self.hi > self.lo else None, st)
+        if self.hi > self.lo:
+            torch.sum(self.tau_blk, dim=0, out=self.tau)
+        else:
+            self.tau.zero_()
+        if self.world > 1:
+            works = [_all_gather_inplace(v.view(self.P_pad, -1), self.rank, g) for v in self.buf.views.values()]
+            if self.stats is not None:
+                works.append(_all_gather_inplace(self.stats, self.rank, g))
+            works.append(_all_reduce(self.tau, g))
+            for w in works:
+                if w is not None:
+                    w.wait()
+        stats = self.stats[:self.P] if self.stats is not None else None
+        return self.grads, self.tau[self.rank], stats
