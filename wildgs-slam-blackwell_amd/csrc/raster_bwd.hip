@@ -629,6 +629,7 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
 }
 
 
+
 // ---- view-sharded backward (wgsr/dp.py) ---------------------
 // A view's backward is split at the per-Gaussian screen-space partial sums:
 // k_view_records writes each Gaussian's 12-float record (the ten sums g[10]
