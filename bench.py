@@ -128,9 +128,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the N > 1 code path on a one-GPU box (never used by
+    # the driver): WGSR_BENCH_BACKEND=gloo, WGSR_BENCH_SHARE_GPU=1 (all ranks
+    # on cuda:0; wgsr.dp stages gloo collectives through host memory)
+    backend = os.environ.get("WGSR_BENCH_BACKEND", "nccl")
+    if os.environ.get("WGSR_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
 
     from diff_gaussian_rasterization import _C
@@ -197,7 +206,7 @@ def main():
         prof.__exit__(None, None, None)
     dt = t1 - t0
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
