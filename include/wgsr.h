@@ -151,6 +151,56 @@ int wgsr_gauss_backward_views(const wgsr_raster_args* params, int lo, int hi, in
                               float* dL_dopacity, float* dL_dscales, float* dL_drotations,
                               float* tau_partials, float* stats, void* stream);
 
+/* ---- the mapping iteration around the path ----
+ * src/mapper.py:1083-1219 per iteration, as fused launches (csrc/mapping.hip;
+ * driven by wgsr/mapping.py).  Partial sums are one float (or float pair) per
+ * workgroup of wgsr_map_blocks(n) workgroups; callers reduce them in order. */
+int wgsr_map_blocks(int64_t n);
+
+/* GaussianModel.get_opacity / get_scaling / get_rotation (gaussian_model.py:
+ * sigmoid, exp, F.normalize(eps 1e-12)) of the raw [P,1] / [P,3] / [P,4]
+ * parameters, plus iso_partials[wgsr_map_blocks(P)] = per-block sums of
+ * sum_k |exp(s_k) - mean_k exp(s_k)| (mapper.py:1167-1169). */
+int wgsr_gaussian_activate(int P, const float* opacity_raw, const float* scaling_raw,
+                           const float* rotation_raw, float* opacity, float* scales,
+                           float* rotations, float* iso_partials, void* stream);
+
+/* Chain rule of wgsr_gaussian_activate back to the raw parameters; adds the
+ * gradient of iso_weight * sum |exp(s) - mean_row exp(s)| (iso_weight = 10 /
+ * (3 P) for the reference's 10 * isotropic_loss.mean()). */
+int wgsr_gaussian_activate_backward(int P, const float* opacity_raw, const float* scaling_raw,
+                                    const float* rotation_raw, const float* dL_dopacity,
+                                    const float* dL_dscales, const float* dL_drotations,
+                                    float iso_weight, float* dL_dopacity_raw,
+                                    float* dL_dscaling_raw, float* dL_drotation_raw, void* stream);
+
+/* get_loss_mapping_rgbd (slam_utils.py:107-143) without its SSIM term:
+ * image_ab = exp(exposure_a) image + exposure_b ([3,H,W], written for the
+ * SSIM kernels); partials[wgsr_map_blocks(H*W)][2] = per-block sums of the
+ * boundary-masked rgb L1 (mask: sum_c gt > rgb_threshold) and of the masked
+ * depth L1 (gt_depth > 0.01).  exposure_a/b: device scalars. */
+int wgsr_mapping_loss_forward(int H, int W, const float* image, const float* gt_image,
+                              const float* depth, const float* gt_depth, const float* exposure_a,
+                              const float* exposure_b, float rgb_threshold, float* image_ab,
+                              float* partials, void* stream);
+
+/* Backward of w_rgb * sum(rgb L1) + w_depth * sum(depth L1) + the SSIM term
+ * whose gradient w.r.t. image_ab is ssim_grad ([3,H,W], already scaled; NULL =
+ * none): dL_dimage [3,H,W], dL_ddepth [1,H,W] and partials[blocks][2] = per-
+ * block sums of dL/dexposure_a and dL/dexposure_b. */
+int wgsr_mapping_loss_backward(int H, int W, const float* image, const float* image_ab,
+                               const float* gt_image, const float* depth, const float* gt_depth,
+                               const float* exposure_a, float rgb_threshold, float w_rgb,
+                               float w_depth, const float* ssim_grad, float* dL_dimage,
+                               float* dL_ddepth, float* partials, void* stream);
+
+/* One view's densification bookkeeping (mapper.py:1177-1183,
+ * gaussian_model.py:745-749) for Gaussians with radii > 0:
+ * max_radii2D = max(max_radii2D, radii); grad_accum += ||dL_dmeans2D[:2]||;
+ * denom += 1. */
+int wgsr_densification_stats(int P, const int32_t* radii, const float* dL_dmeans2D,
+                             float* max_radii2D, float* grad_accum, float* denom, void* stream);
+
 /* Replaces _C.mark_visible: present[i] = (view-space z of point i > 0.2). */
 int wgsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
                       const float* projmatrix, uint8_t* present, void* stream);
@@ -173,6 +223,13 @@ typedef struct wgsr_adam_tensor {
   int64_t numel;
   float step_size;
   float bias_correction2_sqrt;
+  /* Optional two-rate split (0 = off): element e with e % split_period >=
+   * split_len steps with step_size_tail instead of step_size.  Lets one
+   * [P,16,3] SH storage carry the reference's f_dc (first 3 floats of each
+   * 48, lr 2.5e-3) and f_rest (lr / 20) parameter groups in one tensor. */
+  int64_t split_period;
+  int64_t split_len;
+  float step_size_tail;
 } wgsr_adam_tensor;
 #define WGSR_ADAM_MAX_TENSORS 16
 

@@ -42,11 +42,18 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = p + neg_step * (m / denom);
 }
 
+// -step size of element e (the optional two-rate split, wgsr.h)
+__device__ __forceinline__ float neg_step_of(const wgsr_adam_tensor& T, int64_t e) {
+  if (T.split_period <= 0) return -T.step_size;
+  const int64_t c = (T.numel < (int64_t)1 << 32) ? (int64_t)((uint32_t)e % (uint32_t)T.split_period) : e % T.split_period;
+  return c >= T.split_len ? -T.step_size_tail : -T.step_size;
+}
+
 __device__ __forceinline__ void adam_scalar(const wgsr_adam_tensor& T, int64_t e0, float w1, float beta2, float w2,
                                             float eps) {
   for (int64_t e = e0; e < min(e0 + 4, T.numel); ++e) {
     float p = T.param[e], m = T.exp_avg[e], v = T.exp_avg_sq[e];
-    adam_elem(p, T.grad[e], m, v, w1, beta2, w2, eps, -T.step_size, T.bias_correction2_sqrt);
+    adam_elem(p, T.grad[e], m, v, w1, beta2, w2, eps, neg_step_of(T, e), T.bias_correction2_sqrt);
     T.param[e] = p;
     T.exp_avg[e] = m;
     T.exp_avg_sq[e] = v;
@@ -96,11 +103,16 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
         adam_scalar(T, e0[j], w1, beta2, w2, eps);
         continue;
       }
-      const float ns = -T.step_size, bc2s = T.bias_correction2_sqrt;
-      adam_elem(p[j].x, g[j].x, m[j].x, v[j].x, w1, beta2, w2, eps, ns, bc2s);
-      adam_elem(p[j].y, g[j].y, m[j].y, v[j].y, w1, beta2, w2, eps, ns, bc2s);
-      adam_elem(p[j].z, g[j].z, m[j].z, v[j].z, w1, beta2, w2, eps, ns, bc2s);
-      adam_elem(p[j].w, g[j].w, m[j].w, v[j].w, w1, beta2, w2, eps, ns, bc2s);
+      const float bc2s = T.bias_correction2_sqrt;
+      float ns[4] = {-T.step_size, -T.step_size, -T.step_size, -T.step_size};
+      if (T.split_period > 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ns[k] = neg_step_of(T, e0[j] + k);
+      }
+      adam_elem(p[j].x, g[j].x, m[j].x, v[j].x, w1, beta2, w2, eps, ns[0], bc2s);
+      adam_elem(p[j].y, g[j].y, m[j].y, v[j].y, w1, beta2, w2, eps, ns[1], bc2s);
+      adam_elem(p[j].z, g[j].z, m[j].z, v[j].z, w1, beta2, w2, eps, ns[2], bc2s);
+      adam_elem(p[j].w, g[j].w, m[j].w, v[j].w, w1, beta2, w2, eps, ns[3], bc2s);
       *reinterpret_cast<float4*>(T.param + e0[j]) = p[j];
       *reinterpret_cast<float4*>(T.exp_avg + e0[j]) = m[j];
       *reinterpret_cast<float4*>(T.exp_avg_sq + e0[j]) = v[j];

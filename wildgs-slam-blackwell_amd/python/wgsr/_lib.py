@@ -43,7 +43,8 @@ class AdamTensor(ctypes.Structure):
 
     _fields_ = [("param", _fp), ("grad", _fp), ("exp_avg", _fp), ("exp_avg_sq", _fp),
                 ("numel", ctypes.c_int64), ("step_size", ctypes.c_float),
-                ("bias_correction2_sqrt", ctypes.c_float)]
+                ("bias_correction2_sqrt", ctypes.c_float), ("split_period", ctypes.c_int64),
+                ("split_len", ctypes.c_int64), ("step_size_tail", ctypes.c_float)]
 
 
 class RowTensor(ctypes.Structure):
@@ -101,6 +102,19 @@ def load():
         L.wgsr_gauss_backward_views_blocks.argtypes = [c_int, c_int]
         L.wgsr_gauss_backward_views.restype = c_int
         L.wgsr_gauss_backward_views.argtypes = [P_ARGS, c_int, c_int, c_int, _fp, _fp, c_i64] + [_fp] * 7 + [_fp]
+        L.wgsr_map_blocks.restype = c_int
+        L.wgsr_map_blocks.argtypes = [c_i64]
+        L.wgsr_gaussian_activate.restype = c_int
+        L.wgsr_gaussian_activate.argtypes = [c_int] + [_fp] * 7 + [_fp]
+        L.wgsr_gaussian_activate_backward.restype = c_int
+        L.wgsr_gaussian_activate_backward.argtypes = [c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 3 + [_fp]
+        L.wgsr_mapping_loss_forward.restype = c_int
+        L.wgsr_mapping_loss_forward.argtypes = [c_int, c_int] + [_fp] * 6 + [ctypes.c_float, _fp, _fp, _fp]
+        L.wgsr_mapping_loss_backward.restype = c_int
+        L.wgsr_mapping_loss_backward.argtypes = ([c_int, c_int] + [_fp] * 6 + [ctypes.c_float] * 3 +
+                                                 [_fp] * 4 + [_fp])
+        L.wgsr_densification_stats.restype = c_int
+        L.wgsr_densification_stats.argtypes = [c_int] + [_fp] * 5 + [_fp]
         L.wgsr_mark_visible.restype = c_int
         L.wgsr_mark_visible.argtypes = [c_int, _fp, _fp, _fp, _fp, _fp]
         L.wgsr_dist_cuda2.restype = c_int
@@ -154,6 +168,8 @@ EXPORTED_SYMBOLS = (
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",
     "wgsr_gauss_backward_views",
+    "wgsr_map_blocks", "wgsr_gaussian_activate", "wgsr_gaussian_activate_backward",
+    "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
 )
 
 VIEW_RECORD_FLOATS = 12   # WGSR_VIEW_RECORD_FLOATS

@@ -1,0 +1,205 @@
+"""One WildGS mapping iteration on the gfx950 path (SURVEY.md 8(f) f1 + f2).
+
+The reference's inner mapping loop (src/mapper.py:1083-1219, the
+non-uncertainty branch) runs, per iteration, ~100 small torch kernels around
+the rasteriser: GaussianModel's activations and the SH ``torch.cat``
+(gaussian_model.py get_*), get_loss_mapping_rgbd (slam_utils.py:107-143:
+exposure correction, 0.8 L1 + 0.2 (1 - SSIM) on rgb with the boundary mask,
+masked depth L1), ``10 * isotropic_loss.mean()`` (mapper.py:1167-1169), the
+autograd backward of all of it, the densification statistics with boolean
+indexing (mapper.py:1177-1183, gaussian_model.py:745-749) and
+``torch.optim.Adam`` over six parameter groups (gaussian_model.py:309).
+
+``MappingStep`` runs the same iteration as ~15 launches: one activation
+kernel, the rasteriser forward, one loss kernel + the fused SSIM, the SSIM
+backward, one loss-backward kernel, the rasteriser backward (writing straight
+into the parameter-gradient storage), one activation-backward kernel (with
+the isotropic term folded in), one statistics kernel and ONE Adam launch.
+The SH coefficients live in one [P, M, 3] storage: ``f_dc`` / ``f_rest`` are
+views of it (no per-iteration cat, no gradient split), and their different
+learning rates ride in one Adam tensor (``wgsr_adam_tensor.split_*``).
+
+Gradients, loss, statistics and Adam arithmetic match the reference's torch
+composition (tests/test_gpu_mapping.py).  No fallback: libwgsr.so must load.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+# gaussian_model.py:271-309 (training_setup) with opt_params of the configs
+DEFAULT_LR = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 2.5e-3 / 20.0, "opacity": 5e-2, "scaling": 5e-3,
+              "rotation": 1e-3}
+
+
+def _blocks(n):
+    return int(_lib.load().wgsr_map_blocks(int(n)))
+
+
+class MappingStep:
+    """GaussianModel state in the fused layout + one-call mapping iterations."""
+
+    def __init__(self, xyz, features_dc, features_rest, opacity, scaling, rotation, sh_degree: int,
+                 lr: dict | None = None, betas=(0.9, 0.999), eps: float = 1e-15):
+        dev = xyz.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.P = P = xyz.shape[0]
+        self.D = int(sh_degree)
+        self.xyz = xyz.detach().to(**f32).contiguous().clone()
+        self.features = torch.cat([features_dc, features_rest], dim=1).detach().to(**f32).contiguous()
+        self.M = self.features.shape[1]
+        self.opacity = opacity.detach().to(**f32).reshape(P, 1).contiguous().clone()
+        self.scaling = scaling.detach().to(**f32).contiguous().clone()
+        self.rotation = rotation.detach().to(**f32).contiguous().clone()
+        self.lr = dict(DEFAULT_LR, **(lr or {}))
+        self.betas, self.eps = betas, eps
+        self.step_count = 0
+        names = ("xyz", "features", "opacity", "scaling", "rotation")
+        self.grad = {n: torch.zeros_like(getattr(self, n)) for n in names}
+        self.exp_avg = {n: torch.zeros_like(getattr(self, n)) for n in names}
+        self.exp_avg_sq = {n: torch.zeros_like(getattr(self, n)) for n in names}
+        # densification state (gaussian_model.py: max_radii2D, xyz_gradient_accum, denom)
+        self.max_radii2D = torch.zeros(P, **f32)
+        self.xyz_gradient_accum = torch.zeros(P, 1, **f32)
+        self.denom = torch.zeros(P, 1, **f32)
+        # activated parameters and their gradients (scratch)
+        self.act = {"opacity": torch.empty(P, 1, **f32), "scales": torch.empty(P, 3, **f32),
+                    "rotations": torch.empty(P, 4, **f32)}
+        self.act_grad = {k: torch.empty_like(v) for k, v in self.act.items()}
+        self.iso_part = torch.empty(max(1, _blocks(P)), **f32)
+
+    # reference-style views -------------------------------------------------
+    @property
+    def f_dc(self):
+        return self.features[:, :1]
+
+    @property
+    def f_rest(self):
+        return self.features[:, 1:]
+
+    @property
+    def get_opacity(self):
+        return torch.sigmoid(self.opacity)
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self.scaling)
+
+    @property
+    def get_rotation(self):
+        return torch.nn.functional.normalize(self.rotation)
+
+    # -----------------------------------------------------------------------
+    def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
+                         alpha: float = 0.95, lambda_dssim: float = 0.2, rgb_threshold: float = 0.01,
+                         iso_weight: float = 10.0):
+        """Loss of one view and the gradients of every raw parameter (written
+        to ``self.grad``), plus the densification statistics update.
+
+        cam: viewmatrix, projmatrix, projmatrix_raw, campos (device tensors),
+        tanfovx, tanfovy (floats).  Returns a dict: ``loss`` (0-d device
+        tensor), ``dexposure_a`` / ``dexposure_b`` ([1]), ``dtheta`` / ``drho``
+        ([3], the keyframe pose gradient), ``radii``, ``image``, ``depth``."""
+        from diff_gaussian_rasterization import _C
+        L = _lib.load()
+        P, dev = self.P, self.xyz.device
+        H, W = gt_image.shape[-2], gt_image.shape[-1]
+        HW = H * W
+        st = _lib.stream_handle(dev)
+        p = _lib.ptr
+        e = torch.empty(0, device=dev)
+        a = self.act
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_gaussian_activate(P, p(self.opacity), p(self.scaling), p(self.rotation),
+                                                p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
+                                                p(self.iso_part), st))
+        nr, image, radii, geom, binning, img, depth, opac_img, n_touched = _C.rasterize_gaussians(
+            bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
+            cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
+            self.D, cam["campos"], False, False)
+        gt = gt_image.contiguous()
+        gtd = gt_depth.contiguous()
+        ea, eb = exposure_a.detach().contiguous(), exposure_b.detach().contiguous()
+        nb = max(1, _blocks(HW))
+        image_ab = torch.empty_like(image)
+        lpart = torch.empty(nb, 2, device=dev)
+        ssim_dmap = torch.empty(3 * 3 * HW, device=dev)
+        ssim_plane = torch.empty(3, device=dev)
+        ssim_mean = torch.empty((), device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_mapping_loss_forward(H, W, p(image), p(gt), p(depth), p(gtd), p(ea), p(eb),
+                                                   float(rgb_threshold), p(image_ab), p(lpart), st))
+            with _lib.AllocRequest(dev):
+                _lib.check(L.wgsr_ssim_forward(p(image_ab), p(gt), 3, H, W, 11, p(ssim_dmap), p(ssim_plane),
+                                               p(ssim_mean), _lib.ALLOC_SCRATCH, None, st))
+        sums = lpart.sum(0)
+        w_rgb = alpha * (1.0 - lambda_dssim) / (3 * HW)
+        w_depth = (1.0 - alpha) / HW
+        w_iso = iso_weight / (3 * P) if P else 0.0
+        loss = (w_rgb * sums[0] + alpha * lambda_dssim * (1.0 - ssim_mean) + w_depth * sums[1]
+                + w_iso * self.iso_part.sum())
+        # backward: SSIM term (dL/dssim = -alpha lambda, size-averaged over 3HW)
+        scale = torch.full((3,), -alpha * lambda_dssim / (3 * HW), device=dev)
+        ssim_grad = torch.empty_like(image_ab)
+        d_image = torch.empty_like(image)
+        d_depth = torch.empty_like(depth)
+        epart = torch.empty(nb, 2, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_ssim_backward(p(image_ab), p(gt), 3, H, W, 11, p(ssim_dmap), p(scale), p(ssim_grad),
+                                            st))
+            _lib.check(L.wgsr_mapping_loss_backward(H, W, p(image), p(image_ab), p(gt), p(depth), p(gtd), p(ea),
+                                                    float(rgb_threshold), float(w_rgb), float(w_depth),
+                                                    p(ssim_grad), p(d_image), p(d_depth), p(epart), st))
+        out = {"means3D": self.grad["xyz"], "shs": self.grad["features"], "opacities": self.act_grad["opacity"],
+               "scales": self.act_grad["scales"], "rotations": self.act_grad["rotations"]}
+        g = _C.rasterize_gaussians_backward(
+            bg, self.xyz, radii, e, a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"], cam["projmatrix"],
+            cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], d_image, d_depth, self.features, self.D,
+            cam["campos"], geom, nr, binning, img, False, out=out)
+        dL_dmeans2D, dL_dtau = g[0], g[8]
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_gaussian_activate_backward(
+                P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
+                p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
+                p(self.grad["scaling"]), p(self.grad["rotation"]), st))
+            _lib.check(L.wgsr_densification_stats(P, p(radii), p(dL_dmeans2D), p(self.max_radii2D),
+                                                  p(self.xyz_gradient_accum), p(self.denom), st))
+        esum = epart.sum(0)
+        tau = dL_dtau.sum(0)
+        return {"loss": loss, "dexposure_a": esum[0:1], "dexposure_b": esum[1:2], "drho": tau[:3],
+                "dtheta": tau[3:], "radii": radii, "image": image, "depth": depth, "num_rendered": nr}
+
+    @torch.no_grad()
+    def optimizer_step(self):
+        """torch.optim.Adam(param_groups, lr=0.0, eps=1e-15).step() over the six
+        reference groups, ONE launch (f_dc / f_rest as a two-rate split)."""
+        L = _lib.load()
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2s = math.sqrt(1.0 - b2 ** self.step_count)
+        lr = self.lr
+        ts = []
+        for name, step, tail in (("xyz", lr["xyz"], None), ("features", lr["f_dc"], lr["f_rest"]),
+                                 ("opacity", lr["opacity"], None), ("scaling", lr["scaling"], None),
+                                 ("rotation", lr["rotation"], None)):
+            prm = getattr(self, name)
+            t = _lib.AdamTensor(prm.data_ptr(), self.grad[name].data_ptr(), self.exp_avg[name].data_ptr(),
+                                self.exp_avg_sq[name].data_ptr(), prm.numel(), step / bc1, bc2s)
+            if tail is not None:
+                t.split_period, t.split_len, t.step_size_tail = 3 * self.M, 3, tail / bc1
+            ts.append(t)
+        arr = (_lib.AdamTensor * len(ts))(*ts)
+        dev = self.xyz.device
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_adam_step(arr, len(ts), b1, b2, self.eps, _lib.stream_handle(dev)))
+
+    def step(self, *args, **kwargs):
+        """forward_backward + optimizer_step (one reference mapping iteration
+        without densify / prune / opacity reset)."""
+        out = self.forward_backward(*args, **kwargs)
+        self.optimizer_step()
+        return out
