@@ -227,13 +227,21 @@ def _all_gather_inplace(full, rank, group):
                                        async_op=True)
 
 
-def _all_reduce(t, group):
-    if _gloo_cuda(group) and t.is_cuda:
-        h = t.cpu()
-        dist.all_reduce(h, group=group)
-        t.copy_(h)
+def _all_gather_inplace_many(fulls, rank, group):
+    """In-place all-gathers of several [world * S, ...] buffers (each rank's
+    block holds its shard) as ONE coalesced collective: RCCL runs the group
+    as a single launch, so the small buffers ride along with the SH block
+    instead of paying a collective's latency each."""
+    if any(_gloo_cuda(group) and f.is_cuda for f in fulls):
+        for f in fulls:
+            _all_gather_inplace(f, rank, group)
         return None
-    return dist.all_reduce(t, group=group, async_op=True)
+    world = dist.get_world_size(group)
+    with dist._coalescing_manager(group, async_ops=True) as cm:
+        for f in fulls:
+            S = f.size(0) // world
+            dist.all_gather_into_tensor(f.view(-1), f[rank * S:(rank + 1) * S].view(-1), group=group)
+    return cm
 
 
 class ViewShardedBackward:
@@ -270,6 +278,9 @@ class ViewShardedBackward:
         self.cams = torch.empty(self.world, 64, **f32)
         nb = self.k.tau_blocks(self.lo, self.hi)
         self.tau_blk = torch.zeros(max(nb, 1), self.world, 6, **f32)
+        # per-owner pose-gradient sums [owner, view, 6]: gathered with the
+        # gradient shards, summed over owners locally (no separate all-reduce)
+        self.tau_own = torch.zeros(self.world, self.world, 6, **f32)
         self.tau = torch.zeros(self.world, 6, **f32)
         self.stats = torch.zeros(self.P_pad, 3, **f32) if stats else None
 
@@ -303,17 +314,19 @@ class ViewShardedBackward:
         st = self.stats[self.lo:self.hi] if self.stats is not None else None
         self.k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
                            self.recv, self.buf.views, self.tau_blk if self.hi > self.lo else None, st)
+        mine = self.tau_own[self.rank]
         if self.hi > self.lo:
-            torch.sum(self.tau_blk, dim=0, out=self.tau)
+            torch.sum(self.tau_blk, dim=0, out=mine)
         else:
-            self.tau.zero_()
+            mine.zero_()
         if self.world > 1:
-            works = [_all_gather_inplace(v.view(self.P_pad, -1), self.rank, g) for v in self.buf.views.values()]
+            fulls = [v.view(self.P_pad, -1) for v in self.buf.views.values()]
             if self.stats is not None:
-                works.append(_all_gather_inplace(self.stats, self.rank, g))
-            works.append(_all_reduce(self.tau, g))
-            for w in works:
-                if w is not None:
-                    w.wait()
+                fulls.append(self.stats)
+            fulls.append(self.tau_own)
+            w = _all_gather_inplace_many(fulls, self.rank, g)
+            if w is not None:
+                w.wait()
+        torch.sum(self.tau_own, dim=0, out=self.tau)
         stats = self.stats[:self.P] if self.stats is not None else None
         return self.grads, self.tau[self.rank], stats
