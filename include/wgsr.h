@@ -194,6 +194,57 @@ int wgsr_mapping_loss_backward(int H, int W, const float* image, const float* im
                                float w_depth, const float* ssim_grad, float* dL_dimage,
                                float* dL_ddepth, float* partials, void* stream);
 
+/* ---- The uncertainty-aware mapping loss ---------
+ * get_loss_mapping_uncertainty (src/utils/slam_utils.py:146-258) with
+ * compute_mapping_loss_components (src/utils/dyn_uncertainty/mapping_utils.py:
+ * 206-323): the reference's default mapping loss (uncertainty_params.activate).
+ * csrc/uncertainty.hip; driven by wgsr/mapping.py.  Images are [3,H,W] /
+ * [1,H,W]; the uncertainty map (the MLP output) is [h,w] (h, w > 2).
+ * median_depth: device scalar = ref_depth.median(); the depth threshold is
+ * min(10 median, 50).  Partials: per block of wgsr_uncer_blocks(n). */
+typedef struct wgsr_uncer_params {
+  int H, W;               /* image */
+  int h, w;               /* uncertainty map */
+  float rgb_threshold;    /* Training.rgb_boundary_threshold */
+  float data_rate;        /* 1 + compute_bias_factor(train_frac, 0.8) */
+  float ssim_weight;      /* 100 + 900 compute_bias_factor(ssim_frac, 0.8) */
+  float opacity_th;       /* uncertainty_params.opacity_th_for_uncer_loss */
+  float uncer_depth_mult; /* uncertainty_params.uncer_depth_mult */
+  int initialization;     /* 1: no exposure correction */
+} wgsr_uncer_params;
+int wgsr_uncer_blocks(int64_t n);
+/* image_ab = exp(a) image + b; partials[blocks(H*W)][3] = sums of
+ * w * masked rgb L1 (over channels), of w, and of the re-weighted depth L1
+ * (w where ref_depth < depth + 1), w = the uncertainty weight map. */
+int wgsr_uncer_loss_forward(const wgsr_uncer_params* prm, const float* image, const float* gt_image,
+                            const float* depth, const float* ref_depth, const float* exposure_a,
+                            const float* exposure_b, const float* uncertainty, const float* median_depth,
+                            float* image_ab, float* partials, void* stream);
+/* The feature-resolution inputs of the uncertainty loss: bilinear downsamples
+ * of the opacity image and of clip(opacity ssim_weight (1-l)(1-s)(1-c), 5)
+ * (l, c, s: wgsr_ssim_components of (gt, image_ab), full resolution) and the
+ * bicubic clipped depth L1, zeroed where the bicubic ref depth > threshold. */
+int wgsr_uncer_small_maps(const wgsr_uncer_params* prm, const float* opacity, const float* depth,
+                          const float* ref_depth, const float* median_depth, const float* luminance,
+                          const float* contrast, const float* structure, float* small_ssim_loss,
+                          float* small_depth_loss, float* small_opacity, void* stream);
+/* uncertainty_loss (5x5 reflect median of the SSIM loss; zero where the small
+ * opacity < opacity_th): loss_map [h,w] (optional), partials[blocks(h*w)],
+ * dL_duncertainty = grad_scale * d(loss)/d(uncertainty) (optional; grad_scale
+ * = ssim_mult / (h w) for the reference's ssim_mult * mean). */
+int wgsr_uncer_loss_small(const wgsr_uncer_params* prm, const float* uncertainty, const float* small_ssim_loss,
+                          const float* small_depth_loss, const float* small_opacity, float grad_scale,
+                          float* loss_map, float* partials, float* dL_duncertainty, void* stream);
+/* dL_dimage / dL_ddepth of loss_grad x (w_rgb sum(w rgb L1) + w_depth
+ * sum(re-weighted depth L1)) + the SSIM term (ssim_grad: its gradient w.r.t.
+ * image_ab, already scaled; NULL = none); loss_grad: device scalar (NULL = 1);
+ * partials[blocks(H*W)][2] = dL/dexposure_a, _b. */
+int wgsr_uncer_loss_backward(const wgsr_uncer_params* prm, const float* image, const float* image_ab,
+                             const float* gt_image, const float* depth, const float* ref_depth,
+                             const float* exposure_a, const float* uncertainty, const float* median_depth,
+                             float w_rgb, float w_depth, const float* loss_grad, const float* ssim_grad,
+                             float* dL_dimage, float* dL_ddepth, float* partials, void* stream);
+
 /* One view's densification bookkeeping (mapper.py:1177-1183,
  * gaussian_model.py:745-749) for Gaussians with radii > 0:
  * max_radii2D = max(max_radii2D, radii); grad_accum += ||dL_dmeans2D[:2]||;

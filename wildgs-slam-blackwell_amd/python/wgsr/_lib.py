@@ -59,6 +59,15 @@ class PlyColumnSet(ctypes.Structure):
     _fields_ = [("data", _fp), ("cols", ctypes.c_int), ("record_col", ctypes.POINTER(ctypes.c_int))]
 
 
+class UncerParams(ctypes.Structure):
+    """Mirror of ``wgsr_uncer_params``."""
+
+    _fields_ = [("H", ctypes.c_int), ("W", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("rgb_threshold", ctypes.c_float), ("data_rate", ctypes.c_float),
+                ("ssim_weight", ctypes.c_float), ("opacity_th", ctypes.c_float),
+                ("uncer_depth_mult", ctypes.c_float), ("initialization", ctypes.c_int)]
+
+
 PLY_MAX_TENSORS = 8
 PLY_MAX_COLS = 128
 ADAM_MAX_TENSORS = 16
@@ -113,6 +122,17 @@ def load():
         L.wgsr_mapping_loss_backward.restype = c_int
         L.wgsr_mapping_loss_backward.argtypes = ([c_int, c_int] + [_fp] * 6 + [ctypes.c_float] * 3 +
                                                  [_fp] * 4 + [_fp])
+        U = ctypes.POINTER(UncerParams)
+        L.wgsr_uncer_blocks.restype = c_int
+        L.wgsr_uncer_blocks.argtypes = [c_i64]
+        L.wgsr_uncer_loss_forward.restype = c_int
+        L.wgsr_uncer_loss_forward.argtypes = [U] + [_fp] * 10 + [_fp]
+        L.wgsr_uncer_small_maps.restype = c_int
+        L.wgsr_uncer_small_maps.argtypes = [U] + [_fp] * 10 + [_fp]
+        L.wgsr_uncer_loss_small.restype = c_int
+        L.wgsr_uncer_loss_small.argtypes = [U] + [_fp] * 4 + [ctypes.c_float] + [_fp] * 3 + [_fp]
+        L.wgsr_uncer_loss_backward.restype = c_int
+        L.wgsr_uncer_loss_backward.argtypes = [U] + [_fp] * 8 + [ctypes.c_float] * 2 + [_fp] * 5 + [_fp]
         L.wgsr_densification_stats.restype = c_int
         L.wgsr_densification_stats.argtypes = [c_int] + [_fp] * 5 + [_fp]
         L.wgsr_mark_visible.restype = c_int
@@ -170,6 +190,8 @@ EXPORTED_SYMBOLS = (
     "wgsr_gauss_backward_views",
     "wgsr_map_blocks", "wgsr_gaussian_activate", "wgsr_gaussian_activate_backward",
     "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
+    "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
+    "wgsr_uncer_loss_backward",
 )
 
 VIEW_RECORD_FLOATS = 12   # WGSR_VIEW_RECORD_FLOATS

@@ -93,6 +93,51 @@ class MappingStep:
         return torch.nn.functional.normalize(self.rotation)
 
     # -----------------------------------------------------------------------
+    def _render(self, cam: dict, H: int, W: int, bg):
+        """Activations (+ isotropic partial sums) and the rasteriser forward."""
+        from diff_gaussian_rasterization import _C
+        L = _lib.load()
+        dev = self.xyz.device
+        p = _lib.ptr
+        e = torch.empty(0, device=dev)
+        a = self.act
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_gaussian_activate(self.P, p(self.opacity), p(self.scaling), p(self.rotation),
+                                                p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
+                                                p(self.iso_part), _lib.stream_handle(dev)))
+        return _C.rasterize_gaussians(
+            bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
+            cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
+            self.D, cam["campos"], False, False)
+
+    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float):
+        """Rasteriser backward straight into the gradient storage, activation
+        backward (isotropic term folded in), densification statistics.
+        -> (dL/dmeans2D, dL/dtau summed over P)."""
+        from diff_gaussian_rasterization import _C
+        L = _lib.load()
+        dev = self.xyz.device
+        p = _lib.ptr
+        st = _lib.stream_handle(dev)
+        e = torch.empty(0, device=dev)
+        a = self.act
+        nr, _, radii, geom, binning, img = fwd[:6]
+        out = {"means3D": self.grad["xyz"], "shs": self.grad["features"], "opacities": self.act_grad["opacity"],
+               "scales": self.act_grad["scales"], "rotations": self.act_grad["rotations"]}
+        g = _C.rasterize_gaussians_backward(
+            bg, self.xyz, radii, e, a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"], cam["projmatrix"],
+            cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], d_image, d_depth, self.features, self.D,
+            cam["campos"], geom, nr, binning, img, False, out=out)
+        dL_dmeans2D, dL_dtau = g[0], g[8]
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_gaussian_activate_backward(
+                self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
+                p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
+                p(self.grad["scaling"]), p(self.grad["rotation"]), st))
+            _lib.check(L.wgsr_densification_stats(self.P, p(radii), p(dL_dmeans2D), p(self.max_radii2D),
+                                                  p(self.xyz_gradient_accum), p(self.denom), st))
+        return dL_dmeans2D, dL_dtau.sum(0)
+
     def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
                          alpha: float = 0.95, lambda_dssim: float = 0.2, rgb_threshold: float = 0.01,
                          iso_weight: float = 10.0):
@@ -103,23 +148,14 @@ class MappingStep:
         tanfovx, tanfovy (floats).  Returns a dict: ``loss`` (0-d device
         tensor), ``dexposure_a`` / ``dexposure_b`` ([1]), ``dtheta`` / ``drho``
         ([3], the keyframe pose gradient), ``radii``, ``image``, ``depth``."""
-        from diff_gaussian_rasterization import _C
         L = _lib.load()
         P, dev = self.P, self.xyz.device
         H, W = gt_image.shape[-2], gt_image.shape[-1]
         HW = H * W
         st = _lib.stream_handle(dev)
         p = _lib.ptr
-        e = torch.empty(0, device=dev)
-        a = self.act
-        with torch.cuda.device(dev):
-            _lib.check(L.wgsr_gaussian_activate(P, p(self.opacity), p(self.scaling), p(self.rotation),
-                                                p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
-                                                p(self.iso_part), st))
-        nr, image, radii, geom, binning, img, depth, opac_img, n_touched = _C.rasterize_gaussians(
-            bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
-            cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
-            self.D, cam["campos"], False, False)
+        fwd = self._render(cam, H, W, bg)
+        nr, image, radii, depth = fwd[0], fwd[1], fwd[2], fwd[6]
         gt = gt_image.contiguous()
         gtd = gt_depth.contiguous()
         ea, eb = exposure_a.detach().contiguous(), exposure_b.detach().contiguous()
@@ -153,24 +189,48 @@ class MappingStep:
             _lib.check(L.wgsr_mapping_loss_backward(H, W, p(image), p(image_ab), p(gt), p(depth), p(gtd), p(ea),
                                                     float(rgb_threshold), float(w_rgb), float(w_depth),
                                                     p(ssim_grad), p(d_image), p(d_depth), p(epart), st))
-        out = {"means3D": self.grad["xyz"], "shs": self.grad["features"], "opacities": self.act_grad["opacity"],
-               "scales": self.act_grad["scales"], "rotations": self.act_grad["rotations"]}
-        g = _C.rasterize_gaussians_backward(
-            bg, self.xyz, radii, e, a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"], cam["projmatrix"],
-            cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], d_image, d_depth, self.features, self.D,
-            cam["campos"], geom, nr, binning, img, False, out=out)
-        dL_dmeans2D, dL_dtau = g[0], g[8]
-        with torch.cuda.device(dev):
-            _lib.check(L.wgsr_gaussian_activate_backward(
-                P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
-                p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
-                p(self.grad["scaling"]), p(self.grad["rotation"]), st))
-            _lib.check(L.wgsr_densification_stats(P, p(radii), p(dL_dmeans2D), p(self.max_radii2D),
-                                                  p(self.xyz_gradient_accum), p(self.denom), st))
+        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso)
         esum = epart.sum(0)
-        tau = dL_dtau.sum(0)
         return {"loss": loss, "dexposure_a": esum[0:1], "dexposure_b": esum[1:2], "drho": tau[:3],
                 "dtheta": tau[3:], "radii": radii, "image": image, "depth": depth, "num_rendered": nr}
+
+    def forward_backward_uncertainty(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg, uncertainty,
+                                     train_frac: float, ssim_frac: float, config: dict | None = None,
+                                     initialization: bool = False, freeze_uncertainty_loss: bool = False,
+                                     median_depth=None, iso_weight: float = 10.0):
+        """The reference's DEFAULT mapping iteration (uncertainty_params.activate,
+        mapper.py:1120-1138): get_loss_mapping_uncertainty (slam_utils.py:
+        146-258) + 10 * isotropic loss, and their backward.
+
+        ``uncertainty`` is the uncertainty MLP's output map [h, w] for this
+        view (``uncer_network(viewpoint.features)``, run by the caller in
+        torch); its gradient is fed back with ``uncertainty.backward`` (as
+        the reference's ``loss.backward()`` reaches the MLP) unless
+        ``freeze_uncertainty_loss``.  ``config``: the reference's mapping config
+        dict (Training.alpha / rgb_boundary_threshold / ssim_loss,
+        opt_params.lambda_dssim, uncertainty_params.*); defaults are
+        configs/wildgs_slam.yaml's.  ``median_depth``: optional cached
+        ``gt_depth.median()`` (constant per keyframe).  ``full_resolution``
+        (depth rendered at another size) is not supported.  Returns the dict of
+        ``forward_backward`` plus ``uncertainty_grad`` and ``uncertainty_loss``."""
+        from . import uncertainty as U
+        cfg = U.flatten_config(config)
+        P = self.P
+        H, W = gt_image.shape[-2], gt_image.shape[-1]
+        fwd = self._render(cam, H, W, bg)
+        nr, image, radii, depth, opac_img = fwd[0], fwd[1], fwd[2], fwd[6], fwd[7]
+        loss, state = U.loss_forward(image, depth, opac_img, gt_image, gt_depth, exposure_a, exposure_b, uncertainty,
+                                     train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
+                                     median_depth)
+        w_iso = iso_weight / (3 * P) if P else 0.0
+        loss = loss + w_iso * self.iso_part.sum()
+        d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state)
+        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso)
+        if uncertainty.requires_grad and not freeze_uncertainty_loss:
+            uncertainty.backward(d_unc.to(uncertainty.dtype))
+        return {"loss": loss, "dexposure_a": d_a, "dexposure_b": d_b, "drho": tau[:3], "dtheta": tau[3:],
+                "radii": radii, "image": image, "depth": depth, "num_rendered": nr, "uncertainty_grad": d_unc,
+                "uncertainty_loss": state.uncertainty_loss}
 
     @torch.no_grad()
     def optimizer_step(self):
