@@ -281,6 +281,28 @@ def main():
         if issue:
             out["render_valu_issue"] = issue
 
+    if rank == 0 and world == 1:
+        # simple_knn.distCUDA2 over the scene's points
+        # (outside the timed region; device time per call, HIP events)
+        from simple_knn._C import distCUDA2
+        for _ in range(3):
+            d2 = distCUDA2(means)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(10):
+            d2 = distCUDA2(means)
+        ev1.record()
+        torch.cuda.synchronize()
+        out["distcuda2"] = {"points": P, "ms_per_call": ev0.elapsed_time(ev1) / 10,
+                            "points_per_s": P / (ev0.elapsed_time(ev1) / 10 * 1e-3)}
+        if not args.no_cpu_baseline:
+            from oracle import cpu_oracle
+            t0 = time.perf_counter()
+            d2c = cpu_oracle.dist_knn(scene.means3D.numpy())
+            tc = time.perf_counter() - t0
+            out["distcuda2"]["cpu_baseline_ms"] = 1e3 * tc
+            out["distcuda2"]["bitexact_vs_cpu"] = bool(np.array_equal(d2.cpu().numpy(), d2c))
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_oracle
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))

@@ -4,12 +4,12 @@
 // points -- exact, like upstream's box-pruned search.  Pipeline:
 //   bbox (min/max, seeded with 0 as upstream's cub::DeviceReduce init)
 //   -> 30-bit Morton codes -> radix sort (sort.hip) -> points gathered into
-//   Morton order -> bounds of 256-point boxes and of 64-box super-boxes
-//   -> per point: seed a reject bound from the +-3 Morton neighbours, then
-//      scan every box whose distance to the point is within the current
-//      3rd-best distance.  A wave scans a box when ANY of its lanes needs it;
-//      the box's points are then wave-uniform loads (scalar path), and
-//      scanning a box a lane did not need cannot change its exact answer.
+//   Morton order -> bounds of 64-point leaf boxes and of 64-leaf super-boxes
+//   -> per point: seed a reject bound from the +-3 Morton neighbours, scan
+//      the wave's own leaf, then every leaf whose distance to the point is
+//      within the current 3rd-best distance.  A wave scans a leaf when ANY of
+//      its lanes needs it (staged through LDS, read as broadcasts); scanning
+//      a leaf a lane did not need cannot change its exact answer.
 // Distances are evaluated unfused (dx*dx + dy*dy + dz*dz) so results are
 // bitwise identical to the CPU restatement (oracle/cpu_raster.cpp).
 #include <cfloat>
@@ -21,7 +21,7 @@ namespace wgsr {
 
 namespace {
 
-constexpr int kBox = 256;
+constexpr int kBox = 64;  // points per leaf box == one k_knn wave
 constexpr int kSuper = 64;  // boxes per super-box
 
 struct KnnLayout {
@@ -72,11 +72,19 @@ __global__ __launch_bounds__(256) void k_bbox_partial(int P, const float* __rest
 }
 
 __global__ __launch_bounds__(64) void k_bbox_final(int nparts, const float* __restrict__ part, float* __restrict__ bbox) {
+  // lane l folds partials l, l + 64, ...; then a wave reduction per component
   const int t = threadIdx.x;
-  if (t >= 6) return;
-  float v = part[t];
-  for (int b = 1; b < nparts; ++b) v = (t < 3) ? fminf(v, part[6 * b + t]) : fmaxf(v, part[6 * b + t]);
-  bbox[t] = v;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    float v = part[k];  // partial 0 is always present
+    for (int b = t; b < nparts; b += 64) v = (k < 3) ? fminf(v, part[6 * b + k]) : fmaxf(v, part[6 * b + k]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float o = __shfl_xor(v, off, 64);
+      v = (k < 3) ? fminf(v, o) : fmaxf(v, o);
+    }
+    if (t == 0) bbox[k] = v;
+  }
 }
 
 __device__ __forceinline__ uint32_t prep_morton(uint32_t x) {
@@ -161,11 +169,54 @@ __device__ __forceinline__ void update3(float d, float& b0, float& b1, float& b2
   if (b2 > d) { b2 = d; }
 }
 
+// LDS written by some lanes of a wave and read by others: a wave's LDS
+// operations complete in order, so a compiler-level fence is all it takes.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave = 64 consecutive Morton-ordered points = one leaf.  Each wave
+// scans its own leaf first (the bound it leaves prunes almost every other
+// leaf), then walks the super-boxes and, inside the ones ANY lane still
+// needs, the leaves ANY lane still needs.  Every level is staged through the
+// wave's LDS slots by one coalesced load per lane (64 super-box bounds, a
+// super-box's 64 leaf bounds, a leaf's 64 points) and read back as
+// broadcasts, so the walk never waits on a dependent global load per box.
+// distances from p to the n staged points of a leaf starting at sorted index
+// i0 (self excluded by index), folded into the running 3 best; branch-free
+// and unrolled so the broadcast LDS reads of a group issue together
+__device__ __forceinline__ void scan_leaf(const float4* pts, int i0, int n, int s, float4 p, float& b0, float& b1,
+                                          float& b2) {
+  if (n == 64) {
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+      const float d = sqdist(p, pts[j]);
+      update3(i0 + j == s ? FLT_MAX : d, b0, b1, b2);
+    }
+  } else {
+    for (int j = 0; j < n; ++j) {
+      const float d = sqdist(p, pts[j]);
+      update3(i0 + j == s ? FLT_MAX : d, b0, b1, b2);
+    }
+  }
+}
+
+struct KnnWaveLds {
+  float4 pts[64];
+  float4 leaf_lo[64], leaf_hi[64];
+  float4 sup_lo[64], sup_hi[64];
+};
+
 __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ spts,
                                              const uint32_t* __restrict__ idx, const float4* __restrict__ boxes,
                                              int nbox, const float4* __restrict__ supers, int nsup,
                                              float* __restrict__ out) {
+  __shared__ KnnWaveLds sl[4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int s0 = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x * 256 + w * 64 >= P) return;  // whole wave past the end (wave-uniform)
   const bool valid = s0 < P;
   const int s = valid ? s0 : P - 1;
   const float4 p = spts[s];
@@ -174,17 +225,43 @@ __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ s
     if (i != s) update3(sqdist(p, spts[i]), b0, b1, b2);
   const float reject = b2;
   b0 = b1 = b2 = FLT_MAX;
-  for (int sb = 0; sb < nsup; ++sb) {
-    const bool need_s = box_dist(supers[2 * sb], supers[2 * sb + 1], p) <= fminf(reject, b2);
-    if (!__any(need_s)) continue;
-    const int bend = min(nbox, (sb + 1) * kSuper);
-    for (int b = sb * kSuper; b < bend; ++b) {
-      const bool need_b = box_dist(boxes[2 * b], boxes[2 * b + 1], p) <= fminf(reject, b2);
-      if (!__any(need_b)) continue;
-      const int iend = min(P, (b + 1) * kBox);
-      for (int i = b * kBox; i < iend; ++i) {
-        const float d = sqdist(p, spts[i]);
-        if (i != s) update3(d, b0, b1, b2);
+  KnnWaveLds& L = sl[w];
+  const int own = (blockIdx.x * 256 + w * 64) / kBox;
+  L.pts[lane] = p;  // invalid lanes' copies lie past P and are never read
+  wave_lds_sync();
+  scan_leaf(L.pts, own * kBox, min(kBox, P - own * kBox), s, p, b0, b1, b2);
+  for (int c = 0; c < nsup; c += 64) {
+    const int ns = min(64, nsup - c);
+    {
+      const int k = c + min(lane, ns - 1);
+      const float4 lo = supers[2 * k], hi = supers[2 * k + 1];
+      wave_lds_sync();
+      L.sup_lo[lane] = lo;
+      L.sup_hi[lane] = hi;
+      wave_lds_sync();
+    }
+    for (int js = 0; js < ns; ++js) {
+      if (!__any(box_dist(L.sup_lo[js], L.sup_hi[js], p) <= fminf(reject, b2))) continue;
+      const int sb = c + js;
+      const int l0 = sb * kSuper, nl = min(kSuper, nbox - l0);
+      {
+        const int k = l0 + min(lane, nl - 1);
+        const float4 lo = boxes[2 * k], hi = boxes[2 * k + 1];
+        wave_lds_sync();
+        L.leaf_lo[lane] = lo;
+        L.leaf_hi[lane] = hi;
+        wave_lds_sync();
+      }
+      for (int jl = 0; jl < nl; ++jl) {
+        const int b = l0 + jl;
+        if (b == own) continue;
+        if (!__any(box_dist(L.leaf_lo[jl], L.leaf_hi[jl], p) <= fminf(reject, b2))) continue;
+        const int i0 = b * kBox, n = min(kBox, P - i0);
+        const float4 q = spts[min(i0 + lane, P - 1)];
+        wave_lds_sync();  // every lane is done reading the previous leaf
+        L.pts[lane] = q;
+        wave_lds_sync();
+        scan_leaf(L.pts, i0, n, s, p, b0, b1, b2);
       }
     }
   }
