@@ -245,6 +245,25 @@ int wgsr_uncer_loss_backward(const wgsr_uncer_params* prm, const float* image, c
                              float w_rgb, float w_depth, const float* loss_grad, const float* ssim_grad,
                              float* dL_dimage, float* dL_ddepth, float* partials, void* stream);
 
+/* ---- The mapper's pose-refinement loss (tracking) --
+ * csrc/tracking.hip; driven by wgsr/tracking.py.
+ * wgsr_tracking_loss: get_loss_tracking(..., monocular=True) (src/utils/
+ * slam_utils.py:47-82) forward AND backward in one pass: partials[blocks(H*W)]
+ * [3] = per-block sums of the opacity-weighted L1 (divide by 3HW for the
+ * loss), of dL/dexposure_a and of dL/dexposure_b; dL_dimage [3,H,W] and
+ * dL_dopacity [1,H,W] (optional) for dL/dloss = 1.  grad_mask ([1,H,W], the
+ * keyframe's Camera.grad_mask) and uncertainty ([H,W], already resized) are
+ * optional (NULL: ones / no weights). */
+int wgsr_track_blocks(int64_t n);
+int wgsr_tracking_loss(int H, int W, const float* image, const float* gt_image, const float* opacity,
+                       const float* grad_mask, const float* uncertainty, const float* exposure_a,
+                       const float* exposure_b, float rgb_threshold, float* dL_dimage, float* dL_dopacity,
+                       float* partials, void* stream);
+/* Camera.compute_grad_mask (src/utils/camera_utils.py:157-180): grad_mask
+ * [H,W] of the [3,H,W] image (edge_threshold: Training.edge_threshold).
+ * Needs (H/32)(W/32) <= 8192. */
+int wgsr_grad_mask(int H, int W, const float* image, float edge_threshold, float* grad_mask, void* stream);
+
 /* One view's densification bookkeeping (mapper.py:1177-1183,
  * gaussian_model.py:745-749) for Gaussians with radii > 0:
  * max_radii2D = max(max_radii2D, radii); grad_accum += ||dL_dmeans2D[:2]||;

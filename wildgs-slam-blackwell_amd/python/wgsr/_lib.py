@@ -133,6 +133,12 @@ def load():
         L.wgsr_uncer_loss_small.argtypes = [U] + [_fp] * 4 + [ctypes.c_float] + [_fp] * 3 + [_fp]
         L.wgsr_uncer_loss_backward.restype = c_int
         L.wgsr_uncer_loss_backward.argtypes = [U] + [_fp] * 8 + [ctypes.c_float] * 2 + [_fp] * 5 + [_fp]
+        L.wgsr_track_blocks.restype = c_int
+        L.wgsr_track_blocks.argtypes = [c_i64]
+        L.wgsr_tracking_loss.restype = c_int
+        L.wgsr_tracking_loss.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float] + [_fp] * 3 + [_fp]
+        L.wgsr_grad_mask.restype = c_int
+        L.wgsr_grad_mask.argtypes = [c_int, c_int, _fp, ctypes.c_float, _fp, _fp]
         L.wgsr_densification_stats.restype = c_int
         L.wgsr_densification_stats.argtypes = [c_int] + [_fp] * 5 + [_fp]
         L.wgsr_mark_visible.restype = c_int
@@ -191,7 +197,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_map_blocks", "wgsr_gaussian_activate", "wgsr_gaussian_activate_backward",
     "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
     "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
-    "wgsr_uncer_loss_backward",
+    "wgsr_uncer_loss_backward", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
 )
 
 VIEW_RECORD_FLOATS = 12   # WGSR_VIEW_RECORD_FLOATS
