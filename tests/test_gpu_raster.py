@@ -157,6 +157,18 @@ def test_matches_cpu_restatement_random(P, W, H, deg, view):
     check_against(out, _cpu_expect(inputs, settings, grads))
 
 
+@pytest.mark.parametrize("kernel", ["quad", "split"])
+@pytest.mark.parametrize("P,W,H,deg,view", [(20_000, 640, 480, 3, 2), (3_000, 200, 136, 1, 1)])
+def test_both_backward_render_kernels(P, W, H, deg, view, kernel, monkeypatch):
+    """k_render_bwd_quad (one wave per tile) and k_render_bwd_split (four
+    waves per tile, chosen below 3072 tiles) both match the CPU restatement;
+    WGSR_BWD_SPLIT_BELOW forces either."""
+    monkeypatch.setenv("WGSR_BWD_SPLIT_BELOW", "0" if kernel == "quad" else "1000000")
+    inputs, settings, grads = _synthetic(P, W, H, deg, view)
+    out = run_c(inputs, settings, grads)
+    check_against(out, _cpu_expect(inputs, settings, grads))
+
+
 def test_exact_tile_lists_elongated_splats():
     """Stress the exact tile lists (row_span) and the per-wave ellipse culling:
     needle-like rotated splats (per-axis scales over 2.6 decades) and opacities

@@ -25,6 +25,9 @@ namespace wgsr {
 namespace {
 
 constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
+// below this many tiles the backward runs k_render_bwd_split (four waves per
+// tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
+constexpr int kBwdSplitBelowTiles = 3072;
 
 constexpr float SH_C0 = 0.28209479177387814f;
 constexpr float SH_C1 = 0.4886025119029199f;
@@ -207,6 +210,152 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
       partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
       pflag[k] = 1;
+    }
+  }
+}
+
+// Small images (few tiles: TUM's 512x384 has 768) leave most SIMDs without a
+// wave under k_render_bwd_quad, and each tile's serial walk sets the time.
+// This variant gives a tile FOUR waves, one per 8x8 quadrant: wave 0 stages
+// the batch records for all of them, each wave culls and evaluates only its
+// quadrant and reduces its own sums, and wave 0 adds the (up to) four
+// quadrant sums of each hit entry into the pair's record.  Same arithmetic per
+// pixel; only the order of the final cross-quadrant sum differs.
+__global__ __launch_bounds__(256) void k_render_bwd_split(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
+    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W,
+    int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag) {
+  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
+  __shared__ uint32_t sG[kBatch];
+  __shared__ float sP[4][kBatch][11];
+  __shared__ uint64_t sHitW[4];
+  __shared__ uint32_t sEnd[4];
+  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tx = (int)(tile % gx), ty = (int)(tile / gx);
+  const int qx0 = tx * kTile + (w & 1) * 8, qy0 = ty * kTile + (w >> 1) * 8;  // this wave's quadrant
+  const size_t HW = (size_t)H * W;
+  const uint2 range = ranges[tile];
+  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+
+  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+  const v2f p0{(float)px, (float)py};
+  const bool inside = px < W && py < H;
+  const size_t pid = (size_t)py * W + px;
+  const float Tf = inside ? final_Ts[pid] : 0.f;
+  const uint32_t last = inside ? n_contrib[pid] : 0u;
+  const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
+  const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
+  const v2f dp01{d0, d1}, dp2d{d2, dd};
+  const float tb = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);
+  float T = Tf;
+  v2f acc01{0.f, 0.f}, acc2d{0.f, 0.f};
+  uint32_t x = last;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
+  const uint32_t mq = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+  if (lane == 0) sEnd[w] = mq;
+  __syncthreads();
+  const uint32_t end = range.x + max(max(sEnd[0], sEnd[1]), max(sEnd[2], sEnd[3]));
+
+  uint32_t gcur = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (w == 0) {
+    if (end >= range.x + 1 + lane) {
+      gcur = point_g[end - 1 - lane];
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+    }
+    if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
+  }
+
+  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
+    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
+    __syncthreads();
+    if (w == 0) {
+      sA[lane] = nA;
+      sB[lane] = nB;
+      sC[lane] = nC;
+      sG[lane] = gcur;
+    }
+    __syncthreads();
+    if (w == 0) {
+      gcur = gnext;
+      if (b_end >= range.x + 1 + kBatch + lane) {
+        nA = splat[3 * (size_t)gcur];
+        nB = splat[3 * (size_t)gcur + 1];
+        nC = splat[3 * (size_t)gcur + 2];
+      }
+      if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
+    }
+    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
+    uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < mq &&
+                                ellipse_hits(sA[lane], sB[lane], qx0, qx0 + 7, qy0, qy0 + 7));
+    uint64_t hits = 0;
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t cidx = cfirst - j;
+      const float4 A = sA[j];
+      const float4 B = sB[j];
+      const float4 Cc = sC[j];
+      const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
+      const float cxy = B.x, op = B.y;
+      const v2f d = mxy - p0;
+      const v2f q2 = cd * d * d;
+      const float power = q2.x + q2.y + (cxy * d.x) * d.y;
+      const float G = __builtin_amdgcn_exp2f(power);
+      const float av = fminf(kMaxAlpha, op * G);
+      const bool v = cidx < last && power <= 0.0f && av >= kMinAlpha;
+      if (!wave_any(v)) continue;
+      const float alpha = v ? av : 0.f;
+      const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+      const float Tn = T * rinv;
+      T = Tn;
+      const float dch = alpha * Tn;
+      const v2f e01 = c01 - acc01, e2d = c2d - acc2d;
+      const v2f s2 = e01 * dp01 + e2d * dp2d;
+      float dLda = (s2.x + s2.y) * Tn + tb * rinv;
+      dLda = v ? dLda : 0.f;
+      acc01 += alpha * e01;
+      acc2d += alpha * e2d;
+      const float wg = op * dLda;
+      const v2f gd = G * d;
+      const v2f g01 = wg * (gd * (cd + cd) + v2f{gd.y, gd.x} * cxy);
+      const v2f u = wg * gd;
+      const v2f g23 = u.x * d;
+      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, u.y * d.y, G * dLda, dch * dp01.x, dch * dp01.y,
+                            dch * dp2d.x, dch * dp2d.y};
+      wave_sum10_store(gv, &sP[w][j][0]);
+      hits |= 1ull << j;
+    }
+    if (lane == 0) sHitW[w] = hits;
+    __syncthreads();
+    if (w == 0 && lane < cnt) {
+      const uint64_t h0 = sHitW[0], h1 = sHitW[1], h2 = sHitW[2], h3 = sHitW[3];
+      const uint64_t bit = 1ull << lane;
+      if ((h0 | h1 | h2 | h3) & bit) {
+        float sv[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) sv[k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t hq = q == 0 ? h0 : (q == 1 ? h1 : (q == 2 ? h2 : h3));
+          if (hq & bit)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) sv[k] += sP[q][lane][k];
+        }
+        const uint32_t gid = sG[lane];
+        const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], rowtab[gid], tx, ty);
+        partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+        partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
+        pflag[k] = 1;
+      }
     }
   }
 }
@@ -790,6 +939,16 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
+  // few tiles (small images): four waves per tile keep the SIMDs busy
+  const char* env = getenv("WGSR_BWD_SPLIT_BELOW");  // read per launch: tests switch kernels
+  const int split_below = env ? atoi(env) : kBwdSplitBelowTiles;
+  if (nt < split_below) {
+    hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), point_g,
+                       at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
+                       at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
+                       dL_ddepth, partial, pflag);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
                      at<float4>(geom, L.splat),
                      at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
