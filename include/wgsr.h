@@ -264,6 +264,25 @@ int wgsr_tracking_loss(int H, int W, const float* image, const float* gt_image, 
  * Needs (H/32)(W/32) <= 8192. */
 int wgsr_grad_mask(int H, int W, const float* image, float edge_threshold, float* grad_mask, void* stream);
 
+/* ---- The uncertainty MLP ------------------------
+ * uncertainty_model.MLPNetwork with its defaults (src/utils/dyn_uncertainty/
+ * uncertainty_model.py:5-68): C -> 64 -> 64 -> 1, ReLU, dropout p after each
+ * hidden layer, softplus.  csrc/mlp.hip; driven by wgsr/mlp.py.  X [N][C]
+ * (C a multiple of 64), weights row-major as torch.nn.Linear keeps them.
+ * Forward keeps h1d/h2d ([N][64], post-dropout) and o_pre ([N]) for the
+ * backward; dropout masks are a counter hash of (seed, layer, row, column).
+ * Backward: grad (wgsr_mlp_grad_floats(C) floats) = dW1 [64][C] | db1 [64] |
+ * dW2 [64][64] | db2 [64] | dW3 [64] | db3 [1] for dL_du [N]; scratch:
+ * wgsr_mlp_scratch_bytes(N, C). */
+size_t wgsr_mlp_scratch_bytes(int N, int C);
+int wgsr_mlp_grad_floats(int C);
+int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                     const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed,
+                     float* h1d, float* h2d, float* o_pre, float* u, void* stream);
+int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                      const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
+                      float* scratch, float* grad, void* stream);
+
 /* One view's densification bookkeeping (mapper.py:1177-1183,
  * gaussian_model.py:745-749) for Gaussians with radii > 0:
  * max_radii2D = max(max_radii2D, radii); grad_accum += ||dL_dmeans2D[:2]||;

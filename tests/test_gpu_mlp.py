@@ -1,0 +1,78 @@
+"""GPU parity of the uncertainty MLP (wgsr.mlp.UncertaintyMLP; SURVEY.md 8(f)
+row f2) against a torch fp32 restatement of MLPNetwork (src/utils/
+dyn_uncertainty/uncertainty_model.py:5-64) with the same weights: with
+dropout off, and with dropout on using the kernel's masks (restated in
+wgsr.mlp.dropout_mask).  Tolerances: outputs rel 1e-5, parameter gradients
+rel-L1 1e-5 (fp32 reduction order differs from hipBLASLt's)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().sum() / b.abs().sum().clamp_min(1e-30))
+
+
+def _torch_mlp(net, x, masks=None, p=0.0):
+    """MLPNetwork.forward with explicit dropout masks (torch's dropout:
+    x * mask / (1 - p))."""
+    H, W, C = x.shape[-3:]
+    y = x.reshape(-1, C)
+    for i, layer in enumerate(net.layers):
+        y = F.relu(F.linear(y, layer.weight, layer.bias))
+        if masks is not None:
+            y = y * masks[i] * (1.0 / (1.0 - p))
+    y = F.softplus(F.linear(y, net.output_layer.weight, net.output_layer.bias))
+    return y.view(x.shape[:-1])
+
+
+@pytest.mark.parametrize("shape,p", [((27, 36, 384), 0.0), ((77, 137, 384), 0.0), ((2, 9, 13, 128), 0.0),
+                                     ((27, 36, 384), 0.2), ((5, 7, 64), 0.5)])
+def test_forward_backward_matches_torch(shape, p):
+    from wgsr.mlp import UncertaintyMLP, dropout_mask
+    torch.manual_seed(0)
+    C = shape[-1]
+    net = UncertaintyMLP(input_dim=C, dropout_p=p).to(DEV)
+    x = torch.randn(*shape, device=DEV)
+    u = net(x)
+    g = torch.randn_like(u)
+    (u * g).sum().backward()
+    got = [prm.grad.clone() for prm in net.parameters()]
+    for prm in net.parameters():
+        prm.grad = None
+    N = x.numel() // C
+    masks = None
+    if p > 0:
+        masks = [torch.from_numpy(dropout_mask(net.last_seed, i, N, p)).to(DEV).float() for i in range(2)]
+    want_u = _torch_mlp(net, x, masks, p)
+    (want_u * g).sum().backward()
+    assert u.shape == want_u.shape
+    assert _rel(u, want_u) <= 1e-5
+    for a, b in zip(got, [prm.grad for prm in net.parameters()]):
+        assert _rel(a, b) <= 1e-5
+
+
+def test_dropout_rate_and_fresh_masks():
+    from wgsr.mlp import UncertaintyMLP
+    torch.manual_seed(1)
+    net = UncertaintyMLP(input_dim=64).to(DEV)
+    x = torch.randn(100, 100, 64, device=DEV)
+    u1, s1 = net(x), net.last_seed
+    u2, s2 = net(x), net.last_seed
+    assert s1 != s2 and not torch.equal(u1, u2)   # new masks per call, like F.dropout
+    torch.manual_seed(1)
+    net2 = UncertaintyMLP(input_dim=64).to(DEV)
+    assert torch.equal(net2(x), u1)               # torch.manual_seed makes it repeatable
+
+
+def test_state_dict_matches_reference_layout():
+    from wgsr.mlp import UncertaintyMLP
+    net = UncertaintyMLP(input_dim=384)
+    assert sorted(net.state_dict()) == sorted(["layers.0.weight", "layers.0.bias", "layers.1.weight",
+                                               "layers.1.bias", "output_layer.weight", "output_layer.bias"])
+    assert net.layers[0].weight.shape == (64, 384) and net.output_layer.weight.shape == (1, 64)

@@ -77,6 +77,30 @@ def test_fused_adam_matches_torch_adam(P):
     _assert_same_state(ref, ours)
 
 
+def test_fused_adam_weight_decay_matches_torch_adam():
+    """The uncertainty MLP's optimiser: torch.optim.Adam(params, lr=4e-4,
+    weight_decay=1e-5) (mapper.py:129-133); .grad is left untouched."""
+    from wgsr.mlp import UncertaintyMLP
+    from wgsr.optim import FusedAdam
+    torch.manual_seed(0)
+    a, b = UncertaintyMLP(input_dim=128).to(DEV), UncertaintyMLP(input_dim=128).to(DEV)
+    b.load_state_dict(a.state_dict())
+    ref = torch.optim.Adam(b.parameters(), lr=4e-4, weight_decay=1e-5)
+    ours = FusedAdam(a.parameters(), lr=4e-4, weight_decay=1e-5)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for it in range(4):
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            gr = torch.randn(pa.shape, generator=g).to(DEV)
+            pa.grad, pb.grad = gr.clone(), gr.clone()
+        keep = [pa.grad.clone() for pa in a.parameters()]
+        ref.step()
+        ours.step()
+        for k, pa in zip(keep, a.parameters()):
+            assert torch.equal(k, pa.grad)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa.detach(), pb.detach(), rtol=1e-5, atol=1e-7)
+
+
 def test_fused_adam_unaligned_and_many_tensors():
     """More tensors than one launch holds and storage offsets that rule out
     16-byte vector access (the scalar tail path)."""

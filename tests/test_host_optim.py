@@ -6,11 +6,11 @@ import torch
 from torch import nn
 
 
-def test_fused_adam_rejects_weight_decay_and_cpu_params():
+def test_fused_adam_rejects_negative_weight_decay_and_cpu_params():
     from wgsr.optim import FusedAdam
     p = nn.Parameter(torch.zeros(8))
     with pytest.raises(ValueError):
-        FusedAdam([p], weight_decay=0.1)
+        FusedAdam([p], weight_decay=-0.1)
     opt = FusedAdam([{"params": [p], "lr": 1e-3, "name": "xyz"}], lr=0.0, eps=1e-15)
     assert opt.param_groups[0]["name"] == "xyz" and opt.defaults["eps"] == 1e-15
     p.grad = torch.ones(8)

@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", choices=("fused", "mi355x", "torch"), default=None)
     ap.add_argument("--loss", choices=("rgbd", "uncertainty"), default="rgbd")
+    ap.add_argument("--torch-mlp", action="store_true",
+                    help="uncertainty mode, fused path: keep the MLP in torch (default: wgsr.mlp + FusedAdam)")
     a = ap.parse_args()
     if a.loss == "uncertainty":
         return main_uncertainty(a)
@@ -318,8 +320,14 @@ def main_uncertainty(a):
         f = synthetic_camera(W, H, 0).raster_fields()
         camd = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in f.items()}
         torch.manual_seed(0)
-        net = UncerMLP().to(dev)
-        uopt = torch.optim.Adam(net.parameters(), lr=4e-4, weight_decay=1e-5)
+        if a.torch_mlp:
+            net = UncerMLP().to(dev)
+            uopt = torch.optim.Adam(net.parameters(), lr=4e-4, weight_decay=1e-5)
+        else:
+            from wgsr.mlp import UncertaintyMLP
+            from wgsr.optim import FusedAdam
+            net = UncertaintyMLP(384).to(dev)
+            uopt = FusedAdam(net.parameters(), lr=4e-4, weight_decay=1e-5)
         ea = torch.zeros(1, device=dev, requires_grad=True)
         eb = torch.zeros(1, device=dev, requires_grad=True)
         kopt = torch.optim.Adam([ea, eb], lr=0.01)
@@ -342,7 +350,8 @@ def main_uncertainty(a):
                       "ms_per_iter_fused_mapping_step": ms_fused,
                       "ms_per_iter_reference_torch_composition": ms_torch,
                       "speedup_fused_vs_torch": ms_torch / ms_fused,
-                      "note": "same rasteriser in both; fused = MLP (torch) + MappingStep.forward_backward_uncertainty"
+                      "mlp": "torch" if a.torch_mlp else "wgsr.mlp (HIP) + FusedAdam",
+                      "note": "same rasteriser in both; fused = MLP + MappingStep.forward_backward_uncertainty"
                               " + fused Adam; torch = the reference's ops (conv2d SSIM and components, interpolate, "
                               "unfold median, torch.optim.Adam)"}))
 

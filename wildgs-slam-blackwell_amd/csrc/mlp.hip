@@ -1,0 +1,303 @@
+// The uncertainty MLP of WildGS-SLAM's mapping loss, gfx950 (SURVEY.md 8(f)
+// row f2: src/utils/dyn_uncertainty/uncertainty_model.py:5-68, MLPNetwork with
+// its defaults -- input C (384 DINO features), two hidden layers of 64 with
+// ReLU and dropout 0.2 (applied unconditionally, :55), one output, softplus).
+// It runs on every mapping iteration over the [H/14, W/14] feature map.
+//
+//   mlp_fwd     64 rows per workgroup: layer 1 as a 64 x 64 x C tile product
+//               with X and W1 staged through LDS in 64-wide K slabs (4 x 4
+//               outputs per thread), bias + ReLU + dropout in registers, layer
+//               2 from LDS, layer 3 + softplus; keeps the post-dropout
+//               activations and the pre-softplus output for the backward.
+//   mlp_bwd     the same 64 rows backward: softplus', layer 3, the two
+//               ReLU/dropout masks (read off the kept activations: a kept
+//               activation is > 0 exactly when ReLU passed and dropout kept
+//               it), and per-workgroup partial weight / bias gradients.
+//   mlp_reduce  sums the per-workgroup partials in a fixed order
+//               (deterministic), one thread per parameter element.
+// Dropout masks come from a counter hash of (seed, layer, row, column) -- the
+// same draw in forward and backward, and reproducible from the seed
+// (wgsr/mlp.py restates it for the tests).  Everything is fp32.
+#include "wgsr_common.h"
+#include "wgsr_internal.h"
+
+namespace wgsr {
+
+namespace {
+
+constexpr int kHid = 64;    // hidden width (MLPNetwork default)
+constexpr int kRows = 64;   // rows per workgroup
+constexpr int kLd = 65;     // padded LDS row
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {  // lowbias32
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// keep (1) or drop (0) for element (row, col) of dropout layer `layer`
+__device__ __forceinline__ bool keep_elem(uint32_t seed, int layer, uint32_t row, int col, float p) {
+  const uint32_t h = mix32(seed ^ mix32((uint32_t)layer * 0x9E3779B9U ^ mix32(row * 64U + (uint32_t)col)));
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+// acc[4][4] += A[rows ty*4.., k] * B[cols tx*4.., k] over k in [0, 64) (both in LDS, [64][kLd])
+__device__ __forceinline__ void tile_mac(const float (*A)[kLd], const float (*B)[kLd], int ty, int tx,
+                                         float (&acc)[4][4]) {
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) {
+    float a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = B[tx * 4 + j][k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+  }
+}
+
+// dst[r][c] = src[(r0 + r) * ld + c0 + c] for a 64 x 64 slab (zeros past n rows)
+__device__ __forceinline__ void load_slab(float (*dst)[kLd], const float* __restrict__ src, int r0, int n, int ld,
+                                          int c0) {
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    dst[r][c] = (r0 + r < n) ? src[(size_t)(r0 + r) * ld + c0 + c] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __restrict__ X,
+                                                 const float* __restrict__ W1, const float* __restrict__ b1,
+                                                 const float* __restrict__ W2, const float* __restrict__ b2,
+                                                 const float* __restrict__ W3, const float* __restrict__ b3, float p,
+                                                 uint32_t seed, float* __restrict__ h1d, float* __restrict__ h2d,
+                                                 float* __restrict__ o_pre, float* __restrict__ u) {
+  __shared__ float sA[64][kLd], sB[64][kLd];
+  const int t = threadIdx.x, ty = t >> 4, tx = t & 15;
+  const int r0 = blockIdx.x * kRows;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < C; k0 += 64) {
+    __syncthreads();
+    load_slab(sA, X, r0, N, C, k0);
+    load_slab(sB, W1, 0, kHid, C, k0);
+    __syncthreads();
+    tile_mac(sA, sB, ty, tx, acc);
+  }
+  __syncthreads();
+  // layer 1 epilogue -> sA (the 64 x 64 layer-2 input), h1d
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = ty * 4 + i, c = tx * 4 + j;
+      float v = fmaxf(acc[i][j] + b1[c], 0.f);
+      v = keep_elem(seed, 0, (uint32_t)(r0 + r), c, p) ? v * scale : 0.f;
+      sA[r][c] = v;
+      if (r0 + r < N) h1d[(size_t)(r0 + r) * kHid + c] = v;
+      acc[i][j] = 0.f;
+    }
+  load_slab(sB, W2, 0, kHid, kHid, 0);
+  __syncthreads();
+  tile_mac(sA, sB, ty, tx, acc);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = ty * 4 + i, c = tx * 4 + j;
+      float v = fmaxf(acc[i][j] + b2[c], 0.f);
+      v = keep_elem(seed, 1, (uint32_t)(r0 + r), c, p) ? v * scale : 0.f;
+      sB[r][c] = v;  // layer-3 input
+      if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + c] = v;
+    }
+  __syncthreads();
+  if (t < kRows && r0 + t < N) {
+    float o = 0.f;
+    for (int k = 0; k < kHid; ++k) o = fmaf(sB[t][k], W3[k], o);
+    o += b3[0];
+    o_pre[r0 + t] = o;
+    u[r0 + t] = o > 20.f ? o : log1pf(expf(o));  // nn.Softplus(beta 1, threshold 20)
+  }
+}
+
+// partial layout per workgroup: dW1 [64][C] | db1 [64] | dW2 [64][64] | db2 [64] | dW3 [64] | db3
+__host__ __device__ inline int mlp_partial_floats(int C) { return kHid * C + kHid + kHid * kHid + kHid + kHid + 1; }
+
+__global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __restrict__ X,
+                                                 const float* __restrict__ W2, const float* __restrict__ W3, float p,
+                                                 const float* __restrict__ h1d, const float* __restrict__ h2d,
+                                                 const float* __restrict__ o_pre, const float* __restrict__ du,
+                                                 float* __restrict__ part) {
+  __shared__ float sH1[64][kLd], sDA2[64][kLd], sDA1[64][kLd], sT[64][kLd];
+  __shared__ float sDo[kRows];
+  const int t = threadIdx.x, ty = t >> 4, tx = t & 15;
+  const int r0 = blockIdx.x * kRows;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  float* out = part + (size_t)blockIdx.x * mlp_partial_floats(C);
+  float* gW1 = out;
+  float* gb1 = gW1 + kHid * C;
+  float* gW2 = gb1 + kHid;
+  float* gb2 = gW2 + kHid * kHid;
+  float* gW3 = gb2 + kHid;
+  float* gb3 = gW3 + kHid;
+  if (t < kRows) {
+    float d = 0.f;
+    if (r0 + t < N) {
+      const float o = o_pre[r0 + t], g = du[r0 + t];
+      const float z = expf(o);
+      d = o > 20.f ? g : g * z / (z + 1.f);  // softplus backward
+    }
+    sDo[t] = d;
+  }
+  load_slab(sH1, h1d, r0, N, kHid, 0);
+  load_slab(sT, h2d, r0, N, kHid, 0);
+  __syncthreads();
+  // layer 3: dW3[k] = sum_r do[r] h2d[r][k], db3; dA2 = do W3 through ReLU/dropout
+  if (t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s = fmaf(sDo[r], sT[r][t], s);
+    gW3[t] = s;
+  } else if (t == kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sDo[r];
+    gb3[0] = s;
+  }
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    sDA2[r][c] = sT[r][c] > 0.f ? sDo[r] * W3[c] * scale : 0.f;
+  }
+  __syncthreads();
+  // dW2[o][i] = sum_r dA2[r][o] h1d[r][i]: transpose so tile_mac's K runs over rows
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    sT[c][r] = sDA2[r][c];  // sT[o][r]
+  }
+  __syncthreads();
+  {
+    // h1d transposed into sDA1 temporarily: sDA1[i][r]
+    for (int e = t; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      sDA1[c][r] = sH1[r][c];
+    }
+    __syncthreads();
+    float acc[4][4] = {};
+    tile_mac(sT, sDA1, ty, tx, acc);  // acc[o][i]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
+  }
+  if (t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sDA2[r][t];
+    gb2[t] = s;
+  }
+  __syncthreads();
+  // dA1[r][i] = sum_o dA2[r][o] W2[o][i] through ReLU/dropout: B = W2 transposed (sDA1[i][o])
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int o = e >> 6, i = e & 63;
+    sDA1[i][o] = W2[o * kHid + i];
+  }
+  __syncthreads();
+  {
+    float acc[4][4] = {};
+    tile_mac(sDA2, sDA1, ty, tx, acc);  // acc[r][i]
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = ty * 4 + i, c = tx * 4 + j;
+        sT[c][r] = sH1[r][c] > 0.f ? acc[i][j] * scale : 0.f;  // sT[i][r] = dA1 transposed
+      }
+  }
+  __syncthreads();
+  if (t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sT[t][r];
+    gb1[t] = s;
+  }
+  // dW1[o][c] = sum_r dA1[r][o] X[r][c], 64 columns of X at a time (sDA1[c][r] = X slab transposed)
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    __syncthreads();
+    for (int e = t; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      sDA1[c][r] = (r0 + r < N) ? X[(size_t)(r0 + r) * C + c0 + c] : 0.f;
+    }
+    __syncthreads();
+    float acc[4][4] = {};
+    tile_mac(sT, sDA1, ty, tx, acc);  // acc[o][c]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gW1[(size_t)(ty * 4 + i) * C + c0 + tx * 4 + j] = acc[i][j];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mlp_reduce(int nblocks, int total, const float* __restrict__ part,
+                                                    float* __restrict__ grad) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * total + e];
+  grad[e] = s;
+}
+
+}  // namespace
+}  // namespace wgsr
+
+using namespace wgsr;
+
+#define MLPCHK(name)                                                                         \
+  do {                                                                                       \
+    const hipError_t _e = hipGetLastError();                                                 \
+    if (_e != hipSuccess) return set_error(WGSR_EHIP, "%s: %s", name, hipGetErrorString(_e)); \
+  } while (0)
+
+extern "C" {
+
+size_t wgsr_mlp_scratch_bytes(int N, int C) {
+  if (N <= 0 || C <= 0) return 0;
+  return sizeof(float) * (size_t)((N + kRows - 1) / kRows) * (size_t)mlp_partial_floats(C);
+}
+
+int wgsr_mlp_grad_floats(int C) { return C > 0 ? mlp_partial_floats(C) : 0; }
+
+int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                     const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed, float* h1d,
+                     float* h2d, float* o_pre, float* u, void* stream) {
+  if (N < 0 || C <= 0 || C % 64 != 0) return set_error(WGSR_EINVAL, "wgsr_mlp_forward: C must be a positive multiple of 64");
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return set_error(WGSR_EINVAL, "wgsr_mlp_forward: dropout_p in [0, 1)");
+  if (N == 0) return WGSR_OK;
+  if (!X || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !h1d || !h2d || !o_pre || !u)
+    return set_error(WGSR_EINVAL, "wgsr_mlp_forward: null pointer");
+  hipLaunchKernelGGL(k_mlp_fwd, dim3((N + kRows - 1) / kRows), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
+                     b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
+  MLPCHK("wgsr_mlp_forward");
+  return WGSR_OK;
+}
+
+int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                      const float* h1d, const float* h2d, const float* o_pre, const float* dL_du, float* scratch,
+                      float* grad, void* stream) {
+  if (N < 0 || C <= 0 || C % 64 != 0) return set_error(WGSR_EINVAL, "wgsr_mlp_backward: C must be a positive multiple of 64");
+  const int total = mlp_partial_floats(C);
+  if (N == 0) return hipMemsetAsync(grad, 0, sizeof(float) * total, (hipStream_t)stream) == hipSuccess
+                         ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_mlp_backward: memset");
+  if (!X || !W2 || !W3 || !h1d || !h2d || !o_pre || !dL_du || !scratch || !grad)
+    return set_error(WGSR_EINVAL, "wgsr_mlp_backward: null pointer");
+  const int nb = (N + kRows - 1) / kRows;
+  hipLaunchKernelGGL(k_mlp_bwd, dim3(nb), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p, h1d, h2d,
+                     o_pre, dL_du, scratch);
+  hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nb, total, scratch,
+                     grad);
+  MLPCHK("wgsr_mlp_backward");
+  return WGSR_OK;
+}
+
+}  // extern "C"

@@ -139,6 +139,14 @@ def load():
         L.wgsr_tracking_loss.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float] + [_fp] * 3 + [_fp]
         L.wgsr_grad_mask.restype = c_int
         L.wgsr_grad_mask.argtypes = [c_int, c_int, _fp, ctypes.c_float, _fp, _fp]
+        L.wgsr_mlp_scratch_bytes.restype = c_sz
+        L.wgsr_mlp_scratch_bytes.argtypes = [c_int, c_int]
+        L.wgsr_mlp_grad_floats.restype = c_int
+        L.wgsr_mlp_grad_floats.argtypes = [c_int]
+        L.wgsr_mlp_forward.restype = c_int
+        L.wgsr_mlp_forward.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float, ctypes.c_uint32] + [_fp] * 4 + [_fp]
+        L.wgsr_mlp_backward.restype = c_int
+        L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
         L.wgsr_densification_stats.restype = c_int
         L.wgsr_densification_stats.argtypes = [c_int] + [_fp] * 5 + [_fp]
         L.wgsr_mark_visible.restype = c_int
@@ -198,6 +206,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
     "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
     "wgsr_uncer_loss_backward", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
+    "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
 )
 
 VIEW_RECORD_FLOATS = 12   # WGSR_VIEW_RECORD_FLOATS

@@ -9,8 +9,11 @@ per-parameter ``state`` dicts (``"step"``, ``"exp_avg"``, ``"exp_avg_sq"``)
 that ``replace_tensor_to_optimizer``, ``_prune_optimizer`` and
 ``cat_tensors_to_optimizer`` (:495-600) read and rebuild.  ``step()`` updates
 every parameter that has a gradient in ONE HIP launch (``wgsr_adam_step``)
-instead of torch's ~7 foreach passes.  Scope as used by the reference: no
-weight decay, no amsgrad, no maximize, fp32 CUDA tensors.
+instead of torch's ~7 foreach passes.  ``weight_decay`` is torch.optim.Adam's
+L2 form (the gradient used is grad + weight_decay * param; ``.grad`` itself
+is left untouched, one extra foreach launch) -- the uncertainty MLP's
+optimiser uses it (mapper.py:129-133).  Scope as used by the reference: no
+amsgrad, no maximize, fp32 CUDA tensors.
 """
 from __future__ import annotations
 
@@ -24,8 +27,8 @@ from . import _lib
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
-        if weight_decay != 0.0:
-            raise ValueError("FusedAdam: weight_decay is not supported (the reference uses 0)")
+        if weight_decay < 0.0:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
         if not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
             raise ValueError(f"Invalid beta parameters: {betas}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -39,6 +42,12 @@ class FusedAdam(torch.optim.Optimizer):
         batches = {}  # (betas, eps, device) -> [AdamTensor]
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
+            wd = group.get("weight_decay", 0.0)
+            decayed = {}
+            if wd != 0.0:
+                live = [p for p in group["params"] if p.grad is not None]
+                if live:
+                    decayed = dict(zip(map(id, live), torch._foreach_add([p.grad for p in live], live, alpha=wd)))
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -56,7 +65,8 @@ class FusedAdam(torch.optim.Optimizer):
                 step = float(step_t)
                 bc1 = 1.0 - beta1 ** step
                 bc2 = 1.0 - beta2 ** step
-                grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                grad = decayed.get(id(p), p.grad)
+                grad = grad if grad.is_contiguous() else grad.contiguous()
                 for t in (p, state["exp_avg"], state["exp_avg_sq"]):
                     if not t.is_contiguous():
                         raise RuntimeError("FusedAdam: parameters and states must be contiguous")
