@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--sh", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the stage timers")
+    ap.add_argument("--no-knn", action="store_true", help="skip the distCUDA2 measurement (rocprof runs)")
     ap.add_argument("--dp-exchange", choices=("views", "allreduce"), default=None,
                     help="N > 1 gradient exchange: 'views' (default: screen-space records to the "
                          "Gaussians' owners, owner-computed shards all-gathered; wgsr.dp."
@@ -281,7 +282,7 @@ def main():
         if issue:
             out["render_valu_issue"] = issue
 
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_knn:
         # simple_knn.distCUDA2 over the scene's points
         # (outside the timed region; device time per call, HIP events)
         from simple_knn._C import distCUDA2
