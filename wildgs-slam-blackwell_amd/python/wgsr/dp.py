@@ -237,11 +237,28 @@ def _all_gather_inplace_many(fulls, rank, group):
             _all_gather_inplace(f, rank, group)
         return None
     world = dist.get_world_size(group)
-    with dist._coalescing_manager(group, async_ops=True) as cm:
-        for f in fulls:
-            S = f.size(0) // world
-            dist.all_gather_into_tensor(f.view(-1), f[rank * S:(rank + 1) * S].view(-1), group=group)
-    return cm
+    try:
+        with dist._coalescing_manager(group, async_ops=True) as cm:
+            for f in fulls:
+                S = f.size(0) // world
+                dist.all_gather_into_tensor(f.view(-1), f[rank * S:(rank + 1) * S].view(-1), group=group)
+        return cm
+    except (RuntimeError, AttributeError, NotImplementedError):
+        # a backend / torch build without the coalesced fast path: every rank
+        # takes this branch alike (same code, same backend), so the collectives
+        # still pair up -- one gather per buffer
+        works = [_all_gather_inplace(f, rank, group) for f in fulls]
+        return _WaitAll(works)
+
+
+class _WaitAll:
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            if w is not None:
+                w.wait()
 
 
 class ViewShardedBackward:
