@@ -76,3 +76,14 @@ def test_state_dict_matches_reference_layout():
     assert sorted(net.state_dict()) == sorted(["layers.0.weight", "layers.0.bias", "layers.1.weight",
                                                "layers.1.bias", "output_layer.weight", "output_layer.bias"])
     assert net.layers[0].weight.shape == (64, 384) and net.output_layer.weight.shape == (1, 64)
+
+
+def test_single_row_and_batched_shapes():
+    from wgsr.mlp import UncertaintyMLP
+    torch.manual_seed(2)
+    net = UncertaintyMLP(input_dim=64, dropout_p=0.0).to(DEV)
+    for shape in ((1, 1, 64), (1, 303, 64), (3, 2, 5, 64)):
+        x = torch.randn(*shape, device=DEV)
+        u = net(x)
+        assert u.shape == x.shape[:-1]
+        torch.testing.assert_close(u, _torch_mlp(net, x), rtol=1e-5, atol=1e-6)

@@ -140,3 +140,16 @@ def test_refinement_iteration_pose_gradients():
     assert abs(out["hip"][0] - out["oracle"][0]) <= 1e-5 * abs(out["oracle"][0])
     for x, y in zip(out["hip"][1:], out["oracle"][1:]):
         assert _rel(x, y) <= 1e-3
+
+
+def test_grad_mask_tiny_and_blockless_images():
+    """Images smaller than the 32 x 32 block grid keep the raw intensity
+    everywhere (the reference's blocks are empty slices)."""
+    from wgsr.tracking import compute_grad_mask
+    for H, W in ((20, 40), (33, 31), (2, 2)):
+        img = torch.rand(3, H, W, generator=torch.Generator().manual_seed(H * W)).to(DEV)
+        got = compute_grad_mask(img, 4)
+        want = ot.compute_grad_mask(img, 4)
+        torch.cuda.synchronize()
+        assert got.shape == (1, H, W)
+        torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)  # tap-order rounding of ~0 sums

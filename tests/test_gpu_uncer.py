@@ -208,3 +208,26 @@ def test_rejects_cpu_and_bad_shapes():
         mapping_loss_uncertainty(ren, dep, opa, gt, ref, ea, eb, unc[:2], 0.3, 0.3)
     with pytest.raises(NotImplementedError):
         mapping_loss_uncertainty(ren, dep, opa, gt, ref, ea, eb, unc, 0.3, 0.3, {"full_resolution": True})
+
+
+def test_smallest_maps_and_initialization_mode():
+    """h, w = 3 (the reflect padding's minimum), an image not a multiple of
+    the feature grid, and the initialization branch (no exposure term)."""
+    from wgsr.uncertainty import mapping_loss_uncertainty
+    gt, ren, ref, dep, opa, unc, ea, eb = _frame(45, 61, 3, 3, seed=9)
+    for init in (False, True):
+        ins = {}
+        for who in ("oracle", "hip"):
+            r, d, u = (x.clone().requires_grad_(True) for x in (ren, dep, unc))
+            if who == "oracle":
+                loss = ou.loss_mapping_uncertainty(ou.DEFAULT_CONFIG, r, d, gt, ref, ea, eb, opa, u, 0.5, 0.5,
+                                                   initialization=init)
+            else:
+                loss = mapping_loss_uncertainty(r, d, opa, gt, ref, ea, eb, u, 0.5, 0.5, ou.DEFAULT_CONFIG,
+                                                initialization=init)
+            loss.backward()
+            ins[who] = (float(loss), r.grad, d.grad, u.grad)
+        torch.cuda.synchronize()
+        assert abs(ins["hip"][0] - ins["oracle"][0]) <= 1e-5 * abs(ins["oracle"][0])
+        for x, y in zip(ins["hip"][1:], ins["oracle"][1:]):
+            assert _rel(x, y) <= 1e-4
