@@ -235,6 +235,17 @@ int wgsr_uncer_small_maps(const wgsr_uncer_params* prm, const float* opacity, co
 int wgsr_uncer_loss_small(const wgsr_uncer_params* prm, const float* uncertainty, const float* small_ssim_loss,
                           const float* small_depth_loss, const float* small_opacity, float grad_scale,
                           float* loss_map, float* partials, float* dL_duncertainty, void* stream);
+/* The loss epilogue in one launch: fixed-order sums of partials
+ * ([blocks(H*W)][3] from wgsr_uncer_loss_forward) and small_partials
+ * (wgsr_uncer_loss_small), *loss = alpha rgb + (1 - alpha) depth + ssim_mult
+ * mean(uncertainty loss) + extra_weight sum(extra_partials[n_extra]) (e.g. the
+ * isotropic term), sums[3] = the three full-resolution sums, ssim_scale[3] =
+ * the SSIM backward's per-plane dL/dS (ssim_mean: device scalar from
+ * wgsr_ssim_forward; ignored unless ssim_loss). */
+int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials, const float* small_partials,
+                            const float* ssim_mean, const float* extra_partials, int n_extra, float extra_weight,
+                            float alpha, float lambda_dssim, float ssim_mult, int ssim_loss, float* loss,
+                            float* sums, float* ssim_scale, void* stream);
 /* dL_dimage / dL_ddepth of loss_grad x (w_rgb sum(w rgb L1) + w_depth
  * sum(re-weighted depth L1)) + the SSIM term (ssim_grad: its gradient w.r.t.
  * image_ab, already scaled; NULL = none); loss_grad: device scalar (NULL = 1);

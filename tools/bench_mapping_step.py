@@ -320,17 +320,17 @@ def main_uncertainty(a):
         f = synthetic_camera(W, H, 0).raster_fields()
         camd = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in f.items()}
         torch.manual_seed(0)
+        from wgsr.optim import FusedAdam
         if a.torch_mlp:
             net = UncerMLP().to(dev)
             uopt = torch.optim.Adam(net.parameters(), lr=4e-4, weight_decay=1e-5)
         else:
             from wgsr.mlp import UncertaintyMLP
-            from wgsr.optim import FusedAdam
             net = UncertaintyMLP(384).to(dev)
             uopt = FusedAdam(net.parameters(), lr=4e-4, weight_decay=1e-5)
         ea = torch.zeros(1, device=dev, requires_grad=True)
         eb = torch.zeros(1, device=dev, requires_grad=True)
-        kopt = torch.optim.Adam([ea, eb], lr=0.01)
+        kopt = (torch.optim.Adam if a.torch_mlp else FusedAdam)([ea, eb], lr=0.01)  # keyframe exposure optimiser
         med = gt_depth.median()  # constant per keyframe
 
         def it():

@@ -4,15 +4,16 @@
 // ReLU and dropout 0.2 (applied unconditionally, :55), one output, softplus).
 // It runs on every mapping iteration over the [H/14, W/14] feature map.
 //
-//   mlp_fwd     64 rows per workgroup: layer 1 as a 64 x 64 x C tile product
-//               with X and W1 staged through LDS in 64-wide K slabs (4 x 4
-//               outputs per thread), bias + ReLU + dropout in registers, layer
-//               2 from LDS, layer 3 + softplus; keeps the post-dropout
+//   mlp_fwd     64 (or, for few rows, 16) rows per workgroup: layer 1 as a
+//               rows x 64 x C tile product with X and W1 staged through LDS in
+//               64-wide K slabs, bias + ReLU + dropout in registers, layer 2
+//               from LDS, layer 3 + softplus; keeps the post-dropout
 //               activations and the pre-softplus output for the backward.
-//   mlp_bwd     the same 64 rows backward: softplus', layer 3, the two
-//               ReLU/dropout masks (read off the kept activations: a kept
-//               activation is > 0 exactly when ReLU passed and dropout kept
-//               it), and per-workgroup partial weight / bias gradients.
+//   mlp_bwd     64 rows x one 64-column chunk of dW1 per workgroup:
+//               softplus', layer 3, the two ReLU/dropout masks (read off the
+//               kept activations: a kept activation is > 0 exactly when ReLU
+//               passed and dropout kept it), per-workgroup partial weight /
+//               bias gradients.
 //   mlp_reduce  sums the per-workgroup partials in a fixed order
 //               (deterministic), one thread per parameter element.
 // Dropout masks come from a counter hash of (seed, layer, row, column) -- the
@@ -44,57 +45,63 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, int layer, uint32_t row
   return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
-// acc[4][4] += A[rows ty*4.., k] * B[cols tx*4.., k] over k in [0, 64) (both in LDS, [64][kLd])
-__device__ __forceinline__ void tile_mac(const float (*A)[kLd], const float (*B)[kLd], int ty, int tx,
-                                         float (&acc)[4][4]) {
+// acc[4][CW] += A[rows ty*4.., k] * B[cols tx*CW.., k] over k in [0, 64) (both in LDS, [.][kLd])
+template <int CW>
+__device__ __forceinline__ void tile_mac_cw(const float (*A)[kLd], const float (*B)[kLd], int ty, int tx,
+                                            float (&acc)[4][CW]) {
 #pragma unroll 8
   for (int k = 0; k < 64; ++k) {
-    float a[4], b[4];
+    float a[4], b[CW];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][k];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = B[tx * 4 + j][k];
+    for (int j = 0; j < CW; ++j) b[j] = B[tx * CW + j][k];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < CW; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
   }
 }
 
-// dst[r][c] = src[(r0 + r) * ld + c0 + c] for a 64 x 64 slab (zeros past n rows)
+// dst[r][c] = src[(r0 + r) * ld + c0 + c] for an R x 64 slab (zeros past n rows)
+template <int R = 64>
 __device__ __forceinline__ void load_slab(float (*dst)[kLd], const float* __restrict__ src, int r0, int n, int ld,
                                           int c0) {
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+  for (int e = threadIdx.x; e < R * 64; e += 256) {
     const int r = e >> 6, c = e & 63;
     dst[r][c] = (r0 + r < n) ? src[(size_t)(r0 + r) * ld + c0 + c] : 0.f;
   }
 }
 
+// R rows per workgroup (64, or 16 when there are few rows: more workgroups);
+// each thread owns 4 rows x R/16 columns of every 64-wide layer output.
+template <int R>
 __global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __restrict__ X,
                                                  const float* __restrict__ W1, const float* __restrict__ b1,
                                                  const float* __restrict__ W2, const float* __restrict__ b2,
                                                  const float* __restrict__ W3, const float* __restrict__ b3, float p,
                                                  uint32_t seed, float* __restrict__ h1d, float* __restrict__ h2d,
                                                  float* __restrict__ o_pre, float* __restrict__ u) {
-  __shared__ float sA[64][kLd], sB[64][kLd];
-  const int t = threadIdx.x, ty = t >> 4, tx = t & 15;
-  const int r0 = blockIdx.x * kRows;
+  constexpr int CW = R / 16, TXN = 64 / CW;
+  __shared__ float sA[R][kLd], sB[64][kLd];
+  const int t = threadIdx.x, ty = t / TXN, tx = t % TXN;
+  const int r0 = blockIdx.x * R;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
-  float acc[4][4] = {};
+  float acc[4][CW] = {};
   for (int k0 = 0; k0 < C; k0 += 64) {
     __syncthreads();
-    load_slab(sA, X, r0, N, C, k0);
+    load_slab<R>(sA, X, r0, N, C, k0);
     load_slab(sB, W1, 0, kHid, C, k0);
     __syncthreads();
-    tile_mac(sA, sB, ty, tx, acc);
+    tile_mac_cw<CW>(sA, sB, ty, tx, acc);
   }
   __syncthreads();
-  // layer 1 epilogue -> sA (the 64 x 64 layer-2 input), h1d
+  // layer 1 epilogue -> sA (the R x 64 layer-2 input), h1d
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = ty * 4 + i, c = tx * 4 + j;
+    for (int j = 0; j < CW; ++j) {
+      const int r = ty * 4 + i, c = tx * CW + j;
       float v = fmaxf(acc[i][j] + b1[c], 0.f);
       v = keep_elem(seed, 0, (uint32_t)(r0 + r), c, p) ? v * scale : 0.f;
       sA[r][c] = v;
@@ -103,22 +110,22 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __re
     }
   load_slab(sB, W2, 0, kHid, kHid, 0);
   __syncthreads();
-  tile_mac(sA, sB, ty, tx, acc);
+  tile_mac_cw<CW>(sA, sB, ty, tx, acc);
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = ty * 4 + i, c = tx * 4 + j;
+    for (int j = 0; j < CW; ++j) {
+      const int r = ty * 4 + i, c = tx * CW + j;
       float v = fmaxf(acc[i][j] + b2[c], 0.f);
       v = keep_elem(seed, 1, (uint32_t)(r0 + r), c, p) ? v * scale : 0.f;
-      sB[r][c] = v;  // layer-3 input
+      sA[r][c] = v;  // layer-3 input
       if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + c] = v;
     }
   __syncthreads();
-  if (t < kRows && r0 + t < N) {
+  if (t < R && r0 + t < N) {
     float o = 0.f;
-    for (int k = 0; k < kHid; ++k) o = fmaf(sB[t][k], W3[k], o);
+    for (int k = 0; k < kHid; ++k) o = fmaf(sA[t][k], W3[k], o);
     o += b3[0];
     o_pre[r0 + t] = o;
     u[r0 + t] = o > 20.f ? o : log1pf(expf(o));  // nn.Softplus(beta 1, threshold 20)
@@ -158,11 +165,12 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   load_slab(sT, h2d, r0, N, kHid, 0);
   __syncthreads();
   // layer 3: dW3[k] = sum_r do[r] h2d[r][k], db3; dA2 = do W3 through ReLU/dropout
-  if (t < kHid) {
+  const bool head = blockIdx.y == 0;  // writes the non-dW1 gradients
+  if (head && t < kHid) {
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s = fmaf(sDo[r], sT[r][t], s);
     gW3[t] = s;
-  } else if (t == kHid) {
+  } else if (head && t == kHid) {
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s += sDo[r];
     gb3[0] = s;
@@ -186,13 +194,14 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
     }
     __syncthreads();
     float acc[4][4] = {};
-    tile_mac(sT, sDA1, ty, tx, acc);  // acc[o][i]
+    tile_mac_cw<4>(sT, sDA1, ty, tx, acc);  // acc[o][i]
+    if (head)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
+        for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
   }
-  if (t < kHid) {
+  if (head && t < kHid) {
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s += sDA2[r][t];
     gb2[t] = s;
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   __syncthreads();
   {
     float acc[4][4] = {};
-    tile_mac(sDA2, sDA1, ty, tx, acc);  // acc[r][i]
+    tile_mac_cw<4>(sDA2, sDA1, ty, tx, acc);  // acc[r][i]
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -217,13 +226,15 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
       }
   }
   __syncthreads();
-  if (t < kHid) {
+  if (head && t < kHid) {
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s += sT[t][r];
     gb1[t] = s;
   }
   // dW1[o][c] = sum_r dA1[r][o] X[r][c], 64 columns of X at a time (sDA1[c][r] = X slab transposed)
-  for (int c0 = 0; c0 < C; c0 += 64) {
+  // this workgroup's 64-column chunk of dW1 (grid.y splits C; every chunk
+  // recomputes the cheap 64 x 64 part above, chunk 0 alone writes it)
+  for (int c0 = 64 * (int)blockIdx.y; c0 < 64 * (int)blockIdx.y + 64; c0 += 64) {
     __syncthreads();
     for (int e = t; e < 64 * 64; e += 256) {
       const int r = e >> 6, c = e & 63;
@@ -231,7 +242,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
     }
     __syncthreads();
     float acc[4][4] = {};
-    tile_mac(sT, sDA1, ty, tx, acc);  // acc[o][c]
+    tile_mac_cw<4>(sT, sDA1, ty, tx, acc);  // acc[o][c]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -276,8 +287,12 @@ int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float*
   if (N == 0) return WGSR_OK;
   if (!X || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !h1d || !h2d || !o_pre || !u)
     return set_error(WGSR_EINVAL, "wgsr_mlp_forward: null pointer");
-  hipLaunchKernelGGL(k_mlp_fwd, dim3((N + kRows - 1) / kRows), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
-                     b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
+  if ((N + 63) / 64 >= 1024)  // enough 64-row workgroups to fill the chip
+    hipLaunchKernelGGL(k_mlp_fwd<64>, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
+                       b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
+  else
+    hipLaunchKernelGGL(k_mlp_fwd<16>, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
+                       b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
   MLPCHK("wgsr_mlp_forward");
   return WGSR_OK;
 }
@@ -292,8 +307,8 @@ int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float
   if (!X || !W2 || !W3 || !h1d || !h2d || !o_pre || !dL_du || !scratch || !grad)
     return set_error(WGSR_EINVAL, "wgsr_mlp_backward: null pointer");
   const int nb = (N + kRows - 1) / kRows;
-  hipLaunchKernelGGL(k_mlp_bwd, dim3(nb), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p, h1d, h2d,
-                     o_pre, dL_du, scratch);
+  hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p, h1d,
+                     h2d, o_pre, dL_du, scratch);
   hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nb, total, scratch,
                      grad);
   MLPCHK("wgsr_mlp_backward");

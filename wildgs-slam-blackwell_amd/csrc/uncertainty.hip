@@ -321,6 +321,43 @@ __global__ __launch_bounds__(kUBlock) void k_unc_bwd(wgsr_uncer_params prm, cons
   }
 }
 
+// One workgroup: the scalar epilogue of the loss (fixed-order partial sums,
+// the loss value, the SSIM backward's per-plane scale) -- one launch instead
+// of ~15 tiny torch ops per iteration.
+__device__ __forceinline__ float wg_sum(const float* __restrict__ a, int n, int stride, float* sred) {
+  float v = 0.f;
+  for (int i = threadIdx.x; i < n; i += kUBlock) v += a[(size_t)i * stride];
+  return ublock_sum(v, sred);  // thread 0
+}
+
+__global__ __launch_bounds__(kUBlock) void k_unc_combine(int HW, int hw, const float* __restrict__ lpart, int nb,
+                                                         const float* __restrict__ upart, int nbs,
+                                                         const float* __restrict__ ssim_mean,
+                                                         const float* __restrict__ extra, int nextra, float w_extra,
+                                                         float alpha, float lam, float ssim_mult, int ssim_loss,
+                                                         float* __restrict__ loss, float* __restrict__ sums,
+                                                         float* __restrict__ ssim_scale) {
+  __shared__ float sred[kUBlock / 64];
+  const float s0 = wg_sum(lpart, nb, 3, sred);
+  const float s1 = wg_sum(lpart + 1, nb, 3, sred);
+  const float s2 = wg_sum(lpart + 2, nb, 3, sred);
+  const float u = wg_sum(upart, nbs, 1, sred);
+  const float x = extra ? wg_sum(extra, nextra, 1, sred) : 0.f;
+  if (threadIdx.x == 0) {
+    const float n3 = 3.f * (float)HW;
+    const float rgb = ssim_loss ? ((1.f - lam) * s0 + 3.f * lam * (1.f - ssim_mean[0]) * s1) / n3 : s0 / n3;
+    loss[0] = alpha * rgb + (1.f - alpha) * s2 / (float)HW + ssim_mult * (u / (float)hw) + w_extra * x;
+    sums[0] = s0;
+    sums[1] = s1;
+    sums[2] = s2;
+    // dL/dS per pixel of the SSIM map: -alpha lambda (sum w) / HW / (3 HW)
+    const float sc = s1 * (-alpha * lam / ((float)HW * n3));
+    ssim_scale[0] = sc;
+    ssim_scale[1] = sc;
+    ssim_scale[2] = sc;
+  }
+}
+
 int ublocks(int64_t n) { return n > 0 ? (int)((n + kUBlock - 1) / kUBlock) : 0; }
 
 int check_params(const wgsr_uncer_params* p, const char* who) {
@@ -389,6 +426,22 @@ int wgsr_uncer_loss_small(const wgsr_uncer_params* prm, const float* uncertainty
                      small_ssim_loss, small_depth_loss, small_opacity, grad_scale, loss_map, partials,
                      dL_duncertainty);
   UNCCHK("wgsr_uncer_loss_small");
+  return WGSR_OK;
+}
+
+int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials, const float* small_partials,
+                            const float* ssim_mean, const float* extra_partials, int n_extra, float extra_weight,
+                            float alpha, float lambda_dssim, float ssim_mult, int ssim_loss, float* loss,
+                            float* sums, float* ssim_scale, void* stream) {
+  if (int e = check_params(prm, "wgsr_uncer_loss_combine")) return e;
+  if (!partials || !small_partials || !loss || !sums || !ssim_scale || (ssim_loss && !ssim_mean) ||
+      (n_extra > 0 && !extra_partials))
+    return set_error(WGSR_EINVAL, "wgsr_uncer_loss_combine: null pointer");
+  hipLaunchKernelGGL(k_unc_combine, dim3(1), dim3(kUBlock), 0, (hipStream_t)stream, prm->H * prm->W,
+                     prm->h * prm->w, partials, ublocks((int64_t)prm->H * prm->W), small_partials,
+                     ublocks((int64_t)prm->h * prm->w), ssim_mean, n_extra > 0 ? extra_partials : nullptr, n_extra,
+                     extra_weight, alpha, lambda_dssim, ssim_mult, ssim_loss, loss, sums, ssim_scale);
+  UNCCHK("wgsr_uncer_loss_combine");
   return WGSR_OK;
 }
 

@@ -131,6 +131,9 @@ def load():
         L.wgsr_uncer_small_maps.argtypes = [U] + [_fp] * 10 + [_fp]
         L.wgsr_uncer_loss_small.restype = c_int
         L.wgsr_uncer_loss_small.argtypes = [U] + [_fp] * 4 + [ctypes.c_float] + [_fp] * 3 + [_fp]
+        L.wgsr_uncer_loss_combine.restype = c_int
+        L.wgsr_uncer_loss_combine.argtypes = ([U] + [_fp] * 4 + [c_int] + [ctypes.c_float] * 4 + [c_int] +
+                                              [_fp] * 3 + [_fp])
         L.wgsr_uncer_loss_backward.restype = c_int
         L.wgsr_uncer_loss_backward.argtypes = [U] + [_fp] * 8 + [ctypes.c_float] * 2 + [_fp] * 5 + [_fp]
         L.wgsr_track_blocks.restype = c_int
@@ -205,7 +208,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_map_blocks", "wgsr_gaussian_activate", "wgsr_gaussian_activate_backward",
     "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
     "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
-    "wgsr_uncer_loss_backward", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
+    "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
     "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
 )
 

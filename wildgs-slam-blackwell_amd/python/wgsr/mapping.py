@@ -219,11 +219,10 @@ class MappingStep:
         H, W = gt_image.shape[-2], gt_image.shape[-1]
         fwd = self._render(cam, H, W, bg)
         nr, image, radii, depth, opac_img = fwd[0], fwd[1], fwd[2], fwd[6], fwd[7]
+        w_iso = iso_weight / (3 * P) if P else 0.0
         loss, state = U.loss_forward(image, depth, opac_img, gt_image, gt_depth, exposure_a, exposure_b, uncertainty,
                                      train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
-                                     median_depth)
-        w_iso = iso_weight / (3 * P) if P else 0.0
-        loss = loss + w_iso * self.iso_part.sum()
+                                     median_depth, extra=(self.iso_part, w_iso))
         d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state)
         _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:

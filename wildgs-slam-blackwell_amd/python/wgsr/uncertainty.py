@@ -90,6 +90,7 @@ class LossState:
     ssim_dmap: torch.Tensor | None
     d_unc: torch.Tensor          # dL/d(uncertainty) for dL/dloss = 1 (zeros when frozen)
     uncertainty_loss: torch.Tensor
+    ssim_scale: torch.Tensor     # [3] the SSIM backward's dL/dS for dL/dloss = 1
 
 
 def _check(t, who):
@@ -99,9 +100,12 @@ def _check(t, who):
 
 def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, uncertainty, train_frac: float,
                  ssim_frac: float, cfg: dict, initialization: bool = False, freeze_uncertainty_loss: bool = False,
-                 median_depth=None):
+                 median_depth=None, extra=None):
     """-> (loss 0-d device tensor, LossState).  image/gt [3,H,W], depth /
-    ref_depth / opacity [1,H,W] (or [H,W]), uncertainty [h,w]."""
+    ref_depth / opacity [1,H,W] (or [H,W]), uncertainty [h,w].  ``extra``:
+    optional (partials [n] device tensor, weight) added to the loss as
+    weight * sum(partials) in the same epilogue launch (MappingStep's
+    isotropic term)."""
     L = _lib.load()
     H, W = gt.shape[-2], gt.shape[-1]
     if uncertainty.dim() != 2:
@@ -161,14 +165,17 @@ def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, u
         gscale = 0.0 if freeze_uncertainty_loss else cfg["ssim_mult"] / hw
         _lib.check(L.wgsr_uncer_loss_small(ctypes.byref(prm), p(unc), *[p(s) for s in small], float(gscale),
                                            p(uloss), p(upart), p(d_unc), st))
-    sums = lpart.sum(0)
-    alpha, lam = cfg["alpha"], cfg["lambda_dssim"]
-    if cfg["ssim_loss"]:
-        rgb = ((1.0 - lam) * sums[0] + 3.0 * lam * (1.0 - ssim_mean) * sums[1]) / (3 * HW)
-    else:
-        rgb = sums[0] / (3 * HW)
-    loss = alpha * rgb + (1.0 - alpha) * sums[2] / HW + cfg["ssim_mult"] * (upart.sum() / hw)
-    state = LossState(prm, cfg, image, image_ab, gt, depth, ref, ea, eb, unc, med, sums, ssim_dmap, d_unc, uloss)
+    loss = torch.empty((), device=dev)
+    sums = torch.empty(3, device=dev)
+    ssim_scale = torch.empty(3, device=dev)
+    ex, exw = (None, 0.0) if extra is None else (extra[0].contiguous(), float(extra[1]))
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_uncer_loss_combine(ctypes.byref(prm), p(lpart), p(upart), p(ssim_mean), p(ex),
+                                             0 if ex is None else ex.numel(), exw, float(cfg["alpha"]),
+                                             float(cfg["lambda_dssim"]), float(cfg["ssim_mult"]),
+                                             int(bool(cfg["ssim_loss"])), p(loss), p(sums), p(ssim_scale), st))
+    state = LossState(prm, cfg, image, image_ab, gt, depth, ref, ea, eb, unc, med, sums, ssim_dmap, d_unc, uloss,
+                      ssim_scale)
     return loss, state
 
 
@@ -191,10 +198,7 @@ def loss_backward(s: LossState, loss_grad=None):
     with torch.cuda.device(dev):
         if s.cfg["ssim_loss"]:
             # dL/dS per pixel = -alpha lambda (sum w) / HW / (3 HW) (x dL/dloss)
-            scale = s.sums[1] * (-alpha * lam / (HW * 3.0 * HW))
-            if lg is not None:
-                scale = scale * lg[0]
-            scale = scale.reshape(1).expand(3).contiguous()
+            scale = s.ssim_scale if lg is None else (s.ssim_scale * lg[0]).contiguous()
             ssim_grad = torch.empty_like(s.image_ab)
             _lib.check(L.wgsr_ssim_backward(p(s.image_ab), p(s.gt), 3, H, W, 11, p(s.ssim_dmap), p(scale),
                                             p(ssim_grad), st))
