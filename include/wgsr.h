@@ -270,6 +270,20 @@ int wgsr_tracking_loss(int H, int W, const float* image, const float* gt_image, 
                        const float* grad_mask, const float* uncertainty, const float* exposure_a,
                        const float* exposure_b, float rgb_threshold, float* dL_dimage, float* dL_dopacity,
                        float* partials, void* stream);
+/* One pose-refinement update (mapper.py:884-906 after loss.backward()): Adam
+ * (torch semantics; bias corrections of `step`) over cam_rot_delta (grad =
+ * dtau[3:6]), cam_trans_delta (dtau[0:3]), exposure_a / exposure_b (sums of
+ * columns 1 / 2 of wgsr_tracking_loss's partials), then update_pose
+ * (pose_utils.py:81-98: w2c <- SE3_exp([trans, rot]) w2c, deltas back to 0,
+ * *converged = |tau| < threshold) and the next iteration's rasteriser camera
+ * (viewmatrix, projmatrix, campos).  state: wgsr_pose_state_floats() floats,
+ * layout in csrc/tracking.hip (R, T, exposures, Adam moments, camera).
+ * camera_only = 1 only writes the camera fields from the stored (R, T). */
+int wgsr_pose_state_floats(void);
+int wgsr_pose_step(float* state, const float* dtau, const float* loss_partials, int n_partials,
+                   const float* projection_matrix, float lr_rot, float lr_trans, float lr_exposure, float beta1,
+                   float beta2, float eps, int step, float converged_threshold, int* converged, int camera_only,
+                   void* stream);
 /* Camera.compute_grad_mask (src/utils/camera_utils.py:157-180): grad_mask
  * [H,W] of the [3,H,W] image (edge_threshold: Training.edge_threshold).
  * Needs (H/32)(W/32) <= 8192. */

@@ -153,3 +153,73 @@ def test_grad_mask_tiny_and_blockless_images():
         torch.cuda.synchronize()
         assert got.shape == (1, H, W)
         torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)  # tap-order rounding of ~0 sums
+
+
+def _reference_refine(sc, deg, bg, cam_p, gt, gm, unc, ea0, eb0, iters, lr=(0.003, 0.001, 0.01), thr=1e-4):
+    """mapper.py:856-911 in torch: render (autograd rasteriser), the oracle
+    tracking loss, torch.optim.Adam over the four groups, update_pose with the
+    restated SE3_exp (pose_utils.py:30-98)."""
+    from wgsr.camera import PinholeCamera, se3_exp
+    from wgsr.render import DeviceCamera, render
+    R, T = cam_p.R.clone(), cam_p.T.clone()
+    rot = torch.zeros(3, device=DEV, requires_grad=True)
+    trans = torch.zeros(3, device=DEV, requires_grad=True)
+    a = ea0.clone().requires_grad_(True)
+    b = eb0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([{"params": [rot], "lr": lr[0]}, {"params": [trans], "lr": lr[1]},
+                            {"params": [a], "lr": lr[2]}, {"params": [b], "lr": lr[2]}])
+    it = 0
+    for it in range(1, iters + 1):
+        pc = PinholeCamera(R=R, T=T, fx=cam_p.fx, fy=cam_p.fy, cx=cam_p.cx, cy=cam_p.cy, W=cam_p.W, H=cam_p.H)
+        cam = DeviceCamera.from_pinhole(pc, DEV)
+        cam.cam_rot_delta, cam.cam_trans_delta = rot, trans
+        pkg = render(cam, sc.means3D.to(DEV), sc.opacities.to(DEV), sc.scales.to(DEV), sc.rotations.to(DEV),
+                     sc.shs.to(DEV), deg, bg)
+        opt.zero_grad()
+        ot.loss_tracking(pkg["render"], pkg["opacity"], gt, a, b, gm, unc).backward()
+        opt.step()
+        with torch.no_grad():
+            tau = torch.cat([trans, rot]).cpu()
+            w2c = torch.eye(4)
+            w2c[:3, :3], w2c[:3, 3] = R, T
+            new = se3_exp(tau) @ w2c
+            R, T = new[:3, :3].clone(), new[:3, 3].clone()
+            rot.zero_()
+            trans.zero_()
+            if float(tau.norm()) < thr:
+                break
+    return R, T, a.detach(), b.detach(), it
+
+
+@pytest.mark.parametrize("iters", [1, 6])
+def test_pose_refine_matches_reference_loop(iters):
+    """wgsr.tracking.PoseRefine (device Adam + SE3 update + camera in one
+    launch per iteration) vs the reference loop from a perturbed pose."""
+    import math
+    from wgsr.camera import synthetic_camera
+    from wgsr.render import render, DeviceCamera
+    from wgsr.scene import make_scene
+    from wgsr.tracking import PoseRefine, compute_grad_mask
+    P, W, H, deg = 4000, 160, 120, 2
+    sc = make_scene(P, W, H, deg, seed=21)
+    bg = torch.zeros(3, device=DEV)
+    true_cam = synthetic_camera(W, H, 0)
+    with torch.no_grad():  # the target: the scene rendered from the true pose
+        gt = render(DeviceCamera.from_pinhole(true_cam, DEV), sc.means3D.to(DEV), sc.opacities.to(DEV),
+                    sc.scales.to(DEV), sc.rotations.to(DEV), sc.shs.to(DEV), deg, bg)["render"].detach()
+    start = synthetic_camera(W, H, 1)  # 2 degrees and 5 cm off
+    gm = compute_grad_mask(gt, 4)
+    unc = (torch.rand(H, W, generator=torch.Generator().manual_seed(3)) * 2 + 0.05).to(DEV)
+    ea0, eb0 = torch.tensor([0.02], device=DEV), torch.tensor([-0.01], device=DEV)
+    Rr, Tr, ar, br, itr = _reference_refine(sc, deg, bg, start, gt, gm, unc, ea0, eb0, iters)
+    pr = PoseRefine(sc.means3D.to(DEV), sc.opacities.to(DEV), sc.scales.to(DEV), sc.rotations.to(DEV),
+                    sc.shs.to(DEV), deg, bg, start.projection_matrix.to(DEV), H, W, start.FoVx, start.FoVy)
+    R, T, a, b, it = pr.refine(start.R, start.T, ea0, eb0, gt, gm, unc, iters=iters)
+    torch.cuda.synchronize()
+    assert it == itr
+    assert float((R.cpu() - Rr).abs().max()) <= 1e-5 * max(1, iters)
+    assert float((T.cpu() - Tr).abs().max()) <= 1e-5 * max(1, iters)
+    assert abs(float(a) - float(ar)) <= 1e-5 * max(1, iters)
+    assert abs(float(b) - float(br)) <= 1e-5 * max(1, iters)
+    # the refinement moved the pose (toward the truth)
+    assert float((R.cpu() - start.R).abs().max()) > 1e-4 and not math.isnan(float(R.sum()))

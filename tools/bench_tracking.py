@@ -9,12 +9,15 @@ src/utils/slam_utils.py:10-82 and src/utils/camera_utils.py:157-180):
 * the tracking loss forward + backward vs wgsr.tracking.tracking_loss (one
   pass);
 * one whole refinement iteration (mapper.py:884-906: render -> loss ->
-  backward -> Adam over rot/trans/exposure) with each loss, same rasteriser.
+  backward -> Adam over rot/trans/exposure) with each loss, same rasteriser;
+* the whole refinement loop with the reference's per-iteration Camera
+  matrices and update_pose vs wgsr.tracking.PoseRefine.
 
 Synthetic scene/targets (BASELINE.md distribution); device time per call.
 """
 import argparse
 import json
+import math
 import os
 import sys
 
@@ -122,8 +125,86 @@ def main():
 
     out["refine_iter_ms_reference_loss"] = refine(ref_loss)
     out["refine_iter_ms_hip_loss"] = refine(tracking_loss)
-    out["note"] = ("same rasteriser in both refinement loops (update_pose's SE3 step is caller-side torch in both "
-                   "and not included); reference = slam_utils / camera_utils torch ops restated")
+
+    # the whole refinement loop as mapper.py:884-906 runs it, including the
+    # Camera properties recomputed on the device each iteration
+    # (getWorld2View2's two 4x4 inversions, camera_utils.py:137-151) and
+    # update_pose (pose_utils.py:81-98), vs wgsr.tracking.PoseRefine
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from wgsr.tracking import PoseRefine
+    cam0 = synthetic_camera(W, H, 0)
+    Pt = cam0.projection_matrix.to(dev)
+    tanx, tany = math.tan(cam0.FoVx * 0.5), math.tan(cam0.FoVy * 0.5)
+
+    def w2v(R, T):
+        Rt = torch.zeros((4, 4), device=dev)
+        Rt[:3, :3] = R
+        Rt[:3, 3] = T
+        Rt[3, 3] = 1.0
+        return torch.linalg.inv(torch.linalg.inv(Rt))
+
+    def skew(x):
+        m = torch.zeros(3, 3, device=dev)
+        m[0, 1], m[0, 2], m[1, 0], m[1, 2], m[2, 0], m[2, 1] = -x[2], x[1], x[2], -x[0], -x[1], x[0]
+        return m
+
+    def se3(tau):
+        rho, theta = tau[:3], tau[3:]
+        Wm = skew(theta)
+        W2 = Wm @ Wm
+        ang = torch.norm(theta)
+        I = torch.eye(3, device=dev)
+        if ang < 1e-5:
+            Rx, Vx = I + Wm + 0.5 * W2, I + 0.5 * Wm + (1.0 / 6.0) * W2
+        else:
+            Rx = I + (torch.sin(ang) / ang) * Wm + ((1 - torch.cos(ang)) / (ang ** 2)) * W2
+            Vx = I + Wm * ((1.0 - torch.cos(ang)) / (ang ** 2)) + W2 * ((ang - torch.sin(ang)) / (ang ** 3))
+        Tm = torch.eye(4, device=dev)
+        Tm[:3, :3] = Rx
+        Tm[:3, 3] = Vx @ rho
+        return Tm
+
+    def ref_loop(n):
+        R, T = cam0.R.to(dev).clone(), cam0.T.to(dev).clone()
+        rot = torch.zeros(3, device=dev, requires_grad=True)
+        trans = torch.zeros(3, device=dev, requires_grad=True)
+        xa = torch.zeros(1, device=dev, requires_grad=True)
+        xb = torch.zeros(1, device=dev, requires_grad=True)
+        opt = torch.optim.Adam([{"params": [rot], "lr": 0.003}, {"params": [trans], "lr": 0.001},
+                                {"params": [xa], "lr": 0.01}, {"params": [xb], "lr": 0.01}])
+        for _ in range(n):
+            wv = w2v(R, T).transpose(0, 1)
+            full = w2v(R, T).transpose(0, 1).unsqueeze(0).bmm(Pt.unsqueeze(0)).squeeze(0)
+            center = w2v(R, T).transpose(0, 1).inverse()[3, :3]
+            st = GaussianRasterizationSettings(H, W, tanx, tany, bg, 1.0, wv, full, Pt, 3, center, False, False)
+            m2d = torch.zeros_like(means, requires_grad=True) + 0
+            img, _, _, op, _ = GaussianRasterizer(st)(means3D=means, means2D=m2d, shs=shs, colors_precomp=None,
+                                                      opacities=opac, scales=scales, rotations=rots,
+                                                      cov3D_precomp=None, theta=rot, rho=trans)
+            opt.zero_grad()
+            ref_loss(img, op, gt, xa, xb, gm, unc).backward()
+            opt.step()
+            with torch.no_grad():
+                tau = torch.cat([trans, rot], axis=0)
+                w2c = torch.eye(4, device=dev)
+                w2c[0:3, 0:3], w2c[0:3, 3] = R, T
+                new = se3(tau) @ w2c
+                R, T = new[0:3, 0:3], new[0:3, 3]
+                converged = tau.norm() < 0.0
+                rot.data.fill_(0)
+                trans.data.fill_(0)
+                if converged:
+                    break
+
+    pr = PoseRefine(means, opac, scales, rots, shs, 3, bg, Pt, H, W, cam0.FoVx, cam0.FoVy)
+    z = torch.zeros(1, device=dev)
+    n = a.iters
+    out["refine_loop_ms_per_iter_reference"] = timed(lambda: ref_loop(n), 2, 1) / n
+    out["refine_loop_ms_per_iter_pose_refine"] = timed(
+        lambda: pr.refine(cam0.R, cam0.T, z, z, gt, gm, unc, iters=n, converged_threshold=0.0), 2, 1) / n
+    out["note"] = ("same rasteriser everywhere; refine_iter_*: render + loss + backward + Adam only; "
+                   "refine_loop_*: the whole mapper.py:884-906 iteration incl. the Camera matrices and update_pose; "
+                   "reference = slam_utils / camera_utils / pose_utils torch ops restated")
     print(json.dumps(out))
 
 

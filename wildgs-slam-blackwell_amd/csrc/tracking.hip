@@ -16,6 +16,8 @@
 //               grid of blocks thresholded at 4 x the block median.  The
 //               reference runs ~3000 small kernels per keyframe for this (a
 //               Python loop of 1024 medians); here it is two launches.
+#include <math.h>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -173,6 +175,129 @@ __global__ __launch_bounds__(kTBlock) void k_grad_block(int H, int W, int bh, in
   }
 }
 
+// ---- one pose-refinement update (mapper.py:884-906 after the backward) ----
+// state (floats): [0,9) R row-major | [9,12) T | 12 exposure_a | 13 exposure_b |
+// [16,24) Adam exp_avg of (rot 3, trans 3, exposure_a, exposure_b) | [24,32)
+// exp_avg_sq | [32,48) viewmatrix | [48,64) projmatrix | [64,67) campos |
+// 67 |tau| of the update.  The viewmatrix / projmatrix / campos are the
+// rasteriser inputs of the NEXT iteration (Camera.world_view_transform,
+// full_proj_transform, camera_center).
+constexpr int kPoseState = 68;
+
+__device__ __forceinline__ void mat3_mul(const float A[9], const float B[9], float C[9]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// rasteriser camera fields from (R, T) and the stored projection matrix
+__device__ void pose_camera(const float R[9], const float T[3], const float* __restrict__ proj_t, float* st) {
+  float Wv[16];
+  // getWorld2View2(R, T).transpose(0, 1) = [[R^T, 0], [T^T, 1]]
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Wv[4 * i + j] = R[3 * j + i];
+    Wv[4 * i + 3] = 0.f;
+  }
+  Wv[12] = T[0]; Wv[13] = T[1]; Wv[14] = T[2]; Wv[15] = 1.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) st[32 + k] = Wv[k];
+  // full_proj_transform = world_view_transform @ projection_matrix
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      st[48 + 4 * i + j] = Wv[4 * i] * proj_t[j] + Wv[4 * i + 1] * proj_t[4 + j] + Wv[4 * i + 2] * proj_t[8 + j] +
+                           Wv[4 * i + 3] * proj_t[12 + j];
+  // camera_center = inverse(world_view_transform)[3, :3] = -T^T R
+#pragma unroll
+  for (int j = 0; j < 3; ++j) st[64 + j] = -(T[0] * R[j] + T[1] * R[3 + j] + T[2] * R[6 + j]);
+}
+
+__global__ __launch_bounds__(64) void k_pose_step(float* __restrict__ st, const float* __restrict__ dtau,
+                                                  const float* __restrict__ part, int nb,
+                                                  const float* __restrict__ proj_t, float lr_rot, float lr_trans,
+                                                  float lr_expo, float beta1, float beta2, float eps, float bc1,
+                                                  float bc2_sqrt, float conv_th, int* __restrict__ converged,
+                                                  int camera_only) {
+  const int lane = threadIdx.x;
+  float ga = 0.f, gb = 0.f;
+  for (int b = lane; b < nb; b += 64) {
+    ga += part[3 * b + 1];
+    gb += part[3 * b + 2];
+  }
+  ga = wave_sum(ga);
+  gb = wave_sum(gb);
+  if (lane != 0) return;
+  float R[9], T[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = st[k];
+  T[0] = st[9]; T[1] = st[10]; T[2] = st[11];
+  if (camera_only) {
+    pose_camera(R, T, proj_t, st);
+    return;
+  }
+  // Adam over (cam_rot_delta, cam_trans_delta, exposure_a, exposure_b), whose
+  // deltas are 0 at every step start (update_pose resets them)
+  const float g[8] = {dtau[3], dtau[4], dtau[5], dtau[0], dtau[1], dtau[2], ga, gb};
+  const float lr[8] = {lr_rot, lr_rot, lr_rot, lr_trans, lr_trans, lr_trans, lr_expo, lr_expo};
+  float pnew[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float m = beta1 * st[16 + k] + (1.f - beta1) * g[k];
+    const float v = beta2 * st[24 + k] + (1.f - beta2) * g[k] * g[k];
+    st[16 + k] = m;
+    st[24 + k] = v;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    const float p0 = k < 6 ? 0.f : st[12 + (k - 6)];
+    pnew[k] = p0 - (lr[k] / bc1) * (m / denom);
+  }
+  st[12] = pnew[6];
+  st[13] = pnew[7];
+  // update_pose (pose_utils.py:81-98): tau = [trans, rot], new_w2c = SE3_exp(tau) @ w2c
+  const float rho[3] = {pnew[3], pnew[4], pnew[5]}, th[3] = {pnew[0], pnew[1], pnew[2]};
+  const float Wm[9] = {0.f, -th[2], th[1], th[2], 0.f, -th[0], -th[1], th[0], 0.f};
+  float W2[9];
+  mat3_mul(Wm, Wm, W2);
+  const float angle = sqrtf(th[0] * th[0] + th[1] * th[1] + th[2] * th[2]);
+  float Rx[9], Vm[9];
+  if (angle < 1e-5f) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float I = (k % 4 == 0) ? 1.f : 0.f;
+      Rx[k] = I + Wm[k] + 0.5f * W2[k];
+      Vm[k] = I + 0.5f * Wm[k] + (1.f / 6.f) * W2[k];
+    }
+  } else {
+    const float sa = sinf(angle), ca = cosf(angle), a2 = angle * angle;
+    const float c1 = sa / angle, c2 = (1.f - ca) / a2, c3 = (angle - sa) / (a2 * angle);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float I = (k % 4 == 0) ? 1.f : 0.f;
+      Rx[k] = I + c1 * Wm[k] + c2 * W2[k];
+      Vm[k] = I + Wm[k] * c2 + W2[k] * c3;
+    }
+  }
+  float Rn[9];
+  mat3_mul(Rx, R, Rn);
+  float Tn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float t = Vm[3 * i] * rho[0] + Vm[3 * i + 1] * rho[1] + Vm[3 * i + 2] * rho[2];
+    Tn[i] = Rx[3 * i] * T[0] + Rx[3 * i + 1] * T[1] + Rx[3 * i + 2] * T[2] + t;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) st[k] = Rn[k];
+  st[9] = Tn[0]; st[10] = Tn[1]; st[11] = Tn[2];
+  const float tn = sqrtf(rho[0] * rho[0] + rho[1] * rho[1] + rho[2] * rho[2] + th[0] * th[0] + th[1] * th[1] +
+                         th[2] * th[2]);
+  st[67] = tn;
+  converged[0] = tn < conv_th ? 1 : 0;
+  pose_camera(Rn, Tn, proj_t, st);
+}
+
 }  // namespace
 }  // namespace wgsr
 
@@ -217,6 +342,23 @@ int wgsr_grad_mask(int H, int W, const float* image, float edge_threshold, float
     hipLaunchKernelGGL(k_grad_block, dim3(32 * 32), dim3(kTBlock), 0, (hipStream_t)stream, H, W, bh, bw,
                        edge_threshold, grad_mask);
   TRKCHK("wgsr_grad_mask");
+  return WGSR_OK;
+}
+
+int wgsr_pose_state_floats(void) { return kPoseState; }
+
+int wgsr_pose_step(float* state, const float* dtau, const float* loss_partials, int n_partials,
+                   const float* projection_matrix, float lr_rot, float lr_trans, float lr_exposure, float beta1,
+                   float beta2, float eps, int step, float converged_threshold, int* converged, int camera_only,
+                   void* stream) {
+  if (!state || !projection_matrix || (!camera_only && (!dtau || !loss_partials || !converged || step < 1)))
+    return set_error(WGSR_EINVAL, "wgsr_pose_step: bad arguments");
+  const double bc1 = camera_only ? 1.0 : 1.0 - pow((double)beta1, step);
+  const double bc2 = camera_only ? 1.0 : 1.0 - pow((double)beta2, step);
+  hipLaunchKernelGGL(k_pose_step, dim3(1), dim3(64), 0, (hipStream_t)stream, state, dtau, loss_partials,
+                     camera_only ? 0 : n_partials, projection_matrix, lr_rot, lr_trans, lr_exposure, beta1, beta2,
+                     eps, (float)bc1, (float)sqrt(bc2), converged_threshold, converged, camera_only);
+  TRKCHK("wgsr_pose_step");
   return WGSR_OK;
 }
 

@@ -140,6 +140,11 @@ def load():
         L.wgsr_track_blocks.argtypes = [c_i64]
         L.wgsr_tracking_loss.restype = c_int
         L.wgsr_tracking_loss.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float] + [_fp] * 3 + [_fp]
+        L.wgsr_pose_state_floats.restype = c_int
+        L.wgsr_pose_state_floats.argtypes = []
+        L.wgsr_pose_step.restype = c_int
+        L.wgsr_pose_step.argtypes = ([_fp] * 3 + [c_int, _fp] + [ctypes.c_float] * 6 + [c_int, ctypes.c_float, _fp,
+                                                                                          c_int, _fp])
         L.wgsr_grad_mask.restype = c_int
         L.wgsr_grad_mask.argtypes = [c_int, c_int, _fp, ctypes.c_float, _fp, _fp]
         L.wgsr_mlp_scratch_bytes.restype = c_sz
@@ -209,6 +214,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_mapping_loss_forward", "wgsr_mapping_loss_backward", "wgsr_densification_stats",
     "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
     "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
+    "wgsr_pose_state_floats", "wgsr_pose_step",
     "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
 )
 
