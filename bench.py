@@ -220,9 +220,9 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": ("configs[2]: 1M Gaussians, 1920x1080, SH3, single-view fwd+bwd, pose grad on"
+            "workload": (f"configs[2]: {P} Gaussians, {W}x{H}, SH{deg}, single-view fwd+bwd, pose grad on"
                          if world == 1 else
-                         f"configs[3]: 1M Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
+                         f"configs[3]: {P} Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
                          "+ the SUM over views of the per-Gaussian gradients on every rank "
                          f"(RCCL, exchange: {exchange})"),
             "gaussians": P, "image": f"{W}x{H}", "sh_degree": deg, "num_rendered": N,
