@@ -25,8 +25,14 @@ struct HostCounters {
   uint32_t* buf = nullptr;
   hipEvent_t ev = nullptr;
 };
+// one pinned block + event per (host thread, device): an event recorded on a
+// stream must belong to that stream's device
+constexpr int kMaxDevices = 64;
 HostCounters& host_counters() {
-  thread_local HostCounters hc;
+  thread_local HostCounters per_dev[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+  HostCounters& hc = per_dev[dev];
   if (!hc.buf) {
     void* p = nullptr;
     if (hipHostMalloc(&p, kCounterBytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
