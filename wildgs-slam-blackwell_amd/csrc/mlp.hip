@@ -181,6 +181,8 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   }
   __syncthreads();
   // dW2[o][i] = sum_r dA2[r][o] h1d[r][i]: transpose so tile_mac's K runs over rows
+  // (head chunk only; the block-uniform branch keeps every barrier matched)
+  if (head) {
   for (int e = t; e < 64 * 64; e += 256) {
     const int r = e >> 6, c = e & 63;
     sT[c][r] = sDA2[r][c];  // sT[o][r]
@@ -195,12 +197,12 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
     __syncthreads();
     float acc[4][4] = {};
     tile_mac_cw<4>(sT, sDA1, ty, tx, acc);  // acc[o][i]
-    if (head)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
+      for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
   }
+  }  // head
   if (head && t < kHid) {
     float s = 0.f;
     for (int r = 0; r < kRows; ++r) s += sDA2[r][t];
@@ -250,12 +252,26 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   }
 }
 
-__global__ __launch_bounds__(256) void k_mlp_reduce(int nblocks, int total, const float* __restrict__ part,
+// two-stage fixed-order sum over the row blocks' partials: grid.y segments of
+// kSeg blocks each write a segment sum (stage 1), then stage 2 adds the
+// segments in order
+constexpr int kSeg = 16;
+__global__ __launch_bounds__(256) void k_mlp_reduce_seg(int nblocks, int total, const float* __restrict__ part,
+                                                        float* __restrict__ seg) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int b0 = blockIdx.y * kSeg, b1 = min(nblocks, b0 + kSeg);
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) s += part[(size_t)b * total + e];
+  seg[(size_t)blockIdx.y * total + e] = s;
+}
+
+__global__ __launch_bounds__(256) void k_mlp_reduce(int nseg, int total, const float* __restrict__ seg,
                                                     float* __restrict__ grad) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * total + e];
+  for (int b = 0; b < nseg; ++b) s += seg[(size_t)b * total + e];
   grad[e] = s;
 }
 
@@ -274,7 +290,8 @@ extern "C" {
 
 size_t wgsr_mlp_scratch_bytes(int N, int C) {
   if (N <= 0 || C <= 0) return 0;
-  return sizeof(float) * (size_t)((N + kRows - 1) / kRows) * (size_t)mlp_partial_floats(C);
+  const size_t nb = (N + kRows - 1) / kRows, nseg = (nb + kSeg - 1) / kSeg;
+  return sizeof(float) * (nb + nseg) * (size_t)mlp_partial_floats(C);  // partials + segment sums
 }
 
 int wgsr_mlp_grad_floats(int C) { return C > 0 ? mlp_partial_floats(C) : 0; }
@@ -309,7 +326,11 @@ int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float
   const int nb = (N + kRows - 1) / kRows;
   hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p, h1d,
                      h2d, o_pre, dL_du, scratch);
-  hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nb, total, scratch,
+  const int nseg = (nb + kSeg - 1) / kSeg;
+  float* seg = scratch + (size_t)nb * total;
+  hipLaunchKernelGGL(k_mlp_reduce_seg, dim3((total + 255) / 256, nseg), dim3(256), 0, (hipStream_t)stream, nb, total,
+                     scratch, seg);
+  hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nseg, total, seg,
                      grad);
   MLPCHK("wgsr_mlp_backward");
   return WGSR_OK;

@@ -216,21 +216,34 @@ __device__ void pose_camera(const float R[9], const float T[3], const float* __r
   for (int j = 0; j < 3; ++j) st[64 + j] = -(T[0] * R[j] + T[1] * R[3 + j] + T[2] * R[6 + j]);
 }
 
-__global__ __launch_bounds__(64) void k_pose_step(float* __restrict__ st, const float* __restrict__ dtau,
+constexpr int kPoseThreads = 1024;
+
+__global__ __launch_bounds__(kPoseThreads) void k_pose_step(float* __restrict__ st, const float* __restrict__ dtau,
                                                   const float* __restrict__ part, int nb,
                                                   const float* __restrict__ proj_t, float lr_rot, float lr_trans,
                                                   float lr_expo, float beta1, float beta2, float eps, float bc1,
                                                   float bc2_sqrt, float conv_th, int* __restrict__ converged,
                                                   int camera_only) {
-  const int lane = threadIdx.x;
+  __shared__ float sred[2][kPoseThreads / 64];
+  const int t = threadIdx.x;
   float ga = 0.f, gb = 0.f;
-  for (int b = lane; b < nb; b += 64) {
+  for (int b = t; b < nb; b += kPoseThreads) {  // exposure gradients: fixed-order sums of the loss partials
     ga += part[3 * b + 1];
     gb += part[3 * b + 2];
   }
   ga = wave_sum(ga);
   gb = wave_sum(gb);
-  if (lane != 0) return;
+  if ((t & 63) == 0) {
+    sred[0][t >> 6] = ga;
+    sred[1][t >> 6] = gb;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  ga = gb = 0.f;
+  for (int w = 0; w < kPoseThreads / 64; ++w) {
+    ga += sred[0][w];
+    gb += sred[1][w];
+  }
   float R[9], T[3];
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = st[k];
@@ -355,7 +368,7 @@ int wgsr_pose_step(float* state, const float* dtau, const float* loss_partials, 
     return set_error(WGSR_EINVAL, "wgsr_pose_step: bad arguments");
   const double bc1 = camera_only ? 1.0 : 1.0 - pow((double)beta1, step);
   const double bc2 = camera_only ? 1.0 : 1.0 - pow((double)beta2, step);
-  hipLaunchKernelGGL(k_pose_step, dim3(1), dim3(64), 0, (hipStream_t)stream, state, dtau, loss_partials,
+  hipLaunchKernelGGL(k_pose_step, dim3(1), dim3(kPoseThreads), 0, (hipStream_t)stream, state, dtau, loss_partials,
                      camera_only ? 0 : n_partials, projection_matrix, lr_rot, lr_trans, lr_exposure, beta1, beta2,
                      eps, (float)bc1, (float)sqrt(bc2), converged_threshold, converged, camera_only);
   TRKCHK("wgsr_pose_step");

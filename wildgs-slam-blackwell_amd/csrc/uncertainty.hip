@@ -323,39 +323,54 @@ __global__ __launch_bounds__(kUBlock) void k_unc_bwd(wgsr_uncer_params prm, cons
 
 // One workgroup: the scalar epilogue of the loss (fixed-order partial sums,
 // the loss value, the SSIM backward's per-plane scale) -- one launch instead
-// of ~15 tiny torch ops per iteration.
-__device__ __forceinline__ float wg_sum(const float* __restrict__ a, int n, int stride, float* sred) {
-  float v = 0.f;
-  for (int i = threadIdx.x; i < n; i += kUBlock) v += a[(size_t)i * stride];
-  return ublock_sum(v, sred);  // thread 0
-}
+// of ~15 tiny torch ops per iteration.  1024 threads read the partial arrays
+// in one strided pass (5 running sums each), then one fixed-order block
+// reduction of all five.
+constexpr int kCombine = 1024;
 
-__global__ __launch_bounds__(kUBlock) void k_unc_combine(int HW, int hw, const float* __restrict__ lpart, int nb,
-                                                         const float* __restrict__ upart, int nbs,
-                                                         const float* __restrict__ ssim_mean,
-                                                         const float* __restrict__ extra, int nextra, float w_extra,
-                                                         float alpha, float lam, float ssim_mult, int ssim_loss,
-                                                         float* __restrict__ loss, float* __restrict__ sums,
-                                                         float* __restrict__ ssim_scale) {
-  __shared__ float sred[kUBlock / 64];
-  const float s0 = wg_sum(lpart, nb, 3, sred);
-  const float s1 = wg_sum(lpart + 1, nb, 3, sred);
-  const float s2 = wg_sum(lpart + 2, nb, 3, sred);
-  const float u = wg_sum(upart, nbs, 1, sred);
-  const float x = extra ? wg_sum(extra, nextra, 1, sred) : 0.f;
-  if (threadIdx.x == 0) {
-    const float n3 = 3.f * (float)HW;
-    const float rgb = ssim_loss ? ((1.f - lam) * s0 + 3.f * lam * (1.f - ssim_mean[0]) * s1) / n3 : s0 / n3;
-    loss[0] = alpha * rgb + (1.f - alpha) * s2 / (float)HW + ssim_mult * (u / (float)hw) + w_extra * x;
-    sums[0] = s0;
-    sums[1] = s1;
-    sums[2] = s2;
-    // dL/dS per pixel of the SSIM map: -alpha lambda (sum w) / HW / (3 HW)
-    const float sc = s1 * (-alpha * lam / ((float)HW * n3));
-    ssim_scale[0] = sc;
-    ssim_scale[1] = sc;
-    ssim_scale[2] = sc;
+__global__ __launch_bounds__(kCombine) void k_unc_combine(int HW, int hw, const float* __restrict__ lpart, int nb,
+                                                          const float* __restrict__ upart, int nbs,
+                                                          const float* __restrict__ ssim_mean,
+                                                          const float* __restrict__ extra, int nextra, float w_extra,
+                                                          float alpha, float lam, float ssim_mult, int ssim_loss,
+                                                          float* __restrict__ loss, float* __restrict__ sums,
+                                                          float* __restrict__ ssim_scale) {
+  __shared__ float sred[5][kCombine / 64];
+  const int t = threadIdx.x;
+  float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = t; i < nb; i += kCombine) {
+    v[0] += lpart[3 * i];
+    v[1] += lpart[3 * i + 1];
+    v[2] += lpart[3 * i + 2];
   }
+  for (int i = t; i < nbs; i += kCombine) v[3] += upart[i];
+  if (extra)
+    for (int i = t; i < nextra; i += kCombine) v[4] += extra[i];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    v[k] = wave_sum(v[k]);
+    if ((t & 63) == 0) sred[k][t >> 6] = v[k];
+  }
+  __syncthreads();
+  if (t != 0) return;
+  float r[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    r[k] = 0.f;
+    for (int w = 0; w < kCombine / 64; ++w) r[k] += sred[k][w];
+  }
+  const float s0 = r[0], s1 = r[1], s2 = r[2], u = r[3], x = r[4];
+  const float n3 = 3.f * (float)HW;
+  const float rgb = ssim_loss ? ((1.f - lam) * s0 + 3.f * lam * (1.f - ssim_mean[0]) * s1) / n3 : s0 / n3;
+  loss[0] = alpha * rgb + (1.f - alpha) * s2 / (float)HW + ssim_mult * (u / (float)hw) + w_extra * x;
+  sums[0] = s0;
+  sums[1] = s1;
+  sums[2] = s2;
+  // dL/dS per pixel of the SSIM map: -alpha lambda (sum w) / HW / (3 HW)
+  const float sc = s1 * (-alpha * lam / ((float)HW * n3));
+  ssim_scale[0] = sc;
+  ssim_scale[1] = sc;
+  ssim_scale[2] = sc;
 }
 
 int ublocks(int64_t n) { return n > 0 ? (int)((n + kUBlock - 1) / kUBlock) : 0; }
@@ -437,7 +452,7 @@ int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials,
   if (!partials || !small_partials || !loss || !sums || !ssim_scale || (ssim_loss && !ssim_mean) ||
       (n_extra > 0 && !extra_partials))
     return set_error(WGSR_EINVAL, "wgsr_uncer_loss_combine: null pointer");
-  hipLaunchKernelGGL(k_unc_combine, dim3(1), dim3(kUBlock), 0, (hipStream_t)stream, prm->H * prm->W,
+  hipLaunchKernelGGL(k_unc_combine, dim3(1), dim3(kCombine), 0, (hipStream_t)stream, prm->H * prm->W,
                      prm->h * prm->w, partials, ublocks((int64_t)prm->H * prm->W), small_partials,
                      ublocks((int64_t)prm->h * prm->w), ssim_mean, n_extra > 0 ? extra_partials : nullptr, n_extra,
                      extra_weight, alpha, lambda_dssim, ssim_mult, ssim_loss, loss, sums, ssim_scale);
