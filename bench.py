@@ -16,9 +16,11 @@ always computed) at 1920x1080, all inputs resident in HBM before timing.
   (wgsr.dp.ViewShardedBackward): each view's 12-float screen-space record of
   every Gaussian goes to the Gaussian's owner rank (RCCL all-to-all), owners
   run the camera-side backward of all N views for their 1/N shard, and the
-  shards are all-gathered -- 71 instead of 118 floats per Gaussian per rank
-  at N = 8 (``--dp-exchange allreduce``: the plain RCCL all-reduce).  Weak
-  scaling; value = P * N * K / max_rank(t).
+  shards are all-gathered.  Only rows with a non-zero record / gradient
+  travel (exactly the same sums: the other rows are zero), ~10 % of the
+  Gaussians in this scene; ``--dp-exchange views-dense`` moves every row (71
+  instead of 118 floats per Gaussian per rank at N = 8) and ``allreduce`` runs
+  the plain RCCL all-reduce.  Weak scaling; value = P * N * K / max_rank(t).
 
 Extra fields: ``roofline`` for the dominant kernel (stage times from HIP
 events recorded on the launch stream inside the timed region; algorithmic
@@ -119,10 +121,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the stage timers")
     ap.add_argument("--no-knn", action="store_true", help="skip the distCUDA2 measurement (rocprof runs)")
-    ap.add_argument("--dp-exchange", choices=("views", "allreduce"), default=None,
+    ap.add_argument("--dp-exchange", choices=("views", "views-dense", "allreduce"), default=None,
                     help="N > 1 gradient exchange: 'views' (default: screen-space records to the "
-                         "Gaussians' owners, owner-computed shards all-gathered; wgsr.dp."
-                         "ViewShardedBackward) or 'allreduce' (59-float gradient all-reduce). "
+                         "Gaussians' owners, owner-computed shards all-gathered, only rows with "
+                         "non-zero gradient moved; wgsr.dp.ViewShardedBackward), 'views-dense' (the "
+                         "same with every row moved) or 'allreduce' (59-float gradient all-reduce). "
                          "Giving it at N = 1 runs that path on one GPU.")
     args = ap.parse_args()
 
@@ -166,7 +169,8 @@ def main():
     tanx, tany = f["tanfovx"], f["tanfovy"]
     gbuf = GradBuffer.allocate(P, M, dev)
     exchange = args.dp_exchange or ("views" if world > 1 else None)
-    vsb = ViewShardedBackward(P, M, dev) if exchange == "views" else None
+    vsb = (ViewShardedBackward(P, M, dev, sparse=(exchange == "views"))
+           if exchange in ("views", "views-dense") else None)
     camd = dict(viewmatrix=view, projmatrix=proj, projmatrix_raw=praw, campos=campos, tanfovx=tanx,
                 tanfovy=tany, bg=bg)
     state = {}
@@ -231,9 +235,16 @@ def main():
             "exchange_bytes_per_rank_per_step": (
                 0 if world == 1 else
                 int(2 * (world - 1) / world * gbuf.flat.numel() * 4) if exchange == "allreduce" else
+                vsb.last_exchange["bytes_in"] if vsb.last_exchange is not None else
                 int((world - 1) / world * vsb.P_pad * (12 + gbuf.floats_per_gaussian) * 4)),
         },
     }
+
+    if vsb is not None and vsb.last_exchange is not None:
+        out["config"]["sparse_exchange"] = {
+            "record_rows_in": vsb.last_exchange["record_rows_in"],
+            "grad_rows_per_owner": vsb.last_exchange["grad_rows_per_owner"],
+            "note": "rows of Gaussians with zero gradient in every view are exactly zero and stay home"}
 
     if prof:
         stages = prof.stages

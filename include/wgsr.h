@@ -151,6 +151,48 @@ int wgsr_gauss_backward_views(const wgsr_raster_args* params, int lo, int hi, in
                               float* dL_dopacity, float* dL_dscales, float* dL_drotations,
                               float* tau_partials, float* stats, void* stream);
 
+/* ---- sparse view-sharded exchange (csrc/dp_sparse.hip, wgsr/dp.py) ----
+ * Most visible Gaussians get no gradient from a view (their pixels saturate
+ * before them), so ranks move only rows with a non-zero record / gradient.
+ * No reference counterpart: this replaces the dense exchange behind
+ * ViewShardedBackward, which stands in for the reference's per-view
+ * optimiser.step() accumulation (mapper.py:1089-1219). */
+
+/* Floats per packed gradient row: index, dL/dmeans3D (3), dL/dsh (3M),
+ * dL/dopacity, dL/dscales (3), dL/drotations (4). */
+int wgsr_sparse_grad_row_floats(int M);
+
+/* records [P_pad, 12] of one view -> per owner o (segment [o S, (o+1) S)),
+ * the rows with a non-zero partial sum compacted to packed + o S * 12, field
+ * 10 replaced by the row's index inside the segment (uint32 bits).
+ * counts[P_pad / S] (zeroed by the caller) receive the rows per owner.
+ * Row order inside a segment is unspecified. */
+int wgsr_sparse_pack_records(const float* records, int64_t P_pad, int64_t S, uint32_t* counts,
+                             float* packed, void* stream);
+
+/* Owner side: received [n_views][S][12] (view v's counts[v] packed rows at
+ * v S) scattered into records [n_views][S][12] (zeroed by the caller) and
+ * mask[S] (zeroed) set for every received row.  keep_radius: keep the
+ * radius field already in `records` (wgsr_sparse_fill_radius), else 1. */
+int wgsr_sparse_unpack_records(const float* received, const uint32_t* counts, int n_views, int64_t S,
+                               int keep_radius, float* records, uint8_t* mask, void* stream);
+
+/* records[j].radius = radii[j] for j < n (rows of WGSR_VIEW_RECORD_FLOATS). */
+int wgsr_sparse_fill_radius(const float* radii, int64_t n, float* records, void* stream);
+
+/* Gradient rows [lo, hi) whose mask[i - lo] is set -> packed rows of
+ * wgsr_sparse_grad_row_floats(M) floats; *count (zeroed) = rows written. */
+int wgsr_sparse_pack_grads(int64_t lo, int64_t hi, int M, const uint8_t* mask, const float* dL_dmeans3D,
+                           const float* dL_dsh, const float* dL_dopacity, const float* dL_dscales,
+                           const float* dL_drotations, uint32_t* count, float* packed, void* stream);
+
+/* gathered [world][cap][row floats]: owner r's counts[r] rows, indices into
+ * shard r (rows r S + index).  Scatters every owner's rows except `rank`'s
+ * into the [P, ...] gradient tensors (zeroed by the caller). */
+int wgsr_sparse_unpack_grads(const float* gathered, const uint32_t* counts, int world, int rank, int64_t cap,
+                             int64_t S, int64_t P, int M, float* dL_dmeans3D, float* dL_dsh,
+                             float* dL_dopacity, float* dL_dscales, float* dL_drotations, void* stream);
+
 /* ---- the mapping iteration around the path ----
  * src/mapper.py:1083-1219 per iteration, as fused launches (csrc/mapping.hip;
  * driven by wgsr/mapping.py).  Partial sums are one float (or float pair) per

@@ -132,6 +132,11 @@ def _mock_rec(view, P_pad):
     k = torch.arange(12, dtype=torch.float32)[None, :]
     r = torch.sin(i * 1.3 + k * 0.7 + view * 2.1)
     r[:, 10] = ((torch.arange(P_pad) + view) % 3).float()  # radius 0 -> not visible
+    # visible but no gradient (every pixel saturated before it): an all-zero
+    # record apart from the radius -- the rows the sparse exchange skips
+    quiet = (torch.arange(P_pad) + view) % 4 == 0
+    r[quiet, :10] = 0
+    r[quiet, 11] = 0
     r[VP:] = 0
     return r
 
@@ -151,6 +156,8 @@ class _MockKernels:
         n = hi - lo
         for name, t in grads.items():
             t[lo:hi] = 0
+        if stats_out is not None:
+            stats_out.zero_()  # the kernel writes the statistics, it does not accumulate
         for v in range(cams.size(0)):
             r = recs[v, :n]
             s = cams[v, 0] + 1
@@ -169,6 +176,55 @@ class _MockKernels:
                 stats_out[:, 0] += torch.where(vis, r[:, 0:2].norm(dim=1), torch.zeros(()))
                 stats_out[:, 1] += vis.float()
                 stats_out[:, 2] = torch.maximum(stats_out[:, 2], r[:, 10])
+
+
+    # sparse exchange stand-ins (csrc/dp_sparse.hip semantics; packed rows
+    # in reverse order: the device order is unspecified)
+    def grad_row_floats(self, M):
+        return 12 + 3 * M
+
+    def sparse_pack_records(self, send, S, counts, packed):
+        for o in range(send.size(0) // S):
+            seg = send[o * S:(o + 1) * S]
+            idx = (seg[:, :10] != 0).any(1).nonzero().flatten()
+            rows = seg[idx].clone()
+            rows[:, 10] = idx.to(torch.int32).view(torch.float32)
+            packed[o * S:o * S + idx.numel()] = rows.flip(0)
+            counts[o] = idx.numel()
+
+    def sparse_unpack_records(self, recvp, counts, S, keep_radius, recv, mask):
+        for v in range(recv.size(0)):
+            rows = recvp[v, :int(counts[v])]
+            idx = rows[:, 10].contiguous().view(torch.int32).long()
+            rad = recv[v, idx, 10].clone() if keep_radius else torch.ones(idx.numel())
+            recv[v, idx] = rows
+            recv[v, idx, 10] = rad
+            mask[idx] = 1
+
+    def sparse_fill_radius(self, radii, recv):
+        recv[:, 10] = radii
+
+    def sparse_pack_grads(self, grads, lo, hi, mask, count, packed):
+        n = hi - lo
+        idx = mask[:n].nonzero().flatten()
+        rows = torch.cat([grads["means3D"][lo:hi], grads["shs"][lo:hi].reshape(n, -1), grads["opacities"][lo:hi],
+                          grads["scales"][lo:hi], grads["rotations"][lo:hi]], 1)[idx].flip(0)
+        packed[:idx.numel(), 0] = idx.flip(0).to(torch.int32).view(torch.float32)
+        packed[:idx.numel(), 1:] = rows
+        count[0] = idx.numel()
+
+    def sparse_unpack_grads(self, gathered, counts, rank, cap, S, P, grads):
+        M = grads["shs"].size(1)
+        for r in range(counts.numel()):
+            if r == rank:
+                continue
+            rows = gathered[r, :int(counts[r])]
+            i = r * S + rows[:, 0].contiguous().view(torch.int32).long()
+            grads["means3D"][i] = rows[:, 1:4]
+            grads["shs"][i] = rows[:, 4:4 + 3 * M].reshape(-1, M, 3)
+            grads["opacities"][i] = rows[:, 4 + 3 * M:5 + 3 * M]
+            grads["scales"][i] = rows[:, 5 + 3 * M:8 + 3 * M]
+            grads["rotations"][i] = rows[:, 8 + 3 * M:12 + 3 * M]
 
 
 def _mock_expected():
@@ -192,7 +248,7 @@ def _mock_expected():
     return out, taus, st
 
 
-def _vsb_worker(rank, port, out_dir):
+def _vsb_worker(rank, port, out_dir, sparse=True):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     for p in (os.path.join(root, "wildgs-slam-blackwell_amd", "python"), root):
@@ -200,19 +256,25 @@ def _vsb_worker(rank, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=VWORLD)
     from wgsr.dp import ViewShardedBackward
-    vsb = ViewShardedBackward(VP, VM, "cpu", stats=True, kernels=_MockKernels())
+    vsb = ViewShardedBackward(VP, VM, "cpu", stats=True, kernels=_MockKernels(), sparse=sparse)
+    assert vsb.sparse == sparse
     assert vsb.P_pad == 39 and vsb.S == 13
     e = torch.zeros(3, 4, 5)
     fwd = (torch.zeros(VP, 3), None, None, None, 0, {"id": rank})
-    grads, tau, stats = vsb.backward(fwd, e, e[:1])
+    for _ in range(2):  # repeated steps reuse (and must re-zero) the buffers
+        grads, tau, stats = vsb.backward(fwd, e, e[:1])
+    if sparse:
+        # rows with a non-zero record only: a quarter of the visible rows stay home
+        assert 0 < vsb.last_exchange["record_rows_in"] < (VWORLD - 1) * vsb.S
     torch.save({"grads": {k: v.clone() for k, v in grads.items()}, "tau": tau.clone(), "stats": stats.clone()},
                os.path.join(out_dir, f"vsb{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_view_sharded_exchange_routes_records_to_owners(tmp_path):
-    mp.spawn(_vsb_worker, args=(_free_port(), str(tmp_path)), nprocs=VWORLD, join=True)
+@pytest.mark.parametrize("sparse", [True, False])
+def test_view_sharded_exchange_routes_records_to_owners(tmp_path, sparse):
+    mp.spawn(_vsb_worker, args=(_free_port(), str(tmp_path), sparse), nprocs=VWORLD, join=True)
     exp, taus, st = _mock_expected()
     for r in range(VWORLD):
         o = torch.load(tmp_path / f"vsb{r}.pt", weights_only=True)

@@ -148,7 +148,7 @@ def _free_port():
     return port
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_main(rank, world, port, out_dir, sparse=True):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     for p in (os.path.join(root, "wildgs-slam-blackwell_amd", "python"), root):
@@ -163,7 +163,7 @@ def _rank_main(rank, world, port, out_dir):
     params, views = _setup(dev, nviews=world, P_=P + 1)  # P + 1: ragged shards
     cam, gc, gd = views[rank]
     nr, color, radii, geom, binning, img, depth, opac, nt = _forward(params, cam)
-    vsb = ViewShardedBackward(P + 1, (DEG + 1) ** 2, dev, stats=True)
+    vsb = ViewShardedBackward(P + 1, (DEG + 1) ** 2, dev, stats=True, sparse=sparse)
     fwd = (params["means3D"], params["scales"], params["rotations"], params["shs"], DEG, cam, nr, radii, geom,
            binning, img)
     for _ in range(2):  # repeated steps reuse the buffers
@@ -175,10 +175,11 @@ def _rank_main(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_two_ranks_gloo_match_sum_of_views(tmp_path):
+@pytest.mark.parametrize("sparse", [True, False])
+def test_two_ranks_gloo_match_sum_of_views(tmp_path, sparse):
     import torch.multiprocessing as mp
     world = 2
-    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path), sparse), nprocs=world, join=True)
     dev = torch.device("cuda:0")
     params, views = _setup(dev, nviews=world, P_=P + 1)
     ref, taus, (rn, rc, rr) = _reference(params, views)
@@ -190,3 +191,72 @@ def test_two_ranks_gloo_match_sum_of_views(tmp_path):
         assert _rel(o["tau"], taus[r]) <= 1e-4
         assert _rel(o["stats"][:, 0], rn) <= 1e-6
         assert torch.equal(o["stats"][:, 1], rc.cpu()) and torch.equal(o["stats"][:, 2], rr.cpu())
+
+
+@pytest.mark.parametrize("world,S", [(3, 1000), (4, 777), (1, 64)])
+def test_sparse_record_and_gradient_round_trip(world, S):
+    """csrc/dp_sparse.hip: records packed per owner and scattered back equal
+    the dense records of the non-zero rows (radius kept or set to 1), the
+    mask is their union, and packed gradient rows land at their indices."""
+    from wgsr.dp import GradBuffer, _HipViewKernels
+    dev = torch.device("cuda:0")
+    k = _HipViewKernels()
+    g = torch.Generator().manual_seed(7)
+    P_pad = world * S
+    views = []
+    for v in range(world):
+        r = torch.randn(P_pad, 12, generator=g)
+        quiet = torch.rand(P_pad, generator=g) < 0.8  # most rows carry no gradient
+        r[quiet, :10] = 0
+        r[:, 10] = torch.randint(0, 5, (P_pad,), generator=g).float()
+        views.append(r.to(dev))
+    for keep_radius in (False, True):
+        for owner in range(world):
+            recvp = torch.zeros(world, S, 12, device=dev)
+            counts = torch.zeros(world, dtype=torch.int32, device=dev)
+            for v, r in enumerate(views):
+                c = torch.zeros(world, dtype=torch.int32, device=dev)
+                packed = torch.full((P_pad, 12), float("nan"), device=dev)
+                k.sparse_pack_records(r, S, c, packed)
+                n = int(c[owner])
+                recvp[v, :n] = packed[owner * S:owner * S + n]
+                counts[v] = n
+                seg = r[owner * S:(owner + 1) * S]
+                assert n == int((seg[:, :10] != 0).any(1).sum())
+            dense = torch.zeros(world, S, 12, device=dev)
+            if keep_radius:
+                k.sparse_fill_radius(torch.stack([r[owner * S:(owner + 1) * S, 10] for r in views]).reshape(-1),
+                                     dense.view(-1, 12))
+            mask = torch.zeros(S, dtype=torch.uint8, device=dev)
+            k.sparse_unpack_records(recvp, counts, S, keep_radius, dense, mask)
+            union = torch.zeros(S, dtype=torch.bool, device=dev)
+            for v, r in enumerate(views):
+                seg = r[owner * S:(owner + 1) * S]
+                nz = (seg[:, :10] != 0).any(1)
+                union |= nz
+                exp = torch.where(nz[:, None], seg, torch.zeros_like(seg))
+                exp[:, 10] = seg[:, 10] if keep_radius else nz.float()
+                assert torch.equal(dense[v], exp), (owner, v, keep_radius)
+            assert torch.equal(mask.bool(), union)
+    # gradient rows: every owner packs its masked rows, rank 0 unpacks the others
+    M = 16
+    src = GradBuffer.allocate(P_pad, M, dev)
+    src.flat.copy_(torch.randn(src.flat.numel(), generator=g).to(dev))
+    F = k.grad_row_floats(M)
+    assert F == 12 + 3 * M
+    masks = [(torch.rand(S, generator=g) < 0.3).to(torch.uint8).to(dev) for _ in range(world)]
+    counts = torch.zeros(world, dtype=torch.int32, device=dev)
+    gathered = torch.full((world, S, F), float("nan"), device=dev)
+    for r in range(world):
+        c = torch.zeros(1, dtype=torch.int32, device=dev)
+        k.sparse_pack_grads(src.views, r * S, (r + 1) * S, masks[r], c, gathered[r])
+        counts[r] = c[0]
+        assert int(c[0]) == int(masks[r].sum())
+    dst = GradBuffer.allocate(P_pad, M, dev)
+    dst.flat.zero_()
+    k.sparse_unpack_grads(gathered, counts, 0, S, S, P_pad, dst.views)
+    keep = torch.cat([torch.zeros(S, dtype=torch.bool, device=dev)] + [m.bool() for m in masks[1:]])
+    for name in src.views:
+        exp = src.views[name].clone()
+        exp[~keep] = 0
+        assert torch.equal(dst.views[name], exp), name

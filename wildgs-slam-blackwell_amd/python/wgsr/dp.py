@@ -190,6 +190,44 @@ class _HipViewKernels:
         _lib.check(code)
 
 
+    # ---- sparse exchange (csrc/dp_sparse.hip) ----
+    def grad_row_floats(self, M):
+        from wgsr import _lib
+        return int(_lib.load().wgsr_sparse_grad_row_floats(int(M)))
+
+    def sparse_pack_records(self, send, S, counts, packed):
+        from wgsr import _lib
+        _lib.check(_lib.load().wgsr_sparse_pack_records(send.data_ptr(), send.size(0), int(S), counts.data_ptr(),
+                                                        packed.data_ptr(), _lib.stream_handle(send.device)))
+
+    def sparse_unpack_records(self, recvp, counts, S, keep_radius, recv, mask):
+        from wgsr import _lib
+        _lib.check(_lib.load().wgsr_sparse_unpack_records(recvp.data_ptr(), counts.data_ptr(), recv.size(0), int(S),
+                                                          int(keep_radius), recv.data_ptr(), mask.data_ptr(),
+                                                          _lib.stream_handle(recv.device)))
+
+    def sparse_fill_radius(self, radii, recv):
+        from wgsr import _lib
+        _lib.check(_lib.load().wgsr_sparse_fill_radius(radii.data_ptr(), radii.numel(), recv.data_ptr(),
+                                                       _lib.stream_handle(recv.device)))
+
+    def sparse_pack_grads(self, grads, lo, hi, mask, count, packed):
+        from wgsr import _lib
+        M = grads["shs"].size(1)
+        _lib.check(_lib.load().wgsr_sparse_pack_grads(
+            int(lo), int(hi), int(M), mask.data_ptr(), grads["means3D"].data_ptr(), grads["shs"].data_ptr(),
+            grads["opacities"].data_ptr(), grads["scales"].data_ptr(), grads["rotations"].data_ptr(),
+            count.data_ptr(), packed.data_ptr(), _lib.stream_handle(packed.device)))
+
+    def sparse_unpack_grads(self, gathered, counts, rank, cap, S, P, grads):
+        from wgsr import _lib
+        M = grads["shs"].size(1)
+        _lib.check(_lib.load().wgsr_sparse_unpack_grads(
+            gathered.data_ptr(), counts.data_ptr(), counts.numel(), int(rank), int(cap), int(S), int(P), int(M),
+            grads["means3D"].data_ptr(), grads["shs"].data_ptr(), grads["opacities"].data_ptr(),
+            grads["scales"].data_ptr(), grads["rotations"].data_ptr(), _lib.stream_handle(gathered.device)))
+
+
 def _gloo_cuda(group):
     """gloo has no device collectives for every op: stage device tensors
     through host memory (test rigs only -- RCCL is the product backend)."""
@@ -227,28 +265,53 @@ def _all_gather_inplace(full, rank, group):
                                        async_op=True)
 
 
-def _all_gather_inplace_many(fulls, rank, group):
-    """In-place all-gathers of several [world * S, ...] buffers (each rank's
-    block holds its shard) as ONE coalesced collective: RCCL runs the group
-    as a single launch, so the small buffers ride along with the SH block
-    instead of paying a collective's latency each."""
-    if any(_gloo_cuda(group) and f.is_cuda for f in fulls):
-        for f in fulls:
-            _all_gather_inplace(f, rank, group)
+def _all_to_all_var(outs, ins, group):
+    """outs[v] <- rank v's ins[me]: uneven row blocks, one collective."""
+    if dist.get_backend(group) == "gloo":  # test rigs: one alltoallv through host memory
+        flat = [t.reshape(t.size(0), -1) for t in ins]
+        inp = torch.cat(flat).cpu()
+        out = torch.empty((sum(o.size(0) for o in outs),) + tuple(inp.shape[1:]), dtype=inp.dtype)
+        dist.all_to_all_single(out, inp, output_split_sizes=[o.size(0) for o in outs],
+                               input_split_sizes=[t.size(0) for t in ins], group=group)
+        off = 0
+        for o in outs:
+            n = o.size(0)
+            o.copy_(out[off:off + n].view_as(o))
+            off += n
         return None
-    world = dist.get_world_size(group)
+    return dist.all_to_all(outs, ins, group=group, async_op=True)
+
+
+def _all_gather_many(pairs, group):
+    """all_gather_into_tensor of several (out_flat, in_flat) pairs as ONE
+    coalesced RCCL group (a single grouped launch, one collective latency)."""
+    if any(_gloo_cuda(group) and i.is_cuda for _, i in pairs):
+        for o, i in pairs:
+            _all_gather_into(o, i, group)
+        return None
     try:
         with dist._coalescing_manager(group, async_ops=True) as cm:
-            for f in fulls:
-                S = f.size(0) // world
-                dist.all_gather_into_tensor(f.view(-1), f[rank * S:(rank + 1) * S].view(-1), group=group)
+            for o, i in pairs:
+                dist.all_gather_into_tensor(o, i, group=group)
         return cm
     except (RuntimeError, AttributeError, NotImplementedError):
         # a backend / torch build without the coalesced fast path: every rank
         # takes this branch alike (same code, same backend), so the collectives
         # still pair up -- one gather per buffer
-        works = [_all_gather_inplace(f, rank, group) for f in fulls]
-        return _WaitAll(works)
+        return _WaitAll([_all_gather_into(o, i, group) for o, i in pairs])
+
+
+def _all_gather_inplace_many(fulls, rank, group):
+    """In-place all-gathers of several [world * S, ...] buffers (each rank's
+    block holds its shard) as ONE coalesced collective: RCCL runs the group
+    as a single launch, so the small buffers ride along with the SH block
+    instead of paying a collective's latency each."""
+    world = dist.get_world_size(group)
+    pairs = []
+    for f in fulls:
+        S = f.size(0) // world
+        pairs.append((f.view(-1), f[rank * S:(rank + 1) * S].view(-1)))
+    return _all_gather_many(pairs, group)
 
 
 class _WaitAll:
@@ -274,7 +337,7 @@ class ViewShardedBackward:
     Gaussians are sharded by index: rank s owns [s S, (s+1) S), S = ceil(P/N).
     """
 
-    def __init__(self, P: int, M: int, device, group=None, stats: bool = False, kernels=None):
+    def __init__(self, P: int, M: int, device, group=None, stats: bool = False, kernels=None, sparse: bool = True):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -300,6 +363,23 @@ class ViewShardedBackward:
         self.tau_own = torch.zeros(self.world, self.world, 6, **f32)
         self.tau = torch.zeros(self.world, 6, **f32)
         self.stats = torch.zeros(self.P_pad, 3, **f32) if stats else None
+        # sparse exchange (N > 1): only rows with a non-zero record / gradient
+        # travel (csrc/dp_sparse.hip); `last_exchange` reports what moved
+        self.sparse = bool(sparse) and self.world > 1
+        self.last_exchange = None
+        if self.sparse:
+            i32 = dict(dtype=torch.int32, device=dev)
+            self.F = self.k.grad_row_floats(M)
+            self.packed = torch.empty(self.P_pad, 12, **f32)
+            self.recvp = torch.empty(self.P_pad, 12, **f32)
+            self.mask = torch.zeros(self.S, dtype=torch.uint8, device=dev)
+            self.cbuf = torch.zeros(2, self.world, **i32)  # [rows sent to each owner, rows got from each view]
+            self.gcount = torch.zeros(1, **i32)
+            self.gcounts = torch.zeros(self.world, **i32)
+            self.gpack = torch.empty(self.S, self.F, **f32)
+            if stats:
+                self.rad_send = torch.empty(self.P_pad, **f32)
+                self.rad_recv = torch.empty(self.P_pad, **f32)
 
     def backward(self, fwd, dL_dcolor, dL_ddepth, scale_modifier: float = 1.0):
         """fwd = (means3D, scales, rotations, shs, D, cam, num_rendered, radii,
@@ -307,6 +387,8 @@ class ViewShardedBackward:
         camera tensors/scalars (viewmatrix, projmatrix, projmatrix_raw,
         campos, tanfovx, tanfovy, bg).  -> (grads dict, tau [6] of this
         rank's view, stats [P, 3] or None)."""
+        if self.sparse:
+            return self._backward_sparse(fwd, dL_dcolor, dL_ddepth, scale_modifier)
         means3D, scales, rotations, shs, D, cam = fwd[:6]
         H, W = dL_dcolor.size(1), dL_dcolor.size(2)
         g = self.group
@@ -347,3 +429,83 @@ class ViewShardedBackward:
         torch.sum(self.tau_own, dim=0, out=self.tau)
         stats = self.stats[:self.P] if self.stats is not None else None
         return self.grads, self.tau[self.rank], stats
+
+    def _backward_sparse(self, fwd, dL_dcolor, dL_ddepth, scale_modifier):
+        """The same result as the dense exchange, moving only non-zero rows:
+        each view's records with a non-zero partial sum go to their owners
+        (uneven all-to-all), and each owner gathers only the gradient rows of
+        Gaussians some view gave gradient to (padded to the largest owner's
+        count).  Two host reads of row counts per step size the collectives."""
+        means3D, scales, rotations, shs, D, cam = fwd[:6]
+        H, W = dL_dcolor.size(1), dL_dcolor.size(2)
+        g, S, world, rank = self.group, self.S, self.world, self.rank
+        self.k.pack_camera(cam, W, H, self.cam_row)
+        w_cam = _all_gather_into(self.cams.view(-1), self.cam_row, g)
+        self.k.records(fwd, dL_dcolor, dL_ddepth, self.P_pad, self.send)
+        cb = self.cbuf
+        cb.zero_()
+        self.k.sparse_pack_records(self.send, S, cb[0], self.packed)
+        w_rad = None
+        if self.stats is not None:  # the statistics need every visible Gaussian's radius
+            self.rad_send.copy_(self.send[:, 10])
+            w_rad = _all_to_all_equal(self.rad_recv, self.rad_send, g)
+        w = _all_to_all_equal(cb[1], cb[0], g)
+        if w is not None:
+            w.wait()
+        sent, got = cb.tolist()  # host read 1: the row counts
+        ins = [self.packed[o * S:o * S + sent[o]] for o in range(world)]
+        outs = [self.recvp[v * S:v * S + got[v]] for v in range(world)]
+        w = _all_to_all_var(outs, ins, g)
+        self.recv.zero_()
+        self.mask.zero_()
+        if self.stats is not None:
+            if w_rad is not None:
+                w_rad.wait()
+            self.k.sparse_fill_radius(self.rad_recv, self.recv.view(-1, 12))
+        if w is not None:
+            w.wait()
+        self.k.sparse_unpack_records(self.recvp.view(world, S, 12), cb[1], S, self.stats is not None, self.recv,
+                                     self.mask)
+        if w_cam is not None:
+            w_cam.wait()
+        # rows no owner writes stay zero: the sparse gather leaves them alone
+        self.buf.flat.zero_()
+        st = self.stats[self.lo:self.hi] if self.stats is not None else None
+        self.k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
+                           self.recv, self.buf.views, self.tau_blk if self.hi > self.lo else None, st)
+        mine = self.tau_own[rank]
+        if self.hi > self.lo:
+            torch.sum(self.tau_blk, dim=0, out=mine)
+        else:
+            mine.zero_()
+        self.gcount.zero_()
+        self.k.sparse_pack_grads(self.buf.views, self.lo, self.hi, self.mask, self.gcount, self.gpack)
+        w = _all_gather_into(self.gcounts, self.gcount, g)
+        if w is not None:
+            w.wait()
+        counts = self.gcounts.tolist()  # host read 2: gradient rows per owner
+        cap = max(counts)
+        pairs = []
+        gathered = None
+        if cap > 0:
+            gathered = torch.empty(world * cap * self.F, dtype=torch.float32, device=self.gpack.device)
+            pairs.append((gathered, self.gpack[:cap].reshape(-1)))
+        fulls = ([self.stats] if self.stats is not None else []) + [self.tau_own]
+        for f in fulls:
+            n = f.size(0) // world
+            pairs.append((f.view(-1), f[rank * n:(rank + 1) * n].reshape(-1)))
+        w = _all_gather_many(pairs, g)
+        if w is not None:
+            w.wait()
+        if gathered is not None:
+            self.k.sparse_unpack_grads(gathered.view(world, cap, self.F), self.gcounts, rank, cap, S, self.P,
+                                       self.buf.views)
+        torch.sum(self.tau_own, dim=0, out=self.tau)
+        others = sum(got) - got[rank]
+        self.last_exchange = {
+            "record_rows_in": others, "grad_rows_per_owner": counts, "grad_rows_cap": cap,
+            "bytes_in": int(others * 48 + (world - 1) * cap * self.F * 4 +
+                            ((world - 1) * S * 16 if self.stats is not None else 0) + (world - 1) * world * 24),
+        }
+        stats = self.stats[:self.P] if self.stats is not None else None
+        return self.grads, self.tau[rank], stats
