@@ -675,11 +675,13 @@ __device__ __forceinline__ void cov_to_scale_rot(float4 q, f3 sv, float scale_mo
 __device__ __forceinline__ void gauss_bwd_one(
     int i, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ clamped, const float g[10],
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
-    const float* __restrict__ cov_pre, float* shrow, float scale_mod,
+    const float* __restrict__ cov_pre, float* shrow, f3 dm_sh, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
     const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
     float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
     float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  // dm_sh: the SH term of dL/dmean when the caller ran sh_backward itself
+  // (shrow null); zero otherwise.
   const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
   if (!(radii[i] > 0)) {
     for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
@@ -712,7 +714,7 @@ __device__ __forceinline__ void gauss_bwd_one(
   cam_backward(c, praw[0], praw[5], praw[11], mean, cv, g, cb);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o_cov[i6 + k] = cb.ocov[k];
-  f3 dm = cb.dm;
+  f3 dm = add3(cb.dm, dm_sh);
   const f3 tau_rho = cb.rho, tau_theta = cb.theta;
   if (shrow) {
     const f3 dmsh = sh_backward(D, M, shrow, mean, mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i],
@@ -735,7 +737,13 @@ __device__ __forceinline__ void gauss_bwd_one(
 // coefficients are read and dL/dsh written as coalesced 256-byte rows instead
 // of 3M-float strided per-thread runs; rows are padded to 3M + 1 floats so
 // each lane's row walk is bank-conflict free.
+//
+// kHalf: the slab moves through LDS 32 rows at a time (two passes, lanes
+// 0-31 then 32-63 run sh_backward), before the camera-side backward.  The
+// 64 x (3M+1) slab (12.5 KB at SH3) caps residency at 12 waves per CU; the
+// 32-row slab lets the VGPR limit (4 waves per SIMD) decide instead.
 constexpr int kGbWave = 64;
+template <bool kHalf>
 __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_gauss_bwd(
     int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
     const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
@@ -763,14 +771,50 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
     sum_partials(s0, s1, pflag, partial, g);
     scale_partial_sums(g, W, H);
   }
+  if (kHalf) {
+    // camera-side backward first (its registers are dead before the SH
+    // phase); the SH term of dL/dmean is added to the stored value after.
+    if (i < P)
+      gauss_bwd_one(i, D, M, radii, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
+                    viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
+                    o_tau);
+    if (sh) {
+      const bool live = i < P && radii[i] > 0;
+      const f3 campos = mk3(campos_p[0], campos_p[1], campos_p[2]);
+      for (int h = 0; h < 2; ++h) {
+        const int h0 = i0 + 32 * h, nh = min(32, P - h0);
+        if (nh <= 0) break;  // uniform: P is the same for every lane
+        slab_to_lds(shs + (size_t)h0 * S, nh, S, s_sh, lane);
+        __syncthreads();
+        if ((lane >> 5) == h && i < P) {
+          float* row = &s_sh[(lane & 31) * SP];
+          if (live) {
+            const size_t i3 = 3 * (size_t)i;
+            const f3 dm_sh = sh_backward(D, M, row, mk3(means[i3], means[i3 + 1], means[i3 + 2]), campos,
+                                         clamped[i], mk3(g[6], g[7], g[8]), row);
+            // same sum as the full-slab path: (camera term) + (SH term)
+            o_m3d[i3] += dm_sh.x;
+            o_m3d[i3 + 1] += dm_sh.y;
+            o_m3d[i3 + 2] += dm_sh.z;
+          } else {
+            for (int k = 0; k < S; ++k) row[k] = 0.f;
+          }
+        }
+        __syncthreads();
+        lds_to_slab(s_sh, nh, S, o_sh + (size_t)h0 * S, lane);
+        __syncthreads();
+      }
+    }
+    return;
+  }
   if (sh) {
     slab_to_lds(shs + (size_t)i0 * S, ng, S, s_sh, lane);
     __syncthreads();
   }
   if (i < P)
     gauss_bwd_one(i, D, M, radii, clamped, g, means, scales, rots, cov_pre,
-                  sh ? &s_sh[lane * SP] : nullptr, scale_mod, viewm, projm, praw, campos_p, W, H, tanx, tany,
-                  o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
+                  sh ? &s_sh[lane * SP] : nullptr, mk3(0.f, 0.f, 0.f), scale_mod, viewm, projm, praw, campos_p, W, H,
+                  tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   if (sh) {
     __syncthreads();
     lds_to_slab(s_sh, ng, S, o_sh + (size_t)i0 * S, lane);
@@ -972,8 +1016,12 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
   } else {
     gsum = nullptr;
   }
-  const size_t lds = a.shs ? sizeof(float) * kGbWave * (3 * (size_t)a.M + 1) : 0;
-  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M, radii,
+  static const bool full_slab = [] {  // WGSR_GB_FULLSLAB=1: the 64-row slab variant (A/B runs)
+    const char* e = getenv("WGSR_GB_FULLSLAB");
+    return e && atoi(e) != 0;
+  }();
+  const size_t lds = a.shs ? sizeof(float) * (full_slab ? kGbWave : 32) * (3 * (size_t)a.M + 1) : 0;
+  hipLaunchKernelGGL(full_slab ? k_gauss_bwd<false> : k_gauss_bwd<true>, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M, radii,
                      at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
                      partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
