@@ -253,9 +253,14 @@ typedef struct wgsr_uncer_params {
   float opacity_th;       /* uncertainty_params.opacity_th_for_uncer_loss */
   float uncer_depth_mult; /* uncertainty_params.uncer_depth_mult */
   int initialization;     /* 1: no exposure correction */
+  int pre_exposed;        /* 1: fuse the mapper's own exposure step: map_opt_online passes
+                             exp(a) x + b into the loss (mapper.py:1127-1129), which applies
+                             it again (slam_utils.py:179-181).  `image` is the raw render,
+                             image_ab = exp(a) (exp(a) x + b) + b, and the image and
+                             exposure gradients chain through both applications. */
 } wgsr_uncer_params;
 int wgsr_uncer_blocks(int64_t n);
-/* image_ab = exp(a) image + b; partials[blocks(H*W)][3] = sums of
+/* image_ab = exp(a) image + b (applied twice when pre_exposed); partials[blocks(H*W)][3] = sums of
  * w * masked rgb L1 (over channels), of w, and of the re-weighted depth L1
  * (w where ref_depth < depth + 1), w = the uncertainty weight map. */
 int wgsr_uncer_loss_forward(const wgsr_uncer_params* prm, const float* image, const float* gt_image,
@@ -291,10 +296,11 @@ int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials,
 /* dL_dimage / dL_ddepth of loss_grad x (w_rgb sum(w rgb L1) + w_depth
  * sum(re-weighted depth L1)) + the SSIM term (ssim_grad: its gradient w.r.t.
  * image_ab, already scaled; NULL = none); loss_grad: device scalar (NULL = 1);
- * partials[blocks(H*W)][2] = dL/dexposure_a, _b. */
+ * partials[blocks(H*W)][2] = dL/dexposure_a, _b.  exposure_b is read only
+ * when pre_exposed (NULL otherwise allowed). */
 int wgsr_uncer_loss_backward(const wgsr_uncer_params* prm, const float* image, const float* image_ab,
                              const float* gt_image, const float* depth, const float* ref_depth,
-                             const float* exposure_a, const float* uncertainty, const float* median_depth,
+                             const float* exposure_a, const float* exposure_b, const float* uncertainty, const float* median_depth,
                              float w_rgb, float w_depth, const float* loss_grad, const float* ssim_grad,
                              float* dL_dimage, float* dL_ddepth, float* partials, void* stream);
 

@@ -82,6 +82,22 @@ def test_bad_means_shape_raises_runtime_error():
                                torch.empty(0), 0, torch.zeros(3), False, False)
 
 
+def test_host_tensors_are_rejected_before_any_launch():
+    """A host pointer reaching a kernel would fault the GPU: the boundary
+    raises RuntimeError instead (upstream's .data<T>() raises too)."""
+    from diff_gaussian_rasterization import _C
+    from simple_knn._C import distCUDA2
+    with pytest.raises(RuntimeError, match="HIP device"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(4, 3), torch.empty(0), torch.zeros(4, 1),
+                               torch.zeros(4, 3), torch.zeros(4, 4), 1.0, torch.empty(0),
+                               torch.eye(4), torch.eye(4), torch.eye(4), 1.0, 1.0, 8, 8,
+                               torch.zeros(4, 1, 3), 0, torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        _C.mark_visible(torch.zeros(4, 3), torch.eye(4), torch.eye(4))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        distCUDA2(torch.zeros(4, 3))
+
+
 def test_simple_knn_module_surface():
     from simple_knn._C import distCUDA2
     assert callable(distCUDA2)

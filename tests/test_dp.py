@@ -68,8 +68,13 @@ def _worker(rank, port, out_dir):
     vis = torch.from_numpy(g["radii"] > 0)
     denom = vis.float()[:, None]
     radii = torch.from_numpy(g["radii"]).float()
-    reduce_densification_stats(accum, denom, radii)
-    torch.save({"flat": buf.flat, "accum": accum, "denom": denom, "radii": radii},
+    # persistent accumulators with earlier steps' totals (identical on every
+    # rank, as after a previous reduction): only this step's deltas travel
+    prior = torch.arange(P, dtype=torch.float32)[:, None] * 0.5
+    acc_total, den_total, rmax_total = prior.clone(), prior.clone() + 3, torch.full((P,), 2.0)
+    reduce_densification_stats(accum, denom, radii, acc_total, den_total, rmax_total)
+    torch.save({"flat": buf.flat, "accum": accum, "denom": denom, "radii": radii, "acc_total": acc_total,
+                "den_total": den_total, "rmax_total": rmax_total},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -96,6 +101,11 @@ def test_allreduced_gradients_equal_sum_of_views(tmp_path):
     assert torch.equal(outs[0]["denom"][:, 0], sum(torch.from_numpy(g["radii"] > 0).float() for g in views))
     rmax = torch.maximum(*[torch.from_numpy(g["radii"]).float() for g in views])
     assert torch.equal(outs[0]["radii"], rmax)
+    prior = torch.arange(P, dtype=torch.float32) * 0.5
+    for o in outs:  # accumulators = earlier totals + this step's reduced deltas, counted once
+        assert torch.allclose(o["acc_total"][:, 0], prior + acc, rtol=1e-6, atol=1e-6)
+        assert torch.equal(o["den_total"][:, 0], prior + 3 + outs[0]["denom"][:, 0])
+        assert torch.equal(o["rmax_total"], torch.maximum(rmax, torch.full((P,), 2.0)))
 
 
 def test_grad_buffer_layout_is_contiguous_views():

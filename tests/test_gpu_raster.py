@@ -266,6 +266,43 @@ def test_empty_and_culled():
     assert float(opac.abs().sum()) == 0.0 and float(depth.abs().sum()) == 0.0
 
 
+def test_wrong_dtype_or_device_raises():
+    """float64 / host / int64 arguments raise RuntimeError instead of being
+    read as float32 garbage through a raw pointer."""
+    C = _c()
+    from wgsr.camera import synthetic_camera
+    from wgsr.scene import make_scene
+    f = synthetic_camera(32, 24, 0).raster_fields()
+    sc = make_scene(64, 32, 24, 0, seed=1)
+    e = torch.empty(0, device=DEV)
+    d = lambda x: x.to(DEV)  # noqa: E731
+
+    def fwd(bg=None, vm=None, sh=None):
+        return C.rasterize_gaussians(
+            torch.zeros(3, device=DEV) if bg is None else bg, d(sc.means3D), e, d(sc.opacities), d(sc.scales),
+            d(sc.rotations), 1.0, e, d(f["viewmatrix"]) if vm is None else vm, d(f["projmatrix"]),
+            d(f["projmatrix_raw"]), f["tanfovx"], f["tanfovy"], 24, 32, d(sc.shs) if sh is None else sh, 0,
+            d(f["campos"]), False, False)
+    with pytest.raises(RuntimeError, match="bg: expected torch.float32"):
+        fwd(bg=torch.zeros(3, device=DEV, dtype=torch.float64))
+    with pytest.raises(RuntimeError, match="viewmatrix: expected a tensor on"):
+        fwd(vm=f["viewmatrix"])
+    with pytest.raises(RuntimeError, match="sh: expected torch.float32"):
+        fwd(sh=d(sc.shs).double())
+    nr, color, radii, geom, binning, img, *_ = fwd()
+    g = torch.zeros(3, 24, 32, device=DEV)
+    gd = torch.zeros(1, 24, 32, device=DEV)
+    args = lambda r, gc: (torch.zeros(3, device=DEV), d(sc.means3D), r, e, d(sc.scales), d(sc.rotations), 1.0,  # noqa
+                          e, d(f["viewmatrix"]), d(f["projmatrix"]), d(f["projmatrix_raw"]), f["tanfovx"],
+                          f["tanfovy"], gc, gd, d(sc.shs), 0, d(f["campos"]), geom, nr, binning, img, False)
+    with pytest.raises(RuntimeError, match="radii: expected torch.int32"):
+        C.rasterize_gaussians_backward(*args(radii.long(), g))
+    with pytest.raises(RuntimeError, match="dL_dout_color: expected torch.float32"):
+        C.rasterize_gaussians_backward(*args(radii, g.double()))
+    C.rasterize_gaussians_backward(*args(radii, g))
+    torch.cuda.synchronize()
+
+
 def test_mark_visible():
     from wgsr.camera import synthetic_camera
     from wgsr.scene import make_scene

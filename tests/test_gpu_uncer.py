@@ -146,7 +146,14 @@ def test_drop_in_signature_and_mlp_gradient():
         assert _rel(g1, g0) <= 1e-3
 
 
-def test_mapping_iteration_uncertainty_matches_torch_composition():
+@pytest.mark.parametrize("mode", ["map_opt_online", "final_refine", "initialize"])
+def test_mapping_iteration_uncertainty_matches_torch_composition(mode):
+    """MappingStep.forward_backward_uncertainty against the mapper's own call
+    of each of its three call sites: map_opt_online passes the exposure-corrected
+    render into the loss, which corrects it again (mapper.py:1127-1129,
+    slam_utils.py:179-181); final_refine passes the raw render
+    (mapper.py:1298-1306); initialize_map_opt uses initialization=True
+    (mapper.py:974-984)."""
     from wgsr.camera import synthetic_camera
     from wgsr.mapping import MappingStep
     from wgsr.render import DeviceCamera, render
@@ -170,8 +177,11 @@ def test_mapping_iteration_uncertainty_matches_torch_composition():
     pkg = render(cam, leaf["xyz"], torch.sigmoid(leaf["opacity"]), torch.exp(leaf["scaling"]),
                  F.normalize(leaf["rotation"]), torch.cat((leaf["f_dc"], leaf["f_rest"]), dim=1), DEG,
                  torch.zeros(3, device=DEV))
-    lm = ou.loss_mapping_uncertainty(ou.DEFAULT_CONFIG, pkg["render"], pkg["depth"], gt, ref, a, b, pkg["opacity"],
-                                     u_ref, 0.3, 0.3)
+    img = pkg["render"]
+    if mode == "map_opt_online":
+        img = torch.exp(a) * img + b  # mapper.py:1129
+    lm = ou.loss_mapping_uncertainty(ou.DEFAULT_CONFIG, img, pkg["depth"], gt, ref, a, b, pkg["opacity"],
+                                     u_ref, 0.3, 0.3, initialization=(mode == "initialize"))
     scaling = torch.exp(leaf["scaling"])
     lm = lm + 10 * torch.abs(scaling - scaling.mean(dim=1).view(-1, 1)).mean()
     lm.backward()
@@ -182,7 +192,8 @@ def test_mapping_iteration_uncertainty_matches_torch_composition():
     camd = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in f.items()}
     u = unc0.clone().requires_grad_(True)
     out = ms.forward_backward_uncertainty(camd, gt, ref, ea, eb, torch.zeros(3, device=DEV), u, 0.3, 0.3,
-                                          config=ou.DEFAULT_CONFIG)
+                                          config=ou.DEFAULT_CONFIG, initialization=(mode == "initialize"),
+                                          pre_exposed=(mode == "map_opt_online"))
     torch.cuda.synchronize()
     assert abs(float(out["loss"]) - float(lm)) <= 1e-5 * abs(float(lm))
     assert _rel(ms.grad["xyz"], leaf["xyz"].grad) <= 1e-4
@@ -192,8 +203,11 @@ def test_mapping_iteration_uncertainty_matches_torch_composition():
     assert _rel(ms.grad["scaling"], leaf["scaling"].grad) <= 1e-4
     assert _rel(ms.grad["rotation"], leaf["rotation"].grad) <= 1e-4
     assert _rel(u.grad, u_ref.grad) <= 1e-4
-    assert _rel(out["dexposure_a"], a.grad) <= 1e-3
-    assert _rel(out["dexposure_b"], b.grad) <= 1e-3
+    if mode == "initialize":
+        assert a.grad is None and b.grad is None
+    else:
+        assert _rel(out["dexposure_a"], a.grad) <= 1e-3
+        assert _rel(out["dexposure_b"], b.grad) <= 1e-3
     assert _rel(out["dtheta"], cam.cam_rot_delta.grad) <= 1e-3
     assert _rel(out["drho"], cam.cam_trans_delta.grad) <= 1e-3
 

@@ -296,7 +296,8 @@ def main_uncertainty(a):
             pkg = render(cam, m.xyz, torch.sigmoid(m.opacity), torch.exp(m.scaling),
                          torch.nn.functional.normalize(m.rotation), torch.cat((m.f_dc, m.f_rest), dim=1), deg, bg)
             vpt, vis, radii = pkg["viewspace_points"], pkg["visibility_filter"], pkg["radii"]
-            lm = ref_uncer_loss(pkg["render"], pkg["depth"], pkg["opacity"], gt_image, gt_depth, ea, eb, net(feats),
+            img = torch.exp(ea) * pkg["render"] + eb  # map_opt_online's pre-exposed input (mapper.py:1129)
+            lm = ref_uncer_loss(img, pkg["depth"], pkg["opacity"], gt_image, gt_depth, ea, eb, net(feats),
                                 w11, w7)
             scaling = torch.exp(m.scaling)
             lm = lm + 10 * torch.abs(scaling - scaling.mean(dim=1).view(-1, 1)).mean()

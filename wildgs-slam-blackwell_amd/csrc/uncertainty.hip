@@ -113,11 +113,13 @@ struct UParams {
   int H, W, h, w;
   float rgb_th, data_rate, ssim_weight, opacity_th, depth_mult;
   int init;
+  int pre;  // pre_exposed: the correction is applied twice (mapper.py:1127 + slam_utils.py:179-181)
 };
 
 __device__ __forceinline__ UParams uparams(const wgsr_uncer_params& p) {
   return UParams{p.H, p.W, p.h, p.w, p.rgb_threshold, p.data_rate, p.ssim_weight, p.opacity_th,
-                 p.uncer_depth_mult, p.initialization};
+                 p.uncer_depth_mult, p.initialization,
+                 p.initialization ? 0 : p.pre_exposed};
 }
 
 // processed_uncertainty = clip(u, min=0.1) + 1e-3 (mapping_utils.py:262)
@@ -152,6 +154,11 @@ __global__ __launch_bounds__(kUBlock) void k_unc_fwd(wgsr_uncer_params prm, cons
     const float g0 = gt[p], g1 = gt[HW + p], g2 = gt[2 * HW + p];
     const float m = ((g0 + g1) + g2) > q.rgb_th ? 1.f : 0.f;
     float a0 = image[p], a1 = image[HW + p], a2 = image[2 * HW + p];
+    if (q.pre) {  // the mapper's own torch.exp(a) * image + b, in its op order
+      a0 = __fadd_rn(__fmul_rn(ea, a0), b);
+      a1 = __fadd_rn(__fmul_rn(ea, a1), b);
+      a2 = __fadd_rn(__fmul_rn(ea, a2), b);
+    }
     if (!q.init) {
       a0 = ea * a0 + b;
       a1 = ea * a1 + b;
@@ -279,7 +286,8 @@ __global__ __launch_bounds__(kUBlock) void k_unc_loss(wgsr_uncer_params prm, con
 __global__ __launch_bounds__(kUBlock) void k_unc_bwd(wgsr_uncer_params prm, const float* __restrict__ image,
                                                      const float* __restrict__ image_ab, const float* __restrict__ gt,
                                                      const float* __restrict__ depth, const float* __restrict__ ref,
-                                                     const float* __restrict__ expo_a, const float* __restrict__ unc,
+                                                     const float* __restrict__ expo_a,
+                                                     const float* __restrict__ expo_b, const float* __restrict__ unc,
                                                      const float* __restrict__ med, float w_rgb, float w_depth,
                                                      const float* __restrict__ lgrad,
                                                      const float* __restrict__ ssim_grad, float* __restrict__ d_image,
@@ -289,6 +297,7 @@ __global__ __launch_bounds__(kUBlock) void k_unc_bwd(wgsr_uncer_params prm, cons
   const int HW = q.H * q.W;
   const int p = blockIdx.x * kUBlock + threadIdx.x;
   const float ea = q.init ? 1.f : expf(expo_a[0]);
+  const float b1 = q.pre ? expo_b[0] : 0.f;
   const float lg = lgrad ? lgrad[0] : 1.f;  // upstream dL/dloss
   w_rgb = w_rgb * lg;
   w_depth = w_depth * lg;
@@ -303,9 +312,18 @@ __global__ __launch_bounds__(kUBlock) void k_unc_bwd(wgsr_uncer_params prm, cons
       const size_t k = (size_t)c * HW + p;
       float gab = w_rgb * wgt * usgn(image_ab[k] * m - g[c] * m) * m;
       if (ssim_grad) gab += ssim_grad[k];
-      d_image[k] = gab * ea;
-      da += gab * image[k] * ea;
-      db += gab;
+      if (q.pre) {
+        // x2 = ea x1 + b, x1 = ea x + b:  dx2/dx = ea^2, dx2/da = ea (x1 + ea x), dx2/db = ea + 1
+        const float x = image[k];
+        const float x1 = __fadd_rn(__fmul_rn(ea, x), b1);
+        d_image[k] = (gab * ea) * ea;
+        da += gab * ea * (x1 + ea * x);
+        db += gab * (ea + 1.f);
+      } else {
+        d_image[k] = gab * ea;
+        da += gab * image[k] * ea;
+        db += gab;
+      }
     }
     const float rd = ref[p], d = depth[p];
     const float thr = depth_threshold(med);
@@ -462,16 +480,18 @@ int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials,
 
 int wgsr_uncer_loss_backward(const wgsr_uncer_params* prm, const float* image, const float* image_ab,
                              const float* gt_image, const float* depth, const float* ref_depth,
-                             const float* exposure_a, const float* uncertainty, const float* median_depth, float w_rgb,
-                             float w_depth, const float* loss_grad, const float* ssim_grad, float* dL_dimage,
+                             const float* exposure_a, const float* exposure_b, const float* uncertainty,
+                             const float* median_depth, float w_rgb, float w_depth, const float* loss_grad, const float* ssim_grad, float* dL_dimage,
                              float* dL_ddepth, float* partials, void* stream) {
   if (int e = check_params(prm, "wgsr_uncer_loss_backward")) return e;
   if (!image || !image_ab || !gt_image || !depth || !ref_depth || !uncertainty || !median_depth || !dL_dimage ||
-      !dL_ddepth || !partials || (!prm->initialization && !exposure_a))
+      !dL_ddepth || !partials || (!prm->initialization && !exposure_a) ||
+      (!prm->initialization && prm->pre_exposed && !exposure_b))
     return set_error(WGSR_EINVAL, "wgsr_uncer_loss_backward: null pointer");
   const int HW = prm->H * prm->W;
   hipLaunchKernelGGL(k_unc_bwd, dim3(ublocks(HW)), dim3(kUBlock), 0, (hipStream_t)stream, *prm, image, image_ab,
-                     gt_image, depth, ref_depth, exposure_a, uncertainty, median_depth, w_rgb, w_depth, loss_grad,
+                     gt_image, depth, ref_depth, exposure_a, exposure_b, uncertainty, median_depth, w_rgb, w_depth,
+                     loss_grad,
                      ssim_grad, dL_dimage, dL_ddepth, partials);
   UNCCHK("wgsr_uncer_loss_backward");
   return WGSR_OK;

@@ -17,10 +17,21 @@ from wgsr import _lib
 NUM_CHANNELS = 3
 
 
-def _f32(t):
+def _on(t, dev, dtype, name):
+    """Upstream's ``.data<T>()`` raises on a dtype mismatch; a raw pointer
+    would not.  Reject anything that is not ``dtype`` on the HIP device
+    ``dev`` (a host pointer reaching a kernel faults the GPU)."""
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.device != dev or t.device.type != "cuda":
+        raise RuntimeError(f"{name}: expected a tensor on {dev}, got {t.device}")
+    return t.contiguous()
+
+
+def _f32(t, dev, name):
     if t is None or t.numel() == 0:
         return None
-    return t.contiguous()
+    return _on(t, dev, torch.float32, name)
 
 
 def _args(P, D, M, W, H, bg, means3D, colors, opacity, scales, rotations, cov3D_precomp, sh,
@@ -56,13 +67,17 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     out_opacity = torch.empty(1, H, W, **fopts)
     radii = torch.empty(P, dtype=torch.int32, device=dev)
     n_touched = torch.empty(P, dtype=torch.int32, device=dev)
-    shc = _f32(sh)
+    if dev.type != "cuda":
+        raise RuntimeError(f"means3D: expected a HIP device tensor, got {dev}")
+    shc = _f32(sh, dev, "sh")
     M = shc.size(1) if shc is not None else 0
     keep = []
-    a = _args(P, int(degree), M, W, H, _f32(background), _f32(means3D), _f32(colors), _f32(opacity),
-              _f32(scales), _f32(rotations), _f32(cov3D_precomp), shc, _f32(viewmatrix),
-              _f32(projmatrix), _f32(projmatrix_raw), _f32(campos), scale_modifier, tan_fovx,
-              tan_fovy, prefiltered, debug, keep)
+    a = _args(P, int(degree), M, W, H, _f32(background, dev, "bg"), _f32(means3D, dev, "means3D"),
+              _f32(colors, dev, "colors"), _f32(opacity, dev, "opacity"), _f32(scales, dev, "scales"),
+              _f32(rotations, dev, "rotations"), _f32(cov3D_precomp, dev, "cov3D_precomp"), shc,
+              _f32(viewmatrix, dev, "viewmatrix"), _f32(projmatrix, dev, "projmatrix"),
+              _f32(projmatrix_raw, dev, "projmatrix_raw"), _f32(campos, dev, "campos"), scale_modifier,
+              tan_fovx, tan_fovy, prefiltered, debug, keep)
     nr = ctypes.c_int64(0)
     with torch.cuda.device(dev), _lib.AllocRequest(dev) as req:
         code = L.wgsr_rasterize_forward(
@@ -92,7 +107,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dev = means3D.device
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
-    shc = _f32(sh)
+    if dev.type != "cuda":
+        raise RuntimeError(f"means3D: expected a HIP device tensor, got {dev}")
+    shc = _f32(sh, dev, "sh")
     M = shc.size(1) if shc is not None else 0
     fopts = dict(dtype=torch.float32, device=dev)
     dL_dmeans2D = torch.empty(P, 3, **fopts)
@@ -108,8 +125,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             t = out.get(name)
             if t is None:
                 return default
-            if t.shape != default.shape or t.dtype != torch.float32 or not t.is_contiguous():
-                raise RuntimeError(f"out[{name!r}] must be a contiguous float32 {tuple(default.shape)}")
+            if (t.shape != default.shape or t.dtype != torch.float32 or not t.is_contiguous()
+                    or t.device != dev):
+                raise RuntimeError(f"out[{name!r}] must be a contiguous float32 {tuple(default.shape)} on {dev}")
             return t
         dL_dmeans3D = take("means3D", dL_dmeans3D)
         dL_dsh = take("shs", dL_dsh)
@@ -121,14 +139,22 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                 dL_drotations, dL_dtau)
     keep = []
-    means = _f32(means3D)
+    means = _f32(means3D, dev, "means3D")
+    radii = _on(radii, dev, torch.int32, "radii")
+    if radii.numel() != P:
+        raise RuntimeError(f"radii: expected {P} entries, got {radii.numel()}")
+    for buf, name in ((geomBuffer, "geomBuffer"), (binningBuffer, "binningBuffer"), (imageBuffer, "imageBuffer")):
+        if buf.numel():
+            _on(buf, dev, torch.uint8, name)
     # the backward does not read opacities (they live in the geometry buffer);
     # any valid device pointer satisfies the argument check
-    a = _args(P, int(degree), M, W, H, _f32(background), means, _f32(colors), means,
-              _f32(scales), _f32(rotations), _f32(cov3D_precomp), shc, _f32(viewmatrix),
-              _f32(projmatrix), _f32(projmatrix_raw), _f32(campos), scale_modifier, tan_fovx,
-              tan_fovy, False, debug, keep)
-    gc, gd = dL_dout_color.contiguous(), dL_dout_depth.contiguous()
+    a = _args(P, int(degree), M, W, H, _f32(background, dev, "bg"), means, _f32(colors, dev, "colors"), means,
+              _f32(scales, dev, "scales"), _f32(rotations, dev, "rotations"),
+              _f32(cov3D_precomp, dev, "cov3D_precomp"), shc, _f32(viewmatrix, dev, "viewmatrix"),
+              _f32(projmatrix, dev, "projmatrix"), _f32(projmatrix_raw, dev, "projmatrix_raw"),
+              _f32(campos, dev, "campos"), scale_modifier, tan_fovx, tan_fovy, False, debug, keep)
+    gc = _on(dL_dout_color, dev, torch.float32, "dL_dout_color")
+    gd = _on(dL_dout_depth, dev, torch.float32, "dL_dout_depth")
     p = _lib.ptr
     with torch.cuda.device(dev), _lib.AllocRequest(dev):
         code = L.wgsr_rasterize_backward(
@@ -147,8 +173,12 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     L = _lib.load()
     dev = means3D.device
     P = means3D.size(0)
+    if dev.type != "cuda":
+        raise RuntimeError(f"means3D: expected a HIP device tensor, got {dev}")
     present = torch.empty(P, dtype=torch.bool, device=dev)
-    m, v, pm = means3D.contiguous(), viewmatrix.contiguous(), projmatrix.contiguous()
+    m = _on(means3D, dev, torch.float32, "means3D")
+    v = _on(viewmatrix, dev, torch.float32, "viewmatrix")
+    pm = _on(projmatrix, dev, torch.float32, "projmatrix")
     with torch.cuda.device(dev):
         code = L.wgsr_mark_visible(P, m.data_ptr(), v.data_ptr(), pm.data_ptr(),
                                    present.data_ptr() if P else None, _lib.stream_handle(dev))

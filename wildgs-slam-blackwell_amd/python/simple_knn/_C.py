@@ -13,6 +13,8 @@ def distCUDA2(points: torch.Tensor) -> torch.Tensor:
         raise RuntimeError("points must have dimensions (num_points, 3)")
     L = _lib.load()
     dev = points.device
+    if dev.type != "cuda":
+        raise RuntimeError(f"points: expected a HIP device tensor, got {dev}")
     P = points.size(0)
     pts = points.contiguous().float()
     out = torch.empty(P, dtype=torch.float32, device=dev)

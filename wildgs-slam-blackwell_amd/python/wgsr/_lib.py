@@ -65,7 +65,8 @@ class UncerParams(ctypes.Structure):
     _fields_ = [("H", ctypes.c_int), ("W", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
                 ("rgb_threshold", ctypes.c_float), ("data_rate", ctypes.c_float),
                 ("ssim_weight", ctypes.c_float), ("opacity_th", ctypes.c_float),
-                ("uncer_depth_mult", ctypes.c_float), ("initialization", ctypes.c_int)]
+                ("uncer_depth_mult", ctypes.c_float), ("initialization", ctypes.c_int),
+                ("pre_exposed", ctypes.c_int)]
 
 
 PLY_MAX_TENSORS = 8
@@ -135,7 +136,7 @@ def load():
         L.wgsr_uncer_loss_combine.argtypes = ([U] + [_fp] * 4 + [c_int] + [ctypes.c_float] * 4 + [c_int] +
                                               [_fp] * 3 + [_fp])
         L.wgsr_uncer_loss_backward.restype = c_int
-        L.wgsr_uncer_loss_backward.argtypes = [U] + [_fp] * 8 + [ctypes.c_float] * 2 + [_fp] * 5 + [_fp]
+        L.wgsr_uncer_loss_backward.argtypes = [U] + [_fp] * 9 + [ctypes.c_float] * 2 + [_fp] * 5 + [_fp]
         L.wgsr_track_blocks.restype = c_int
         L.wgsr_track_blocks.argtypes = [c_i64]
         L.wgsr_tracking_loss.restype = c_int

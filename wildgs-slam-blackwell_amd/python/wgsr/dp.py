@@ -13,8 +13,9 @@ exchange is one reduction of the per-Gaussian parameter gradients per step.
 * ``allreduce_grads`` issues SUM all-reduces over that buffer in large
   buckets (xGMI is point-to-point: RCCL's rings are per-link bound, so few,
   large collectives), optionally asynchronously so a caller can overlap them.
-* ``reduce_densification_stats`` sums the per-view ||dL/dmeans2D|| statistics
-  and visibility counts and takes the MAX of the screen radii -- the reference
+* ``reduce_densification_stats`` sums this step's per-view ||dL/dmeans2D||
+  contributions and visibility counts and takes the MAX of the screen radii,
+  then folds them into the persistent accumulators -- the reference
   accumulates per-view norms (gaussian_model.py:745-749, mapper.py:1177-1183),
   not the norm of the summed gradient, so these cannot ride in the gradient
   sum.
@@ -84,15 +85,32 @@ def allreduce_grads(buf: GradBuffer, bucket_bytes: int = 256 << 20, async_op: bo
     return None
 
 
-def reduce_densification_stats(grad_norm_accum: torch.Tensor, denom: torch.Tensor,
-                               max_radii2D: torch.Tensor):
-    """In place: SUM of per-view ||dL/dmeans2D[:, :2]|| accumulations and of
-    the visibility counts; MAX of the per-Gaussian screen radii."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
-        return
-    dist.all_reduce(grad_norm_accum, op=dist.ReduceOp.SUM)
-    dist.all_reduce(denom, op=dist.ReduceOp.SUM)
-    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX)
+def reduce_densification_stats(step_grad_norm: torch.Tensor, step_count: torch.Tensor,
+                               step_radii: torch.Tensor, xyz_gradient_accum: torch.Tensor | None = None,
+                               denom: torch.Tensor | None = None, max_radii2D: torch.Tensor | None = None):
+    """Reduce THIS STEP's densification contributions over the ranks' views.
+
+    ``step_grad_norm`` / ``step_count`` / ``step_radii`` must hold only this
+    step's per-view contributions (||dL/dmeans2D[:, :2]|| of the visible
+    Gaussians, their visibility 0/1 count, their screen radii); they are
+    reduced in place (SUM, SUM, MAX).  Passing the persistent accumulators
+    here instead would re-add the totals of every earlier step ~world-size
+    times, so the accumulators are separate, optional arguments: when given,
+    the reduced step values are folded into them the way the reference does
+    per view (gaussian_model.py:745-749, mapper.py:1177-1183):
+    ``xyz_gradient_accum += step_grad_norm``, ``denom += step_count``,
+    ``max_radii2D = max(max_radii2D, step_radii)``.
+    """
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(step_grad_norm, op=dist.ReduceOp.SUM)
+        dist.all_reduce(step_count, op=dist.ReduceOp.SUM)
+        dist.all_reduce(step_radii, op=dist.ReduceOp.MAX)
+    if xyz_gradient_accum is not None:
+        xyz_gradient_accum += step_grad_norm.view_as(xyz_gradient_accum)
+    if denom is not None:
+        denom += step_count.view_as(denom)
+    if max_radii2D is not None:
+        torch.maximum(max_radii2D, step_radii.view_as(max_radii2D).to(max_radii2D.dtype), out=max_radii2D)
 
 
 def views_for_rank(num_views: int, rank: int, world: int):

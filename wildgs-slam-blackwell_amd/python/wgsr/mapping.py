@@ -197,15 +197,27 @@ class MappingStep:
     def forward_backward_uncertainty(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg, uncertainty,
                                      train_frac: float, ssim_frac: float, config: dict | None = None,
                                      initialization: bool = False, freeze_uncertainty_loss: bool = False,
-                                     median_depth=None, iso_weight: float = 10.0):
-        """The reference's DEFAULT mapping iteration (uncertainty_params.activate,
-        mapper.py:1120-1138): get_loss_mapping_uncertainty (slam_utils.py:
-        146-258) + 10 * isotropic loss, and their backward.
+                                     median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True):
+        """The reference's DEFAULT mapping iteration (uncertainty_params.activate):
+        get_loss_mapping_uncertainty (slam_utils.py:146-258) + 10 * isotropic
+        loss, and their backward.
+
+        Which of the mapper's three call sites is fused is chosen by the flags:
+
+        * ``pre_exposed=True`` (default) -- map_opt_online (mapper.py:1120-1138),
+          which passes ``exp(a) * image + b`` into the loss, where the exposure
+          correction is applied a second time (slam_utils.py:179-181).  Both
+          applications are fused into the loss kernels, and the image and
+          exposure gradients chain through both.
+        * ``pre_exposed=False`` -- final_refine (mapper.py:1290-1306): the raw
+          render goes in and the loss applies the correction once.
+        * ``initialization=True`` -- initialize_map_opt (mapper.py:974-984): no
+          exposure correction at all (``pre_exposed`` is ignored).
 
         ``uncertainty`` is the uncertainty MLP's output map [h, w] for this
-        view (``uncer_network(viewpoint.features)``, run by the caller in
-        torch); its gradient is fed back with ``uncertainty.backward`` (as
-        the reference's ``loss.backward()`` reaches the MLP) unless
+        view (``uncer_network(viewpoint.features)``, run by the caller); its
+        gradient is fed back with ``uncertainty.backward`` (as the reference's
+        ``loss.backward()`` reaches the MLP) unless
         ``freeze_uncertainty_loss``.  ``config``: the reference's mapping config
         dict (Training.alpha / rgb_boundary_threshold / ssim_loss,
         opt_params.lambda_dssim, uncertainty_params.*); defaults are
@@ -222,7 +234,7 @@ class MappingStep:
         w_iso = iso_weight / (3 * P) if P else 0.0
         loss, state = U.loss_forward(image, depth, opac_img, gt_image, gt_depth, exposure_a, exposure_b, uncertainty,
                                      train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
-                                     median_depth, extra=(self.iso_part, w_iso))
+                                     median_depth, extra=(self.iso_part, w_iso), pre_exposed=pre_exposed)
         d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state)
         _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:

@@ -100,12 +100,17 @@ def _check(t, who):
 
 def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, uncertainty, train_frac: float,
                  ssim_frac: float, cfg: dict, initialization: bool = False, freeze_uncertainty_loss: bool = False,
-                 median_depth=None, extra=None):
+                 median_depth=None, extra=None, pre_exposed: bool = False):
     """-> (loss 0-d device tensor, LossState).  image/gt [3,H,W], depth /
     ref_depth / opacity [1,H,W] (or [H,W]), uncertainty [h,w].  ``extra``:
     optional (partials [n] device tensor, weight) added to the loss as
     weight * sum(partials) in the same epilogue launch (MappingStep's
-    isotropic term)."""
+    isotropic term).  ``pre_exposed``: ``image`` is the raw render and the
+    loss is the one map_opt_online computes, which passes
+    ``exp(a) * image + b`` into get_loss_mapping_uncertainty (mapper.py:
+    1127-1129), where the exposure is applied again (slam_utils.py:179-181);
+    the returned image / exposure gradients chain through both applications.
+    Ignored with ``initialization``."""
     L = _lib.load()
     H, W = gt.shape[-2], gt.shape[-1]
     if uncertainty.dim() != 2:
@@ -137,7 +142,8 @@ def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, u
         torch.float32).reshape(1).contiguous()
     prm = _lib.UncerParams(H, W, h, w, cfg["rgb_boundary_threshold"], 1.0 + bias_factor(train_frac, 0.8),
                            100.0 + 900.0 * bias_factor(ssim_frac, 0.8), cfg["opacity_th_for_uncer_loss"],
-                           cfg["uncer_depth_mult"], int(bool(initialization)))
+                           cfg["uncer_depth_mult"], int(bool(initialization)),
+                           int(bool(pre_exposed) and not initialization))
     image_ab = torch.empty_like(image)
     lpart = torch.empty(_blocks(HW), 3, device=dev)
     comps = [torch.empty(1, H, W, device=dev) for _ in range(3)]
@@ -204,7 +210,7 @@ def loss_backward(s: LossState, loss_grad=None):
                                             p(ssim_grad), st))
         w_rgb = alpha * ((1.0 - lam) if s.cfg["ssim_loss"] else 1.0) / (3 * HW)
         _lib.check(L.wgsr_uncer_loss_backward(ctypes.byref(s.prm), p(s.image), p(s.image_ab), p(s.gt), p(s.depth),
-                                              p(s.ref), p(s.ea), p(s.unc), p(s.med), float(w_rgb),
+                                              p(s.ref), p(s.ea), p(s.eb), p(s.unc), p(s.med), float(w_rgb),
                                               float((1.0 - alpha) / HW), p(lg), p(ssim_grad), p(d_image), p(d_depth),
                                               p(epart), st))
     esum = epart.sum(0)
