@@ -169,6 +169,57 @@ def test_both_backward_render_kernels(P, W, H, deg, view, kernel, monkeypatch):
     check_against(out, _cpu_expect(inputs, settings, grads))
 
 
+@pytest.mark.parametrize("P,W,H,deg,view", [(20_000, 640, 480, 3, 2), (8_000, 320, 240, 1, 1), (5_000, 200, 136, 0, 0)])
+def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
+    """The per-Gaussian backward modes agree and match the CPU restatement:
+    WGSR_GB=dense (k_gauss_bwd over every Gaussian, each lane walking its own
+    records) and sparse, the default (k_sum_active sums the records of the
+    Gaussians the render backward marked, 16 lanes per Gaussian; k_gauss_bwd
+    loads and computes only their lanes).  Zero rows must coincide exactly;
+    values within fp32 summation-order noise (the record sums are a tree in
+    sparse mode, a chain in dense mode).  Golden scenes cover the precomputed
+    colour / covariance paths in the default mode."""
+    inputs, settings, grads = _synthetic(P, W, H, deg, view)
+    outs = {}
+    for mode in ("dense", "sparse"):
+        monkeypatch.setenv("WGSR_GB", mode)
+        outs[mode] = run_c(inputs, settings, grads)
+    check_against(outs["sparse"], _cpu_expect(inputs, settings, grads))
+    for k in GRAD_KEYS + ("dL_dtau", "dL_dcov3D"):
+        a, b = outs["sparse"][k], outs["dense"][k]
+        np.testing.assert_array_equal(a == 0, b == 0, err_msg=f"{k} zero rows")
+        np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6 * float(np.abs(b).max() + 1e-30), err_msg=k)
+
+
+def test_repeated_backward_of_one_forward_is_identical():
+    """The per-Gaussian 'received gradient' flags are set by each backward of
+    a forward (zeroed once by the forward): a second backward with other
+    upstream gradients sees the same set and matches a fresh forward."""
+    C = _c()
+    inputs, settings, (gc, gd) = _synthetic(10_000, 320, 240, 3, 1)
+    d = lambda x: x.to(DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    st = settings
+    fargs = (d(st["bg"]), d(inputs["means3D"]), e, d(inputs["opacities"]), d(inputs["scales"]),
+             d(inputs["rotations"]), 1.0, e, d(st["viewmatrix"]), d(st["projmatrix"]), d(st["projmatrix_raw"]),
+             st["tanfovx"], st["tanfovy"], st["H"], st["W"], d(inputs["shs"]), 3, d(st["campos"]), False, False)
+
+    def bwd(fw, gcol, gdep):
+        nr, _, radii, geom, binning, img = fw[:6]
+        return C.rasterize_gaussians_backward(
+            fargs[0], fargs[1], radii, e, fargs[4], fargs[5], 1.0, e, fargs[8], fargs[9], fargs[10], st["tanfovx"],
+            st["tanfovy"], gcol, gdep, fargs[15], 3, fargs[17], geom, nr, binning, img, False)
+    fw = C.rasterize_gaussians(*fargs)
+    g1 = bwd(fw, d(gc), d(gd))
+    g2 = bwd(fw, d(gc) * 0.5, torch.zeros_like(d(gd)))
+    g3 = bwd(fw, d(gc), d(gd))
+    fresh = bwd(C.rasterize_gaussians(*fargs), d(gc) * 0.5, torch.zeros_like(d(gd)))
+    torch.cuda.synchronize()
+    for a, b, c in zip(g1, g3, zip(g2, fresh)):
+        assert torch.equal(a, b)
+        assert torch.equal(c[0], c[1])
+
+
 def test_exact_tile_lists_elongated_splats():
     """Stress the exact tile lists (row_span) and the per-wave ellipse culling:
     needle-like rotated splats (per-axis scales over 2.6 decades) and opacities

@@ -41,6 +41,7 @@ HostCounters& host_counters() {
   }
   return hc;
 }
+
 }
 
 int set_error(int code, const char* fmt, ...) {
@@ -362,7 +363,8 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
                         : nullptr;
   StageTimer T(8, s);
   STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, gsum, dL_dmeans2D, dL_dcolors, dL_dopacity,
-                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
+                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, gauss_bwd_mode(),
+                               s));
   return WGSR_OK;
 }
 

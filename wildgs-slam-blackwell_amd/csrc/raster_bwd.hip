@@ -49,7 +49,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
-    uint8_t* __restrict__ pflag) {
+    uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag) {
   constexpr int Q = 4;
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sG[kBatch];
@@ -210,6 +210,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
       partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
       pflag[k] = 1;
+      gflag[gid] = 1;  // same value from every tile: a benign race
     }
   }
 }
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
     const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W,
     int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
-    float4* __restrict__ partial, uint8_t* __restrict__ pflag) {
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag) {
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sG[kBatch];
   __shared__ float sP[4][kBatch][11];
@@ -355,6 +356,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
         partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
         partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
         pflag[k] = 1;
+        gflag[gid] = 1;
       }
     }
   }
@@ -368,7 +370,7 @@ __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k]
 // kAcc: dsh is a caller register array of 48 floats that receives += (the
 // multi-view backward); otherwise dsh is written, zeros past K.
 template <bool kAcc = false>
-__device__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
+__device__ __forceinline__ f3 sh_backward(int deg, int M, const float* sh, f3 pos, f3 campos, uint32_t cbits, f3 dRGB, float* dsh) {
   const f3 dir_orig = sub3(pos, campos);
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const f3 dir = mk3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
@@ -529,6 +531,87 @@ __global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __re
   for (int q = 0; q < 10; ++q) gsum[(size_t)q * P + i] = g[q];
 }
 
+// First half of the sparse per-Gaussian backward: the record sums of the
+// Gaussians the render backward marked (gflag), 16 lanes per Gaussian, four
+// Gaussians per round, into gsum[10][P] (live rows only).  Lane l of a group
+// reads slots 4l .. 4l + 3 of each 64-slot pass, flags and records in ONE
+// round trip, and a DPP row reduction sums the group.  A per-lane walk
+// (sum_partials) pays about one round trip per 4 records and the wave waits
+// for its largest splat (foreground Gaussians cover ~100 tiles); done here,
+// in a lean kernel with many waves in flight, k_gauss_bwd's waves start from
+// independent loads (sums, parameters, SH row).
+__global__ __launch_bounds__(64) void k_sum_active(int P, const uint8_t* __restrict__ gflag,
+                                                   const uint32_t* __restrict__ slot_start,
+                                                   const uint32_t* __restrict__ tiles,
+                                                   const uint8_t* __restrict__ pflag,
+                                                   const float4* __restrict__ partial, int W, int H,
+                                                   float* __restrict__ gsum) {
+  __shared__ float s_g[64][11];
+  const int lane = threadIdx.x, i0 = blockIdx.x * 64, i = i0 + lane;
+  const int q = lane >> 4, l = lane & 15;
+  // flag, slot range and list length in one round trip (coalesced)
+  const bool in = i < P;
+  const bool live = in && gflag[i] != 0;
+  const uint32_t my_s0 = in ? slot_start[i] : 0u, my_n = in ? tiles[i] : 0u;
+  uint64_t act = wave_ballot(live);
+  if (!act) return;  // wave-uniform
+  while (act) {
+    int jq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      jq[k] = act ? __builtin_ctzll(act) : -1;
+      act &= act - 1;
+    }
+    const int j = q == 0 ? jq[0] : q == 1 ? jq[1] : q == 2 ? jq[2] : jq[3];
+    // every lane takes part in both shuffles (a ds_bpermute from a lane
+    // outside EXEC reads 0): the group's slot range comes from lane j
+    const int src = j < 0 ? 0 : j;
+    const uint32_t s0 = (uint32_t)__shfl((int)my_s0, src, 64);
+    const uint32_t nj = (uint32_t)__shfl((int)my_n, src, 64);
+    const uint32_t n = j < 0 ? 0u : nj;
+    float acc[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+    for (uint32_t b = 0; b < n; b += 64) {
+      // flags and records of the lane's 4 slots in one round trip: records of
+      // unflagged slots are stale bytes, dropped by a select (never a multiply)
+      bool f[4];
+      float4 r[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = b + 4 * l + u;
+        const bool ok = k < n;
+        const size_t sl = (size_t)s0 + (ok ? k : 0u);
+        f[u] = ok && pflag[sl] != 0;
+#pragma unroll
+        for (int h = 0; h < 3; ++h) r[u][h] = ok ? partial[3 * sl + h] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 a0 = r[u][0], a1 = r[u][1], a2 = r[u][2];
+        acc[0] += f[u] ? a0.x : 0.f; acc[1] += f[u] ? a0.y : 0.f;
+        acc[2] += f[u] ? a0.z : 0.f; acc[3] += f[u] ? a0.w : 0.f;
+        acc[4] += f[u] ? a1.x : 0.f; acc[5] += f[u] ? a1.y : 0.f;
+        acc[6] += f[u] ? a1.z : 0.f; acc[7] += f[u] ? a1.w : 0.f;
+        acc[8] += f[u] ? a2.x : 0.f; acc[9] += f[u] ? a2.y : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[k] = dpp_row_sum16(acc[k]);
+    if (l == 15 && j >= 0)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) s_g[j][k] = acc[k];
+  }
+  __syncthreads();
+  if (!live) return;
+  float g[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) g[k] = s_g[lane][k];
+  scale_partial_sums(g, W, H);
+#pragma unroll
+  for (int k = 0; k < 10; ++k) gsum[(size_t)k * P + i] = g[k];
+}
+
 // Camera-side backward of one Gaussian in one view (upstream
 // computeCov2DCUDA + the projection / depth terms of preprocessCUDA backward,
 // plus the w-pose gradient): from its screen-space partial sums g[10] to
@@ -673,7 +756,7 @@ __device__ __forceinline__ void cov_to_scale_rot(float4 q, f3 sv, float scale_mo
 // Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
 // holds its 3M SH coefficients on entry and its dL/dsh row on exit.
 __device__ __forceinline__ void gauss_bwd_one(
-    int i, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ clamped, const float g[10],
+    int i, int D, int M, bool live, const uint32_t* __restrict__ clamped, const float g[10],
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
     const float* __restrict__ cov_pre, float* shrow, f3 dm_sh, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
@@ -683,7 +766,7 @@ __device__ __forceinline__ void gauss_bwd_one(
   // dm_sh: the SH term of dL/dmean when the caller ran sh_backward itself
   // (shrow null); zero otherwise.
   const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
-  if (!(radii[i] > 0)) {
+  if (!live) {  // culled, or (sparse) no partial record: every output is zero
     for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
     for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
     reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -743,9 +826,18 @@ __device__ __forceinline__ void gauss_bwd_one(
 // 64 x (3M+1) slab (12.5 KB at SH3) caps residency at 12 waves per CU; the
 // 32-row slab lets the VGPR limit (4 waves per SIMD) decide instead.
 constexpr int kGbWave = 64;
-template <bool kHalf>
+//
+// kSparse: a Gaussian is live only if the render backward marked it in gflag
+// (wrote a partial record for it: bench scene 7.5 %); the others' outputs are
+// exactly zero, so their lanes skip every load (slot flags, parameters, SH
+// row) and only store zeros.  The stores stay the dense kernel's: every row
+// of the wave's span written by its own lane, the dL/dsh slab through LDS as
+// full coalesced rows -- scattered partial-line writes (a kernel that visits
+// only the marked rows) measured 20-40 % slower than these full lines.
+template <bool kHalf, bool kSparse>
 __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_gauss_bwd(
-    int P, int D, int M, const int32_t* __restrict__ radii, const uint32_t* __restrict__ slot_start,
+    int P, int D, int M, const uint8_t* __restrict__ gflag, const int32_t* __restrict__ radii,
+    const uint32_t* __restrict__ slot_start,
     const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
     const uint8_t* __restrict__ pflag, const float* __restrict__ gsum,
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
@@ -762,11 +854,15 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
   const bool sh = o_sh != nullptr;
   // partial-record walk first: its loads are in flight before the SH staging
   float g[10];
-  if (gsum) {  // summed by k_sum_partials
+  if (gsum && !kSparse) {  // summed by k_sum_partials
 #pragma unroll
     for (int q = 0; q < 10; ++q) g[q] = i < P ? gsum[(size_t)q * P + i] : 0.f;
-  } else {
-    const bool live = i < P && radii[i] > 0;
+  }
+  const bool live = i < P && (kSparse ? gflag[i] != 0 : radii[i] > 0);
+  if (kSparse) {  // summed by k_sum_active (live rows only)
+#pragma unroll
+    for (int q = 0; q < 10; ++q) g[q] = live ? gsum[(size_t)q * P + i] : 0.f;
+  } else if (!gsum) {
     const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
     sum_partials(s0, s1, pflag, partial, g);
     scale_partial_sums(g, W, H);
@@ -775,23 +871,25 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // camera-side backward first (its registers are dead before the SH
     // phase); the SH term of dL/dmean is added to the stored value after.
     if (i < P)
-      gauss_bwd_one(i, D, M, radii, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
+      gauss_bwd_one(i, D, M, live, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
                     viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
                     o_tau);
     if (sh) {
-      const bool live = i < P && radii[i] > 0;
       const f3 campos = mk3(campos_p[0], campos_p[1], campos_p[2]);
       for (int h = 0; h < 2; ++h) {
         const int h0 = i0 + 32 * h, nh = min(32, P - h0);
         if (nh <= 0) break;  // uniform: P is the same for every lane
-        slab_to_lds(shs + (size_t)h0 * S, nh, S, s_sh, lane);
+        // sparse: the live rows are read by their own lanes below (few per
+        // wave), not staged as a whole slab
+        if (!kSparse) slab_to_lds(shs + (size_t)h0 * S, nh, S, s_sh, lane);
         __syncthreads();
         if ((lane >> 5) == h && i < P) {
           float* row = &s_sh[(lane & 31) * SP];
           if (live) {
             const size_t i3 = 3 * (size_t)i;
-            const f3 dm_sh = sh_backward(D, M, row, mk3(means[i3], means[i3 + 1], means[i3 + 2]), campos,
-                                         clamped[i], mk3(g[6], g[7], g[8]), row);
+            const f3 dm_sh = sh_backward(D, M, kSparse ? shs + (size_t)i * S : row,
+                                         mk3(means[i3], means[i3 + 1], means[i3 + 2]), campos, clamped[i],
+                                         mk3(g[6], g[7], g[8]), row);
             // same sum as the full-slab path: (camera term) + (SH term)
             o_m3d[i3] += dm_sh.x;
             o_m3d[i3 + 1] += dm_sh.y;
@@ -811,8 +909,9 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
     slab_to_lds(shs + (size_t)i0 * S, ng, S, s_sh, lane);
     __syncthreads();
   }
+  static_assert(kHalf || !kSparse, "the sparse variant reads SH rows per lane (32-row output slab)");
   if (i < P)
-    gauss_bwd_one(i, D, M, radii, clamped, g, means, scales, rots, cov_pre,
+    gauss_bwd_one(i, D, M, live, clamped, g, means, scales, rots, cov_pre,
                   sh ? &s_sh[lane * SP] : nullptr, mk3(0.f, 0.f, 0.f), scale_mod, viewm, projm, praw, campos_p, W, H,
                   tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   if (sh) {
@@ -990,27 +1089,35 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
     hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), point_g,
                        at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
-                       dL_ddepth, partial, pflag);
+                       dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag));
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
                      at<float4>(geom, L.splat),
                      at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
-                     a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag);
+                     a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag,
+                     at<uint8_t>(const_cast<void*>(geom), L.gflag));
   return hipGetLastError();
+}
+
+GbMode gauss_bwd_mode() {
+  const char* e = getenv("WGSR_GB");  // read per call: tests switch modes
+  return (e && strcmp(e, "dense") == 0) ? kGbDense : kGbSparse;
 }
 
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
                             const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
                             float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                            float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau, hipStream_t s) {
+                            float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau, GbMode mode,
+                            hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   static const bool split = [] {
     const char* e = getenv("WGSR_GB_SPLIT");
     return e && atoi(e) != 0;
   }();
-  if (split) {
+  float* const gsum_buf = gsum;  // scratch [10][P]
+  if (split && mode == kGbDense) {
     hipLaunchKernelGGL(k_sum_partials, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii,
                        at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), pflag, partial, a.W, a.H, gsum);
   } else {
@@ -1020,8 +1127,19 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
     const char* e = getenv("WGSR_GB_FULLSLAB");
     return e && atoi(e) != 0;
   }();
-  const size_t lds = a.shs ? sizeof(float) * (full_slab ? kGbWave : 32) * (3 * (size_t)a.M + 1) : 0;
-  hipLaunchKernelGGL(full_slab ? k_gauss_bwd<false> : k_gauss_bwd<true>, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M, radii,
+  const bool sparse = mode == kGbSparse;
+  if (sparse) {
+    // (no pair listed: gflag is all zero and k_gauss_bwd never reads gsum)
+    gsum = gsum_buf;
+    if (partial)
+      hipLaunchKernelGGL(k_sum_active, dim3((a.P + 63) / 64), dim3(64), 0, s, a.P, at<uint8_t>(geom, L.gflag),
+                         at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), pflag, partial, a.W, a.H,
+                         gsum);
+  }
+  const size_t lds = a.shs ? sizeof(float) * (full_slab && !sparse ? kGbWave : 32) * (3 * (size_t)a.M + 1) : 0;
+  auto k = sparse ? k_gauss_bwd<true, true> : full_slab ? k_gauss_bwd<false, false> : k_gauss_bwd<true, false>;
+  hipLaunchKernelGGL(k, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M,
+                     at<uint8_t>(geom, L.gflag), radii,
                      at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
                      partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
-    unsigned long long* __restrict__ list_pairs) {
+    unsigned long long* __restrict__ list_pairs, uint8_t* __restrict__ gflag) {
 
   extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
@@ -199,6 +199,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     __syncthreads();
   }
   uint2 ac = make_uint2(0u, 0u);
+  if (i < P) gflag[i] = 0;  // the backward's "received gradient" flag
   if (i < P)
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
                         W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, tiles, clamped, dkey, radii,
@@ -536,7 +537,8 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
-                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs);
+                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs,
+                     at<uint8_t>(geom, L.gflag));
   return hipGetLastError();
 }
 

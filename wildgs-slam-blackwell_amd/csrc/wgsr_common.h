@@ -526,7 +526,7 @@ constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 // Per-Gaussian state (geometry buffer).
 struct GeomLayout {
   size_t splat, rect, rowtab, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, hist, totals,
-      bsum, counter, total;
+      bsum, counter, gflag, total;
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -545,6 +545,8 @@ struct GeomLayout {
     totals = take(kSortTotalsBytes);
     bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
     counter = take(kCounterBytes);  // see kCounterBytes
+    gflag = take(P);               // per Gaussian: some tile's backward wrote a partial record
+                                   // (zeroed by k_preprocess, set by the render backward)
     total = o;
   }
 };
