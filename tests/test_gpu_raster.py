@@ -84,7 +84,7 @@ def check_against(out, expect, grad_keys=GRAD_KEYS, exact_touched=False):
         np.testing.assert_array_equal(out["n_touched"], expect["n_touched"])
     else:
         bad = np.count_nonzero(out["n_touched"] != expect["n_touched"])
-        assert bad <= N_TOUCHED_MISMATCH_TOL * len(out["n_touched"]), bad
+        assert bad <= max(1.0, N_TOUCHED_MISMATCH_TOL * len(out["n_touched"])), bad
     for k in ("color", "depth", "opacity"):
         r = rel_l1(out[k], expect[k])
         assert r <= IMG_TOL, (k, r)
@@ -189,6 +189,29 @@ def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
         a, b = outs["sparse"][k], outs["dense"][k]
         np.testing.assert_array_equal(a == 0, b == 0, err_msg=f"{k} zero rows")
         np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6 * float(np.abs(b).max() + 1e-30), err_msg=k)
+
+
+@pytest.mark.parametrize("P,W,H,deg,view", [(20_000, 640, 480, 3, 2), (6_000, 200, 136, 1, 1),
+                                            (30_000, 1000, 120, 0, 0)])
+def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):
+    """The sorted lists are built per bin of 2^s x 2^s tiles (WGSR_BIN_SHIFT,
+    default 2) and every wave culls the entries that cannot reach it: each
+    pixel blends the same entries in the same order for every s, so images,
+    n_touched and gradients are bit-identical to the per-tile exact lists
+    (s = 0), and match the CPU restatement.  Image sizes that are not
+    multiples of a bin (partial bins on the right / bottom edges) included."""
+    inputs, settings, grads = _synthetic(P, W, H, deg, view)
+    outs = {}
+    for sh in (0, 1, 2, 3):
+        monkeypatch.setenv("WGSR_BIN_SHIFT", str(sh))
+        outs[sh] = run_c(inputs, settings, grads)
+    check_against(outs[2], _cpu_expect(inputs, settings, grads))
+    for sh in (1, 2, 3):
+        for k, v in outs[0].items():
+            if k == "num_rendered":
+                assert outs[sh][k] == v
+            else:
+                np.testing.assert_array_equal(outs[sh][k], v, err_msg=f"shift {sh} {k}")
 
 
 def test_repeated_backward_of_one_forward_is_identical():

@@ -114,8 +114,23 @@ struct Grid {
 };
 
 int tile_sort_bits(const Grid& g) { return num_bits((uint32_t)g.nt) > 0 ? num_bits((uint32_t)g.nt) : 1; }
-// the LSD sort alternates buffers every 8-bit pass
-bool tile_sort_in_alt(const Grid& g) { return ((tile_sort_bits(g) + 7) / 8) % 2 == 1; }
+
+// Sort-bin shift (Bins, wgsr_common.h): the duplicate + radix sort work on
+// (Gaussian, bin) pairs of 2^s x 2^s tiles, and k_expand_bins cuts the sorted
+// bin lists into the exact per-tile lists (the pair key carries the
+// Gaussian's exact tile mask inside the bin).  Default 4 x 4 tiles: at 1080p
+// 510 bins, ~1.3 sorted pairs per visible Gaussian instead of ~9.
+// WGSR_BIN_SHIFT overrides; the forward and its backward must see the same
+// value (the backward recomputes it to find the lists).
+constexpr int kDefaultBinShift = 2;
+int bin_shift(const wgsr_raster_args& a) {
+  const char* e = getenv("WGSR_BIN_SHIFT");
+  int sh = e ? atoi(e) : kDefaultBinShift;
+  sh = sh < 0 ? 0 : (sh > kMaxBinShift ? kMaxBinShift : sh);
+  const Grid g(a);
+  // bin ids fit the key's low 16 bits, list lengths the packed scan's 16 bits
+  return sh > 0 && g.nt > 65535 ? 0 : sh;
+}
 constexpr int kDepthBits = 32;
 constexpr bool kDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;
 
@@ -225,9 +240,11 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // k_preprocess
   uint32_t* counter = at<uint32_t>(geom, GL.counter);
   HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
+  const int bshift = bin_shift(a);
+  const Bins bins(grid.gx, grid.gy, bshift);
   { StageTimer T(0, s);
   STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
-                                reinterpret_cast<unsigned long long*>(counter + 4), s)); }
+                                reinterpret_cast<unsigned long long*>(counter + 4), bshift, s)); }
 
   // The pair counts are known once k_preprocess is done: copy them to pinned
   // host memory behind it and let the depth sort + scan run while the host
@@ -243,52 +260,89 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
                                at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
                                kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt)); }
   const uint32_t* depth_order = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
-  // duplicate-slot offsets in depth order; Gaussian -> first slot
+  // in depth order: duplicate-slot offsets of the exact tile lists (the
+  // backward's record slots; Gaussian -> first slot), and with sort bins the
+  // bin-pair offsets -- their down-sweep writes the pairs, after the binning
+  // buffer exists
   StageTimer* scan_timer = new StageTimer(2, s);
-  STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.offs),
-                                    at<uint32_t>(geom, GL.slot_start), at<uint32_t>(geom, GL.bsum), counter, s));
+  if (bshift) {  // offs[r] = first BIN pair of rank r
+    STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.bsum),
+                                   s));
+    STAGE(a, s, launch_scan_bins_down(a, geom, depth_order, s));
+  } else {
+    STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P,
+                                      at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
+                                      at<uint32_t>(geom, GL.bsum), counter, s));
+  }
   delete scan_timer;
   HIPCHK(hipEventSynchronize(hc.ev));
   const uint32_t* host_counter = hc.buf;
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
   const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
-  size_t N_rect = 0, N = 0;  // upstream num_rendered, pairs actually listed (<= N_rect)
+  // upstream num_rendered, exact (Gaussian, tile) pairs (<= N_rect), (Gaussian, bin) pairs
+  size_t N_rect = 0, N = 0, N_bin = 0;
   for (int i = 0; i < kRectPairLanes; ++i) {
     N_rect += partial[i];
     N += partial[kRectPairLanes + i];
+    N_bin += partial[2 * kRectPairLanes + i];
   }
   if (N > N_rect) return set_error(WGSR_EHIP, "internal: exact tile lists exceed the rectangles");
+  if (N_bin > N_rect) return set_error(WGSR_EHIP, "internal: bin pairs exceed the rectangles");
 
   // the binning layout is sized by upstream's num_rendered (returned to the
-  // caller and handed back to the backward), so both sides agree on it
+  // caller and handed back to the backward), so both sides agree on it; with
+  // sort bins the per-tile lists follow it (2^2s entries per bin pair)
   const BinLayout BL(N_rect);
-  void* binning = call_alloc(binning_alloc, ctx, BL.total);
-  if (!binning && BL.total) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
-  const uint32_t* sorted_keys = nullptr;
-  const uint32_t* sorted_g = nullptr;  // tile lists (Gaussian ids)
-  if (N > 0) {
+  const size_t lists_bytes = bshift ? align256(4 * ((size_t)N_bin << (2 * bshift))) : 0;
+  void* binning = call_alloc(binning_alloc, ctx, BL.total + lists_bytes);
+  if (!binning && BL.total + lists_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  uint32_t* lists = bshift ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
+  uint2* ranges = at<uint2>(image, IL.ranges);
+  // sorted pairs: (Gaussian, bin) pairs, or with bin shift 0 the exact
+  // (Gaussian, tile) pairs themselves
+  const size_t NL = bshift ? N_bin : N;
+  if (NL > 0) {
+    const int bits = bshift ? (num_bits((uint32_t)bins.n) > 0 ? num_bits((uint32_t)bins.n) : 1) : tile_sort_bits(grid);
+    // the LSD sort alternates buffers every pass: start the payload in the
+    // buffer that makes it end in point_g
+    const bool odd = ((bits + 7) / 8) % 2 == 1;
+    uint32_t* vin = at<uint32_t>(binning, odd ? BL.slot_g : BL.point_g);
+    uint32_t* valt = at<uint32_t>(binning, odd ? BL.point_g : BL.slot_g);
     { StageTimer T(3, s);
-    STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key),
-                                 at<uint32_t>(binning, BL.slot_g), at<uint8_t>(binning, BL.flag), s)); }
+    if (bshift) {
+      // the backward's record flags live on the exact slots: zero them here
+      HIPCHK(hipMemsetAsync(at<uint8_t>(binning, BL.flag), 0, N, s));
+      STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint32_t>(binning, BL.key), vin, s));
+    } else {
+      STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
+                                   at<uint8_t>(binning, BL.flag), s));
+    } }
     bool talt = false;
     { StageTimer T(4, s);
-    STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt),
-                                 at<uint32_t>(binning, BL.slot_g), at<uint32_t>(binning, BL.point_g), false, N, 0,
-                                 tile_sort_bits(grid), at<uint32_t>(binning, BL.hist),
-                                 at<uint32_t>(binning, BL.totals), s, &talt)); }
-    // the Gaussian ids are the payload: sorted lists end in point_g after an
-    // odd number of passes, in slot_g after an even one.  The backward
-    // recomputes each pair's duplicate slot from (Gaussian, tile) instead of
-    // carrying it through the sort.
-    if (talt != tile_sort_in_alt(grid)) return set_error(WGSR_EHIP, "internal: tile sort parity");
-    sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
-    sorted_g = at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g);
+    STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false,
+                                 NL, 0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s,
+                                 &talt)); }
+    // the Gaussian ids are the payload; the backward recomputes each pair's
+    // record slot from (Gaussian, tile) instead of carrying it through the sort
+    if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
+    const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
+    StageTimer T(5, s);
+    if (bshift) {
+      // bin bounds in the tile_m region (the forward render writes tile_m later)
+      STAGE(a, s, launch_expand_bins(a, sorted_keys, at<uint32_t>(binning, BL.point_g), (uint32_t)NL, bshift,
+                                     at<uint2>(image, IL.tile_m), lists, ranges, at<uint32_t>(image, IL.tile_len),
+                                     s));
+    } else {
+      STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)NL, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
+                                at<uint32_t>(image, IL.order_fwd), s));
+    }
+  } else {
+    StageTimer T(5, s);  // every list is empty
+    STAGE(a, s, launch_ranges(nullptr, 0u, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
+                              at<uint32_t>(image, IL.order_fwd), s));
   }
-  uint2* ranges = at<uint2>(image, IL.ranges);
-  { StageTimer T(5, s);  // (N = 0: every range is empty)
-  STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)N, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
-                            at<uint32_t>(image, IL.order_fwd), s)); }
+  const uint32_t* sorted_g = lists;
   { StageTimer T(6, s);
   STAGE(a, s, launch_render_fwd(a, ranges, at<uint32_t>(image, IL.order_fwd), sorted_g, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
@@ -325,14 +379,13 @@ int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* bin
   const BinLayout BL(N);
   uint8_t* pflag = N > 0 ? at<uint8_t>(binning, BL.flag) : nullptr;
   if (N > 0) {
-    const bool talt = tile_sort_in_alt(grid);
     StageTimer T(7, s);
     uint32_t* order = at<uint32_t>(image, IL.order_bwd);
     STAGE(a, s, launch_tile_order(at<uint32_t>(image, IL.tile_m), grid.nt, order, s));
-    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order,
-                                  at<uint32_t>(binning, talt ? BL.point_g : BL.slot_g),
-                                  geom,
-                                  at<float>(image, IL.final_T),
+    // the tile lists: after the sized layout with sort bins (same shift as
+    // the forward: bin_shift is a function of the arguments and WGSR_BIN_SHIFT)
+    const uint32_t* lists = bin_shift(a) ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
+    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order, lists, geom, at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
   }
   *partial_out = partial;

@@ -67,8 +67,9 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
-// One Gaussian of k_preprocess; returns (rect area, exact list length), 0 if culled.
-__device__ __forceinline__ uint2 preprocess_one(
+// One Gaussian of k_preprocess; returns (rect area, exact list length, bins
+// touched), 0 if culled.
+__device__ __forceinline__ uint3 preprocess_one(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
@@ -76,12 +77,13 @@ __device__ __forceinline__ uint2 preprocess_one(
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
     ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag,
+    uint32_t* __restrict__ err_flag, int bshift, uint32_t* __restrict__ tb,
     int i, int lane, const float* s_sh) {
 #pragma clang fp contract(off)
   radii[i] = 0;
   n_touched[i] = 0;
   tiles[i] = 0;
+  if (bshift) tb[i] = 0;
   dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort last
 
   Cam c;
@@ -93,7 +95,7 @@ __device__ __forceinline__ uint2 preprocess_one(
   const f3 pv = xform43(c.view, p);
   if (pv.z <= kNearZ) {
     if (prefiltered) atomicOr(err_flag, 1u);
-    return make_uint2(0u, 0u);
+    return make_uint3(0u, 0u, 0u);
   }
   float cv[6];
   if (cov_pre) {
@@ -113,7 +115,7 @@ __device__ __forceinline__ uint2 preprocess_one(
   float a, b, cc;
   cov2d(T, S, a, b, cc);
   const float det = a * cc - b * b;
-  if (det == 0.0f) return make_uint2(0u, 0u);
+  if (det == 0.0f) return make_uint3(0u, 0u, 0u);
   const float det_inv = 1.f / det;
   const float mid = 0.5f * (a + cc);
   const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -125,7 +127,7 @@ __device__ __forceinline__ uint2 preprocess_one(
   const int y0 = min(gy, max(0, (int)((py - r) / kTile)));
   const int x1 = min(gx, max(0, (int)((px + r + kTile - 1) / kTile)));
   const int y1 = min(gy, max(0, (int)((py + r + kTile - 1) / kTile)));
-  if ((x1 - x0) * (y1 - y0) == 0) return make_uint2(0u, 0u);
+  if ((x1 - x0) * (y1 - y0) == 0) return make_uint3(0u, 0u, 0u);
 
   f3 rgb;
   uint32_t cbits = 0;
@@ -173,7 +175,13 @@ __device__ __forceinline__ uint2 preprocess_one(
   clamped[i] = cbits;
   dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
   radii[i] = r;
-  return make_uint2((uint32_t)((x1 - x0) * (y1 - y0)), cnt);
+  // bins of the rect (exact lists are per tile; a bin list holds every
+  // Gaussian whose rect meets the bin, and the render waves cull the rest)
+  const uint32_t nb = cnt == 0 ? 0u
+                               : (uint32_t)((((x1 - 1) >> bshift) - (x0 >> bshift) + 1) *
+                                            (((y1 - 1) >> bshift) - (y0 >> bshift) + 1));
+  if (bshift) tb[i] = cnt | (nb << 16);  // both < 2^16: bin_shift() requires <= 65535 tiles
+  return make_uint3((uint32_t)((x1 - x0) * (y1 - y0)), cnt, nb);
 }
 
 // One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
@@ -189,7 +197,8 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
-    unsigned long long* __restrict__ list_pairs, uint8_t* __restrict__ gflag) {
+    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag) {
 
   extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
@@ -198,23 +207,25 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     slab_to_lds(shs + (size_t)i0 * 3 * M, min(kPreWave, P - i0), 3 * M, s_sh, lane);
     __syncthreads();
   }
-  uint2 ac = make_uint2(0u, 0u);
+  uint3 ac = make_uint3(0u, 0u, 0u);
   if (i < P) gflag[i] = 0;  // the backward's "received gradient" flag
   if (i < P)
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
                         W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, tiles, clamped, dkey, radii,
-                        n_touched, err_flag, i, lane, s_sh);
-  // upstream num_rendered and the exact pair count: one atomic per wave each,
-  // spread over kRectPairLanes words
-  unsigned long long area = ac.x, cnt = ac.y;
+                        n_touched, err_flag, bshift, tb, i, lane, s_sh);
+  // upstream num_rendered, the exact pair count and the bin pair count: one
+  // atomic per wave each, spread over kRectPairLanes words
+  unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     area += __shfl_xor(area, off, 64);
     cnt += __shfl_xor(cnt, off, 64);
+    nbin += __shfl_xor(nbin, off, 64);
   }
   if (lane == 0) {
     atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
     atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
+    atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
   }
 }
 
@@ -301,6 +312,218 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
       keys[k] = ty * (uint32_t)gx + tx;
       slot_g[k] = gg;
       pflag[k] = 0;  // the backward's "record written" flag of this slot
+    }
+  }
+}
+
+// Exact tile mask of the splat inside bin (bx, by): bit rr 2^s + c for the
+// tile (bx 2^s + c, by 2^s + rr) of its exact list (the row table, or
+// row_span past it: the same spans k_duplicate enumerates).
+__device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0, int y0, int x1, int y1,
+                                             const uint4& tab, bool tall, const Reach& rg) {
+  const int B = 1 << bshift;
+  const bool use_tab = x1 - x0 <= 255;
+  uint32_t mask = 0;
+  for (int rr = 0; rr < B; ++rr) {
+    const int ty = (by << bshift) + rr;
+    if (ty < y0 || ty >= y1) continue;
+    const int kr = ty - y0;
+    int xa, len;
+    if (!tall || (use_tab && kr < kRowTab)) {
+      xa = x0 + (int)rowtab_x(tab, kr);
+      len = (int)rowtab_len(tab, kr);
+    } else {
+      len = row_span(rg, ty, x0, x1, xa);
+    }
+    const int cl = max(xa, bx << bshift), ch = min(xa + len, (bx << bshift) + B);
+    if (ch > cl) mask |= ((1u << (ch - cl)) - 1u) << (rr * B + (cl - (bx << bshift)));
+  }
+  return mask;
+}
+
+// Down-sweep of the depth-order scan of tb = (exact list length | bins << 16)
+// (packed_scan_blocks did the block sums): slot_start[g] (the backward's
+// record slots) and boffs[r], the first bin pair of depth rank r (boffs[n] =
+// total).
+__global__ __launch_bounds__(256) void k_scan_bins_down(const uint32_t* __restrict__ tb,
+                                                        const uint32_t* __restrict__ idx, uint32_t n,
+                                                        const uint2* __restrict__ bsum,
+                                                        uint32_t* __restrict__ slot_start,
+                                                        uint32_t* __restrict__ boffs) {
+  __shared__ uint2 s_tmp[4];
+  constexpr int PER = kScanTile / 256;
+  const int t = threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * PER;
+  uint32_t g[PER], v[PER];
+  uint2 acc = make_uint2(0u, 0u);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const size_t i = b0 + j;
+    g[j] = i < n ? idx[i] : 0u;
+    v[j] = i < n ? tb[g[j]] : 0u;
+    acc.x += v[j] & 0xFFFFu;
+    acc.y += v[j] >> 16;
+  }
+  uint2 run = block_excl_scan256_2(acc, s_tmp, nullptr);
+  const uint2 bb = bsum[blockIdx.x];
+  run.x += bb.x;
+  run.y += bb.y;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const size_t i = b0 + j;
+    if (i < n) {
+      slot_start[g[j]] = run.x;
+      boffs[i] = run.y;
+    }
+    run.x += v[j] & 0xFFFFu;
+    run.y += v[j] >> 16;
+  }
+  if (blockIdx.x == gridDim.x - 1 && t == 255) boffs[n] = run.y;
+}
+
+// Expand the bin rectangles of depth ranks [r0, r0 + 64) (one wave) into
+// (key, Gaussian) pairs: lane <-> pair, contiguous writes.  key = bin id (low
+// 16 bits: the sort's digits) | the Gaussian's exact tile list inside the bin
+// as a 2^s x 2^s tile mask (bin_mask; high 16 bits, carried through the
+// sort).  A Gaussian's pairs in row-major bin order (the stable sort by bin
+// keeps the depth order inside each bin).
+__global__ __launch_bounds__(256) void k_duplicate_bins(uint32_t P, int bshift, int gbx,
+                                                        const uint32_t* __restrict__ boffs,
+                                                        const uint32_t* __restrict__ sorted_g,
+                                                        const ushort4* __restrict__ rect,
+                                                        const uint4* __restrict__ rowtab,
+                                                        const float4* __restrict__ splat, uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) - lane;
+  if (r0 >= P) return;
+  const uint32_t r = r0 + lane;
+  const uint32_t my_off = boffs[min(r, P)];
+  const uint32_t start = boffs[r0];
+  const uint32_t end = boffs[min(r0 + 64, P)];
+  uint32_t g = 0, rlo = 0, rhi = 0;
+  uint4 tab = make_uint4(0u, 0u, 0u, 0u);
+  bool tall = false;
+  if (r < P && boffs[r + 1] > my_off) {
+    g = sorted_g[r];
+    const ushort4 rc = rect[g];
+    rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
+    rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);  // exclusive
+    tab = rowtab[g];
+    tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
+  }
+  const bool any_tall = wave_any(tall);
+  Reach rr{};
+  if (any_tall && tall) rr = reach_of(splat[3 * (size_t)g], splat[3 * (size_t)g + 1]);
+  for (uint32_t base = start; base < end; base += 64) {
+    const uint32_t k = base + lane;
+    const uint32_t kk = min(k, end - 1);
+    int lo = 0, hi = 64;
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const int mid = (lo + hi) >> 1;
+      const uint32_t v = __shfl(my_off, mid, 64);
+      if (v <= kk) lo = mid; else hi = mid;
+    }
+    const uint32_t local = kk - __shfl(my_off, lo, 64);
+    const uint32_t gg = __shfl(g, lo, 64);
+    const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
+    const int x0 = (int)(a & 0xFFFFu), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFFu), y1 = (int)(b >> 16);
+    const uint4 tb = make_uint4(__shfl(tab.x, lo, 64), __shfl(tab.y, lo, 64), __shfl(tab.z, lo, 64),
+                                __shfl(tab.w, lo, 64));
+    const bool tl = __shfl((int)tall, lo, 64) != 0;
+    Reach rg{};
+    if (any_tall) {  // wave-uniform: the shuffles need every lane
+      rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
+      rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
+      rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
+      rg.ok = __shfl(rr.ok, lo, 64);
+    }
+    const int bx0 = x0 >> bshift, bw = ((x1 - 1) >> bshift) - bx0 + 1;
+    const int row = (int)local / bw;
+    const int bx = bx0 + ((int)local - row * bw), by = (y0 >> bshift) + row;
+    if (k < end) {
+      keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tb, tl, rg) << 16);
+      vals[k] = gg;
+    }
+  }
+}
+
+// [start, end) of every bin in the bin-sorted keys (upstream's
+// identifyTileRanges on bin ids): one thread per entry, bins with no entry
+// keep the zero range written before the launch.
+__global__ __launch_bounds__(256) void k_bin_bounds(const uint32_t* __restrict__ skeys, uint32_t NB,
+                                                    uint2* __restrict__ bounds) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NB) return;
+  const uint32_t b = skeys[e] & 0xFFFFu;
+  if (e == 0 || (skeys[e - 1] & 0xFFFFu) != b) bounds[b].x = e;
+  if (e + 1 == NB || (skeys[e + 1] & 0xFFFFu) != b) bounds[b].y = e + 1;
+}
+
+// One workgroup per (bin, row of its tiles): the exact lists of the row's
+// 2^s tiles, in depth order, out of the bin's sorted entries -- an entry
+// belongs to tile c if bit c of its key's row mask is set; a block-wide
+// stable compaction per tile keeps the order.  Tile (r, c) of a bin whose
+// entries sit at [lo, hi) writes at lists[2^2s lo + (r 2^s + c) (hi - lo) ...],
+// a region as long as the bin's list: no count pass, no overlap.
+__global__ __launch_bounds__(256) void k_expand_bins(const uint32_t* __restrict__ skeys,
+                                                     const uint32_t* __restrict__ sgid,
+                                                     const uint2* __restrict__ bounds, int gx, int gy, int bshift,
+                                                     int gbx, uint32_t* __restrict__ lists, uint2* __restrict__ ranges,
+                                                     uint32_t* __restrict__ tile_len) {
+  __shared__ uint32_t s_wc[4][4];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int B = 1 << bshift;
+  const uint32_t bin = blockIdx.x >> bshift;
+  const int r = (int)(blockIdx.x & (uint32_t)(B - 1));
+  const int bx = (int)(bin % (uint32_t)gbx), by = (int)(bin / (uint32_t)gbx);
+  const int ty = (by << bshift) + r;
+  if (ty >= gy) return;  // block-uniform
+  const uint2 bb = bounds[bin];
+  const uint32_t lo = bb.x, hi = bb.y, len = hi - lo;
+  const size_t base0 = ((size_t)lo << (2 * bshift)) + (size_t)(r << bshift) * len;
+  const uint32_t shift = 16u + ((uint32_t)r << bshift), rmask = (1u << B) - 1u;
+  uint32_t count[4] = {0u, 0u, 0u, 0u};
+  // chunk k + 1's keys and ids are in flight while chunk k is ranked
+  uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
+  for (uint32_t e0 = lo; e0 < hi; e0 += 256) {
+    const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
+    const uint32_t e1 = e0 + 256 + t;
+    key = e1 < hi ? skeys[e1] : 0u;
+    gid = e1 < hi ? sgid[e1] : 0u;
+    uint64_t m[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m[c] = wave_ballot(c < B && ((bits >> c) & 1u));
+      if (lane == 0 && c < B) s_wc[w][c] = (uint32_t)__popcll(m[c]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= B) break;
+      uint32_t off = count[c], tot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = s_wc[k][c];
+        off += k < w ? v : 0u;
+        tot += v;
+      }
+      if ((bits >> c) & 1u) lists[base0 + (size_t)c * len + off + lanes_below(m[c])] = my_gid;
+      count[c] += tot;
+    }
+    __syncthreads();
+  }
+  if (t < B) {
+    const int tx = (bx << bshift) + t;
+    if (tx < gx) {
+      const uint32_t tile = (uint32_t)ty * (uint32_t)gx + (uint32_t)tx;
+      const size_t b0 = base0 + (size_t)t * len;
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c = k == t ? count[k] : c;
+      ranges[tile] = make_uint2((uint32_t)b0, (uint32_t)b0 + c);
+      tile_len[tile] = c;
     }
   }
 }
@@ -398,6 +621,49 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict_
 // ahead).
 constexpr int kFwdBatch = 64;
 
+// One batch of staged list entries for one wave (8x8 quadrant): cull by the
+// exact ellipse test against the wave's pixel box, then blend the survivors
+// front to back.  Contributor number of entry j: cbase + j, or (bin lists)
+// sIdx[j] + 1, its position in the bin's list.  n_touched increments are
+// staged per entry in sTouch and leave as one atomic wave instruction.
+template <bool kIdx>
+__device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const uint32_t* sIdx, const float4* sA,
+                                                const float4* sB, const float4* sC, const uint32_t* sG,
+                                                uint32_t* sTouch, int wx0, int wx1, int wy0, int wy1, v2f pxy,
+                                                int lane, int32_t* __restrict__ n_touched, float& T, v2f& c01,
+                                                v2f& c2d, uint32_t& last, uint64_t& dm) {
+  uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+  sTouch[lane] = 0;
+  while (todo != 0 && dm != ~0ull) {
+    const int j = __builtin_ctzll(todo);
+    todo &= ~(1ull << j);
+    const float4 A = sA[j];
+    const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
+    const float4 Cc = sC[j];
+    const v2f d = v2f{A.x, A.y} - pxy;                     // (dx, dy) = mean - pixel
+    const v2f q2 = v2f{A.z, A.w} * d * d;                  // log2(e) x (-conic_xx dx^2/2, -conic_yy dy^2/2)
+    const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
+    const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
+    const float test_T = fmaf(-T, alpha, T);  // T (1 - alpha)
+    const uint64_t live = wave_ballot(power <= 0.0f) & wave_ballot(alpha >= kMinAlpha) & ~dm;
+    const uint64_t low = wave_ballot(test_T < kMinT);
+    const uint64_t blend = live & ~low;
+    const bool bl = __builtin_amdgcn_inverse_ballot_w64(blend);
+    const float wgt = bl ? alpha * T : 0.f;
+    c01 += wgt * v2f{Cc.x, Cc.y};
+    c2d += wgt * v2f{Cc.z, Cc.w};
+    // upstream n_touched: pixels whose T stays above 0.5 after this blend
+    const uint32_t tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
+    T = bl ? test_T : T;
+    last = bl ? (kIdx ? sIdx[j] + 1u : cbase + j) : last;
+    dm |= live & low;
+    sTouch[j] = tot;  // (every lane stores the same value: no branch)
+  }
+  // one atomic per touched entry, all of the batch's in one wave instruction
+  const uint32_t tv = sTouch[lane];
+  if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
+}
+
 // One 16x16 tile per workgroup of 4 waves; wave w owns the 8x8 quadrant w,
 // one pixel per lane.  Every per-pixel predicate (done, live, low, blend) is
 // an explicit SGPR lane mask combined by scalar ops: the per-entry update is
@@ -464,37 +730,8 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     }
     if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-    const uint32_t cbase = b0 - range.x + 1;  // contributor number of entry j = cbase + j
-    uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-    sTouch[w][lane] = 0;
-    while (todo != 0 && dm != ~0ull) {
-      const int j = __builtin_ctzll(todo);
-      todo &= ~(1ull << j);
-      const float4 A = sA[j];
-      const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
-      const float4 Cc = sC[j];
-      const v2f d = v2f{A.x, A.y} - pxy;                     // (dx, dy) = mean - pixel
-      const v2f q2 = v2f{A.z, A.w} * d * d;                  // log2(e) x (-conic_xx dx^2/2, -conic_yy dy^2/2)
-      const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
-      const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
-      const float test_T = fmaf(-T, alpha, T);  // T (1 - alpha)
-      const uint64_t live = wave_ballot(power <= 0.0f) & wave_ballot(alpha >= kMinAlpha) & ~dm;
-      const uint64_t low = wave_ballot(test_T < kMinT);
-      const uint64_t blend = live & ~low;
-      const bool bl = __builtin_amdgcn_inverse_ballot_w64(blend);
-      const float wgt = bl ? alpha * T : 0.f;
-      c01 += wgt * v2f{Cc.x, Cc.y};
-      c2d += wgt * v2f{Cc.z, Cc.w};
-      // upstream n_touched: pixels whose T stays above 0.5 after this blend
-      const uint32_t tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
-      T = bl ? test_T : T;
-      last = bl ? cbase + j : last;
-      dm |= live & low;
-      sTouch[w][j] = tot;  // (every lane stores the same value: no branch)
-    }
-    // one atomic per touched entry, all of the batch's in one wave instruction
-    const uint32_t tv = sTouch[w][lane];
-    if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
+    fwd_blend_batch<false>(cnt, b0 - range.x + 1, nullptr, sA, sB, sC, sG, sTouch[w], wx0, wx1, wy0, wy1, pxy, lane,
+                           n_touched, T, c01, c2d, last, dm);
   }
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
     uint32_t mx = last;
@@ -527,8 +764,9 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 }  // namespace
 
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s) {
+                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, hipStream_t s) {
   unsigned long long* list_pairs = rect_pairs + kRectPairLanes;
+  unsigned long long* bin_pairs = rect_pairs + 2 * kRectPairLanes;
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
@@ -538,7 +776,41 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
                      at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs,
-                     at<uint8_t>(geom, L.gflag));
+                     bin_pairs, bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag));
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_bins_down(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  const GeomLayout L(a.P);
+  const uint32_t nbs = (uint32_t)((a.P + kScanTile - 1) / kScanTile);
+  hipLaunchKernelGGL(k_scan_bins_down, dim3(nbs), dim3(256), 0, s, at<uint32_t>(geom, L.tb), depth_order,
+                     (uint32_t)a.P, at<uint2>(geom, L.bsum), at<uint32_t>(const_cast<void*>(geom), L.slot_start),
+                     at<uint32_t>(const_cast<void*>(geom), L.offs));
+  return hipGetLastError();
+}
+
+hipError_t launch_duplicate_bins(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, int bshift,
+                                 uint32_t* keys, uint32_t* vals, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  const GeomLayout L(a.P);
+  const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
+  hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + 255) / 256), dim3(256), 0, s, (uint32_t)a.P, bshift, B.bx,
+                     at<uint32_t>(geom, L.offs), depth_order, at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
+                     at<float4>(geom, L.splat), keys, vals);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
+                              uint32_t NB, int bshift, uint2* bounds, uint32_t* lists, uint2* ranges,
+                              uint32_t* tile_len, hipStream_t s) {
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  const Bins B(gx, gy, bshift);
+  hipError_t e = hipMemsetAsync(bounds, 0, sizeof(uint2) * (size_t)B.n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
+  hipLaunchKernelGGL(k_expand_bins, dim3((uint32_t)B.n << bshift), dim3(256), 0, s, sorted_keys, sorted_g, bounds, gx,
+                     gy, bshift, B.bx, lists, ranges, tile_len);
   return hipGetLastError();
 }
 
@@ -594,8 +866,8 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
   hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, fwd_lpt() ? order : nullptr, point_g,
-                     at<float4>(geom, L.splat), a.W,
-                     a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T, n_contrib, n_touched, tile_m);
+                     at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T,
+                     n_contrib, n_touched, tile_m);
   return hipGetLastError();
 }
 

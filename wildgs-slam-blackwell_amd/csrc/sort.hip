@@ -348,6 +348,48 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
   if (blockIdx.x == gridDim.x - 1 && t == 255) out[n] = run;  // grand total at out[n]
 }
 
+// ---- exclusive scan of packed pairs (lo 16 | hi 16 bits) gathered by index --
+// (the exact tile-list length and the bin count of each Gaussian, in depth
+// order: one gather of one word for both sums; sums kept as two u32s)
+__global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed,
+                                                      const uint32_t* __restrict__ idx, uint32_t n,
+                                                      uint2* __restrict__ bsum) {
+  __shared__ uint2 s_tmp[4];
+  const int t = threadIdx.x;
+  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * (kScanTile / 256);
+  uint2 acc = make_uint2(0u, 0u);
+#pragma unroll
+  for (int j = 0; j < kScanTile / 256; ++j) {
+    const size_t i = b0 + j;
+    if (i < n) {
+      const uint32_t v = packed[idx[i]];
+      acc.x += v & 0xFFFFu;
+      acc.y += v >> 16;
+    }
+  }
+  uint2 tot;
+  block_excl_scan256_2(acc, s_tmp, &tot);
+  if (t == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan2_bsum(uint2* __restrict__ bsum, uint32_t nbs) {
+  __shared__ uint2 s_tmp[4];
+  const int t = threadIdx.x;
+  const uint32_t per = (nbs + 255) / 256;
+  const uint32_t b0 = t * per, b1 = min(nbs, b0 + per);
+  uint2 acc = make_uint2(0u, 0u);
+  for (uint32_t b = b0; b < b1; ++b) { acc.x += bsum[b].x; acc.y += bsum[b].y; }
+  uint2 tot;
+  uint2 run = block_excl_scan256_2(acc, s_tmp, &tot);
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint2 x = bsum[b];
+    bsum[b] = run;
+    run.x += x.x;
+    run.y += x.y;
+  }
+  if (t == 0) bsum[nbs] = tot;
+}
+
 }  // namespace
 
 // WGSR_SORT=onesweep | onesweep_small (only sorts of <= kSmallSortN keys) |
@@ -443,6 +485,15 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
   hipLaunchKernelGGL(k_scan_reduce, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum);
   hipLaunchKernelGGL(k_scan_bsum, dim3(1), dim3(256), 0, stream, bsum, nbs, total_out);
   hipLaunchKernelGGL(k_scan_down, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum, out, scatter_out);
+  return hipGetLastError();
+}
+
+hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_t n, void* bsum, hipStream_t stream) {
+  const uint32_t nbs = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  if (n == 0) return hipMemsetAsync(bsum, 0, sizeof(uint2), stream);
+  uint2* bs = static_cast<uint2*>(bsum);
+  hipLaunchKernelGGL(k_scan2_reduce, dim3(nbs), dim3(256), 0, stream, packed, idx, (uint32_t)n, bs);
+  hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(256), 0, stream, bs, nbs);
   return hipGetLastError();
 }
 

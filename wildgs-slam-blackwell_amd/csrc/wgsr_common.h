@@ -109,6 +109,25 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// exclusive scan of two u32 values per thread over a 256-thread block
+__device__ __forceinline__ uint2 block_excl_scan256_2(uint2 v, uint2* s_tmp4, uint2* total) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t ia = wave_incl_scan(v.x), ib = wave_incl_scan(v.y);
+  if (lane == 63) s_tmp4[w] = make_uint2(ia, ib);
+  __syncthreads();
+  uint2 base = make_uint2(0u, 0u), tot = make_uint2(0u, 0u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint2 x = s_tmp4[i];
+    if (i < w) { base.x += x.x; base.y += x.y; }
+    tot.x += x.x;
+    tot.y += x.y;
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return make_uint2(base.x + ia - v.x, base.y + ib - v.y);
+}
+
 // Wave votes on a lane predicate that stays an SGPR lane mask (HIP's int
 // __ballot / __any / __all materialise the predicate in a VGPR first).
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
@@ -508,8 +527,22 @@ __host__ __device__ inline uint32_t sort_blocks(size_t n) {
 // so that the per-wave atomics of k_preprocess do not serialise on one word)
 constexpr int kRectPairLanes = 64;
 // geometry counter block: u32 [0] scan total, [1] error flags, [2..3] pad,
-// then u64 rect-pair partials [kRectPairLanes], then u64 listed-pair partials
-constexpr size_t kCounterBytes = 16 + 2 * 8 * kRectPairLanes;
+// then u64 rect-pair partials [kRectPairLanes], u64 listed-pair partials
+// [kRectPairLanes], u64 bin-pair partials [kRectPairLanes]
+constexpr size_t kCounterBytes = 16 + 3 * 8 * kRectPairLanes;
+
+// ---- sort bins ----------------------------------------------------------------
+// The (Gaussian, tile) lists are sorted as (Gaussian, BIN) pairs of 2^s x 2^s
+// tiles -- ~7x fewer pairs to duplicate and radix-sort at s = 2 -- and then
+// cut into the exact per-tile lists (k_expand_bins).  shift 0 = sort the
+// exact (Gaussian, tile) pairs directly.
+constexpr int kMaxBinShift = 2;  // the exact tile mask of a bin (2^2s bits) rides in 16 key bits
+struct Bins {
+  int shift, bx, by, n;  // bins per row / column, bin count
+  __host__ __device__ Bins(int gx, int gy, int sh)
+      : shift(sh), bx((gx + (1 << sh) - 1) >> sh), by((gy + (1 << sh) - 1) >> sh), n(bx * by) {}
+  __host__ __device__ int of_tile(int tx, int ty) const { return (ty >> shift) * bx + (tx >> shift); }
+};
 // Onesweep radix sort scratch (sort.hip): look-back status words for up to
 // kMaxSortPasses 8-bit passes, and global digit histograms + block counters.
 constexpr int kMaxSortPasses = 4;
@@ -525,8 +558,8 @@ constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
 // Per-Gaussian state (geometry buffer).
 struct GeomLayout {
-  size_t splat, rect, rowtab, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, hist, totals,
-      bsum, counter, gflag, total;
+  size_t splat, rect, rowtab, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, tb, hist,
+      totals, bsum, counter, gflag, total;
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -541,9 +574,10 @@ struct GeomLayout {
     dval_alt = take(4 * P);
     offs = take(4 * (P + 1));      // rank -> first duplicate slot
     slot_start = take(4 * P);      // Gaussian -> first duplicate slot
+    tb = take(4 * P);              // sort bins: exact list length | bins touched << 16
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
-    bsum = take(4 * ((P + kScanTile - 1) / kScanTile + 1));
+    bsum = take(8 * ((P + kScanTile - 1) / kScanTile + 1));  // uint2 block sums of the dual scan
     counter = take(kCounterBytes);  // see kCounterBytes
     gflag = take(P);               // per Gaussian: some tile's backward wrote a partial record
                                    // (zeroed by k_preprocess, set by the render backward)
@@ -575,7 +609,7 @@ struct ImageLayout {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
     const size_t nt = (size_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    ranges = take(8 * nt);
+    ranges = take(8 * nt);     // list [start, end) per tile
     tile_len = take(4 * nt);   // list length per tile (forward work)
     tile_m = take(16 * nt);    // deepest contributor per tile quadrant (backward work)
     order_fwd = take(4 * nt);  // launch orders (heaviest first per XCD chunk)

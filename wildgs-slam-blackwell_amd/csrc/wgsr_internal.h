@@ -21,6 +21,12 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
 hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
                                  uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream);
 
+// First two steps of a scan of packed (lo 16 | hi 16) values gathered as
+// packed[idx[i]]: bsum[b] = exclusive prefix (lo sums, hi sums) of block b of
+// kScanTile elements, bsum[blocks] = totals.  bsum: 8 x (blocks + 1) bytes.
+// The down-sweep is the caller's (k_scan_bins_down emits pairs).
+hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_t n, void* bsum, hipStream_t stream);
+
 int num_bits(uint32_t n);  // bits needed to represent values in [0, n)
 
 // thread-local error message plumbing for the C ABI
@@ -33,10 +39,22 @@ struct RasterGrid {
 // forward stages (raster_fwd.hip)
 // rect_pairs[0..kRectPairLanes) += upstream's num_rendered contributions (rect
 // areas); rect_pairs[kRectPairLanes..2 kRectPairLanes) += exact list lengths
+// rect_pairs[2 kRectPairLanes..3 kRectPairLanes) += bins touched (bshift > 0;
+// geometry tb[g] = exact list length | bins touched << 16)
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, unsigned long long* rect_pairs, hipStream_t s);
+                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, hipStream_t s);
+// Sort bins: the scan's down-sweep (slot_start[g]; offs[r] = first bin pair
+// of depth rank r), then the (bin | exact tile mask << 16, Gaussian) pairs.
+hipError_t launch_scan_bins_down(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, hipStream_t s);
+hipError_t launch_duplicate_bins(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, int bshift,
+                                 uint32_t* keys, uint32_t* vals, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
+// per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
+// tile, the lists in bin-sized regions of `lists` (2^2s x NB entries)
+hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
+                              uint32_t NB, int bshift, uint2* bounds, uint32_t* lists, uint2* ranges,
+                              uint32_t* tile_len, hipStream_t s);
 // tile ranges + the forward's launch order (tiles by list length, per XCD chunk)
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
                          uint32_t* order, hipStream_t s);
