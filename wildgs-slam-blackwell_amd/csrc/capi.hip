@@ -265,10 +265,9 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // bin-pair offsets -- their down-sweep writes the pairs, after the binning
   // buffer exists
   StageTimer* scan_timer = new StageTimer(2, s);
-  if (bshift) {  // offs[r] = first BIN pair of rank r
+  if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
     STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.bsum),
                                    s));
-    STAGE(a, s, launch_scan_bins_down(a, geom, depth_order, s));
   } else {
     STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P,
                                       at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
@@ -311,9 +310,9 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     uint32_t* valt = at<uint32_t>(binning, odd ? BL.point_g : BL.slot_g);
     { StageTimer T(3, s);
     if (bshift) {
-      // the backward's record flags live on the exact slots: zero them here
-      HIPCHK(hipMemsetAsync(at<uint8_t>(binning, BL.flag), 0, N, s));
-      STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint32_t>(binning, BL.key), vin, s));
+      // (the backward's record flags live on the exact slots: zeroed here too)
+      STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
+                                        at<uint32_t>(binning, BL.key), vin, s));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
@@ -360,8 +359,8 @@ namespace {
 // and the view-sharded records path.
 int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* binning, void* image,
                           int64_t num_rendered, const float* dL_dcolor, const float* dL_ddepth,
-                          wgsr_alloc_fn scratch_alloc, void* ctx, hipStream_t s, float4** partial_out,
-                          uint8_t** pflag_out) {
+                          wgsr_alloc_fn scratch_alloc, void* ctx, const ZeroJob& zero, hipStream_t s,
+                          float4** partial_out, uint8_t** pflag_out) {
   if (!geom || !image || (num_rendered > 0 && !binning))
     return set_error(WGSR_EINVAL, "missing forward state buffers");
   const Grid grid(a);
@@ -386,7 +385,11 @@ int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* bin
     // the forward: bin_shift is a function of the arguments and WGSR_BIN_SHIFT)
     const uint32_t* lists = bin_shift(a) ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
     STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order, lists, geom, at<float>(image, IL.final_T),
-                                  at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, s));
+                                  at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, zero,
+                                  s));
+  } else {
+    // no render backward to carry the zero fill
+    for (int j = 0; j < zero.count; ++j) HIPCHK(hipMemsetAsync(zero.p[j], 0, sizeof(float) * zero.n[j], s));
   }
   *partial_out = partial;
   *pflag_out = pflag;
@@ -409,15 +412,29 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   hipStream_t s = (hipStream_t)stream;
   float4* partial = nullptr;
   uint8_t* pflag = nullptr;
+  // sparse per-Gaussian backward: the render backward zero-fills the outputs
+  // and k_gauss_bwd writes only the rows that received gradient
+  const GbMode mode = gauss_bwd_mode();
+  ZeroJob zero{};
+  if (mode == kGbSparse) {
+    const uint64_t P = (uint64_t)a.P;
+    auto add = [&](float* p, uint64_t n) {
+      if (p && n) { zero.p[zero.count] = p; zero.n[zero.count] = n; ++zero.count; }
+    };
+    add(dL_dmeans2D, 3 * P); add(dL_dcolors, 3 * P); add(dL_dopacity, P); add(dL_dmeans3D, 3 * P);
+    add(dL_dcov3D, 6 * P); add(a.shs ? dL_dsh : nullptr, 3 * (uint64_t)a.M * P); add(dL_dscales, 3 * P);
+    add(dL_drotations, 4 * P); add(dL_dtau, 6 * P);
+    for (int j = 0; j < zero.count; ++j)
+      if (reinterpret_cast<uintptr_t>(zero.p[j]) & 3) return set_error(WGSR_EINVAL, "gradient outputs must be 4-byte aligned");
+  }
   if (int e = render_backward_pairs(a, geom, binning, image, num_rendered, dL_dcolor, dL_ddepth, scratch_alloc, ctx,
-                                    s, &partial, &pflag))
+                                    zero, s, &partial, &pflag))
     return e;
   float* gsum = partial ? reinterpret_cast<float*>(reinterpret_cast<char*>(partial) + align256(48 * (size_t)num_rendered))
                         : nullptr;
   StageTimer T(8, s);
   STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, gsum, dL_dmeans2D, dL_dcolors, dL_dopacity,
-                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, gauss_bwd_mode(),
-                               s));
+                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, mode, true, s));
   return WGSR_OK;
 }
 
@@ -443,7 +460,7 @@ int wgsr_rasterize_backward_records(const wgsr_raster_args* args, const int32_t*
   uint8_t* pflag = nullptr;
   if (a.P > 0) {
     if (int e = render_backward_pairs(a, geom, binning, image, num_rendered, dL_dcolor, dL_ddepth, scratch_alloc,
-                                      ctx, s, &partial, &pflag))
+                                      ctx, ZeroJob{}, s, &partial, &pflag))
       return e;
   }
   StageTimer T(8, s);

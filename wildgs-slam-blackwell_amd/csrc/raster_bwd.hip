@@ -49,7 +49,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
-    uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag) {
+    uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
   constexpr int Q = 4;
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sG[kBatch];
@@ -213,6 +213,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       gflag[gid] = 1;  // same value from every tile: a benign race
     }
   }
+  // this tile's share of the per-Gaussian outputs' zero fill (HBM is idle
+  // here; measured at 1M/1080p: render_bwd +2 % with the fill after the walk,
+  // +4.5 % before it, while k_gauss_bwd drops from 86 to 49 us)
+  zero_share(zero, blockIdx.x, gridDim.x, lane, 64);
 }
 
 // Small images (few tiles: TUM's 512x384 has 768) leave most SIMDs without a
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
     const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W,
     int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
-    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag) {
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
   __shared__ uint32_t sG[kBatch];
   __shared__ float sP[4][kBatch][11];
@@ -360,6 +364,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       }
     }
   }
+  zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
 }
 
 __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]); }
@@ -845,7 +850,8 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
     const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
     float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau,
+    bool zeroed) {
   extern __shared__ float s_sh[];  // kGbWave x (3M + 1) floats (dynamic)
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kGbWave, i = i0 + lane;
@@ -866,6 +872,25 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
     const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
     sum_partials(s0, s1, pflag, partial, g);
     scale_partial_sums(g, W, H);
+  }
+  if (kSparse && zeroed) {
+    // the render backward zero-filled every output: only the live rows are
+    // written, each by its own lane (dL/dsh straight to its 3M-float row)
+    if (!wave_any(live)) return;
+    if (!live) return;
+    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
+                  viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
+                  o_tau);
+    if (sh) {
+      const size_t i3 = 3 * (size_t)i;
+      const f3 dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
+                                   mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
+                                   o_sh + (size_t)i * S);
+      o_m3d[i3] += dm_sh.x;  // (camera term) + (SH term), as in the other paths
+      o_m3d[i3 + 1] += dm_sh.y;
+      o_m3d[i3 + 2] += dm_sh.z;
+    }
+    return;
   }
   if (kHalf) {
     // camera-side backward first (its registers are dead before the SH
@@ -1078,7 +1103,7 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd_views(
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
                              const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
-                             float4* partial, uint8_t* pflag, hipStream_t s) {
+                             float4* partial, uint8_t* pflag, const ZeroJob& zero, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
@@ -1089,14 +1114,14 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
     hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), point_g,
                        at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
-                       dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag));
+                       dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
                      at<float4>(geom, L.splat),
                      at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
                      a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag,
-                     at<uint8_t>(const_cast<void*>(geom), L.gflag));
+                     at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
   return hipGetLastError();
 }
 
@@ -1109,7 +1134,7 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                             const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
                             float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
                             float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau, GbMode mode,
-                            hipStream_t s) {
+                            bool zeroed, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   static const bool split = [] {
@@ -1144,7 +1169,7 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                      partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
                      dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
-                     dL_dscales, dL_drot, dL_dtau);
+                     dL_dscales, dL_drot, dL_dtau, sparse && zeroed);
   return hipGetLastError();
 }
 

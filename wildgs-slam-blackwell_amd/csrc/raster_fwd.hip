@@ -341,95 +341,77 @@ __device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0,
   return mask;
 }
 
-// Down-sweep of the depth-order scan of tb = (exact list length | bins << 16)
-// (packed_scan_blocks did the block sums): slot_start[g] (the backward's
-// record slots) and boffs[r], the first bin pair of depth rank r (boffs[n] =
-// total).
-__global__ __launch_bounds__(256) void k_scan_bins_down(const uint32_t* __restrict__ tb,
-                                                        const uint32_t* __restrict__ idx, uint32_t n,
-                                                        const uint2* __restrict__ bsum,
-                                                        uint32_t* __restrict__ slot_start,
-                                                        uint32_t* __restrict__ boffs) {
-  __shared__ uint2 s_tmp[4];
-  constexpr int PER = kScanTile / 256;
-  const int t = threadIdx.x;
-  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * PER;
-  uint32_t g[PER], v[PER];
-  uint2 acc = make_uint2(0u, 0u);
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const size_t i = b0 + j;
-    g[j] = i < n ? idx[i] : 0u;
-    v[j] = i < n ? tb[g[j]] : 0u;
-    acc.x += v[j] & 0xFFFFu;
-    acc.y += v[j] >> 16;
-  }
-  uint2 run = block_excl_scan256_2(acc, s_tmp, nullptr);
-  const uint2 bb = bsum[blockIdx.x];
-  run.x += bb.x;
-  run.y += bb.y;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const size_t i = b0 + j;
-    if (i < n) {
-      slot_start[g[j]] = run.x;
-      boffs[i] = run.y;
-    }
-    run.x += v[j] & 0xFFFFu;
-    run.y += v[j] >> 16;
-  }
-  if (blockIdx.x == gridDim.x - 1 && t == 255) boffs[n] = run.y;
-}
-
-// Expand the bin rectangles of depth ranks [r0, r0 + 64) (one wave) into
-// (key, Gaussian) pairs: lane <-> pair, contiguous writes.  key = bin id (low
-// 16 bits: the sort's digits) | the Gaussian's exact tile list inside the bin
-// as a 2^s x 2^s tile mask (bin_mask; high 16 bits, carried through the
-// sort).  A Gaussian's pairs in row-major bin order (the stable sort by bin
-// keeps the depth order inside each bin).
-__global__ __launch_bounds__(256) void k_duplicate_bins(uint32_t P, int bshift, int gbx,
-                                                        const uint32_t* __restrict__ boffs,
-                                                        const uint32_t* __restrict__ sorted_g,
-                                                        const ushort4* __restrict__ rect,
-                                                        const uint4* __restrict__ rowtab,
-                                                        const float4* __restrict__ splat, uint32_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t r0 = (blockIdx.x * blockDim.x + threadIdx.x) - lane;
-  if (r0 >= P) return;
-  const uint32_t r = r0 + lane;
-  const uint32_t my_off = boffs[min(r, P)];
-  const uint32_t start = boffs[r0];
-  const uint32_t end = boffs[min(r0 + 64, P)];
-  uint32_t g = 0, rlo = 0, rhi = 0;
+// Sort bins, after the dual scan's block sums (packed_scan_blocks: bsum[b]
+// = exclusive prefix of (exact list length, bins touched) over the 256-rank
+// blocks in depth order): each 256-thread workgroup finishes the scan for its
+// ranks (thread <-> rank) -- slot_start[g], the backward's record slots, and
+// the ranks' first bin pair -- zeroes the "record written" flags of its slots,
+// and every wave expands its 64 ranks' bin rectangles into (key, Gaussian)
+// pairs: lane <-> pair, contiguous writes.  key = bin id (low 16 bits: the
+// sort's digits) | the Gaussian's exact tile list inside the bin as a
+// 2^s x 2^s tile mask (bin_mask; high 16 bits, carried through the sort).  A
+// Gaussian's pairs in row-major bin order (the stable sort by bin keeps the
+// depth order inside each bin).
+constexpr int kDupScanThreads = kPackedScanTile;  // one rank per thread
+__global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
+    uint32_t P, int bshift, int gbx, const uint32_t* __restrict__ tbv, const uint32_t* __restrict__ sorted_g,
+    const uint2* __restrict__ bsum, const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab,
+    const float4* __restrict__ splat, uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag,
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  constexpr int NW = kDupScanThreads / 64;
+  __shared__ uint2 s_w[NW];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t r = blockIdx.x * kDupScanThreads + t;
+  const bool in = r < P;
+  const uint32_t g = in ? sorted_g[r] : 0u;
+  const uint32_t v = in ? tbv[g] : 0u;
+  const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
+  uint32_t rlo = 0, rhi = 0;
   uint4 tab = make_uint4(0u, 0u, 0u, 0u);
   bool tall = false;
-  if (r < P && boffs[r + 1] > my_off) {
-    g = sorted_g[r];
+  if (nb) {
     const ushort4 rc = rect[g];
     rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
     rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);  // exclusive
     tab = rowtab[g];
     tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
   }
+  const uint32_t ic = wave_incl_scan(cnt), ib = wave_incl_scan(nb);
+  if (lane == 63) s_w[w] = make_uint2(ic, ib);
+  __syncthreads();
+  uint2 wb = bsum[blockIdx.x];  // this block's first slot / first bin pair
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint2 x = s_w[k];
+    if (k < w) { wb.x += x.x; wb.y += x.y; }
+  }
+  const uint2 wt = s_w[w];  // the wave's totals
+  if (in) slot_start[g] = wb.x + ic - cnt;
+  // the wave's slots are contiguous: one byte store per lane per 64 slots
+  for (uint32_t k = lane; k < wt.x; k += 64) pflag[wb.x + k] = 0;
+  if (wt.y == 0) return;  // wave-uniform; no barrier below
+  const uint32_t my_off = wb.y + ib - nb;  // first bin pair of this rank
+  const uint32_t start = wb.y, end = wb.y + wt.y;
   const bool any_tall = wave_any(tall);
   Reach rr{};
   if (any_tall && tall) rr = reach_of(splat[3 * (size_t)g], splat[3 * (size_t)g + 1]);
   for (uint32_t base = start; base < end; base += 64) {
     const uint32_t k = base + lane;
     const uint32_t kk = min(k, end - 1);
+    // owner lane of pair kk: the highest lane whose first pair is <= kk
+    // (lanes without pairs share their successor's offset and lose the tie)
     int lo = 0, hi = 64;
 #pragma unroll
     for (int it = 0; it < 6; ++it) {
       const int mid = (lo + hi) >> 1;
-      const uint32_t v = __shfl(my_off, mid, 64);
-      if (v <= kk) lo = mid; else hi = mid;
+      const uint32_t x = __shfl(my_off, mid, 64);
+      if (x <= kk) lo = mid; else hi = mid;
     }
     const uint32_t local = kk - __shfl(my_off, lo, 64);
     const uint32_t gg = __shfl(g, lo, 64);
     const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
     const int x0 = (int)(a & 0xFFFFu), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFFu), y1 = (int)(b >> 16);
-    const uint4 tb = make_uint4(__shfl(tab.x, lo, 64), __shfl(tab.y, lo, 64), __shfl(tab.z, lo, 64),
+    const uint4 tq = make_uint4(__shfl(tab.x, lo, 64), __shfl(tab.y, lo, 64), __shfl(tab.z, lo, 64),
                                 __shfl(tab.w, lo, 64));
     const bool tl = __shfl((int)tall, lo, 64) != 0;
     Reach rg{};
@@ -443,7 +425,7 @@ __global__ __launch_bounds__(256) void k_duplicate_bins(uint32_t P, int bshift, 
     const int row = (int)local / bw;
     const int bx = bx0 + ((int)local - row * bw), by = (y0 >> bshift) + row;
     if (k < end) {
-      keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tb, tl, rg) << 16);
+      keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, tl, rg) << 16);
       vals[k] = gg;
     }
   }
@@ -786,24 +768,15 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   return hipGetLastError();
 }
 
-hipError_t launch_scan_bins_down(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, hipStream_t s) {
-  if (a.P == 0) return hipSuccess;
-  const GeomLayout L(a.P);
-  const uint32_t nbs = (uint32_t)((a.P + kScanTile - 1) / kScanTile);
-  hipLaunchKernelGGL(k_scan_bins_down, dim3(nbs), dim3(256), 0, s, at<uint32_t>(geom, L.tb), depth_order,
-                     (uint32_t)a.P, at<uint2>(geom, L.bsum), at<uint32_t>(const_cast<void*>(geom), L.slot_start),
-                     at<uint32_t>(const_cast<void*>(geom), L.offs));
-  return hipGetLastError();
-}
-
-hipError_t launch_duplicate_bins(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, int bshift,
-                                 uint32_t* keys, uint32_t* vals, hipStream_t s) {
+hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
-  hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + 255) / 256), dim3(256), 0, s, (uint32_t)a.P, bshift, B.bx,
-                     at<uint32_t>(geom, L.offs), depth_order, at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
-                     at<float4>(geom, L.splat), keys, vals);
+  hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + kDupScanThreads - 1) / kDupScanThreads), dim3(kDupScanThreads), 0,
+                     s, (uint32_t)a.P, bshift, B.bx, at<uint32_t>(geom, L.tb), depth_order, at<uint2>(geom, L.bsum),
+                     at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<float4>(geom, L.splat),
+                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals);
   return hipGetLastError();
 }
 

@@ -351,15 +351,16 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 // ---- exclusive scan of packed pairs (lo 16 | hi 16 bits) gathered by index --
 // (the exact tile-list length and the bin count of each Gaussian, in depth
 // order: one gather of one word for both sums; sums kept as two u32s)
+template <int PER>
 __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed,
                                                       const uint32_t* __restrict__ idx, uint32_t n,
                                                       uint2* __restrict__ bsum) {
   __shared__ uint2 s_tmp[4];
   const int t = threadIdx.x;
-  const size_t b0 = (size_t)blockIdx.x * kScanTile + (size_t)t * (kScanTile / 256);
+  const size_t b0 = (size_t)blockIdx.x * (256 * PER) + (size_t)t * PER;
   uint2 acc = make_uint2(0u, 0u);
 #pragma unroll
-  for (int j = 0; j < kScanTile / 256; ++j) {
+  for (int j = 0; j < PER; ++j) {
     const size_t i = b0 + j;
     if (i < n) {
       const uint32_t v = packed[idx[i]];
@@ -489,10 +490,11 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
 }
 
 hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_t n, void* bsum, hipStream_t stream) {
-  const uint32_t nbs = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  const uint32_t nbs = (uint32_t)((n + kPackedScanTile - 1) / kPackedScanTile);
   if (n == 0) return hipMemsetAsync(bsum, 0, sizeof(uint2), stream);
   uint2* bs = static_cast<uint2*>(bsum);
-  hipLaunchKernelGGL(k_scan2_reduce, dim3(nbs), dim3(256), 0, stream, packed, idx, (uint32_t)n, bs);
+  hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, idx, (uint32_t)n,
+                     bs);
   hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(256), 0, stream, bs, nbs);
   return hipGetLastError();
 }

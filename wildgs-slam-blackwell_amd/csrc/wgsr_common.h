@@ -287,6 +287,39 @@ __device__ __forceinline__ void lds_to_slab(const float* lds, int ng, int S, flo
   slab_move<false>(dst, ng, S, const_cast<float*>(lds), lane);
 }
 
+// ---- zero fill in the shadow of a VALU-bound kernel --------------------------
+// The sparse per-Gaussian backward writes only the rows of Gaussians that
+// received gradient (~8 % on the bench scene); every other row of its nine
+// outputs must be zero.  The render backward is VALU-issue bound with HBM
+// nearly idle, so its workgroups stream those zeros (float4 stores, a share
+// each) before the per-Gaussian kernel runs.
+constexpr int kZeroRegions = 9;
+struct ZeroJob {
+  float* p[kZeroRegions];
+  uint64_t n[kZeroRegions];  // floats per region
+  int count;
+};
+
+// Worker `w` of `nw` zeroes its share of every region with `nl` lanes (lane
+// l): 16-byte stores over the aligned body, 4-byte stores for the unaligned
+// head / tail (worker 0).  Regions must be 4-byte aligned.
+__device__ __forceinline__ void zero_share(const ZeroJob& z, uint32_t w, uint32_t nw, int l, int nl) {
+  for (int j = 0; j < z.count; ++j) {
+    float* p = z.p[j];
+    const uint64_t n = z.n[j];
+    const uint64_t head = min<uint64_t>(n, ((16u - (reinterpret_cast<uintptr_t>(p) & 15u)) & 15u) >> 2);
+    const uint64_t n4 = (n - head) >> 2, tail0 = head + 4 * n4;
+    if (w == 0) {
+      if ((uint64_t)l < head) p[l] = 0.f;
+      if (tail0 + l < n) p[tail0 + l] = 0.f;
+    }
+    const uint64_t per = (n4 + nw - 1) / nw;
+    const uint64_t b0 = min(n4, (uint64_t)w * per), b1 = min(n4, b0 + per);
+    float4* q = reinterpret_cast<float4*>(p + head);
+    for (uint64_t k = b0 + l; k < b1; k += nl) q[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 // ---- exact tile lists -------------------------------------------------------
 // A splat's reach ellipse {d : d^T conic d <= L}, L = lim * 1.001 + 0.01 (the
 // render culling margin; lim = 2 ln(255 o), k_preprocess), with the invariants
@@ -517,6 +550,9 @@ constexpr int kSortItems = 16;
 constexpr int kSmallSortItems = WGSR_SMALL_SORT_ITEMS;
 constexpr size_t kSmallSortN = size_t(1) << 21;
 constexpr int kScanTile = 1024;                      // elements per scan workgroup
+// elements per block of the dual (list length, bins) scan: one workgroup of
+// k_duplicate_bins per block, thread <-> rank
+constexpr int kPackedScanTile = 256;
 
 __host__ __device__ inline int sort_items(size_t n) { return n <= kSmallSortN ? kSmallSortItems : kSortItems; }
 __host__ __device__ inline uint32_t sort_blocks(size_t n) {
@@ -577,7 +613,7 @@ struct GeomLayout {
     tb = take(4 * P);              // sort bins: exact list length | bins touched << 16
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
-    bsum = take(8 * ((P + kScanTile - 1) / kScanTile + 1));  // uint2 block sums of the dual scan
+    bsum = take(8 * ((P + kPackedScanTile - 1) / kPackedScanTile + 1));  // uint2 block sums of the (dual) scans
     counter = take(kCounterBytes);  // see kCounterBytes
     gflag = take(P);               // per Gaussian: some tile's backward wrote a partial record
                                    // (zeroed by k_preprocess, set by the render backward)

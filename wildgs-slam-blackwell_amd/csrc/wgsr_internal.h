@@ -43,11 +43,11 @@ struct RasterGrid {
 // geometry tb[g] = exact list length | bins touched << 16)
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
                              uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, hipStream_t s);
-// Sort bins: the scan's down-sweep (slot_start[g]; offs[r] = first bin pair
-// of depth rank r), then the (bin | exact tile mask << 16, Gaussian) pairs.
-hipError_t launch_scan_bins_down(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, hipStream_t s);
-hipError_t launch_duplicate_bins(const wgsr_raster_args& a, const void* geom, const uint32_t* depth_order, int bshift,
-                                 uint32_t* keys, uint32_t* vals, hipStream_t s);
+// Sort bins: after packed_scan_blocks, the scan's down-sweep (slot_start[g],
+// the slot flags zeroed) fused with the (bin | exact tile mask << 16,
+// Gaussian) pair expansion.
+hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
@@ -72,7 +72,7 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, c
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
                              const uint32_t* point_g, const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
-                             float4* partial, uint8_t* pflag, hipStream_t s);
+                             float4* partial, uint8_t* pflag, const ZeroJob& zero, hipStream_t s);
 // Per-Gaussian backward.  GbMode:
 //   kGbDense   k_gauss_bwd over every Gaussian (each lane walks its records);
 //   kGbSparse  k_sum_active (record sums of the Gaussians the render
@@ -84,7 +84,8 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
                             const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
                             float* dL_dcolors, float* dL_dopacity,
                             float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                            float* dL_drot, float* dL_dtau, GbMode mode, hipStream_t s);
+                            float* dL_drot, float* dL_dtau, GbMode mode,
+                            bool zeroed, hipStream_t s);
 // view-sharded backward (raster_bwd.hip, wgsr/dp.py)
 hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, const void* geom, const float4* partial,
                                const uint8_t* pflag, int P_pad, float* records, hipStream_t s);
