@@ -184,6 +184,18 @@ def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
     for mode in ("dense", "sparse"):
         monkeypatch.setenv("WGSR_GB", mode)
         outs[mode] = run_c(inputs, settings, grads)
+    # sparse mode's two kernels: k_gauss_bwd_compact (default: live Gaussians
+    # compacted per workgroup, record sums and backward in one launch) and
+    # k_sum_active + k_gauss_bwd (WGSR_GB_COMPACT=0) -- the same record sums in
+    # the same order; the per-Gaussian math may contract differently (FMA)
+    # inside another kernel, so values compare within fp32 noise
+    monkeypatch.setenv("WGSR_GB", "sparse")
+    monkeypatch.setenv("WGSR_GB_COMPACT", "0")
+    outs["sparse2"] = run_c(inputs, settings, grads)
+    for k in GRAD_KEYS + ("dL_dtau", "dL_dcov3D"):
+        a, b = outs["sparse"][k], outs["sparse2"][k]
+        np.testing.assert_array_equal(a == 0, b == 0, err_msg=f"{k} zero rows (compact vs two-kernel)")
+        np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6 * float(np.abs(b).max() + 1e-30), err_msg=k)
     check_against(outs["sparse"], _cpu_expect(inputs, settings, grads))
     for k in GRAD_KEYS + ("dL_dtau", "dL_dcov3D"):
         a, b = outs["sparse"][k], outs["dense"][k]

@@ -947,6 +947,126 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
 
 
 
+// Sparse per-Gaussian backward in one launch, on outputs the render backward
+// zero-filled: a workgroup of 256 threads owns 256 Gaussians and compacts the
+// ones that received gradient (gflag; ~8 % on the bench scene) into an LDS
+// list; 16-lane groups sum each listed Gaussian's flagged records (lane l
+// reads slots 4l .. 4l + 3 of each 64-slot pass, flags and records in one
+// round trip; a DPP row reduction), and the list's first lanes then run the
+// camera-side and SH backward, one Gaussian per lane, writing only their
+// rows.  The per-Gaussian VALU work runs on ~1/12 of the waves a
+// one-lane-per-Gaussian kernel would need.
+constexpr int kGbcThreads = 256;
+// Gaussians per workgroup = kGbcThreads x kGbcRounds (measured at 1M/1080p:
+// 256 -> 86 us, 512 -> 72 us, 1024 -> 86 us, 2048 -> 113 us; the two-kernel
+// sparse path k_sum_active + k_gauss_bwd: 89 us)
+#ifndef WGSR_GBC_ROUNDS
+#define WGSR_GBC_ROUNDS 2
+#endif
+constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
+constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
+__global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
+    int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
+    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const uint8_t* __restrict__ pflag, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
+    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
+    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
+    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+  constexpr int NW = kGbcThreads / 64;
+  __shared__ uint32_t s_list[kGbcSpan];
+  __shared__ float s_g[kGbcSpan][11];
+  __shared__ uint32_t s_wc[kGbcRounds][NW];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int i0 = blockIdx.x * kGbcSpan;
+  // compaction of the live Gaussians (list order = index order)
+  bool live[kGbcRounds];
+  uint64_t bal[kGbcRounds];
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r) {
+    const int i = i0 + r * kGbcThreads + t;
+    live[r] = i < P && gflag[i] != 0;
+  }
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r) {
+    bal[r] = wave_ballot(live[r]);
+    if (lane == 0) s_wc[r][w] = (uint32_t)__popcll(bal[r]);
+  }
+  __syncthreads();
+  uint32_t nlive = 0;
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r) {
+    uint32_t base = nlive;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      base += k < w ? s_wc[r][k] : 0u;
+      nlive += s_wc[r][k];
+    }
+    if (live[r]) s_list[base + lanes_below(bal[r])] = (uint32_t)(i0 + r * kGbcThreads + t);
+  }
+  if (nlive == 0) return;  // block-uniform
+  __syncthreads();
+  {  // record sums: one 16-lane group per listed Gaussian
+    const int grp = t >> 4, l = t & 15;
+    for (uint32_t c = grp; c < ((nlive + 15) & ~15u); c += kGbcThreads / 16) {
+      const bool have = c < nlive;  // (uniform in the group: the row reduction stays whole)
+      const uint32_t gi = have ? s_list[c] : 0u;
+      const uint32_t s0 = have ? slot_start[gi] : 0u, n = have ? tiles[gi] : 0u;
+      float acc[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+      for (uint32_t b = 0; b < n; b += 64) {
+        bool f[4];
+        float4 r[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t k = b + 4 * l + u;
+          const bool ok = k < n;
+          const size_t sl = (size_t)s0 + (ok ? k : 0u);
+          f[u] = ok && pflag[sl] != 0;
+#pragma unroll
+          for (int h = 0; h < 3; ++h) r[u][h] = ok ? partial[3 * sl + h] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 a0 = r[u][0], a1 = r[u][1], a2 = r[u][2];
+          acc[0] += f[u] ? a0.x : 0.f; acc[1] += f[u] ? a0.y : 0.f;
+          acc[2] += f[u] ? a0.z : 0.f; acc[3] += f[u] ? a0.w : 0.f;
+          acc[4] += f[u] ? a1.x : 0.f; acc[5] += f[u] ? a1.y : 0.f;
+          acc[6] += f[u] ? a1.z : 0.f; acc[7] += f[u] ? a1.w : 0.f;
+          acc[8] += f[u] ? a2.x : 0.f; acc[9] += f[u] ? a2.y : 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 10; ++k) acc[k] = dpp_row_sum16(acc[k]);
+      if (l == 15 && have)
+#pragma unroll
+        for (int k = 0; k < 10; ++k) s_g[c][k] = acc[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t c = t; c < nlive; c += kGbcThreads) {
+    const int i = (int)s_list[c];
+    float g[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) g[k] = s_g[c][k];
+    scale_partial_sums(g, W, H);
+    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
+                  viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
+                  o_tau);
+    if (o_sh) {
+      const size_t i3 = 3 * (size_t)i, S = 3 * (size_t)M;
+      const f3 dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
+                                   mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
+                                   o_sh + (size_t)i * S);
+      o_m3d[i3] += dm_sh.x;  // (camera term) + (SH term), as in k_gauss_bwd
+      o_m3d[i3 + 1] += dm_sh.y;
+      o_m3d[i3 + 2] += dm_sh.z;
+    }
+  }
+}
+
 // ---- view-sharded backward (wgsr/dp.py) ---------------------
 // A view's backward is split at the per-Gaussian screen-space partial sums:
 // k_view_records writes each Gaussian's 12-float record (the ten sums g[10]
@@ -1153,6 +1273,17 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
     return e && atoi(e) != 0;
   }();
   const bool sparse = mode == kGbSparse;
+  const char* ce = getenv("WGSR_GB_COMPACT");  // read per call: tests compare the sparse kernels
+  if (sparse && zeroed && !(ce && strcmp(ce, "0") == 0)) {
+    // (no pair listed: gflag is all zero and nothing is written)
+    hipLaunchKernelGGL(k_gauss_bwd_compact, dim3((a.P + kGbcSpan - 1) / kGbcSpan), dim3(kGbcThreads), 0, s, a.P,
+                       a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
+                       at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
+                       a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,
+                       a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, dL_dmeans2D, dL_dcolors,
+                       dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr, dL_dscales, dL_drot, dL_dtau);
+    return hipGetLastError();
+  }
   if (sparse) {
     // (no pair listed: gflag is all zero and k_gauss_bwd never reads gsum)
     gsum = gsum_buf;
