@@ -78,7 +78,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, int bshift, uint32_t* __restrict__ tb,
-    int i, int lane, const float* s_sh) {
+    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits) {
 #pragma clang fp contract(off)
   radii[i] = 0;
   n_touched[i] = 0;
@@ -88,7 +88,6 @@ __device__ __forceinline__ uint3 preprocess_one(
 
   Cam c;
   load_cam(c, viewm, projm, W, H, tanx, tany);
-  const f3 p = mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]);
   const float4 hom = xform44(c.proj, p);
   const float pw = 1.0f / (hom.w + 0.0000001f);
   const f3 pproj = mk3(hom.x * pw, hom.y * pw, hom.z * pw);
@@ -129,15 +128,11 @@ __device__ __forceinline__ uint3 preprocess_one(
   const int y1 = min(gy, max(0, (int)((py + r + kTile - 1) / kTile)));
   if ((x1 - x0) * (y1 - y0) == 0) return make_uint3(0u, 0u, 0u);
 
-  f3 rgb;
-  uint32_t cbits = 0;
+  f3 rgb = sh_rgb;  // SH colour (k_preprocess evaluates it for every lane)
+  uint32_t cbits = sh_cbits;
   if (colors) {
     rgb = mk3(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2]);
-  } else {
-    f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
-    const float len = sqrtf(dot3(dir, dir));
-    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-    rgb = sh_to_rgb(D, &s_sh[lane * (3 * M + 1)], dir, cbits);
+    cbits = 0;
   }
   const float o = opac[i];
   // Reach of the splat: o G >= 1/255  <=>  d^T conic d <= lim = 2 ln(255 o)
@@ -185,9 +180,17 @@ __device__ __forceinline__ uint3 preprocess_one(
 }
 
 // One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
-// (64 x 3M floats, contiguous in HBM) is first staged through LDS with
-// coalesced loads (slab_to_lds), instead of each lane reading its own 3M-float run.
+// (64 x 3M floats, contiguous in HBM) is staged through LDS with coalesced
+// loads (slab_to_lds), kPreRows rows at a time (lanes of those rows evaluate
+// their colour from LDS between two barriers), instead of each lane reading
+// its own 3M-float run.  (A smaller table lets more waves share a CU but
+// measured no faster at 1M/1080p: 8 rows 97 us, 16 rows 95, 32 rows 95, 64
+// rows 90.)
 constexpr int kPreWave = 64;
+#ifndef WGSR_PRE_ROWS
+#define WGSR_PRE_ROWS 64
+#endif
+constexpr int kPreRows = WGSR_PRE_ROWS;
 __global__ __launch_bounds__(kPreWave) void k_preprocess(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
@@ -200,19 +203,31 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
     uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag) {
 
-  extern __shared__ float s_sh[];  // kPreWave x (3M + 1) floats when SH colours are used
+  extern __shared__ float s_sh[];  // kPreRows x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
+  f3 rgb = mk3(0.f, 0.f, 0.f);
+  uint32_t cbits = 0;
   if (shs != nullptr && colors == nullptr) {
-    slab_to_lds(shs + (size_t)i0 * 3 * M, min(kPreWave, P - i0), 3 * M, s_sh, lane);
-    __syncthreads();
+#pragma clang fp contract(off)
+    f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+    const float len = sqrtf(dot3(dir, dir));
+    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+    const int S = 3 * M, ng = min(kPreWave, P - i0);
+    for (int r0 = 0; r0 < ng; r0 += kPreRows) {  // uniform
+      slab_to_lds(shs + (size_t)(i0 + r0) * S, min(kPreRows, ng - r0), S, s_sh, lane);
+      __syncthreads();
+      if (lane >= r0 && lane < r0 + kPreRows && i < P) rgb = sh_to_rgb(D, &s_sh[(lane - r0) * (S + 1)], dir, cbits);
+      __syncthreads();
+    }
   }
   uint3 ac = make_uint3(0u, 0u, 0u);
   if (i < P) gflag[i] = 0;  // the backward's "received gradient" flag
   if (i < P)
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
                         W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, tiles, clamped, dkey, radii,
-                        n_touched, err_flag, bshift, tb, i, lane, s_sh);
+                        n_touched, err_flag, bshift, tb, i, p, rgb, cbits);
   // upstream num_rendered, the exact pair count and the bin pair count: one
   // atomic per wave each, spread over kRectPairLanes words
   unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;
@@ -758,7 +773,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
-  const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreWave * (3 * (size_t)a.M + 1) : 0;
+  const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreRows * (3 * (size_t)a.M + 1) : 0;
   hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
