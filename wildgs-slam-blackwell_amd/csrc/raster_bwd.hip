@@ -37,6 +37,22 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
+// The render backward sums, over a tile's pixels, u = G dL/dalpha (dx, dy),
+// its moments u_x dx, u_x dy, u_y dy and G dL/dalpha; the entry's own
+// constants come out of those sums here, once per (Gaussian, tile) record:
+//   g0 = o (2 A.z Su_x + B.x Su_y), g1 = o (2 A.w Su_y + B.x Su_x)  -- log2(e) x dL/d(mean2D pixel)
+//   g2, g3, g4 = o x moments                                         -- dL/dconic / (-1/2)
+//   g5 = S G dL/dalpha                                               -- dL/dopacity
+// (A.z, A.w, B.x: the log2(e)-scaled conic of the splat record, o = B.y.)
+__device__ __forceinline__ void record_sums(const float4& A, const float4& B, float (&g)[10]) {
+  const float o = B.y, ux = g[0], uy = g[1];
+  g[0] = o * (2.f * A.z * ux + B.x * uy);
+  g[1] = o * (2.f * A.w * uy + B.x * ux);
+  g[2] *= o;
+  g[3] *= o;
+  g[4] *= o;
+}
+
 // ONE wave per 16x16 tile; lane l owns pixel (l & 7,
 // l >> 3) of each of the four 8x8 quadrants.  Lane j tests entry j's ellipse
 // against each quadrant (four ballots), so per entry the wave evaluates only
@@ -151,7 +167,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
       const v2f d0 = mxy - p0;  // (dx, dy) for quadrant 0
       const float cxy = B.x, op = B.y;
-      const v2f cd2 = cd + cd;  // (2 A.z, 2 A.w): d(power2)/d(dx, dy) = (2 A.z dx + B.x dy, 2 A.w dy + B.x dx)
+      // pixel sums of u = G dL/dalpha (dx, dy) and of its moments; the
+      // entry's constants (opacity, conic) multiply the sums afterwards
+      // (record_sums)
       v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
       float g4 = 0.f, g5 = 0.f;
       bool hit = false;
@@ -183,13 +201,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         dLda = v ? dLda : 0.f;
         acc01[p] += alpha * d01;  // = alpha c + (1 - alpha) accum_rec
         acc2d[p] += alpha * d2d;
-        const float wg = op * dLda;  // dL/dG
-        const v2f gd = G * d;        // (G dx, G dy)
-        g01 += wg * (gd * cd2 + v2f{gd.y, gd.x} * cxy);  // log2(e) x dG/d(dx, dy) x dL/dG
-        const v2f u = wg * gd;
-        g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG
+        const float gl = G * dLda;   // dL/dG / opacity
+        const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
+        g01 += u;
+        g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG / opacity
         g4 += u.y * d.y;
-        g5 += G * dLda;
+        g5 += gl;
         g67 += dch * dp01[p];
         g89 += dch * dp2d[p];
       }
@@ -203,9 +220,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       // duplicate slot of (Gaussian, this tile): its first slot plus the
       // tile's index in the Gaussian's exact tile list (k_duplicate)
       const uint32_t gid = sG[lane];
-      const size_t k =
-          slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
-      const float* sv = sP[lane];
+      const float4 A = sA[lane], B = sB[lane];
+      const size_t k = slot_start[gid] + pair_local(A, B, rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
+      float sv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
+      record_sums(A, B, sv);
       partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
       partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
       partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
@@ -328,12 +348,10 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       dLda = v ? dLda : 0.f;
       acc01 += alpha * e01;
       acc2d += alpha * e2d;
-      const float wg = op * dLda;
-      const v2f gd = G * d;
-      const v2f g01 = wg * (gd * (cd + cd) + v2f{gd.y, gd.x} * cxy);
-      const v2f u = wg * gd;
+      const float gl = G * dLda;  // as k_render_bwd_quad: the entry's constants apply after the sums
+      const v2f u = gl * d;
       const v2f g23 = u.x * d;
-      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, u.y * d.y, G * dLda, dch * dp01.x, dch * dp01.y,
+      const float gv[10] = {u.x, u.y, g23.x, g23.y, u.y * d.y, gl, dch * dp01.x, dch * dp01.y,
                             dch * dp2d.x, dch * dp2d.y};
       wave_sum10_store(gv, &sP[w][j][0]);
       hits |= 1ull << j;
@@ -355,6 +373,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
             for (int k = 0; k < 10; ++k) sv[k] += sP[q][lane][k];
         }
         const uint32_t gid = sG[lane];
+        record_sums(sA[lane], sB[lane], sv);
         const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], rowtab[gid], tx, ty);
         partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
