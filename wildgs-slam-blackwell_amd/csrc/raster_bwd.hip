@@ -83,7 +83,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   // quadrant-0 pixel p0 + 8 (p & 1, p >> 1), so (dx, dy) for quadrant p is
   // (mean - p0) minus an immediate (fewer live VGPRs: no spills)
   const v2f p0{(float)(tx0 + (lane & 7)), (float)(ty0 + (lane >> 3))};
-  v2f dp01[Q], dp2d[Q], acc01[Q], acc2d[Q];
+  v2f dp01[Q], dp2d[Q];
+  float accd[Q];  // upstream's accum_rec (colour, depth) dotted with this pixel's dL/d(colour, depth)
   float T[Q], tb[Q];
   uint32_t last[Q], mq[Q];
   uint32_t m = 0;
@@ -100,8 +101,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     dp2d[p] = v2f{d2, dd};
     tb[p] = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);  // background term: dL/dalpha += tb / (1 - alpha)
     T[p] = Tf;
-    acc01[p] = v2f{0.f, 0.f};
-    acc2d[p] = v2f{0.f, 0.f};
+    accd[p] = 0.f;
     // quadrant p takes gradient from list indices < mq[p] only
     uint32_t x = last[p];
 #pragma unroll
@@ -194,13 +194,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const float Tn = T[p] * rinv;
         T[p] = Tn;
         const float dch = alpha * Tn;
-        // colour / depth behind this contributor: upstream's accum_rec
-        const v2f d01 = c01 - acc01[p], d2d = c2d - acc2d[p];
-        const v2f s2 = d01 * dp01[p] + d2d * dp2d[p];
-        float dLda = (s2.x + s2.y) * Tn + tb[p] * rinv;
+        // colour / depth behind this contributor: upstream's accum_rec enters
+        // dL/dalpha only through its dot product with dL/d(colour, depth),
+        // which follows the same recurrence (accd += alpha (c.dp - accd))
+        const v2f cp = c01 * dp01[p] + c2d * dp2d[p];
+        const float sd = (cp.x + cp.y) - accd[p];
+        float dLda = sd * Tn + tb[p] * rinv;
         dLda = v ? dLda : 0.f;
-        acc01[p] += alpha * d01;  // = alpha c + (1 - alpha) accum_rec
-        acc2d[p] += alpha * d2d;
+        accd[p] += alpha * sd;
         const float gl = G * dLda;   // dL/dG / opacity
         const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
         g01 += u;
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
   const v2f dp01{d0, d1}, dp2d{d2, dd};
   const float tb = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);
   float T = Tf;
-  v2f acc01{0.f, 0.f}, acc2d{0.f, 0.f};
+  float accd = 0.f;  // accum_rec . dL/d(colour, depth), as k_render_bwd_quad
   uint32_t x = last;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
@@ -342,12 +343,11 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       const float Tn = T * rinv;
       T = Tn;
       const float dch = alpha * Tn;
-      const v2f e01 = c01 - acc01, e2d = c2d - acc2d;
-      const v2f s2 = e01 * dp01 + e2d * dp2d;
-      float dLda = (s2.x + s2.y) * Tn + tb * rinv;
+      const v2f cp = c01 * dp01 + c2d * dp2d;
+      const float sd = (cp.x + cp.y) - accd;
+      float dLda = sd * Tn + tb * rinv;
       dLda = v ? dLda : 0.f;
-      acc01 += alpha * e01;
-      acc2d += alpha * e2d;
+      accd += alpha * sd;
       const float gl = G * dLda;  // as k_render_bwd_quad: the entry's constants apply after the sums
       const v2f u = gl * d;
       const v2f g23 = u.x * d;
