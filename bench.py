@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--sh", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU baseline sample: repeat the CPU step until this many seconds have passed")
     ap.add_argument("--no-profile", action="store_true", help="skip the stage timers")
     ap.add_argument("--no-knn", action="store_true", help="skip the distCUDA2 measurement (rocprof runs)")
     ap.add_argument("--dp-exchange", choices=("views", "views-dense", "allreduce"), default=None,
@@ -318,19 +320,24 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_oracle
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        t0 = time.perf_counter()
-        cr = cpu_oracle.CpuRaster(means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
-                                  scales=scene.scales, rotations=scene.rotations, H=H, W=W,
-                                  tanfovx=tanx, tanfovy=tany, bg=bg_cpu, scale_modifier=1.0,
-                                  viewmatrix=f["viewmatrix"], projmatrix=f["projmatrix"],
-                                  projmatrix_raw=f["projmatrix_raw"], sh_degree=deg,
-                                  campos=f["campos"])
-        cr.backward(gc_cpu, gd_cpu)
-        tc = time.perf_counter() - t0
+        # bounded sample: whole fwd+bwd steps of the same workload until
+        # args.cpu_seconds of CPU time have passed (at least one step)
+        times = []
+        while not times or (sum(times) < args.cpu_seconds and len(times) < 64):
+            t0 = time.perf_counter()
+            cr = cpu_oracle.CpuRaster(means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
+                                      scales=scene.scales, rotations=scene.rotations, H=H, W=W,
+                                      tanfovx=tanx, tanfovy=tany, bg=bg_cpu, scale_modifier=1.0,
+                                      viewmatrix=f["viewmatrix"], projmatrix=f["projmatrix"],
+                                      projmatrix_raw=f["projmatrix_raw"], sh_degree=deg,
+                                      campos=f["campos"])
+            cr.backward(gc_cpu, gd_cpu)
+            times.append(time.perf_counter() - t0)
+        tc = sum(times) / len(times)
         out["cpu_baseline"] = {
             "value": P / tc, "unit": "Gaussians/s", "cores": threads, "kind": "port",
-            "sample": f"1 full fwd+bwd step of the same workload ({P} Gaussians, {W}x{H}, SH{deg}) "
-                      f"on oracle/cpu_raster.cpp, {tc:.2f} s"}
+            "sample": f"{len(times)} full fwd+bwd steps of the same workload ({P} Gaussians, {W}x{H}, SH{deg}) "
+                      f"on oracle/cpu_raster.cpp, {sum(times):.1f} s in total, {tc:.2f} s per step (mean)"}
         ref = torch.from_numpy(cr.color)
         mine = state["color"].detach().cpu()
         mse = float(((mine - ref) ** 2).mean())

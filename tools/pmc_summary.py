@@ -7,7 +7,7 @@ coalesced reads, so the corrected read bytes are 2 x FETCH_SIZE (reported
 next to the raw value; other access widths are uncalibrated).  Counters come
 from separate passes (FETCH_SIZE and WRITE_SIZE do not fit one pass).
 
-usage: python tools/pmc_summary.py gpurun_out [out.json]
+usage: python tools/pmc_summary.py gpurun_out [out.json [source-label]]
 """
 import csv
 import json
@@ -22,6 +22,9 @@ STAGE_OF = {
     "k_render_fwd_quad": "render_fwd", "k_render_bwd_quad": "render_bwd", "k_sum_partials": "gauss_bwd",
     "k_render_fwd1": "render_fwd", "k_tile_order": "render_bwd",
     "k_scan_reduce": "offsets_scan", "k_scan_bsum": "offsets_scan", "k_scan_down": "offsets_scan",
+    "k_scan2_reduce": "offsets_scan", "k_scan2_bsum": "offsets_scan",
+    "k_duplicate_bins": "duplicate", "k_bin_bounds": "ranges", "k_expand_bins": "ranges",
+    "k_render_bwd_split": "render_bwd", "k_sum_active": "gauss_bwd", "k_gauss_bwd_compact": "gauss_bwd",
 }
 
 
@@ -53,6 +56,7 @@ def stage_for(kernel, grid, P_grid):
 def main():
     root = sys.argv[1]
     out_path = sys.argv[2] if len(sys.argv) > 2 else None
+    source = sys.argv[3] if len(sys.argv) > 3 else "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes of bench.py"
     fetch = load(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"))
     write = load(os.path.join(root, "pmc_write", "run_counter_collection.csv"))
     sq = load(os.path.join(root, "pmc_sq", "run_counter_collection.csv"))
@@ -92,7 +96,7 @@ def main():
             stages[st]["launch_kinds"].append(k)
     print("* HBM_MB = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 FETCH correction)")
     if out_path:
-        json.dump({"source": "profiles/r01/pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)", "note": "per-dispatch averages; radix stage bytes summed over "
+        json.dump({"source": source, "note": "per-dispatch averages; radix stage bytes summed over "
                    "one pass's kernels (multiply by passes for the stage)",
                    "kernels": rows, "stages": stages}, open(out_path, "w"), indent=1)
 

@@ -68,23 +68,21 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
 }
 
 // One Gaussian of k_preprocess; returns (rect area, exact list length, bins
-// touched), 0 if culled.
+// touched), 0 if culled.  The per-Gaussian words every Gaussian gets (radius,
+// list length, tb, depth key) are returned in `w` (radius, cnt, tb, key) and
+// stored once by the caller; the splat record, rect, row table and clamp bits
+// only for visible Gaussians.
 __device__ __forceinline__ uint3 preprocess_one(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
-    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag, int bshift, uint32_t* __restrict__ tb,
-    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits) {
+    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ err_flag, int bshift,
+    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits, uint4& w) {
 #pragma clang fp contract(off)
-  radii[i] = 0;
-  n_touched[i] = 0;
-  tiles[i] = 0;
-  if (bshift) tb[i] = 0;
-  dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort last
+  w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
 
   Cam c;
   load_cam(c, viewm, projm, W, H, tanx, tany);
@@ -165,17 +163,16 @@ __device__ __forceinline__ uint3 preprocess_one(
     }
     cnt += len;
   }
-  tiles[i] = cnt;
   rowtab[i] = tab;
   clamped[i] = cbits;
-  dkey[i] = __float_as_uint(pv.z);  // pv.z > 0.2 > 0: float bits sort like the floats
-  radii[i] = r;
   // bins of the rect (exact lists are per tile; a bin list holds every
   // Gaussian whose rect meets the bin, and the render waves cull the rest)
   const uint32_t nb = cnt == 0 ? 0u
                                : (uint32_t)((((x1 - 1) >> bshift) - (x0 >> bshift) + 1) *
                                             (((y1 - 1) >> bshift) - (y0 >> bshift) + 1));
-  if (bshift) tb[i] = cnt | (nb << 16);  // both < 2^16: bin_shift() requires <= 65535 tiles
+  // tb: both < 2^16 (bin_shift() requires <= 65535 tiles); the key: pv.z > 0.2 > 0,
+  // so float bits sort like the floats
+  w = make_uint4((uint32_t)r, cnt, cnt | (nb << 16), __float_as_uint(pv.z));
   return make_uint3((uint32_t)((x1 - x0) * (y1 - y0)), cnt, nb);
 }
 
@@ -223,11 +220,19 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     }
   }
   uint3 ac = make_uint3(0u, 0u, 0u);
-  if (i < P) gflag[i] = 0;  // the backward's "received gradient" flag
-  if (i < P)
+  if (i < P) {
+    uint4 w;
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, tiles, clamped, dkey, radii,
-                        n_touched, err_flag, bshift, tb, i, p, rgb, cbits);
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, clamped, err_flag, bshift, i, p,
+                        rgb, cbits, w);
+    // every Gaussian's words, one store each
+    radii[i] = (int32_t)w.x;
+    tiles[i] = w.y;
+    if (bshift) tb[i] = w.z;
+    dkey[i] = w.w;
+    n_touched[i] = 0;
+    gflag[i] = 0;  // the backward's "received gradient" flag
+  }
   // upstream num_rendered, the exact pair count and the bin pair count: one
   // atomic per wave each, spread over kRectPairLanes words
   unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;

@@ -373,20 +373,44 @@ __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict
   if (t == 0) bsum[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_scan2_bsum(uint2* __restrict__ bsum, uint32_t nbs) {
-  __shared__ uint2 s_tmp[4];
-  const int t = threadIdx.x;
-  const uint32_t per = (nbs + 255) / 256;
-  const uint32_t b0 = t * per, b1 = min(nbs, b0 + per);
+// single workgroup of 1024 threads: exclusive scan of the nbs block sums in
+// place, total -> bsum[nbs].  Each thread owns a contiguous run of `per`
+// sums, loaded up front in chunks of 8 (independent loads in flight).
+__global__ __launch_bounds__(1024) void k_scan2_bsum(uint2* __restrict__ bsum, uint32_t nbs) {
+  constexpr int NW = 16;
+  __shared__ uint2 s_w[NW];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t per = (nbs + 1023) / 1024;
+  const uint32_t b0 = min(nbs, t * per), b1 = min(nbs, b0 + per);
   uint2 acc = make_uint2(0u, 0u);
-  for (uint32_t b = b0; b < b1; ++b) { acc.x += bsum[b].x; acc.y += bsum[b].y; }
-  uint2 tot;
-  uint2 run = block_excl_scan256_2(acc, s_tmp, &tot);
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint2 x = bsum[b];
-    bsum[b] = run;
-    run.x += x.x;
-    run.y += x.y;
+  for (uint32_t b = b0; b < b1; b += 8) {
+    uint2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = b + u < b1 ? bsum[b + u] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; }
+  }
+  const uint32_t ia = wave_incl_scan(acc.x), ib = wave_incl_scan(acc.y);
+  if (lane == 63) s_w[w] = make_uint2(ia, ib);
+  __syncthreads();
+  uint2 run = make_uint2(ia - acc.x, ib - acc.y), tot = make_uint2(0u, 0u);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint2 x = s_w[k];
+    if (k < w) { run.x += x.x; run.y += x.y; }
+    tot.x += x.x;
+    tot.y += x.y;
+  }
+  for (uint32_t b = b0; b < b1; b += 8) {
+    uint2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = b + u < b1 ? bsum[b + u] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b + u < b1) bsum[b + u] = run;
+      run.x += v[u].x;
+      run.y += v[u].y;
+    }
   }
   if (t == 0) bsum[nbs] = tot;
 }
@@ -495,7 +519,7 @@ hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_
   uint2* bs = static_cast<uint2*>(bsum);
   hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, idx, (uint32_t)n,
                      bs);
-  hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(256), 0, stream, bs, nbs);
+  hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(1024), 0, stream, bs, nbs);
   return hipGetLastError();
 }
 
