@@ -263,6 +263,12 @@ def main():
                            "avg_launch_ms": ms_avg}
         if traffic is not None:
             out["roofline"]["traffic_source"] = src
+            if dom == "render_bwd":
+                # the render backward also streams the zero fill of the nine
+                # per-Gaussian gradient outputs (P x 77 floats at SH3), which
+                # the byte model counts under gauss_bwd
+                out["roofline"]["traffic_note"] = ("includes the per-Gaussian gradient zero fill "
+                                                   f"({P * 4 * (3 + 3 + 1 + 3 + 6 + 3 * M + 3 + 4 + 6)} B)")
         # whole fwd+bwd pass against HBM (the north-star roofline) and the
         # render kernels' pair arithmetic against the fp32 VALU peak
         kernel_ms = sum(v[0] for k, v in timed.items()) / max(1, args.steps)
