@@ -266,12 +266,13 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // buffer exists
   StageTimer* scan_timer = new StageTimer(2, s);
   if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
-    STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), depth_order, (size_t)a.P, at<uint32_t>(geom, GL.bsum),
+    STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, depth_order, (size_t)a.P,
+                                   at<uint32_t>(geom, GL.bsum),
                                    s));
   } else {
-    STAGE(a, s, exclusive_scan_gather(at<uint32_t>(geom, GL.tiles), depth_order, (size_t)a.P,
+    STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
                                       at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
-                                      at<uint32_t>(geom, GL.bsum), counter, s));
+                                      at<uint32_t>(geom, GL.bsum), counter, s, sizeof(ListRec) / 4));
   }
   delete scan_timer;
   HIPCHK(hipEventSynchronize(hc.ev));

@@ -62,7 +62,7 @@ __device__ __forceinline__ void record_sums(const float4& A, const float4& B, fl
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
     const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
     uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
@@ -222,7 +222,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       // tile's index in the Gaussian's exact tile list (k_duplicate)
       const uint32_t gid = sG[lane];
       const float4 A = sA[lane], B = sB[lane];
-      const size_t k = slot_start[gid] + pair_local(A, B, rect[gid], rowtab[gid], (int)(tile % gx), (int)(tile / gx));
+      const size_t k =
+          slot_start[gid] + pair_local(A, B, lr_rect(lrec[gid].w), lrec[gid].tab, (int)(tile % gx), (int)(tile / gx));
       float sv[10];
 #pragma unroll
       for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 __global__ __launch_bounds__(256) void k_render_bwd_split(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
     const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab, const uint32_t* __restrict__ slot_start, int W,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
     int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
     float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
         }
         const uint32_t gid = sG[lane];
         record_sums(sA[lane], sB[lane], sv);
-        const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], rect[gid], rowtab[gid], tx, ty);
+        const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], lr_rect(lrec[gid].w), lrec[gid].tab, tx, ty);
         partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
         partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
@@ -540,14 +541,14 @@ __device__ __forceinline__ void scale_partial_sums(float g[10], int W, int H) {
 // gsum[10][P] (coalesced SoA), so k_gauss_bwd starts without the record walk.
 __global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __restrict__ radii,
                                                       const uint32_t* __restrict__ slot_start,
-                                                      const uint32_t* __restrict__ tiles,
+                                                      const ListRec* __restrict__ lrec,
                                                       const uint8_t* __restrict__ pflag,
                                                       const float4* __restrict__ partial, int W, int H,
                                                       float* __restrict__ gsum) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P) return;
   const bool live = radii[i] > 0;
-  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + lrec[i].w.w : 0u;
   float g[10];
   sum_partials(s0, s1, pflag, partial, g);
   scale_partial_sums(g, W, H);
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __re
 // independent loads (sums, parameters, SH row).
 __global__ __launch_bounds__(64) void k_sum_active(int P, const uint8_t* __restrict__ gflag,
                                                    const uint32_t* __restrict__ slot_start,
-                                                   const uint32_t* __restrict__ tiles,
+                                                   const ListRec* __restrict__ lrec,
                                                    const uint8_t* __restrict__ pflag,
                                                    const float4* __restrict__ partial, int W, int H,
                                                    float* __restrict__ gsum) {
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(64) void k_sum_active(int P, const uint8_t* __restr
   // flag, slot range and list length in one round trip (coalesced)
   const bool in = i < P;
   const bool live = in && gflag[i] != 0;
-  const uint32_t my_s0 = in ? slot_start[i] : 0u, my_n = in ? tiles[i] : 0u;
+  const uint32_t my_s0 = in ? slot_start[i] : 0u, my_n = in ? lrec[i].w.w : 0u;
   uint64_t act = wave_ballot(live);
   if (!act) return;  // wave-uniform
   while (act) {
@@ -862,7 +863,7 @@ template <bool kHalf, bool kSparse>
 __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_gauss_bwd(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const int32_t* __restrict__ radii,
     const uint32_t* __restrict__ slot_start,
-    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
     const uint8_t* __restrict__ pflag, const float* __restrict__ gsum,
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
     const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #pragma unroll
     for (int q = 0; q < 10; ++q) g[q] = live ? gsum[(size_t)q * P + i] : 0.f;
   } else if (!gsum) {
-    const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+    const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + lrec[i].w.w : 0u;
     sum_partials(s0, s1, pflag, partial, g);
     scale_partial_sums(g, W, H);
   }
@@ -986,7 +987,7 @@ constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
 constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
-    const uint32_t* __restrict__ tiles, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
     const uint8_t* __restrict__ pflag, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
@@ -1031,7 +1032,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     for (uint32_t c = grp; c < ((nlive + 15) & ~15u); c += kGbcThreads / 16) {
       const bool have = c < nlive;  // (uniform in the group: the row reduction stays whole)
       const uint32_t gi = have ? s_list[c] : 0u;
-      const uint32_t s0 = have ? slot_start[gi] : 0u, n = have ? tiles[gi] : 0u;
+      const uint32_t s0 = have ? slot_start[gi] : 0u, n = have ? lrec[gi].w.w : 0u;
       float acc[10];
 #pragma unroll
       for (int k = 0; k < 10; ++k) acc[k] = 0.f;
@@ -1096,7 +1097,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
 // shard and sums the views in registers.
 __global__ __launch_bounds__(256) void k_view_records(int P, int P_pad, const int32_t* __restrict__ radii,
                                                       const uint32_t* __restrict__ slot_start,
-                                                      const uint32_t* __restrict__ tiles,
+                                                      const ListRec* __restrict__ lrec,
                                                       const uint32_t* __restrict__ clamped,
                                                       const uint8_t* __restrict__ pflag,
                                                       const float4* __restrict__ partial, int W, int H,
@@ -1105,7 +1106,7 @@ __global__ __launch_bounds__(256) void k_view_records(int P, int P_pad, const in
   if (i >= P_pad) return;
   float g[10];
   const bool live = i < P && radii[i] > 0;
-  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + tiles[i] : 0u;
+  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + lrec[i].w.w : 0u;
   sum_partials(s0, s1, pflag, partial, g);
   scale_partial_sums(g, W, H);
   const float r = live ? (float)radii[i] : 0.f, cb = live ? (float)clamped[i] : 0.f;
@@ -1251,14 +1252,14 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const int split_below = env ? atoi(env) : kBwdSplitBelowTiles;
   if (nt < split_below) {
     hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), point_g,
-                       at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
+                       at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
                        dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
                      at<float4>(geom, L.splat),
-                     at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<uint32_t>(geom, L.slot_start), a.W,
+                     at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.slot_start), a.W,
                      a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag,
                      at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
   return hipGetLastError();
@@ -1283,7 +1284,7 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
   float* const gsum_buf = gsum;  // scratch [10][P]
   if (split && mode == kGbDense) {
     hipLaunchKernelGGL(k_sum_partials, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii,
-                       at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), pflag, partial, a.W, a.H, gsum);
+                       at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), pflag, partial, a.W, a.H, gsum);
   } else {
     gsum = nullptr;
   }
@@ -1297,7 +1298,7 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
     // (no pair listed: gflag is all zero and nothing is written)
     hipLaunchKernelGGL(k_gauss_bwd_compact, dim3((a.P + kGbcSpan - 1) / kGbcSpan), dim3(kGbcThreads), 0, s, a.P,
                        a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
-                       at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
+                       at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
                        a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,
                        a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, dL_dmeans2D, dL_dcolors,
                        dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr, dL_dscales, dL_drot, dL_dtau);
@@ -1308,14 +1309,14 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
     gsum = gsum_buf;
     if (partial)
       hipLaunchKernelGGL(k_sum_active, dim3((a.P + 63) / 64), dim3(64), 0, s, a.P, at<uint8_t>(geom, L.gflag),
-                         at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), pflag, partial, a.W, a.H,
+                         at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), pflag, partial, a.W, a.H,
                          gsum);
   }
   const size_t lds = a.shs ? sizeof(float) * (full_slab && !sparse ? kGbWave : 32) * (3 * (size_t)a.M + 1) : 0;
   auto k = sparse ? k_gauss_bwd<true, true> : full_slab ? k_gauss_bwd<false, false> : k_gauss_bwd<true, false>;
   hipLaunchKernelGGL(k, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M,
                      at<uint8_t>(geom, L.gflag), radii,
-                     at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
+                     at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                      partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
                      a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
                      dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
@@ -1328,7 +1329,7 @@ hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, 
   if (P_pad == 0) return hipSuccess;
   const GeomLayout L(a.P);
   hipLaunchKernelGGL(k_view_records, dim3((P_pad + 255) / 256), dim3(256), 0, s, a.P, P_pad, radii,
-                     at<uint32_t>(geom, L.slot_start), at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped),
+                     at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                      pflag, partial, a.W, a.H, reinterpret_cast<float4*>(records));
   return hipGetLastError();
 }

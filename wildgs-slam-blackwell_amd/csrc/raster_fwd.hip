@@ -78,11 +78,12 @@ __device__ __forceinline__ uint3 preprocess_one(
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ clamped,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
-    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits, uint4& w) {
+    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits, uint4& w, uint2& rcw) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
+  rcw = make_uint2(0u, 0u);
 
   Cam c;
   load_cam(c, viewm, projm, W, H, tanx, tany);
@@ -145,7 +146,7 @@ __device__ __forceinline__ uint3 preprocess_one(
   splat[3 * (size_t)i + 0] = A;
   splat[3 * (size_t)i + 1] = B;
   splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
-  rect[i] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
+  rcw = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
   // exact tile list length (row_span); upstream's num_rendered counts the rect
   const Reach rr = reach_of(A, B);
   uint32_t cnt = 0;
@@ -163,7 +164,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     }
     cnt += len;
   }
-  rowtab[i] = tab;
+  lrec[i].tab = tab;
   clamped[i] = cbits;
   // bins of the rect (exact lists are per tile; a bin list holds every
   // Gaussian whose rect meets the bin, and the render waves cull the rest)
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ushort4* __restrict__ rect, uint4* __restrict__ rowtab, uint32_t* __restrict__ tiles, uint32_t* __restrict__ clamped,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
@@ -222,12 +223,13 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   uint3 ac = make_uint3(0u, 0u, 0u);
   if (i < P) {
     uint4 w;
+    uint2 rcw;
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, rect, rowtab, clamped, err_flag, bshift, i, p,
-                        rgb, cbits, w);
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, p,
+                        rgb, cbits, w, rcw);
     // every Gaussian's words, one store each
     radii[i] = (int32_t)w.x;
-    tiles[i] = w.y;
+    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);  // rect, tb, exact list length
     if (bshift) tb[i] = w.z;
     dkey[i] = w.w;
     n_touched[i] = 0;
@@ -253,8 +255,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
 // wave) into pairs: lane <-> pair, so the writes are contiguous.
 __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uint32_t* __restrict__ offs,
                                                    const uint32_t* __restrict__ sorted_g,
-                                                   const ushort4* __restrict__ rect,
-                                                   const uint4* __restrict__ rowtab,
+                                                   const ListRec* __restrict__ lrec,
                                                    const float4* __restrict__ splat, uint32_t* __restrict__ keys,
                                                    uint32_t* __restrict__ slot_g, uint8_t* __restrict__ pflag) {
   const uint32_t lane = threadIdx.x & 63;
@@ -270,10 +271,11 @@ __global__ __launch_bounds__(256) void k_duplicate(uint32_t P, int gx, const uin
   if (r < P) {
     g = sorted_g[r];
     if (offs[r + 1] > my_off) {
-      const ushort4 rc = rect[g];
-      rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
-      rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);
-      tab = rowtab[g];
+      const uint4 lw = lrec[g].w;
+      const ushort4 rc = lr_rect(lw);
+      rlo = lw.x;
+      rhi = lw.y;
+      tab = lrec[g].tab;
       tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
     }
   }
@@ -374,9 +376,8 @@ __device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0,
 // depth order inside each bin).
 constexpr int kDupScanThreads = kPackedScanTile;  // one rank per thread
 __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
-    uint32_t P, int bshift, int gbx, const uint32_t* __restrict__ tbv, const uint32_t* __restrict__ sorted_g,
-    const uint2* __restrict__ bsum, const ushort4* __restrict__ rect, const uint4* __restrict__ rowtab,
-    const float4* __restrict__ splat, uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag,
+    uint32_t P, int bshift, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
+    const uint2* __restrict__ bsum, const float4* __restrict__ splat, uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag,
     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   constexpr int NW = kDupScanThreads / 64;
   __shared__ uint2 s_w[NW];
@@ -384,16 +385,17 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
   const uint32_t g = in ? sorted_g[r] : 0u;
-  const uint32_t v = in ? tbv[g] : 0u;
+  const uint4 lw = in ? lrec[g].w : make_uint4(0u, 0u, 0u, 0u);  // rect, tb, list length: one 16-byte load
+  const uint32_t v = lw.z;
   const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
   uint32_t rlo = 0, rhi = 0;
   uint4 tab = make_uint4(0u, 0u, 0u, 0u);
   bool tall = false;
   if (nb) {
-    const ushort4 rc = rect[g];
-    rlo = (uint32_t)rc.x | ((uint32_t)rc.y << 16);
-    rhi = (uint32_t)rc.z | ((uint32_t)rc.w << 16);  // exclusive
-    tab = rowtab[g];
+    const ushort4 rc = lr_rect(lw);
+    rlo = lw.x;
+    rhi = lw.y;  // exclusive
+    tab = lrec[g].tab;
     tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
   }
   const uint32_t ic = wave_incl_scan(cnt), ib = wave_incl_scan(nb);
@@ -782,9 +784,9 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
-                     at<float4>(geom, L.splat), at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab),
-                     at<uint32_t>(geom, L.tiles), at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs,
-                     bin_pairs, bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag));
+                     at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
+                     at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs, bshift,
+                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag));
   return hipGetLastError();
 }
 
@@ -794,8 +796,8 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
   hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + kDupScanThreads - 1) / kDupScanThreads), dim3(kDupScanThreads), 0,
-                     s, (uint32_t)a.P, bshift, B.bx, at<uint32_t>(geom, L.tb), depth_order, at<uint2>(geom, L.bsum),
-                     at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<float4>(geom, L.splat),
+                     s, (uint32_t)a.P, bshift, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
+                     at<float4>(geom, L.splat),
                      at<uint32_t>(geom, L.slot_start), pflag, keys, vals);
   return hipGetLastError();
 }
@@ -819,7 +821,7 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
   const GeomLayout L(P);
   const int gx = (a.W + kTile - 1) / kTile;
   hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, s, P, gx, at<uint32_t>(geom, L.offs),
-                     sorted_g, at<ushort4>(geom, L.rect), at<uint4>(geom, L.rowtab), at<float4>(geom, L.splat),
+                     sorted_g, at<ListRec>(geom, L.lrec), at<float4>(geom, L.splat),
                      keys, slot_g, pflag);
   return hipGetLastError();
 }

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
 }
 
 // ---- exclusive scan of u32 values gathered as vals[idx[i]] (idx may be null)
-__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ vals,
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ vals, uint32_t stride,
                                                      const uint32_t* __restrict__ idx, uint32_t n,
                                                      uint32_t* __restrict__ bsum) {
   __shared__ uint32_t s_tmp[4];
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict_
 #pragma unroll
   for (int j = 0; j < kScanTile / 256; ++j) {
     const size_t i = b0 + j;
-    if (i < n) s += vals[idx ? idx[i] : i];
+    if (i < n) s += vals[(size_t)(idx ? idx[i] : i) * stride];
   }
   uint32_t tot;
   block_excl_scan256(s, s_tmp, &tot);
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void k_scan_bsum(uint32_t* __restrict__ bsum, 
 }
 
 // out[i] = exclusive prefix; if scatter_out: scatter_out[idx[i]] = prefix
-__global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ vals,
+__global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ vals, uint32_t stride,
                                                    const uint32_t* __restrict__ idx, uint32_t n,
                                                    const uint32_t* __restrict__ bsum, uint32_t* __restrict__ out,
                                                    uint32_t* __restrict__ scatter_out) {
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const size_t i = b0 + j;
-    v[j] = (i < n) ? vals[idx ? idx[i] : i] : 0u;
+    v[j] = (i < n) ? vals[(size_t)(idx ? idx[i] : i) * stride] : 0u;
     s += v[j];
   }
   uint32_t run = block_excl_scan256(s, s_tmp, nullptr) + bsum[blockIdx.x];
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 // (the exact tile-list length and the bin count of each Gaussian, in depth
 // order: one gather of one word for both sums; sums kept as two u32s)
 template <int PER>
-__global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed,
+__global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed, uint32_t stride,
                                                       const uint32_t* __restrict__ idx, uint32_t n,
                                                       uint2* __restrict__ bsum) {
   __shared__ uint2 s_tmp[4];
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict
   for (int j = 0; j < PER; ++j) {
     const size_t i = b0 + j;
     if (i < n) {
-      const uint32_t v = packed[idx[i]];
+      const uint32_t v = packed[(size_t)idx[i] * stride];
       acc.x += v & 0xFFFFu;
       acc.y += v >> 16;
     }
@@ -500,25 +500,28 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
 }
 
 hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
-                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream) {
+                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream,
+                                 uint32_t stride) {
   const uint32_t nbs = (uint32_t)((n + kScanTile - 1) / kScanTile);
   if (n == 0) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(uint32_t), stream);
     if (e == hipSuccess && total_out) e = hipMemsetAsync(total_out, 0, sizeof(uint32_t), stream);
     return e;
   }
-  hipLaunchKernelGGL(k_scan_reduce, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nbs), dim3(256), 0, stream, vals, stride, idx, (uint32_t)n, bsum);
   hipLaunchKernelGGL(k_scan_bsum, dim3(1), dim3(256), 0, stream, bsum, nbs, total_out);
-  hipLaunchKernelGGL(k_scan_down, dim3(nbs), dim3(256), 0, stream, vals, idx, (uint32_t)n, bsum, out, scatter_out);
+  hipLaunchKernelGGL(k_scan_down, dim3(nbs), dim3(256), 0, stream, vals, stride, idx, (uint32_t)n, bsum, out,
+                     scatter_out);
   return hipGetLastError();
 }
 
-hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_t n, void* bsum, hipStream_t stream) {
+hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
+                              hipStream_t stream) {
   const uint32_t nbs = (uint32_t)((n + kPackedScanTile - 1) / kPackedScanTile);
   if (n == 0) return hipMemsetAsync(bsum, 0, sizeof(uint2), stream);
   uint2* bs = static_cast<uint2*>(bsum);
-  hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, idx, (uint32_t)n,
-                     bs);
+  hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, stride, idx,
+                     (uint32_t)n, bs);
   hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(1024), 0, stream, bs, nbs);
   return hipGetLastError();
 }

@@ -374,6 +374,20 @@ __device__ __forceinline__ int row_span(const Reach& r, int ty, int x0, int x1, 
   return max(b - a, 0);
 }
 
+// Per-Gaussian list record (written by k_preprocess, 32 B per Gaussian): the
+// row table and w = (x0 | y0 << 16, x1 | y1 << 16, tb, tiles) -- the tile
+// rectangle, the sort-bin word (exact list length | bins << 16) and the exact
+// list length.  One record so the depth-order gathers of the scan and the
+// duplicate fetch one 32-byte run per Gaussian, not three arrays.
+struct ListRec {
+  uint4 tab;
+  uint4 w;
+};
+__device__ __forceinline__ ushort4 lr_rect(const uint4& w) {
+  return make_ushort4((unsigned short)(w.x & 0xFFFFu), (unsigned short)(w.x >> 16), (unsigned short)(w.y & 0xFFFFu),
+                      (unsigned short)(w.y >> 16));
+}
+
 // Row table (written by k_preprocess, 16 B per Gaussian): the spans of the
 // first kRowTab rect rows as bytes, x = lengths of rows 0-3, y = rows 4-7,
 // z = start columns - x0 of rows 0-3, w = rows 4-7 (rect widths are < 256
@@ -594,15 +608,13 @@ constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
 // Per-Gaussian state (geometry buffer).
 struct GeomLayout {
-  size_t splat, rect, rowtab, tiles, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, tb, hist,
+  size_t splat, lrec, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, tb, hist,
       totals, bsum, counter, gflag, total;
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
     splat = take(48 * P);          // float4 x3: (x, y, conic_xx, conic_yy) (conic_xy, opacity, lim, -) (r, g, b, depth)
-    rect = take(8 * P);            // ushort4 tile rectangle [x0, y0, x1, y1)
-    rowtab = take(16 * P);         // uint4 row table: spans of the first kRowTab rect rows (RowTable)
-    tiles = take(4 * P);           // exact tile list length
+    lrec = take(32 * P);           // ListRec: row table, tile rectangle, sort-bin word, exact list length
     clamped = take(4 * P);         // SH clamp flags (3 bits)
     dkey = take(4 * P);            // depth sort keys / sorted keys
     dkey_alt = take(4 * P);
@@ -610,7 +622,7 @@ struct GeomLayout {
     dval_alt = take(4 * P);
     offs = take(4 * (P + 1));      // rank -> first duplicate slot
     slot_start = take(4 * P);      // Gaussian -> first duplicate slot
-    tb = take(4 * P);              // sort bins: exact list length | bins touched << 16
+    tb = take(4 * P);              // sort bins: the list records' tb words, dense (the scan's gather stays in L2)
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
     bsum = take(8 * ((P + kPackedScanTile - 1) / kPackedScanTile + 1));  // uint2 block sums of the (dual) scans

@@ -19,13 +19,16 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
 hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
-                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream);
+                                 uint32_t* scatter_out, uint32_t* bsum, uint32_t* total_out, hipStream_t stream,
+                                 uint32_t stride = 1);
 
 // First two steps of a scan of packed (lo 16 | hi 16) values gathered as
 // packed[idx[i]]: bsum[b] = exclusive prefix (lo sums, hi sums) of block b of
 // kScanTile elements, bsum[blocks] = totals.  bsum: 8 x (blocks + 1) bytes.
 // The down-sweep is the caller's (k_scan_bins_down emits pairs).
-hipError_t packed_scan_blocks(const uint32_t* packed, const uint32_t* idx, size_t n, void* bsum, hipStream_t stream);
+// packed[idx[i] * stride]: (lo 16 | hi 16 bits) pairs gathered through idx
+hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
+                              hipStream_t stream);
 
 int num_bits(uint32_t n);  // bits needed to represent values in [0, n)
 
