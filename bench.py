@@ -196,6 +196,36 @@ def main():
         step()
     torch.cuda.synchronize()
 
+    exchange_check = None
+    if vsb is not None:
+        # the views exchange's summed gradients against the plain backward +
+        # RCCL all-reduce of the same views, once before timing; every rank
+        # falls back to the all-reduce exchange if any rank disagrees
+        nr, color, radii, geom, binning, img, depth, opacity, nt = _C.rasterize_gaussians(
+            bg, means, e, opac, scales, rots, 1.0, e, view, proj, praw, tanx, tany, H, W, shs, deg,
+            campos, False, False)
+        got, _, _ = vsb.backward((means, scales, rots, shs, deg, camd, nr, radii, geom, binning, img), gc, gd)
+        ref = GradBuffer.allocate(P, M, dev)
+        _C.rasterize_gaussians_backward(
+            bg, means, radii, e, scales, rots, 1.0, e, view, proj, praw, tanx, tany, gc, gd, shs,
+            deg, campos, geom, nr, binning, img, False, out=ref.views)
+        if world > 1:
+            allreduce_grads(ref)
+        err = 0.0
+        for k, v in ref.views.items():
+            den = float(v.abs().sum())
+            err = max(err, float((got[k] - v).abs().sum()) / max(den, 1e-30))
+        ok = torch.tensor([1.0 if err <= 1e-5 else 0.0], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        exchange_check = {"rel_l1_vs_allreduce": err, "ok": bool(ok.item() > 0.5)}
+        if not exchange_check["ok"]:
+            exchange, vsb = "allreduce", None
+            exchange_check["fallback"] = "allreduce"
+        del ref
+        torch.cuda.synchronize()
+
     prof = _lib.StageProfile() if not args.no_profile else None
     if world > 1:
         dist.barrier()
@@ -242,6 +272,8 @@ def main():
         },
     }
 
+    if exchange_check is not None:
+        out["config"]["exchange_check"] = exchange_check
     if vsb is not None and vsb.last_exchange is not None:
         out["config"]["sparse_exchange"] = {
             "record_rows_in": vsb.last_exchange["record_rows_in"],
