@@ -226,6 +226,22 @@ def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):
                 np.testing.assert_array_equal(outs[sh][k], v, err_msg=f"shift {sh} {k}")
 
 
+def test_wide_radix_pass_matches_8bit_passes(monkeypatch):
+    """At 1080p the 510 sort bins (9 key bits) are sorted in ONE wide radix
+    pass (512 digits); WGSR_SORT_WIDE=0 runs two 5/4-bit passes.  Both are
+    stable sorts of the same keys, so every output is bit-identical."""
+    inputs, settings, grads = _synthetic(100_000, 1920, 1080, 3, 1)
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("WGSR_SORT_WIDE", mode)
+        outs[mode] = run_c(inputs, settings, grads)
+    for k, v in outs["0"].items():
+        if k == "num_rendered":
+            assert outs["1"][k] == v
+        else:
+            np.testing.assert_array_equal(outs["1"][k], v, err_msg=k)
+
+
 def test_repeated_backward_of_one_forward_is_identical():
     """The per-Gaussian 'received gradient' flags are set by each backward of
     a forward (zeroed once by the forward): a second backward with other

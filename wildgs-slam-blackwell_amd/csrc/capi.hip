@@ -306,7 +306,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     const int bits = bshift ? (num_bits((uint32_t)bins.n) > 0 ? num_bits((uint32_t)bins.n) : 1) : tile_sort_bits(grid);
     // the LSD sort alternates buffers every pass: start the payload in the
     // buffer that makes it end in point_g
-    const bool odd = ((bits + 7) / 8) % 2 == 1;
+    const bool odd = radix_passes(0, bits) % 2 == 1;
     uint32_t* vin = at<uint32_t>(binning, odd ? BL.slot_g : BL.point_g);
     uint32_t* valt = at<uint32_t>(binning, odd ? BL.point_g : BL.slot_g);
     { StageTimer T(3, s);

@@ -278,6 +278,121 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   }
 }
 
+// ---- wide single pass (9-10 bit digits) ------------------------------------
+// A sort on 9 or 10 bits (the 510 sort bins of a 1080p frame) in ONE
+// stable pass instead of two 8-bit-or-less passes: the same reduce-then-scan
+// structure with DIG digits, each thread owning DIG / 256 consecutive digits
+// in the per-digit steps.
+template <int DIG, int I>
+__global__ __launch_bounds__(256) void k_radix_hist_wide(const uint32_t* __restrict__ keys, uint32_t n, int shift,
+                                                         int bits, uint32_t nb, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s_h[DIG];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < DIG / 256; ++k) s_h[t + 256 * k] = 0;
+  uint32_t key[I];
+  const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, key);
+  __syncthreads();
+  add_runs(s_h, key, nv, shift, (1u << bits) - 1u);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < DIG / 256; ++k) hist[(size_t)(t + 256 * k) * nb + blockIdx.x] = s_h[t + 256 * k];
+}
+
+template <int DIG, int I>
+__global__ __launch_bounds__(256) void k_radix_scatter_wide(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
+    uint32_t* __restrict__ vout) {
+  constexpr int kT = 256 * I, DPT = DIG / 256;
+  __shared__ uint2 s_buf[kT];
+  __shared__ uint32_t s_wcnt[4][DIG];
+  __shared__ uint32_t s_lbase[DIG];
+  __shared__ uint32_t s_gbase[DIG];
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll
+  for (int i = 0; i < 4 * DPT; ++i) (&s_wcnt[0][0])[t + 256 * i] = 0;
+  const uint32_t bid = blockIdx.x;
+  const size_t blk0 = (size_t)bid * kT;
+  const size_t base = blk0 + (size_t)w * (64 * I);
+  uint32_t key[I], val[I], rank[I];
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    key[j] = valid ? kin[e] : 0u;
+    val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
+  }
+  {  // global base of this block's digits: digit start (scan of totals) + block offset
+    uint32_t tot[DPT], s = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) { tot[k] = totals[t * DPT + k]; s += tot[k]; }
+    uint32_t run = block_excl_scan256(s, s_tmp, nullptr);  // (its barriers publish s_wcnt = 0)
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int d = t * DPT + k;
+      s_gbase[d] = run + hist[(size_t)d * nb + bid];
+      run += tot[k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    const uint32_t d = (key[j] >> shift) & mask;
+    const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    uint32_t old = 0;
+    if (valid && lane == leader) old = atomicAdd(&s_wcnt[w][d], (uint32_t)__popcll(peers));
+    old = (uint32_t)__shfl((int)old, leader & 63, 64);
+    rank[j] = old + lanes_below(peers);
+  }
+  __syncthreads();
+  {  // per digit: exclusive prefix over waves, then over digits (block-local)
+    uint32_t cnt[DPT], s = 0;
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int d = t * DPT + k;
+      const uint32_t c0 = s_wcnt[0][d], c1 = s_wcnt[1][d], c2 = s_wcnt[2][d], c3 = s_wcnt[3][d];
+      cnt[k] = c0 + c1 + c2 + c3;
+      s += cnt[k];
+      s_wcnt[0][d] = 0;
+      s_wcnt[1][d] = c0;
+      s_wcnt[2][d] = c0 + c1;
+      s_wcnt[3][d] = c0 + c1 + c2;
+    }
+    uint32_t run = block_excl_scan256(s, s_tmp, nullptr);
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      s_lbase[t * DPT + k] = run;
+      run += cnt[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const uint32_t d = (key[j] >> shift) & mask;
+    const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];
+    if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
+  }
+  __syncthreads();
+  const uint32_t cnt = (uint32_t)min((size_t)kT, (size_t)n - blk0);
+#pragma unroll
+  for (int r = 0; r < I; ++r) {
+    const uint32_t i = (uint32_t)t + 256u * r;
+    if (i < cnt) {
+      const uint2 kv = s_buf[i];
+      const uint32_t d = (kv.x >> shift) & mask;
+      const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
+      kout[dst] = kv.x;
+      vout[dst] = kv.y;
+    }
+  }
+}
+
 // ---- exclusive scan of u32 values gathered as vals[idx[i]] (idx may be null)
 __global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ vals, uint32_t stride,
                                                      const uint32_t* __restrict__ idx, uint32_t n,
@@ -429,6 +544,18 @@ int sort_mode() {
   return v;
 }
 
+// 9 or 10 key bits sort in one wide pass (WGSR_SORT_WIDE=0 keeps 8-bit passes)
+static bool wide_pass(int bits) {
+  const char* e = getenv("WGSR_SORT_WIDE");  // read per call: tests compare both
+  return bits > 8 && bits <= 10 && !(e && strcmp(e, "0") == 0) && sort_mode() == 0;
+}
+
+int radix_passes(int begin_bit, int end_bit) {
+  const int bits = end_bit - begin_bit;
+  if (bits <= 0) return 0;
+  return wide_pass(bits) ? 1 : (bits + 7) / 8;
+}
+
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt) {
@@ -439,6 +566,45 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
       return hipErrorInvalidValue;
     }
     return hipSuccess;
+  }
+  if (wide_pass(end_bit - begin_bit) && n <= (size_t)kStCount) {
+    const int bits = end_bit - begin_bit;
+    const uint32_t nb = sort_blocks(n);
+    const bool small = sort_items(n) == kSmallSortItems;
+    // status doubles as the [DIG][nb] per-block histogram (DIG <= 1024 <= 256 x kMaxSortPasses rows)
+    if (bits <= 9) {
+      if (small) {
+        hipLaunchKernelGGL((k_radix_hist_wide<512, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys,
+                           (uint32_t)n, begin_bit, bits, nb, status);
+      } else {
+        hipLaunchKernelGGL((k_radix_hist_wide<512, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
+                           begin_bit, bits, nb, status);
+      }
+      hipLaunchKernelGGL(k_radix_rowscan, dim3(512), dim3(256), 0, stream, status, nb, totals);
+      if (small)
+        hipLaunchKernelGGL((k_radix_scatter_wide<512, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+      else
+        hipLaunchKernelGGL((k_radix_scatter_wide<512, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+    } else {
+      if (small) {
+        hipLaunchKernelGGL((k_radix_hist_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys,
+                           (uint32_t)n, begin_bit, bits, nb, status);
+      } else {
+        hipLaunchKernelGGL((k_radix_hist_wide<1024, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
+                           begin_bit, bits, nb, status);
+      }
+      hipLaunchKernelGGL(k_radix_rowscan, dim3(1024), dim3(256), 0, stream, status, nb, totals);
+      if (small)
+        hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+      else
+        hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+    }
+    *result_in_alt = true;
+    return hipGetLastError();
   }
   const int passes = (end_bit - begin_bit + 7) / 8;
   if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;

@@ -12,6 +12,9 @@ namespace wgsr {
 // Input in keys/vals (vals ignored if vals_iota: value = input position); the
 // result lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
 // Scratch: status >= sort_status_bytes(n), totals >= kSortTotalsBytes.
+// number of passes radix_sort_pairs makes over [begin_bit, end_bit) (the
+// result alternates buffers each pass)
+int radix_passes(int begin_bit, int end_bit);
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt);
