@@ -318,21 +318,23 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
     } }
-    bool talt = false;
+    bool talt = false, bounds_done = false;
+    // a one-pass bin sort also hands back each bin's [start, end): into the
+    // tile_m region (16 B per tile; the forward render writes tile_m later)
+    uint2* bin_bounds = (bshift && (size_t)8 << bits <= (size_t)16 * grid.nt) ? at<uint2>(image, IL.tile_m) : nullptr;
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false,
                                  NL, 0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s,
-                                 &talt)); }
+                                 &talt, bin_bounds, &bounds_done)); }
     // the Gaussian ids are the payload; the backward recomputes each pair's
     // record slot from (Gaussian, tile) instead of carrying it through the sort
     if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
     const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
     StageTimer T(5, s);
     if (bshift) {
-      // bin bounds in the tile_m region (the forward render writes tile_m later)
       STAGE(a, s, launch_expand_bins(a, sorted_keys, at<uint32_t>(binning, BL.point_g), (uint32_t)NL, bshift,
-                                     at<uint2>(image, IL.tile_m), lists, ranges, at<uint32_t>(image, IL.tile_len),
-                                     s));
+                                     at<uint2>(image, IL.tile_m), bounds_done, lists, ranges,
+                                     at<uint32_t>(image, IL.tile_len), s));
     } else {
       STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)NL, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
                                 at<uint32_t>(image, IL.order_fwd), s));

@@ -803,13 +803,15 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
 }
 
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
-                              uint32_t NB, int bshift, uint2* bounds, uint32_t* lists, uint2* ranges,
+                              uint32_t NB, int bshift, uint2* bounds, bool bounds_done, uint32_t* lists, uint2* ranges,
                               uint32_t* tile_len, hipStream_t s) {
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const Bins B(gx, gy, bshift);
-  hipError_t e = hipMemsetAsync(bounds, 0, sizeof(uint2) * (size_t)B.n, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
+  if (!bounds_done) {  // (a one-pass sort already wrote them)
+    hipError_t e = hipMemsetAsync(bounds, 0, sizeof(uint2) * (size_t)B.n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
+  }
   hipLaunchKernelGGL(k_expand_bins, dim3((uint32_t)B.n << bshift), dim3(kExpThreads), 0, s, sorted_keys, sorted_g, bounds, gx,
                      gy, bshift, B.bx, lists, ranges, tile_len);
   return hipGetLastError();

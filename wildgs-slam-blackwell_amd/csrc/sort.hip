@@ -303,7 +303,7 @@ template <int DIG, int I>
 __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout) {
+    uint32_t* __restrict__ vout, uint2* __restrict__ digit_bounds) {
   constexpr int kT = 256 * I, DPT = DIG / 256;
   __shared__ uint2 s_buf[kT];
   __shared__ uint32_t s_wcnt[4][DIG];
@@ -334,6 +334,9 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     for (int k = 0; k < DPT; ++k) {
       const int d = t * DPT + k;
       s_gbase[d] = run + hist[(size_t)d * nb + bid];
+      // the sorted output's [start, end) of every digit (the key is the
+      // whole digit: e.g. the bin ranges k_expand_bins needs)
+      if (digit_bounds && bid == 0) digit_bounds[d] = make_uint2(run, run + tot[k]);
       run += tot[k];
     }
   }
@@ -558,8 +561,9 @@ int radix_passes(int begin_bit, int end_bit) {
 
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt) {
+                            hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done) {
   *result_in_alt = false;
+  if (bounds_done) *bounds_done = false;
   if (n == 0 || end_bit <= begin_bit) {
     if (vals_iota && n > 0) {
       // a zero-pass sort still has to materialise the identity permutation
@@ -583,10 +587,12 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
       hipLaunchKernelGGL(k_radix_rowscan, dim3(512), dim3(256), 0, stream, status, nb, totals);
       if (small)
         hipLaunchKernelGGL((k_radix_scatter_wide<512, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                           begin_bit == 0 ? digit_bounds : nullptr);
       else
         hipLaunchKernelGGL((k_radix_scatter_wide<512, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                           begin_bit == 0 ? digit_bounds : nullptr);
     } else {
       if (small) {
         hipLaunchKernelGGL((k_radix_hist_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys,
@@ -598,12 +604,15 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
       hipLaunchKernelGGL(k_radix_rowscan, dim3(1024), dim3(256), 0, stream, status, nb, totals);
       if (small)
         hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                           begin_bit == 0 ? digit_bounds : nullptr);
       else
         hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt);
+                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                           begin_bit == 0 ? digit_bounds : nullptr);
     }
     *result_in_alt = true;
+    if (bounds_done) *bounds_done = digit_bounds && begin_bit == 0;
     return hipGetLastError();
   }
   const int passes = (end_bit - begin_bit + 7) / 8;

@@ -13,11 +13,14 @@ namespace wgsr {
 // result lands in keys_alt/vals_alt when *result_in_alt, else in keys/vals.
 // Scratch: status >= sort_status_bytes(n), totals >= kSortTotalsBytes.
 // number of passes radix_sort_pairs makes over [begin_bit, end_bit) (the
-// result alternates buffers each pass)
+// result alternates buffers each pass).  digit_bounds: when the sort runs as
+// one wide pass over bits [0, end_bit), each digit's [start, end) in the
+// sorted output is written there (*bounds_done = true).
 int radix_passes(int begin_bit, int end_bit);
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt);
+                            hipStream_t stream, bool* result_in_alt,
+                            uint2* digit_bounds = nullptr, bool* bounds_done = nullptr);
 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
@@ -59,7 +62,7 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
 // tile, the lists in bin-sized regions of `lists` (2^2s x NB entries)
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
-                              uint32_t NB, int bshift, uint2* bounds, uint32_t* lists, uint2* ranges,
+                              uint32_t NB, int bshift, uint2* bounds, bool bounds_done, uint32_t* lists, uint2* ranges,
                               uint32_t* tile_len, hipStream_t s);
 // tile ranges + the forward's launch order (tiles by list length, per XCD chunk)
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
