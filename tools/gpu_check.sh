@@ -54,6 +54,17 @@ for s in $STEPS; do
         env WGSR_LIB=$lib $envset timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${tag}_$rep.json 2> $OUT/ab_${tag}_$rep.err; rc=$?
         if [ $rc -ne 0 ]; then break 2; fi
       done; done ;;
+    knnab)
+      # distCUDA2 timings per AB_LIBS entry (tools/bench_knn.py), then a kernel profile of the base lib
+      rc=0
+      for v in ${AB_LIBS}; do
+        if [ "$v" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$v.so; fi
+        WGSR_LIB=$lib timeout -k 10 300 python tools/bench_knn.py > $OUT/knn_$v.json 2> $OUT/knn_$v.err; rc=$?
+        if [ $rc -ne 0 ]; then break; fi
+      done
+      if [ $rc -eq 0 ]; then
+        (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/knnprof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_knn.py > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/knnprof.err); rc=$?
+      fi ;;
     pmc_custom)
       # PMC_COUNTERS="A B C" PMC_NAME=name: one extra counter pass (SQ block: at most 8 counters)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom}.err); rc=$? ;;

@@ -6,10 +6,11 @@
 //   -> 30-bit Morton codes -> radix sort (sort.hip) -> points gathered into
 //   Morton order -> bounds of 64-point leaf boxes and of 64-leaf super-boxes
 //   -> per point: seed a reject bound from the +-3 Morton neighbours, scan
-//      the wave's own leaf, then every leaf whose distance to the point is
-//      within the current 3rd-best distance.  A wave scans a leaf when ANY of
-//      its lanes needs it (staged through LDS, read as broadcasts); scanning
-//      a leaf a lane did not need cannot change its exact answer.
+//      the wave's own leaf, then every 8-point mini-box whose distance to the
+//      point is within the current 3rd-best distance.  A wave scans a
+//      mini-box when ANY of its lanes needs it (staged through LDS, read as
+//      broadcasts); scanning one a lane did not need cannot change its exact
+//      answer.
 // Distances are evaluated unfused (dx*dx + dy*dy + dz*dz) so results are
 // bitwise identical to the CPU restatement (oracle/cpu_raster.cpp).
 #include <cfloat>
@@ -23,9 +24,10 @@ namespace {
 
 constexpr int kBox = 64;  // points per leaf box == one k_knn wave
 constexpr int kSuper = 64;  // boxes per super-box
+constexpr int kMini = 8;  // points per mini-box (8 per leaf)
 
 struct KnnLayout {
-  size_t part, bbox, codes, codes_alt, idx, idx_alt, spts, boxes, supers, hist, totals, total;
+  size_t part, bbox, codes, codes_alt, idx, idx_alt, spts, boxes, minis, supers, hist, totals, total;
   KnnLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -38,6 +40,7 @@ struct KnnLayout {
     idx_alt = take(4 * P);
     spts = take(16 * P);
     boxes = take(32 * nbox);
+    minis = take(32 * nbox * (kBox / kMini));
     supers = take(32 * nsup);
     hist = take(sort_status_bytes(P));
     totals = take(kSortTotalsBytes);
@@ -148,25 +151,76 @@ __global__ __launch_bounds__(256) void k_bounds(int n, int per, const float4* __
   }
 }
 
+// leaf (64-point) and mini (8-point) box bounds of the Morton-ordered
+// points: one wave per leaf, butterfly min/max over 8 then 64 lanes
+__global__ __launch_bounds__(256) void k_leaf_bounds(int P, const float4* __restrict__ spts, float4* __restrict__ boxes,
+                                                     float4* __restrict__ minis) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x * 256 + (threadIdx.x & ~63) >= P) return;  // whole wave past the end
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  if (i < P) {
+    const float4 q = spts[i];
+    lo[0] = hi[0] = q.x; lo[1] = hi[1] = q.y; lo[2] = hi[2] = q.z;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = fminf(lo[k], __shfl_xor(lo[k], off, 64));
+      hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], off, 64));
+    }
+    if (off == kMini / 2 && (lane & (kMini - 1)) == 0) {  // this lane's mini-box is complete
+      const size_t m = (size_t)i / kMini;
+      minis[2 * m] = make_float4(lo[0], lo[1], lo[2], 0.f);
+      minis[2 * m + 1] = make_float4(hi[0], hi[1], hi[2], 0.f);
+    }
+  }
+  if (lane == 0) {
+    const size_t b = (size_t)i / kBox;
+    boxes[2 * b] = make_float4(lo[0], lo[1], lo[2], 0.f);
+    boxes[2 * b + 1] = make_float4(hi[0], hi[1], hi[2], 0.f);
+  }
+}
+
 __device__ __forceinline__ float sqdist(float4 a, float4 b) {
 #pragma clang fp contract(off)
   const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
   return dx * dx + dy * dy + dz * dz;
 }
 
+// squared distance from p to a box, for pruning: it never exceeds sqdist(p,
+// q) of a point q inside the box (per-axis gaps are differences of the same
+// operands and correctly rounded subtraction is monotone; same unfused sums)
 __device__ __forceinline__ float box_dist(float4 lo, float4 hi, float4 p) {
 #pragma clang fp contract(off)
-  float dx = 0.f, dy = 0.f, dz = 0.f;
-  if (p.x < lo.x || p.x > hi.x) dx = fminf(fabsf(p.x - lo.x), fabsf(p.x - hi.x));
-  if (p.y < lo.y || p.y > hi.y) dy = fminf(fabsf(p.y - lo.y), fabsf(p.y - hi.y));
-  if (p.z < lo.z || p.z > hi.z) dz = fminf(fabsf(p.z - lo.z), fabsf(p.z - hi.z));
+  const float dx = fmaxf(fmaxf(lo.x - p.x, p.x - hi.x), 0.f);
+  const float dy = fmaxf(fmaxf(lo.y - p.y, p.y - hi.y), 0.f);
+  const float dz = fmaxf(fmaxf(lo.z - p.z, p.z - hi.z), 0.f);
   return dx * dx + dy * dy + dz * dz;
 }
 
+// squared gap between two boxes: never exceeds box_dist(b, p) for a point p
+// inside box a (same monotonicity argument)
+__device__ __forceinline__ float box_box(float4 alo, float4 ahi, float4 blo, float4 bhi) {
+#pragma clang fp contract(off)
+  const float dx = fmaxf(fmaxf(blo.x - ahi.x, alo.x - bhi.x), 0.f);
+  const float dy = fmaxf(fmaxf(blo.y - ahi.y, alo.y - bhi.y), 0.f);
+  const float dz = fmaxf(fmaxf(blo.z - ahi.z, alo.z - bhi.z), 0.f);
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// fold d into the ascending 3 best (b0 <= b1 <= b2): two medians and a min
 __device__ __forceinline__ void update3(float d, float& b0, float& b1, float& b2) {
-  if (b0 > d) { const float t = b0; b0 = d; d = t; }
-  if (b1 > d) { const float t = b1; b1 = d; d = t; }
-  if (b2 > d) { b2 = d; }
+  b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
+  b1 = __builtin_amdgcn_fmed3f(b0, b1, d);
+  b0 = fminf(b0, d);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
 }
 
 // LDS written by some lanes of a wave and read by others: a wave's LDS
@@ -177,14 +231,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One wave = 64 consecutive Morton-ordered points = one leaf.  Each wave
-// scans its own leaf first (the bound it leaves prunes almost every other
-// leaf), then walks the super-boxes and, inside the ones ANY lane still
-// needs, the leaves ANY lane still needs.  Every level is staged through the
-// wave's LDS slots by one coalesced load per lane (64 super-box bounds, a
-// super-box's 64 leaf bounds, a leaf's 64 points) and read back as
-// broadcasts, so the walk never waits on a dependent global load per box.
-// distances from p to the n staged points of a leaf starting at sorted index
+// Staged leaves are read back from the wave's LDS slots as broadcasts.
+// Distances from p to the n staged points of a leaf starting at sorted index
 // i0 (self excluded by index), folded into the running 3 best; branch-free
 // and unrolled so the broadcast LDS reads of a group issue together
 __device__ __forceinline__ void scan_leaf(const float4* pts, int i0, int n, int s, float4 p, float& b0, float& b1,
@@ -205,14 +253,38 @@ __device__ __forceinline__ void scan_leaf(const float4* pts, int i0, int n, int 
 
 struct KnnWaveLds {
   float4 pts[64];
+  float4 mini[2 * (kBox / kMini)];  // (lo, hi) of the staged leaf's mini-boxes
   float4 leaf_lo[64], leaf_hi[64];
-  float4 sup_lo[64], sup_hi[64];
 };
 
+// a non-own leaf: only its mini-boxes some lane still needs (the own leaf
+// holds every lane's self; no other leaf does, so no self test here)
+__device__ __forceinline__ void scan_minis(const KnnWaveLds& L, int n, float bound, float4 p, float& b0, float& b1,
+                                           float& b2) {
+#pragma unroll
+  for (int m = 0; m < kBox / kMini; ++m) {
+    if (m * kMini >= n) break;
+    if (!__any(box_dist(L.mini[2 * m], L.mini[2 * m + 1], p) <= fminf(bound, b2))) continue;
+    if (n - m * kMini >= kMini) {
+#pragma unroll
+      for (int j = 0; j < kMini; ++j) update3(sqdist(p, L.pts[m * kMini + j]), b0, b1, b2);
+    } else {
+      for (int j = m * kMini; j < n; ++j) update3(sqdist(p, L.pts[j]), b0, b1, b2);
+    }
+  }
+}
+
+// One wave = 64 consecutive Morton-ordered points = one leaf.  Each wave
+// scans its own leaf first (its bound prunes almost every other leaf).  The
+// walk then prunes coarse-to-fine: super-boxes and a super-box's leaves are
+// tested one per lane against the own leaf box grown by the largest bound
+// of the wave (a superset of what any lane needs: box_box <= box_dist), the
+// surviving leaves per lane (any lane within its bound), and inside a
+// staged leaf its 8-point mini-boxes per lane.
 __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ spts,
                                              const uint32_t* __restrict__ idx, const float4* __restrict__ boxes,
-                                             int nbox, const float4* __restrict__ supers, int nsup,
-                                             float* __restrict__ out) {
+                                             int nbox, const float4* __restrict__ minis,
+                                             const float4* __restrict__ supers, int nsup, float* __restrict__ out) {
   __shared__ KnnWaveLds sl[4];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int s0 = blockIdx.x * 256 + threadIdx.x;
@@ -227,41 +299,48 @@ __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ s
   b0 = b1 = b2 = FLT_MAX;
   KnnWaveLds& L = sl[w];
   const int own = (blockIdx.x * 256 + w * 64) / kBox;
+  const float4 olo = boxes[2 * own], ohi = boxes[2 * own + 1];
   L.pts[lane] = p;  // invalid lanes' copies lie past P and are never read
   wave_lds_sync();
   scan_leaf(L.pts, own * kBox, min(kBox, P - own * kBox), s, p, b0, b1, b2);
   for (int c = 0; c < nsup; c += 64) {
-    const int ns = min(64, nsup - c);
+    uint64_t smask;
     {
-      const int k = c + min(lane, ns - 1);
-      const float4 lo = supers[2 * k], hi = supers[2 * k + 1];
-      wave_lds_sync();
-      L.sup_lo[lane] = lo;
-      L.sup_hi[lane] = hi;
-      wave_lds_sync();
+      const float R = wave_max(fminf(reject, b2));
+      const int k = c + lane;
+      bool cand = false;
+      if (k < nsup) cand = box_box(olo, ohi, supers[2 * k], supers[2 * k + 1]) <= R;
+      smask = __ballot(cand);
     }
-    for (int js = 0; js < ns; ++js) {
-      if (!__any(box_dist(L.sup_lo[js], L.sup_hi[js], p) <= fminf(reject, b2))) continue;
-      const int sb = c + js;
+    while (smask) {
+      const int sb = c + __builtin_ctzll(smask);
+      smask &= smask - 1;
       const int l0 = sb * kSuper, nl = min(kSuper, nbox - l0);
+      uint64_t lmask;
       {
+        const float R = wave_max(fminf(reject, b2));
         const int k = l0 + min(lane, nl - 1);
         const float4 lo = boxes[2 * k], hi = boxes[2 * k + 1];
+        lmask = __ballot(lane < nl && k != own && box_box(olo, ohi, lo, hi) <= R);
         wave_lds_sync();
         L.leaf_lo[lane] = lo;
         L.leaf_hi[lane] = hi;
         wave_lds_sync();
       }
-      for (int jl = 0; jl < nl; ++jl) {
-        const int b = l0 + jl;
-        if (b == own) continue;
+      while (lmask) {
+        const int jl = __builtin_ctzll(lmask);
+        lmask &= lmask - 1;
         if (!__any(box_dist(L.leaf_lo[jl], L.leaf_hi[jl], p) <= fminf(reject, b2))) continue;
+        const int b = l0 + jl;
         const int i0 = b * kBox, n = min(kBox, P - i0);
         const float4 q = spts[min(i0 + lane, P - 1)];
+        float4 mb = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < 2 * (kBox / kMini)) mb = minis[2 * (size_t)b * (kBox / kMini) + lane];
         wave_lds_sync();  // every lane is done reading the previous leaf
         L.pts[lane] = q;
+        if (lane < 2 * (kBox / kMini)) L.mini[lane] = mb;
         wave_lds_sync();
-        scan_leaf(L.pts, i0, n, s, p, b0, b1, b2);
+        scan_minis(L, n, reject, p, b0, b1, b2);
       }
     }
   }
@@ -291,10 +370,12 @@ hipError_t launch_dist_cuda2(int P, const float* points, float* out, void* scrat
   hipLaunchKernelGGL(k_gather_sorted, dim3((P + 255) / 256), dim3(256), 0, s, P, points, sidx, spts);
   const int nbox = (P + kBox - 1) / kBox, nsup = (nbox + kSuper - 1) / kSuper;
   float4* boxes = at<float4>(scratch, L.boxes);
+  float4* minis = at<float4>(scratch, L.minis);
   float4* supers = at<float4>(scratch, L.supers);
-  hipLaunchKernelGGL(k_bounds, dim3(nbox), dim3(256), 0, s, P, kBox, spts, 0, boxes);
+  hipLaunchKernelGGL(k_leaf_bounds, dim3((P + 255) / 256), dim3(256), 0, s, P, spts, boxes, minis);
   hipLaunchKernelGGL(k_bounds, dim3(nsup), dim3(256), 0, s, nbox, kSuper, boxes, 1, supers);
-  hipLaunchKernelGGL(k_knn, dim3((P + 255) / 256), dim3(256), 0, s, P, spts, sidx, boxes, nbox, supers, nsup, out);
+  hipLaunchKernelGGL(k_knn, dim3((P + 255) / 256), dim3(256), 0, s, P, spts, sidx, boxes, nbox, minis, supers, nsup,
+                     out);
   return hipGetLastError();
 }
 
