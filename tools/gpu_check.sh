@@ -65,6 +65,8 @@ for s in $STEPS; do
       if [ $rc -eq 0 ]; then
         (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/knnprof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_knn.py > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/knnprof.err); rc=$?
       fi ;;
+    knnpmc)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --pmc ${PMC_COUNTERS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/knnpmc -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_knn.py > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/knnpmc.err); rc=$? ;;
     pmc_custom)
       # PMC_COUNTERS="A B C" PMC_NAME=name: one extra counter pass (SQ block: at most 8 counters)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom}.err); rc=$? ;;

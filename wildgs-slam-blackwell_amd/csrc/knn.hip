@@ -183,10 +183,14 @@ __global__ __launch_bounds__(256) void k_leaf_bounds(int P, const float4* __rest
   }
 }
 
+// (dx*dx + dy*dy) + dz*dz with x, y as packed pairs (the same unfused,
+// correctly rounded operations in the same order)
 __device__ __forceinline__ float sqdist(float4 a, float4 b) {
 #pragma clang fp contract(off)
-  const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
-  return dx * dx + dy * dy + dz * dz;
+  const v2f dxy = v2f{b.x, b.y} - v2f{a.x, a.y};
+  const float dz = b.z - a.z;
+  const v2f sq = dxy * dxy;
+  return (sq.x + sq.y) + dz * dz;
 }
 
 // squared distance from p to a box, for pruning: it never exceeds sqdist(p,
@@ -215,12 +219,6 @@ __device__ __forceinline__ void update3(float d, float& b0, float& b1, float& b2
   b2 = __builtin_amdgcn_fmed3f(b1, b2, d);
   b1 = __builtin_amdgcn_fmed3f(b0, b1, d);
   b0 = fminf(b0, d);
-}
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
 }
 
 // LDS written by some lanes of a wave and read by others: a wave's LDS
@@ -254,17 +252,56 @@ __device__ __forceinline__ void scan_leaf(const float4* pts, int i0, int n, int 
 struct KnnWaveLds {
   float4 pts[64];
   float4 mini[2 * (kBox / kMini)];  // (lo, hi) of the staged leaf's mini-boxes
+  float4 own[2 * (kBox / kMini)];  // (lo, hi) of the wave's own mini-boxes
+  float ownR[kBox / kMini];  // the largest bound among each own mini-box's lanes
+  float4 qp[64];  // the wave's own points (lane order)
+  float qb[64];  // and their current search radii
   float4 leaf_lo[64], leaf_hi[64];
 };
 
-// a non-own leaf: only its mini-boxes some lane still needs (the own leaf
-// holds every lane's self; no other leaf does, so no self test here)
-__device__ __forceinline__ void scan_minis(const KnnWaveLds& L, int n, float bound, float4 p, float& b0, float& b1,
-                                           float& b2) {
+// refresh ownR / qb from the lanes' current radii; returns the wave's largest
+__device__ __forceinline__ float own_bounds(KnnWaveLds& L, float bound, int lane) {
+  const float mine = bound;
+#pragma unroll
+  for (int off = 1; off < kMini; off <<= 1) bound = fmaxf(bound, __shfl_xor(bound, off, 64));
+  wave_lds_sync();
+  L.qb[lane] = mine;
+  if ((lane & (kMini - 1)) == 0) L.ownR[lane / kMini] = bound;
+  wave_lds_sync();
+#pragma unroll
+  for (int off = kMini; off < 64; off <<= 1) bound = fmaxf(bound, __shfl_xor(bound, off, 64));
+  return bound;
+}
+
+// can any lane need a point of box (lo, hi)?  Tested against each own
+// mini-box grown by its lanes' largest bound: box_box(own mini, box) never
+// exceeds box_dist(p, box) for a lane p inside that mini-box, so this is a
+// superset of the per-lane test.  An own mini-box much larger than its
+// lanes' radii (its 8 Morton-consecutive points straddle a jump of the curve:
+// bit m of split_m) would pass a whole slab of the scene, so its lanes are
+// tested one by one instead.
+__device__ __forceinline__ bool near_own(const KnnWaveLds& L, uint32_t split_m, float4 lo, float4 hi) {
+  bool r = false;
 #pragma unroll
   for (int m = 0; m < kBox / kMini; ++m) {
-    if (m * kMini >= n) break;
-    if (!__any(box_dist(L.mini[2 * m], L.mini[2 * m + 1], p) <= fminf(bound, b2))) continue;
+    if (split_m >> m & 1) {
+      for (int j = m * kMini; j < (m + 1) * kMini; ++j) r |= box_dist(lo, hi, L.qp[j]) <= L.qb[j];
+    } else {
+      r |= box_box(L.own[2 * m], L.own[2 * m + 1], lo, hi) <= L.ownR[m];
+    }
+  }
+  return r;
+}
+
+// a non-own leaf: only its mini-boxes some lane still needs (the own leaf
+// holds every lane's self; no other leaf does, so no self test here)
+// mmask: the mini-boxes that pass the wave-level (grown own box) test
+__device__ __forceinline__ void scan_minis(const KnnWaveLds& L, uint32_t mmask, int n, float lim, float4 p,
+                                           float& b0, float& b1, float& b2) {
+  while (mmask) {
+    const int m = __builtin_ctz(mmask);
+    mmask &= mmask - 1;
+    if (!__any(box_dist(L.mini[2 * m], L.mini[2 * m + 1], p) <= fminf(lim, b2))) continue;
     if (n - m * kMini >= kMini) {
 #pragma unroll
       for (int j = 0; j < kMini; ++j) update3(sqdist(p, L.pts[m * kMini + j]), b0, b1, b2);
@@ -274,13 +311,95 @@ __device__ __forceinline__ void scan_minis(const KnnWaveLds& L, int n, float bou
   }
 }
 
+// Every leaf but the own one, pruned coarse-to-fine with each lane's search
+// radius fminf(lim, b2): super-boxes and a super-box's leaves one per lane
+// against the grown own mini-boxes, the surviving leaves per lane (any lane
+// within its radius), and inside a staged leaf its 8-point mini-boxes (first
+// against the own leaf box grown by the wave's largest radius, then per lane).
+__device__ __forceinline__ void walk(KnnWaveLds& L, int P, const float4* __restrict__ spts,
+                                     const float4* __restrict__ boxes, int nbox, const float4* __restrict__ minis,
+                                     const float4* __restrict__ supers, int nsup, int own, float4 olo, float4 ohi,
+                                     float4 p, int lane, float lim, uint32_t split_m, float& b0, float& b1,
+                                     float& b2) {
+  constexpr int kM = kBox / kMini;
+  for (int c = 0; c < nsup; c += 64) {
+    uint64_t smask;
+    {
+      own_bounds(L, fminf(lim, b2), lane);
+      const int k = c + lane;
+      bool cand = false;
+      if (k < nsup) cand = near_own(L, split_m, supers[2 * k], supers[2 * k + 1]);
+      smask = __ballot(cand);
+    }
+    while (smask) {
+      const int sb = c + __builtin_ctzll(smask);
+      smask &= smask - 1;
+      const int l0 = sb * kSuper, nl = min(kSuper, nbox - l0);
+      uint64_t lmask;
+      // (R stays valid for this super-box's leaves and mini-boxes: the
+      // radii only shrink)
+      const float R = own_bounds(L, fminf(lim, b2), lane);
+      {
+        const int k = l0 + min(lane, nl - 1);
+        const float4 lo = boxes[2 * k], hi = boxes[2 * k + 1];
+        lmask = __ballot(lane < nl && k != own && near_own(L, split_m, lo, hi));
+        wave_lds_sync();
+        L.leaf_lo[lane] = lo;
+        L.leaf_hi[lane] = hi;
+        wave_lds_sync();
+      }
+      // the next leaf any lane needs (tested with the radii as they stand)
+      auto next_leaf = [&]() -> int {
+        while (lmask) {
+          const int jl = __builtin_ctzll(lmask);
+          lmask &= lmask - 1;
+          if (__any(box_dist(L.leaf_lo[jl], L.leaf_hi[jl], p) <= fminf(lim, b2))) return jl;
+        }
+        return -1;
+      };
+      // a leaf's points (one per lane) and its mini-box bounds (lanes 0..15:
+      // lo, hi of mini 0, lo, hi of mini 1, ...) are fetched one leaf ahead,
+      // so their load overlaps the scan of the previous leaf
+      float4 q = make_float4(0.f, 0.f, 0.f, 0.f), mb = q;
+      auto fetch = [&](int jl) {
+        const int b = l0 + jl;
+        q = spts[min(b * kBox + lane, P - 1)];
+        mb = minis[2 * (size_t)b * kM + min(lane, 2 * kM - 1)];
+      };
+      int jl = next_leaf();
+      if (jl >= 0) fetch(jl);
+      while (jl >= 0) {
+        const int b = l0 + jl, n = min(kBox, P - b * kBox);
+        wave_lds_sync();  // every lane is done reading the previous leaf
+        L.pts[lane] = q;
+        if (lane < 2 * kM) L.mini[lane] = mb;
+        wave_lds_sync();
+        // chosen before this leaf's scan shrinks the radii: a superset of
+        // the leaves still needed, whose mini-boxes are re-tested below
+        jl = next_leaf();
+        if (jl >= 0) fetch(jl);
+        // lanes 0..7: one mini-box each, tested against the grown own box
+        const int mi = min(lane, kM - 1);
+        const uint32_t mmask = (uint32_t)__ballot(lane < kM && lane * kMini < n &&
+                                                  box_box(olo, ohi, L.mini[2 * mi], L.mini[2 * mi + 1]) <= R);
+        scan_minis(L, mmask, n, lim, p, b0, b1, b2);
+      }
+    }
+  }
+}
+
 // One wave = 64 consecutive Morton-ordered points = one leaf.  Each wave
-// scans its own leaf first (its bound prunes almost every other leaf).  The
-// walk then prunes coarse-to-fine: super-boxes and a super-box's leaves are
-// tested one per lane against the own leaf box grown by the largest bound
-// of the wave (a superset of what any lane needs: box_box <= box_dist), the
-// surviving leaves per lane (any lane within its bound), and inside a
-// staged leaf its 8-point mini-boxes per lane.
+// scans its own leaf first; its bound prunes almost every other leaf.  A
+// lane whose own leaf and +-3 Morton neighbours lie far from it (a jump of
+// the curve) would keep a radius many times its answer and drag its wave
+// through a large part of the scene, so the walk runs in two phases:
+//   1. radii capped at `cap` (16x the smallest own mini-box bound): a lane
+//      that ends with b2 <= cap is exact (every mini-box skipped lay beyond
+//      min(radius, cap) >= its final b2);
+//   2. only if some lane ended above the cap: those lanes restart from their
+//      own-leaf state with radius min(reject, phase-1 b2) (still an upper
+//      bound of the answer), the finished lanes search nothing (radius -1)
+//      and keep their phase-1 result.
 __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ spts,
                                              const uint32_t* __restrict__ idx, const float4* __restrict__ boxes,
                                              int nbox, const float4* __restrict__ minis,
@@ -301,48 +420,37 @@ __global__ __launch_bounds__(256) void k_knn(int P, const float4* __restrict__ s
   const int own = (blockIdx.x * 256 + w * 64) / kBox;
   const float4 olo = boxes[2 * own], ohi = boxes[2 * own + 1];
   L.pts[lane] = p;  // invalid lanes' copies lie past P and are never read
+  if (lane < 2 * (kBox / kMini)) L.own[lane] = minis[2 * (size_t)own * (kBox / kMini) + lane];
   wave_lds_sync();
   scan_leaf(L.pts, own * kBox, min(kBox, P - own * kBox), s, p, b0, b1, b2);
-  for (int c = 0; c < nsup; c += 64) {
-    uint64_t smask;
-    {
-      const float R = wave_max(fminf(reject, b2));
-      const int k = c + lane;
-      bool cand = false;
-      if (k < nsup) cand = box_box(olo, ohi, supers[2 * k], supers[2 * k + 1]) <= R;
-      smask = __ballot(cand);
-    }
-    while (smask) {
-      const int sb = c + __builtin_ctzll(smask);
-      smask &= smask - 1;
-      const int l0 = sb * kSuper, nl = min(kSuper, nbox - l0);
-      uint64_t lmask;
-      {
-        const float R = wave_max(fminf(reject, b2));
-        const int k = l0 + min(lane, nl - 1);
-        const float4 lo = boxes[2 * k], hi = boxes[2 * k + 1];
-        lmask = __ballot(lane < nl && k != own && box_box(olo, ohi, lo, hi) <= R);
-        wave_lds_sync();
-        L.leaf_lo[lane] = lo;
-        L.leaf_hi[lane] = hi;
-        wave_lds_sync();
-      }
-      while (lmask) {
-        const int jl = __builtin_ctzll(lmask);
-        lmask &= lmask - 1;
-        if (!__any(box_dist(L.leaf_lo[jl], L.leaf_hi[jl], p) <= fminf(reject, b2))) continue;
-        const int b = l0 + jl;
-        const int i0 = b * kBox, n = min(kBox, P - i0);
-        const float4 q = spts[min(i0 + lane, P - 1)];
-        float4 mb = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < 2 * (kBox / kMini)) mb = minis[2 * (size_t)b * (kBox / kMini) + lane];
-        wave_lds_sync();  // every lane is done reading the previous leaf
-        L.pts[lane] = q;
-        if (lane < 2 * (kBox / kMini)) L.mini[lane] = mb;
-        wave_lds_sync();
-        scan_minis(L, n, reject, p, b0, b1, b2);
-      }
-    }
+  const float o0 = b0, o1 = b1, o2 = b2;  // own-leaf state (phase 2 restarts here)
+  L.qp[lane] = p;
+  own_bounds(L, fminf(reject, b2), lane);
+  float cap = L.ownR[0];
+#pragma unroll
+  for (int m = 1; m < kBox / kMini; ++m) cap = fminf(cap, L.ownR[m]);
+  cap *= 16.f;
+  uint32_t split_m;
+  {
+    const int m = min(lane, kBox / kMini - 1);
+    const float4 lo = L.own[2 * m], hi = L.own[2 * m + 1];
+    const float ex = hi.x - lo.x, ey = hi.y - lo.y, ez = hi.z - lo.z;
+    // (an empty mini-box of a partial last leaf has negative extents)
+    split_m = (uint32_t)__ballot(lane < kBox / kMini && ex >= 0.f &&
+                                 ex * ex + ey * ey + ez * ez > 36.f * fminf(L.ownR[m], cap));
+  }
+  // (one loop body for both phases keeps a single copy of the walk)
+  float lim = fminf(reject, cap);
+  bool done = false;
+#pragma clang loop unroll(disable)
+  for (int phase = 0;; ++phase) {
+    float c0 = o0, c1 = o1, c2 = o2;
+    walk(L, P, spts, boxes, nbox, minis, supers, nsup, own, olo, ohi, p, lane, lim, split_m, c0, c1, c2);
+    if (!done) { b0 = c0; b1 = c1; b2 = c2; }
+    if (phase == 1) break;
+    done = b2 <= cap;
+    if (!__any(!done)) break;
+    lim = done ? -1.f : fminf(reject, b2);
   }
   if (valid) out[idx[s]] = (b0 + b1 + b2) / 3.0f;
 }
