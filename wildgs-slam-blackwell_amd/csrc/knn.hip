@@ -3,7 +3,7 @@
 // out[i] = mean of the squared distances from point i to its 3 nearest other
 // points -- exact, like upstream's box-pruned search.  Pipeline:
 //   bbox (min/max, seeded with 0 as upstream's cub::DeviceReduce init)
-//   -> 30-bit Morton codes -> radix sort (sort.hip) -> points gathered into
+//   -> 30-bit Morton codes -> radix sort of their top 24 bits (sort.hip) -> points gathered into
 //   Morton order -> bounds of 64-point leaf boxes and of 64-leaf super-boxes
 //   -> per point: seed a reject bound from the +-3 Morton neighbours, scan
 //      the wave's own leaf, then every 8-point mini-box whose distance to the
@@ -25,6 +25,10 @@ namespace {
 constexpr int kBox = 64;  // points per leaf box == one k_knn wave
 constexpr int kSuper = 64;  // boxes per super-box
 constexpr int kMini = 8;  // points per mini-box (8 per leaf)
+// The search is exact in any point order; the order only decides how compact
+// the leaves are.  Sorting the codes' top 24 bits (256^3 cells, 3 radix
+// passes) keeps the leaves as compact as the full 30 bits for a fourth less.
+constexpr int kMortonSortLo = 6;
 
 struct KnnLayout {
   size_t part, bbox, codes, codes_alt, idx, idx_alt, spts, boxes, minis, supers, hist, totals, total;
@@ -74,20 +78,29 @@ __global__ __launch_bounds__(256) void k_bbox_partial(int P, const float* __rest
   if (t < 6) part[6 * blockIdx.x + t] = s[t][0];
 }
 
-__global__ __launch_bounds__(64) void k_bbox_final(int nparts, const float* __restrict__ part, float* __restrict__ bbox) {
-  // lane l folds partials l, l + 64, ...; then a wave reduction per component
+__global__ __launch_bounds__(256) void k_bbox_final(int nparts, const float* __restrict__ part,
+                                                    float* __restrict__ bbox) {
+  // thread t folds partials t, t + 256, ... (partial 0 seeds every thread);
+  // then one LDS tree over the 256 threads per component
+  __shared__ float sm[6][256];
   const int t = threadIdx.x;
+  float v[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    float v = part[k];  // partial 0 is always present
-    for (int b = t; b < nparts; b += 64) v = (k < 3) ? fminf(v, part[6 * b + k]) : fmaxf(v, part[6 * b + k]);
+  for (int k = 0; k < 6; ++k) v[k] = part[k];
+  for (int b = t; b < nparts; b += 256)
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const float o = __shfl_xor(v, off, 64);
-      v = (k < 3) ? fminf(v, o) : fmaxf(v, o);
-    }
-    if (t == 0) bbox[k] = v;
+    for (int k = 0; k < 6; ++k) v[k] = (k < 3) ? fminf(v[k], part[6 * b + k]) : fmaxf(v[k], part[6 * b + k]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) sm[k][t] = v[k];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off)
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        sm[k][t] = (k < 3) ? fminf(sm[k][t], sm[k][t + off]) : fmaxf(sm[k][t], sm[k][t + off]);
+    __syncthreads();
   }
+  if (t < 6) bbox[t] = sm[t][0];
 }
 
 __device__ __forceinline__ uint32_t prep_morton(uint32_t x) {
@@ -464,14 +477,14 @@ hipError_t launch_dist_cuda2(int P, const float* points, float* out, void* scrat
   const KnnLayout L((size_t)P);
   const int nparts = min(1024, (P + 255) / 256);
   hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, P, points, at<float>(scratch, L.part));
-  hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, nparts, at<float>(scratch, L.part),
+  hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(256), 0, s, nparts, at<float>(scratch, L.part),
                      at<float>(scratch, L.bbox));
   hipLaunchKernelGGL(k_morton, dim3((P + 255) / 256), dim3(256), 0, s, P, points, at<float>(scratch, L.bbox),
                      at<uint32_t>(scratch, L.codes));
   bool in_alt = false;
   hipError_t e = radix_sort_pairs(at<uint32_t>(scratch, L.codes), at<uint32_t>(scratch, L.codes_alt),
-                                  at<uint32_t>(scratch, L.idx), at<uint32_t>(scratch, L.idx_alt), true, (size_t)P, 0,
-                                  30, at<uint32_t>(scratch, L.hist), at<uint32_t>(scratch, L.totals), s, &in_alt);
+                                  at<uint32_t>(scratch, L.idx), at<uint32_t>(scratch, L.idx_alt), true, (size_t)P,
+                                  kMortonSortLo, 30, at<uint32_t>(scratch, L.hist), at<uint32_t>(scratch, L.totals), s, &in_alt);
   if (e != hipSuccess) return e;
   const uint32_t* sidx = at<uint32_t>(scratch, in_alt ? L.idx_alt : L.idx);
   float4* spts = at<float4>(scratch, L.spts);
