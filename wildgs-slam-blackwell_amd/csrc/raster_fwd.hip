@@ -80,13 +80,12 @@ __device__ __forceinline__ uint3 preprocess_one(
     int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
     ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
-    int i, const f3 p, const f3 sh_rgb, uint32_t sh_cbits, uint4& w, uint2& rcw) {
+    int i, const Cam& c, const f3 p, const f3 sc, const float4 q, const float o, const f3 sh_rgb,
+    uint32_t sh_cbits, uint4& w, uint2& rcw) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
   rcw = make_uint2(0u, 0u);
 
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
   const float4 hom = xform44(c.proj, p);
   const float pw = 1.0f / (hom.w + 0.0000001f);
   const f3 pproj = mk3(hom.x * pw, hom.y * pw, hom.z * pw);
@@ -100,9 +99,7 @@ __device__ __forceinline__ uint3 preprocess_one(
 #pragma unroll
     for (int k = 0; k < 6; ++k) cv[k] = cov_pre[6 * (size_t)i + k];
   } else {
-    const f3 s = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-    const float4 q = reinterpret_cast<const float4*>(rots)[i];
-    cov3d_from(s, scale_mod, q, cv);
+    cov3d_from(sc, scale_mod, q, cv);
   }
   float S[3][3];
   sym3(cv, S);
@@ -133,7 +130,6 @@ __device__ __forceinline__ uint3 preprocess_one(
     rgb = mk3(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2]);
     cbits = 0;
   }
-  const float o = opac[i];
   // Reach of the splat: o G >= 1/255  <=>  d^T conic d <= lim = 2 ln(255 o)
   // (G = exp(-d^T conic d / 2) <= 1, so lim < 0 means "reaches no pixel").
   // The render loops test each entry's ellipse against a wave's pixel
@@ -205,6 +201,20 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
   const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
+  // every input (camera, per-Gaussian parameters) is loaded up front, so its
+  // latency overlaps the SH slab's instead of following the colour evaluation
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  f3 sc = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  float o = 0.f;
+  if (i < P) {
+    if (!cov_pre) {
+      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+      q = reinterpret_cast<const float4*>(rots)[i];
+    }
+    o = opac[i];
+  }
   f3 rgb = mk3(0.f, 0.f, 0.f);
   uint32_t cbits = 0;
   if (shs != nullptr && colors == nullptr) {
@@ -225,8 +235,8 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     uint4 w;
     uint2 rcw;
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, p,
-                        rgb, cbits, w, rcw);
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
+                        sc, q, o, rgb, cbits, w, rcw);
     // every Gaussian's words, one store each
     radii[i] = (int32_t)w.x;
     lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);  // rect, tb, exact list length
