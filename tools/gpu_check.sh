@@ -47,7 +47,7 @@ for s in $STEPS; do
       # AB_LIBS="name ...": bench each lib/variants/<name>.so ("base" = lib/libwgsr.so), twice, interleaved
       rc=0
       # an entry may carry one env setting: name:VAR=value (e.g. base:WGSR_SORT=onesweep)
-      for rep in 1 2; do for v in ${AB_LIBS}; do
+      for rep in $(seq 1 ${REPS:-2}); do for v in ${AB_LIBS}; do
         lname=${v%%:*}; envset=""; tag=$lname
         if [ "$v" != "$lname" ]; then envset=${v#*:}; tag=${lname}_${envset//=/_}; fi
         if [ "$lname" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$lname.so; fi
