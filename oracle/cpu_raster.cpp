@@ -676,8 +676,12 @@ void cr_distknn(int P, const float* pts, float* out) {
     int maxring = std::max(nc[0], std::max(nc[1], nc[2]));
     for (int ring = 0; ring <= maxring; ++ring) {
       // every point outside the (ring)-neighbourhood is at least this far away
+      // (an axis whose cells the ring already spans bounds nothing: no point
+      // lies outside the neighbourhood along it -- e.g. a flat or collinear
+      // cloud's degenerate axis)
       double lo = DBL_MAX;
       for (int k = 0; k < 3; ++k) {
+        if (ci[k] - ring <= 0 && ci[k] + ring >= nc[k] - 1) continue;
         double cmin = mn[k] + (ci[k] - ring) * csz[k], cmax = mn[k] + (ci[k] + ring + 1) * csz[k];
         lo = std::min(lo, std::min((double)p[k] - cmin, cmax - (double)p[k]));
       }

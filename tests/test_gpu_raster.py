@@ -442,3 +442,29 @@ def test_distcuda2_1M_bitexact_vs_cpu():
     pts = make_points(1_000_000, seed=77)
     got = distCUDA2(pts.to(DEV)).cpu().numpy()
     np.testing.assert_array_equal(got, cpu_oracle.dist_knn(pts.numpy()))
+
+
+def test_distcuda2_adversarial_bitexact():
+    """Layouts that stress the walk's pruning: the
+    frustum scene (Morton-curve jumps between sparse and dense regions), two
+    far clusters plus sparse outliers, collinear points (flat boxes), heavy
+    exact duplicates, and sizes around the 64-point leaf / 4096-point
+    super-box edges.  Bit-exact vs the CPU restatement."""
+    from simple_knn._C import distCUDA2
+    from wgsr.scene import make_scene
+    g = np.random.default_rng(5)
+    cases = {
+        "frustum_200k": make_scene(200_000, 1920, 1080, 0, seed=11).means3D.numpy(),
+        "clusters_outliers": np.concatenate([
+            g.normal(0.0, 0.05, (30_000, 3)), g.normal(50.0, 0.05, (30_000, 3)),
+            g.uniform(-500.0, 500.0, (300, 3))]).astype(np.float32),
+        "line": np.stack([np.linspace(-3, 3, 20_000), np.zeros(20_000), 0.5 * np.linspace(-3, 3, 20_000)],
+                         1).astype(np.float32),
+        "duplicates": np.repeat(g.uniform(-1, 1, (2_000, 3)), 5, axis=0).astype(np.float32),
+    }
+    for n in (5, 63, 64, 65, 127, 4095, 4097, 64 * 64 * 3 + 1):
+        cases[f"uniform_{n}"] = g.uniform(-2, 2, (n, 3)).astype(np.float32)
+    for k, pts in cases.items():
+        pts = np.ascontiguousarray(pts, dtype=np.float32)
+        got = distCUDA2(torch.from_numpy(pts).to(DEV)).cpu().numpy()
+        np.testing.assert_array_equal(got, cpu_oracle.dist_knn(pts), err_msg=k)
