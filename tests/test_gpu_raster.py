@@ -242,6 +242,33 @@ def test_wide_radix_pass_matches_8bit_passes(monkeypatch):
             np.testing.assert_array_equal(outs["1"][k], v, err_msg=k)
 
 
+def test_superblock_radix_matches_rowscan(monkeypatch):
+    """Reduce-then-scan radix passes find each block's digit offsets from
+    superblock sums written by the histogram kernel (default) or from a
+    row-scan kernel (WGSR_SORT_SUP=0): the same stable sort, so the raster
+    outputs (4-pass depth sort; 8-bit bin-sort passes at 640x480) and
+    distCUDA2 (3 Morton passes) are bit-identical."""
+    from simple_knn._C import distCUDA2
+    from wgsr.scene import make_points
+    pts = make_points(300_000, seed=9).to(DEV)
+    for n, w, h in ((100_000, 1920, 1080), (50_000, 640, 480)):
+        inputs, settings, grads = _synthetic(n, w, h, 3, 1)
+        outs = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("WGSR_SORT_SUP", mode)
+            outs[mode] = run_c(inputs, settings, grads)
+        for k, v in outs["0"].items():
+            if k == "num_rendered":
+                assert outs["1"][k] == v
+            else:
+                np.testing.assert_array_equal(outs["1"][k], v, err_msg=f"{k} {w}x{h}")
+    kn = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("WGSR_SORT_SUP", mode)
+        kn[mode] = distCUDA2(pts).cpu().numpy()
+    np.testing.assert_array_equal(kn["1"], kn["0"])
+
+
 def test_repeated_backward_of_one_forward_is_identical():
     """The per-Gaussian 'received gradient' flags are set by each backward of
     a forward (zeroed once by the forward): a second backward with other

@@ -89,9 +89,14 @@ __device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[I], in
 
 // Reduce-then-scan mode, step 1: per-block histogram of one pass, stored
 // digit-major: hist[d * nb + block].
+// With `sup` (superblock mode), each block also adds its counts into its
+// superblock's (kSupBlocks consecutive blocks) per-digit sums, so the scatter
+// can find its offsets without a row-scan kernel in between.
+constexpr uint32_t kSupBlocks = 16;
 template <int I>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                    int bits, uint32_t nb, uint32_t* __restrict__ hist) {
+                                                    int bits, uint32_t nb, uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ sup, uint32_t nsup) {
   __shared__ uint32_t s_h[256];
   const int t = threadIdx.x;
   s_h[t] = 0;
@@ -100,7 +105,46 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
   __syncthreads();
   add_runs(s_h, k, nv, shift, (1u << bits) - 1u);
   __syncthreads();
-  hist[(size_t)t * nb + blockIdx.x] = s_h[t];
+  const uint32_t c = s_h[t];
+  if (sup) {  // block-major [nb][256] and [nsup][256]: coalesced both ways
+    hist[(size_t)blockIdx.x * 256 + t] = c;
+    if (c) atomicAdd(&sup[(size_t)(blockIdx.x / kSupBlocks) * 256 + t], c);
+  } else {
+    hist[(size_t)t * nb + blockIdx.x] = c;
+  }
+}
+
+// Superblock mode: digit t's global base for block bid = (exclusive scan of
+// the digit totals) + (earlier superblocks' counts) + (earlier blocks of its
+// own superblock), every term read straight from the hist kernel's output
+// (block-major layouts: thread t's loads are coalesced across the block).
+__device__ __forceinline__ uint32_t sup_digit_base(const uint32_t* __restrict__ hist,
+                                                   const uint32_t* __restrict__ sup, uint32_t nb, uint32_t nsup,
+                                                   uint32_t bid, int t, uint32_t* s_tmp) {
+  const uint32_t sb = bid / kSupBlocks;
+  // every load of a 32-superblock chunk (and the own superblock's earlier
+  // blocks) is issued before the first add: one round trip per chunk
+  uint32_t h[kSupBlocks - 1];
+#pragma unroll
+  for (uint32_t k = 0; k < kSupBlocks - 1; ++k) {
+    const uint32_t b = sb * kSupBlocks + k;
+    h[k] = b < bid ? hist[(size_t)b * 256 + t] : 0u;
+  }
+  uint32_t total = 0, pre = 0;
+  for (uint32_t q0 = 0; q0 < nsup; q0 += 32) {
+    uint32_t v[32];
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k) v[k] = q0 + k < nsup ? sup[(size_t)(q0 + k) * 256 + t] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k) {
+      total += v[k];
+      pre += q0 + k < sb ? v[k] : 0u;
+    }
+  }
+  uint32_t intra = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kSupBlocks - 1; ++k) intra += h[k];
+  return block_excl_scan256(total, s_tmp, nullptr) + pre + intra;
 }
 
 // Reduce-then-scan mode, step 2: exclusive scan of hist row d (over blocks)
@@ -170,7 +214,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout) {
+    uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup) {
   constexpr int kTile = 256 * I;
   __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16)
   __shared__ uint32_t s_wcnt[4][256];
@@ -196,9 +240,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
   }
   uint32_t gdig = 0;  // reduce-then-scan: this block's global base of digit t
-  if (!kOnesweep) {
-    const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);  // (its barriers publish s_wcnt = 0)
-    gdig = ex + hist[(size_t)t * nb + bid];
+  if (!kOnesweep) {  // (the scans' barriers publish s_wcnt = 0)
+    if (sup) {
+      gdig = sup_digit_base(hist, sup, nb, nsup, bid, t, s_tmp);
+    } else {
+      const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);
+      gdig = ex + hist[(size_t)t * nb + bid];
+    }
   }
 #pragma unroll
   for (int j = 0; j < I; ++j) {
@@ -553,6 +601,11 @@ static bool wide_pass(int bits) {
   return bits > 8 && bits <= 10 && !(e && strcmp(e, "0") == 0) && sort_mode() == 0;
 }
 
+static bool sup_mode() {
+  const char* e = getenv("WGSR_SORT_SUP");  // read per call: tests compare both
+  return !(e && strcmp(e, "0") == 0);
+}
+
 int radix_passes(int begin_bit, int end_bit) {
   const int bits = end_bit - begin_bit;
   if (bits <= 0) return 0;
@@ -633,6 +686,16 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
       hipLaunchKernelGGL(k_onesweep_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
                          end_bit, ghist);
   }
+  // superblock mode (default for reduce-then-scan; WGSR_SORT_SUP=0 keeps the
+  // row-scan kernel): one memset of every pass's superblock sums replaces a
+  // row-scan launch per pass
+  const uint32_t nsup = (nb + kSupBlocks - 1) / kSupBlocks;
+  uint32_t* sup = nullptr;
+  if (!onesweep && sup_mode()) {
+    sup = status + 256 * (size_t)nb;  // (status holds kMaxSortPasses x 256 x nb words; passes x 256 x nsup fit after one)
+    hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
+    if (e != hipSuccess) return e;
+  }
   uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
   bool iota = vals_iota;
   // balanced digits (13 tile-id bits -> 7 + 6, not 8 + 5): wider per-block
@@ -645,26 +708,30 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
       if (small)
         hipLaunchKernelGGL((k_radix_scatter<true, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
                            iota ? 1 : 0, (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                           status + 256 * (size_t)nb * p, ko, vo);
+                           status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
       else
         hipLaunchKernelGGL((k_radix_scatter<true, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
                            (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                           status + 256 * (size_t)nb * p, ko, vo);
+                           status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
     } else {
-      // status doubles as the [256][nb] per-block histogram
+      // status doubles as the [256][nb] per-block histogram (and, in
+      // superblock mode, holds the passes' [256][nsup] superblock sums after it)
+      uint32_t* sp = sup ? sup + (size_t)p * 256 * nsup : nullptr;
       if (small)
         hipLaunchKernelGGL(k_radix_hist<kSmallSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift,
-                           bits, nb, status);
+                           bits, nb, status, sp, nsup);
       else
         hipLaunchKernelGGL(k_radix_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits,
-                           nb, status);
-      hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
+                           nb, status, sp, nsup);
+      if (!sp) hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
       if (small)
         hipLaunchKernelGGL((k_radix_scatter<false, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
-                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
+                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp,
+                           nsup);
       else
         hipLaunchKernelGGL((k_radix_scatter<false, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
-                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo);
+                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp,
+                           nsup);
     }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
