@@ -242,9 +242,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
   const int bshift = bin_shift(a);
   const Bins bins(grid.gx, grid.gy, bshift);
+  // the depth sort's superblock sums are zeroed by k_preprocess's workgroups
+  // (no memset launch)
+  size_t sup_off = 0;
+  const size_t sup_words = sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off);
+  ZeroJob zj{};
+  if (sup_words) {
+    zj.p[0] = reinterpret_cast<float*>(at<uint32_t>(geom, GL.hist) + sup_off);
+    zj.n[0] = sup_words;
+    zj.count = 1;
+  }
   { StageTimer T(0, s);
   STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
-                                reinterpret_cast<unsigned long long*>(counter + 4), bshift, s)); }
+                                reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s)); }
 
   // The pair counts are known once k_preprocess is done: copy them to pinned
   // host memory behind it and let the depth sort + scan run while the host
@@ -258,7 +268,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   { StageTimer T(1, s);
   STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
                                at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
-                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt)); }
+                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt,
+                               nullptr, nullptr, sup_words != 0)); }
   const uint32_t* depth_order = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
   // in depth order: duplicate-slot offsets of the exact tile lists (the
   // backward's record slots; Gaussian -> first slot), and with sort bins the

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag) {
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, const ZeroJob zero) {
 
   extern __shared__ float s_sh[];  // kPreRows x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
@@ -259,6 +259,8 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
     atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
   }
+  // scratch the next kernels need zeroed (the depth sort's superblock sums)
+  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
 }
 
 // Expand the exact tile lists (row_span) of depth ranks [r0, r0 + 64) (one
@@ -784,7 +786,8 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 }  // namespace
 
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, hipStream_t s) {
+                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, const ZeroJob& zero,
+                             hipStream_t s) {
   unsigned long long* list_pairs = rect_pairs + kRectPairLanes;
   unsigned long long* bin_pairs = rect_pairs + 2 * kRectPairLanes;
   if (a.P == 0) return hipSuccess;
@@ -796,7 +799,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                      at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs, bshift,
-                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag));
+                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), zero);
   return hipGetLastError();
 }
 

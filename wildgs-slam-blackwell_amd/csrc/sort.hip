@@ -612,9 +612,23 @@ int radix_passes(int begin_bit, int end_bit) {
   return wide_pass(bits) ? 1 : (bits + 7) / 8;
 }
 
+// Superblock sums of a reduce-then-scan sort of n keys over [begin_bit,
+// end_bit): their place in `status` (words) and size (words); 0 words when the
+// sort does not use them (wide pass, onesweep, WGSR_SORT_SUP=0).  A caller
+// that zeroes this range itself passes sup_zeroed to radix_sort_pairs.
+size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words) {
+  const int bits = end_bit - begin_bit;
+  if (offset_words) *offset_words = 0;
+  if (n == 0 || bits <= 0 || wide_pass(bits) || sort_mode() != 0 || !sup_mode()) return 0;
+  const uint32_t nb = sort_blocks(n);
+  if (offset_words) *offset_words = 256 * (size_t)nb;
+  return 256 * (size_t)((nb + kSupBlocks - 1) / kSupBlocks) * ((bits + 7) / 8);
+}
+
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done) {
+                            hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done,
+                            bool sup_zeroed) {
   *result_in_alt = false;
   if (bounds_done) *bounds_done = false;
   if (n == 0 || end_bit <= begin_bit) {
@@ -693,8 +707,10 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
   uint32_t* sup = nullptr;
   if (!onesweep && sup_mode()) {
     sup = status + 256 * (size_t)nb;  // (status holds kMaxSortPasses x 256 x nb words; passes x 256 x nsup fit after one)
-    hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
-    if (e != hipSuccess) return e;
+    if (!sup_zeroed) {
+      hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
+      if (e != hipSuccess) return e;
+    }
   }
   uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
   bool iota = vals_iota;

@@ -20,7 +20,10 @@ int radix_passes(int begin_bit, int end_bit);
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt,
-                            uint2* digit_bounds = nullptr, bool* bounds_done = nullptr);
+                            uint2* digit_bounds = nullptr, bool* bounds_done = nullptr, bool sup_zeroed = false);
+// words of `status` a reduce-then-scan sort accumulates superblock sums in
+// (zero before the sort; 0 = none), at *offset_words
+size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words);
 
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
@@ -51,7 +54,7 @@ struct RasterGrid {
 // rect_pairs[2 kRectPairLanes..3 kRectPairLanes) += bins touched (bshift > 0;
 // geometry tb[g] = exact list length | bins touched << 16)
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, hipStream_t s);
+                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, const ZeroJob& zero, hipStream_t s);
 // Sort bins: after packed_scan_blocks, the scan's down-sweep (slot_start[g],
 // the slot flags zeroed) fused with the (bin | exact tile mask << 16,
 // Gaussian) pair expansion.
