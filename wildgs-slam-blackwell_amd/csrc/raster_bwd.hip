@@ -968,14 +968,15 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
 
 
 // Sparse per-Gaussian backward in one launch, on outputs the render backward
-// zero-filled: a workgroup of 256 threads owns 256 Gaussians and compacts the
+// zero-filled: a workgroup of 256 threads owns 512 Gaussians and compacts the
 // ones that received gradient (gflag; ~8 % on the bench scene) into an LDS
-// list; 16-lane groups sum each listed Gaussian's flagged records (lane l
-// reads slots 4l .. 4l + 3 of each 64-slot pass, flags and records in one
-// round trip; a DPP row reduction), and the list's first lanes then run the
-// camera-side and SH backward, one Gaussian per lane, writing only their
-// rows.  The per-Gaussian VALU work runs on ~1/12 of the waves a
-// one-lane-per-Gaussian kernel would need.
+// list; the listed Gaussians' record slots are flattened into one list whose
+// flags and records every thread loads (512 slots at a time, coalesced, into
+// LDS), each listed Gaussian's thread sums its own slots in order, and then
+// runs the camera-side and SH backward, writing only its rows.  The
+// per-Gaussian VALU work runs on ~1/12 of the waves a one-lane-per-Gaussian
+// kernel would need.  (WGSR_GBC_FLAT=0: 16-lane groups per listed Gaussian
+// with a dependent slot-range load per group pass: 75 vs 65 us at 1M/1080p.)
 constexpr int kGbcThreads = 256;
 // Gaussians per workgroup = kGbcThreads x kGbcRounds (measured at 1M/1080p:
 // 256 -> 86 us, 512 -> 72 us, 1024 -> 86 us, 2048 -> 113 us; the two-kernel
@@ -985,6 +986,14 @@ constexpr int kGbcThreads = 256;
 #endif
 constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
 constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
+// WGSR_GBC_FLAT=0: one 16-lane group per listed Gaussian sums its records
+// (a dependent slot-range load per group pass)
+#ifndef WGSR_GBC_FLAT
+#define WGSR_GBC_FLAT 1
+#endif
+#if WGSR_GBC_FLAT
+constexpr int kRecChunk = 512;  // flattened record slots staged in LDS at a time
+#endif
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
     const ListRec* __restrict__ lrec, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
@@ -996,7 +1005,13 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
   constexpr int NW = kGbcThreads / 64;
   __shared__ uint32_t s_list[kGbcSpan];
+#if WGSR_GBC_FLAT
+  __shared__ uint32_t s_s0[kGbcSpan], s_n[kGbcSpan], s_off[kGbcSpan + 1];
+  __shared__ uint2 s_tmp4[4];
+  __shared__ float s_rec[kRecChunk][10];
+#else
   __shared__ float s_g[kGbcSpan][11];
+#endif
   __shared__ uint32_t s_wc[kGbcRounds][NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int i0 = blockIdx.x * kGbcSpan;
@@ -1027,6 +1042,85 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   if (nlive == 0) return;  // block-uniform
   __syncthreads();
+#if WGSR_GBC_FLAT
+  // record sums over the listed Gaussians' slots flattened into one list:
+  // their slot ranges in one round trip, then kRecChunk slots at a time every
+  // thread loads one slot's flag and record (coalesced within a range; the
+  // slot's Gaussian by binary search over the range offsets) into LDS, and
+  // each Gaussian's own thread sums its slots in slot order (deterministic)
+  for (uint32_t c = t; c < nlive; c += kGbcThreads) {
+    const uint32_t gi = s_list[c];
+    s_s0[c] = slot_start[gi];
+    s_n[c] = lrec[gi].w.w;
+  }
+  __syncthreads();
+  {
+    uint32_t v[kGbcRounds], loc = 0;
+#pragma unroll
+    for (int r = 0; r < kGbcRounds; ++r) {
+      const uint32_t c = kGbcRounds * t + r;
+      v[r] = c < nlive ? s_n[c] : 0u;
+      loc += v[r];
+    }
+    uint2 tot2;
+    uint32_t ex = block_excl_scan256_2(make_uint2(loc, 0u), s_tmp4, &tot2).x;
+    const uint32_t tot = tot2.x;
+#pragma unroll
+    for (int r = 0; r < kGbcRounds; ++r) {
+      const uint32_t c = kGbcRounds * t + r;
+      if (c < nlive) s_off[c] = ex;
+      ex += v[r];
+    }
+    if (t == 0) s_off[nlive] = tot;
+  }
+  __syncthreads();
+  const uint32_t total = s_off[nlive];
+  float acc[kGbcRounds][10];
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[r][k] = 0.f;
+  for (uint32_t base = 0; base < total; base += kRecChunk) {
+#pragma unroll
+    for (int u = 0; u < kRecChunk / kGbcThreads; ++u) {
+      const uint32_t q = base + u * kGbcThreads + t;
+      if (q < total) {
+        uint32_t lo = 0, hi = nlive;  // s_off[lo] <= q < s_off[hi]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= q) lo = mid; else hi = mid;
+        }
+        const size_t sl = (size_t)s_s0[lo] + (q - s_off[lo]);
+        const bool f = pflag[sl] != 0;
+        const float4 a0 = partial[3 * sl], a1 = partial[3 * sl + 1], a2 = partial[3 * sl + 2];
+        float* d = s_rec[q - base];
+        d[0] = f ? a0.x : 0.f; d[1] = f ? a0.y : 0.f; d[2] = f ? a0.z : 0.f; d[3] = f ? a0.w : 0.f;
+        d[4] = f ? a1.x : 0.f; d[5] = f ? a1.y : 0.f; d[6] = f ? a1.z : 0.f; d[7] = f ? a1.w : 0.f;
+        d[8] = f ? a2.x : 0.f; d[9] = f ? a2.y : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kGbcRounds; ++r) {
+      const uint32_t c = r * kGbcThreads + t;
+      if (c < nlive) {
+        const uint32_t qa = max(s_off[c], base), qb = min(s_off[c + 1], base + kRecChunk);
+        for (uint32_t q = qa; q < qb; ++q)
+#pragma unroll
+          for (int k = 0; k < 10; ++k) acc[r][k] += s_rec[q - base][k];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r) {
+    const uint32_t c = r * kGbcThreads + t;
+    if (c >= nlive) break;
+    const int i = (int)s_list[c];
+    float g[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) g[k] = acc[r][k];
+#else
   {  // record sums: one 16-lane group per listed Gaussian
     const int grp = t >> 4, l = t & 15;
     for (uint32_t c = grp; c < ((nlive + 15) & ~15u); c += kGbcThreads / 16) {
@@ -1071,6 +1165,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) g[k] = s_g[c][k];
+#endif
     scale_partial_sums(g, W, H);
     gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
                   viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
