@@ -1167,18 +1167,17 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     for (int k = 0; k < 10; ++k) g[k] = s_g[c][k];
 #endif
     scale_partial_sums(g, W, H);
-    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
-                  viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
-                  o_tau);
+    // SH backward first: its dL/dmean term goes into gauss_bwd_one's single
+    // store of the row (no read-modify-write of o_m3d behind its stores)
+    f3 dm_sh = mk3(0.f, 0.f, 0.f);
     if (o_sh) {
       const size_t i3 = 3 * (size_t)i, S = 3 * (size_t)M;
-      const f3 dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
-                                   mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
-                                   o_sh + (size_t)i * S);
-      o_m3d[i3] += dm_sh.x;  // (camera term) + (SH term), as in k_gauss_bwd
-      o_m3d[i3 + 1] += dm_sh.y;
-      o_m3d[i3 + 2] += dm_sh.z;
+      dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
+                          mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
+                          o_sh + (size_t)i * S);
     }
+    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, dm_sh, scale_mod, viewm, projm,
+                  praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   }
 }
 
