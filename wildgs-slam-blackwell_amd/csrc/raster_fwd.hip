@@ -397,18 +397,24 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
   const uint32_t g = in ? sorted_g[r] : 0u;
-  const uint4 lw = in ? lrec[g].w : make_uint4(0u, 0u, 0u, 0u);  // rect, tb, list length: one 16-byte load
+  // the whole 32-byte list record in one round trip (row table + rect, tb,
+  // list length: one cache line)
+  uint4 lw = make_uint4(0u, 0u, 0u, 0u), tab = lw;
+  if (in) {
+    lw = lrec[g].w;
+    tab = lrec[g].tab;
+  }
   const uint32_t v = lw.z;
   const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
   uint32_t rlo = 0, rhi = 0;
-  uint4 tab = make_uint4(0u, 0u, 0u, 0u);
   bool tall = false;
   if (nb) {
     const ushort4 rc = lr_rect(lw);
     rlo = lw.x;
     rhi = lw.y;  // exclusive
-    tab = lrec[g].tab;
     tall = rc.w - rc.y > kRowTab || !rowtab_ok(rc);
+  } else {
+    tab = make_uint4(0u, 0u, 0u, 0u);
   }
   const uint32_t ic = wave_incl_scan(cnt), ib = wave_incl_scan(nb);
   if (lane == 63) s_w[w] = make_uint2(ic, ib);
