@@ -269,6 +269,23 @@ def test_superblock_radix_matches_rowscan(monkeypatch):
     np.testing.assert_array_equal(kn["1"], kn["0"])
 
 
+def test_scan_superblocks_match_scan_kernel(monkeypatch):
+    """With sort bins the duplicate kernel derives each block's prefix of the
+    dual scan from superblock sums (default) or takes it from the scan's own
+    prefix kernel (WGSR_SCAN_SUP=0): integer sums, bit-identical outputs."""
+    for n, w, h in ((100_000, 1920, 1080), (30_000, 640, 480)):
+        inputs, settings, grads = _synthetic(n, w, h, 3, 1)
+        outs = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("WGSR_SCAN_SUP", mode)
+            outs[mode] = run_c(inputs, settings, grads)
+        for k, v in outs["0"].items():
+            if k == "num_rendered":
+                assert outs["1"][k] == v
+            else:
+                np.testing.assert_array_equal(outs["1"][k], v, err_msg=f"{k} {w}x{h}")
+
+
 def test_repeated_backward_of_one_forward_is_identical():
     """The per-Gaussian 'received gradient' flags are set by each backward of
     a forward (zeroed once by the forward): a second backward with other

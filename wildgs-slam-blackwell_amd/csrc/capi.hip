@@ -52,6 +52,12 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+// WGSR_SCAN_SUP=0: the dual scan's block prefix by its own scan kernel
+static bool scan_sup_mode() {
+  const char* e = getenv("WGSR_SCAN_SUP");  // read per call: tests compare both
+  return !(e && strcmp(e, "0") == 0);
+}
+
 int num_bits(uint32_t n) {
   int b = 0;
   while (b < 32 && (1ull << b) < n) ++b;
@@ -248,9 +254,14 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   const size_t sup_words = sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off);
   ZeroJob zj{};
   if (sup_words) {
-    zj.p[0] = reinterpret_cast<float*>(at<uint32_t>(geom, GL.hist) + sup_off);
-    zj.n[0] = sup_words;
-    zj.count = 1;
+    zj.p[zj.count] = reinterpret_cast<float*>(at<uint32_t>(geom, GL.hist) + sup_off);
+    zj.n[zj.count++] = sup_words;
+  }
+  // ... and, with sort bins, the dual scan's superblock sums
+  const bool scan_sup = bshift && scan_sup_mode();
+  if (scan_sup) {
+    zj.p[zj.count] = at<float>(geom, GL.bsup);
+    zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
   }
   { StageTimer T(0, s);
   STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
@@ -278,8 +289,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   StageTimer* scan_timer = new StageTimer(2, s);
   if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
     STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, depth_order, (size_t)a.P,
-                                   at<uint32_t>(geom, GL.bsum),
-                                   s));
+                                   at<uint32_t>(geom, GL.bsum), s, scan_sup ? at<uint2>(geom, GL.bsup) : nullptr));
   } else {
     STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
                                       at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
@@ -324,7 +334,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bshift) {
       // (the backward's record flags live on the exact slots: zeroed here too)
       STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
-                                        at<uint32_t>(binning, BL.key), vin, s));
+                                        at<uint32_t>(binning, BL.key), vin, scan_sup, s));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));

@@ -389,10 +389,11 @@ __device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0,
 constexpr int kDupScanThreads = kPackedScanTile;  // one rank per thread
 __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     uint32_t P, int bshift, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
-    const uint2* __restrict__ bsum, const float4* __restrict__ splat, uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag,
-    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
+    uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
+    uint32_t* __restrict__ vals) {
   constexpr int NW = kDupScanThreads / 64;
-  __shared__ uint2 s_w[NW];
+  __shared__ uint2 s_w[NW], s_p[NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
@@ -418,8 +419,36 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   }
   const uint32_t ic = wave_incl_scan(cnt), ib = wave_incl_scan(nb);
   if (lane == 63) s_w[w] = make_uint2(ic, ib);
-  __syncthreads();
-  uint2 wb = bsum[blockIdx.x];  // this block's first slot / first bin pair
+  uint2 wb;  // this block's first slot / first bin pair
+  if (bsup) {
+    // exclusive prefix of the blocks before this one: the earlier
+    // superblocks' sums plus the earlier blocks of its own superblock
+    const uint32_t b = blockIdx.x, sb = b / kScanSupBlocks;
+    uint2 v = make_uint2(0u, 0u);
+    for (uint32_t q = (uint32_t)t; q < sb; q += kDupScanThreads) {
+      const uint2 x = bsup[(size_t)q * kScanSupStride];
+      v.x += x.x;
+      v.y += x.y;
+    }
+    if ((uint32_t)t < kScanSupBlocks && sb * kScanSupBlocks + t < b) {
+      const uint2 x = bsum[sb * kScanSupBlocks + t];
+      v.x += x.x;
+      v.y += x.y;
+    }
+    v.x = wave_sum_u32(v.x);
+    v.y = wave_sum_u32(v.y);
+    if (lane == 0) s_p[w] = v;
+    __syncthreads();
+    wb = make_uint2(0u, 0u);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      wb.x += s_p[k].x;
+      wb.y += s_p[k].y;
+    }
+  } else {
+    __syncthreads();
+    wb = bsum[blockIdx.x];
+  }
 #pragma unroll
   for (int k = 0; k < NW; ++k) {
     const uint2 x = s_w[k];
@@ -810,12 +839,13 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 }
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
-                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, hipStream_t s) {
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
   hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + kDupScanThreads - 1) / kDupScanThreads), dim3(kDupScanThreads), 0,
                      s, (uint32_t)a.P, bshift, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
+                     bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
                      at<uint32_t>(geom, L.slot_start), pflag, keys, vals);
   return hipGetLastError();

@@ -520,7 +520,7 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 template <int PER>
 __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed, uint32_t stride,
                                                       const uint32_t* __restrict__ idx, uint32_t n,
-                                                      uint2* __restrict__ bsum) {
+                                                      uint2* __restrict__ bsum, uint2* __restrict__ bsup) {
   __shared__ uint2 s_tmp[4];
   const int t = threadIdx.x;
   const size_t b0 = (size_t)blockIdx.x * (256 * PER) + (size_t)t * PER;
@@ -536,7 +536,14 @@ __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict
   }
   uint2 tot;
   block_excl_scan256_2(acc, s_tmp, &tot);
-  if (t == 0) bsum[blockIdx.x] = tot;
+  if (t == 0) {
+    bsum[blockIdx.x] = tot;
+    if (bsup) {  // (superblock mode: bsum keeps the raw block sums)
+      uint32_t* sp = reinterpret_cast<uint32_t*>(&bsup[(size_t)(blockIdx.x / kScanSupBlocks) * kScanSupStride]);
+      if (tot.x) atomicAdd(sp, tot.x);
+      if (tot.y) atomicAdd(sp + 1, tot.y);
+    }
+  }
 }
 
 // single workgroup of 1024 threads: exclusive scan of the nbs block sums in
@@ -774,13 +781,13 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
 }
 
 hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
-                              hipStream_t stream) {
+                              hipStream_t stream, void* bsup) {
   const uint32_t nbs = (uint32_t)((n + kPackedScanTile - 1) / kPackedScanTile);
   if (n == 0) return hipMemsetAsync(bsum, 0, sizeof(uint2), stream);
   uint2* bs = static_cast<uint2*>(bsum);
   hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, stride, idx,
-                     (uint32_t)n, bs);
-  hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(1024), 0, stream, bs, nbs);
+                     (uint32_t)n, bs, static_cast<uint2*>(bsup));
+  if (!bsup) hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(1024), 0, stream, bs, nbs);
   return hipGetLastError();
 }
 

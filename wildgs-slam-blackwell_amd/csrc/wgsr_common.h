@@ -607,9 +607,19 @@ __host__ __device__ inline size_t sort_status_bytes(size_t n) {
 constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
 // Per-Gaussian state (geometry buffer).
+// The dual scan's block sums are also summed per kScanSupBlocks consecutive
+// blocks (atomics into a zeroed region), so k_duplicate_bins derives its
+// blocks' exclusive prefix without a scan kernel in between.
+constexpr uint32_t kScanSupBlocks = 16;
+constexpr uint32_t kScanSupStride = 16;  // uint2 per superblock sum: one 128-byte line each (atomic spread)
+__host__ __device__ inline size_t packed_scan_supers(size_t n) {
+  const size_t nbs = (n + kPackedScanTile - 1) / kPackedScanTile;
+  return (nbs + kScanSupBlocks - 1) / kScanSupBlocks;
+}
+
 struct GeomLayout {
   size_t splat, lrec, clamped, dkey, dkey_alt, dval, dval_alt, offs, slot_start, tb, hist,
-      totals, bsum, counter, gflag, total;
+      totals, bsum, bsup, counter, gflag, total;
   __host__ __device__ explicit GeomLayout(size_t P) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -626,6 +636,7 @@ struct GeomLayout {
     hist = take(sort_status_bytes(P));    // radix sort look-back status
     totals = take(kSortTotalsBytes);
     bsum = take(8 * ((P + kPackedScanTile - 1) / kPackedScanTile + 1));  // uint2 block sums of the (dual) scans
+    bsup = take(8 * kScanSupStride * (packed_scan_supers(P) + 1));  // uint2 sums of kScanSupBlocks block sums
     counter = take(kCounterBytes);  // see kCounterBytes
     gflag = take(P);               // per Gaussian: some tile's backward wrote a partial record
                                    // (zeroed by k_preprocess, set by the render backward)

@@ -34,10 +34,13 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
 // First two steps of a scan of packed (lo 16 | hi 16) values gathered as
 // packed[idx[i]]: bsum[b] = exclusive prefix (lo sums, hi sums) of block b of
 // kScanTile elements, bsum[blocks] = totals.  bsum: 8 x (blocks + 1) bytes.
+// With bsup (zeroed, packed_scan_supers(n) uint2): bsum keeps the raw block
+// sums and bsup[s] the sums of blocks [16 s, 16 s + 16); no prefix pass.
 // The down-sweep is the caller's (k_scan_bins_down emits pairs).
 // packed[idx[i] * stride]: (lo 16 | hi 16 bits) pairs gathered through idx
 hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
-                              hipStream_t stream);
+                              hipStream_t stream,
+                              void* bsup = nullptr);
 
 int num_bits(uint32_t n);  // bits needed to represent values in [0, n)
 
@@ -59,7 +62,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 // the slot flags zeroed) fused with the (bin | exact tile mask << 16,
 // Gaussian) pair expansion.
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
-                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, hipStream_t s);
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
