@@ -544,6 +544,10 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
   const uint32_t shift = 16u + ((uint32_t)r << bshift), rmask = (1u << B) - 1u;
   uint32_t count[4] = {0u, 0u, 0u, 0u};
   uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
+  // the next step's entries load while this step runs: the empty asm uses
+  // below make the compiler wait for them at the END of a step (without
+  // them it waits at the top, right after issuing them)
+  asm volatile("" ::"v"(key), "v"(gid));
   for (uint32_t e0 = lo; e0 < hi; e0 += kExpThreads) {
     const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
     const uint32_t e1 = e0 + kExpThreads + t;
@@ -570,6 +574,7 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
       count[c] += tot;
     }
     __syncthreads();
+    asm volatile("" ::"v"(key), "v"(gid));
   }
   if (t < B) {
     const int tx = (bx << bshift) + t;
