@@ -88,19 +88,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   float T[Q], tb[Q];
   uint32_t last[Q], mq[Q];
   uint32_t m = 0;
+  // every quadrant's pixel loads first (one round trip; pixels outside the
+  // image read pixel 0 and are zeroed after), then the sums
+  bool inside[Q];
 #pragma unroll
   for (int p = 0; p < Q; ++p) {
     const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
-    const bool inside = px < W && py < H;
-    const size_t pid = (size_t)py * W + px;
-    const float Tf = inside ? final_Ts[pid] : 0.f;
-    last[p] = inside ? n_contrib[pid] : 0u;
-    const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
-    const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
-    dp01[p] = v2f{d0, d1};
-    dp2d[p] = v2f{d2, dd};
+    inside[p] = px < W && py < H;
+    const size_t pid = inside[p] ? (size_t)py * W + px : 0;
+    T[p] = final_Ts[pid];
+    last[p] = n_contrib[pid];
+    dp01[p] = v2f{dL_dpix[pid], dL_dpix[HW + pid]};
+    dp2d[p] = v2f{dL_dpix[2 * HW + pid], dL_ddep[pid]};
+  }
+#pragma unroll
+  for (int p = 0; p < Q; ++p) {
+    T[p] = inside[p] ? T[p] : 0.f;
+    last[p] = inside[p] ? last[p] : 0u;
+    dp01[p] = inside[p] ? dp01[p] : v2f{0.f, 0.f};
+    dp2d[p] = inside[p] ? dp2d[p] : v2f{0.f, 0.f};
+    const float Tf = T[p], d0 = dp01[p].x, d1 = dp01[p].y, d2 = dp2d[p].x;
     tb[p] = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);  // background term: dL/dalpha += tb / (1 - alpha)
-    T[p] = Tf;
     accd[p] = 0.f;
     // quadrant p takes gradient from list indices < mq[p] only
     uint32_t x = last[p];
