@@ -169,6 +169,18 @@ def test_both_backward_render_kernels(P, W, H, deg, view, kernel, monkeypatch):
     check_against(out, _cpu_expect(inputs, settings, grads))
 
 
+@pytest.mark.parametrize("kernel", ["quad", "split"])
+def test_backward_render_kernels_nonzero_background(kernel, monkeypatch):
+    """Both render-backward kernels with a coloured background (the quad
+    kernel specialises a black one, whose dL/dalpha term vanishes) against
+    the CPU restatement."""
+    monkeypatch.setenv("WGSR_BWD_SPLIT_BELOW", "0" if kernel == "quad" else "1000000")
+    inputs, settings, grads = _synthetic(20_000, 640, 480, 3, 2)
+    settings = dict(settings, bg=torch.tensor([0.3, 0.55, 0.8]))
+    out = run_c(inputs, settings, grads)
+    check_against(out, _cpu_expect(inputs, settings, grads))
+
+
 @pytest.mark.parametrize("P,W,H,deg,view", [(20_000, 640, 480, 3, 2), (8_000, 320, 240, 1, 1), (5_000, 200, 136, 0, 0)])
 def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
     """The per-Gaussian backward modes agree and match the CPU restatement:

@@ -59,24 +59,22 @@ __device__ __forceinline__ void record_sums(const float4& A, const float4& B, fl
 // the quadrants the splat can reach (wave-uniform branches) -- the culling of
 // the 4-wave layout -- but sums all of them with ONE wave reduction and writes
 // the record without a cross-wave combine.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
-    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
-    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
-    const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
-    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
-    uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
+// kBg = false: a black background (the mapper's default), whose term
+// -T_final (bg . dL/dpixel) / (1 - alpha) of dL/dalpha is zero -- one packed
+// multiply and a register move fewer per evaluation
+template <bool kBg>
+__device__ __forceinline__ void render_bwd_quad_tile(
+    const uint32_t tile, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g,
+    const float4* __restrict__ splat, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
+    int H, int gx, float bg0, float bg1, float bg2, const float* __restrict__ final_Ts,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, float4* sA, float4* sB,
+    float4* sC, uint32_t* sG, float (*sP)[11], uint32_t* sHit) {
   constexpr int Q = 4;
-  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
-  __shared__ uint32_t sG[kBatch];
-  __shared__ float sP[kBatch][11];
-  __shared__ uint32_t sHit[kBatch];
-  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const int lane = threadIdx.x;
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
-  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
   // per-quadrant pixel state; pairs are packed for v_pk_* math.  Pixel
   // positions are not kept per quadrant: quadrant p's pixel is this lane's
@@ -108,7 +106,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     dp01[p] = inside[p] ? dp01[p] : v2f{0.f, 0.f};
     dp2d[p] = inside[p] ? dp2d[p] : v2f{0.f, 0.f};
     const float Tf = T[p], d0 = dp01[p].x, d1 = dp01[p].y, d2 = dp2d[p].x;
-    tb[p] = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);  // background term: dL/dalpha += tb / (1 - alpha)
+    tb[p] = kBg ? -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2) : 0.f;  // background: dL/dalpha += tb / (1 - alpha)
     accd[p] = 0.f;
     // quadrant p takes gradient from list indices < mq[p] only
     uint32_t x = last[p];
@@ -207,7 +205,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         // which follows the same recurrence (accd += alpha (c.dp - accd))
         const v2f cp = c01 * dp01[p] + c2d * dp2d[p];
         const float sd = (cp.x + cp.y) - accd[p];
-        float dLda = sd * Tn + tb[p] * rinv;
+        float dLda = kBg ? sd * Tn + tb[p] * rinv : sd * Tn;
         dLda = v ? dLda : 0.f;
         accd[p] += alpha * sd;
         const float gl = G * dLda;   // dL/dG / opacity
@@ -243,10 +241,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       gflag[gid] = 1;  // same value from every tile: a benign race
     }
   }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
+    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
+    const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
+    const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
+    uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
+  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
+  __shared__ uint32_t sG[kBatch];
+  __shared__ float sP[kBatch][11];
+  __shared__ uint32_t sHit[kBatch];
+  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
+  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+  if (bg0 == 0.f && bg1 == 0.f && bg2 == 0.f)  // (uniform)
+    render_bwd_quad_tile<false>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
+                                n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
+  else
+    render_bwd_quad_tile<true>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
+                               n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
   // this tile's share of the per-Gaussian outputs' zero fill (HBM is idle
   // here; measured at 1M/1080p: render_bwd +2 % with the fill after the walk,
   // +4.5 % before it, while k_gauss_bwd drops from 86 to 49 us)
-  zero_share(zero, blockIdx.x, gridDim.x, lane, 64);
+  zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
 }
 
 // Small images (few tiles: TUM's 512x384 has 768) leave most SIMDs without a
