@@ -12,7 +12,8 @@ cp $pkg/csrc/* $tmp/
 cp $over/* $tmp/ 2>/dev/null || true
 mkdir -p $pkg/lib/variants $tmp/obj
 for f in $tmp/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 ${VFLAGS:-} -I$tmp -I$root/include -c $f -o $tmp/obj/$(basename $f .hip).o &
+  extra=""; [ "$(basename $f)" = raster_bwd.hip ] && extra="${BWD_FLAGS--fno-slp-vectorize}"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 ${VFLAGS:-} $extra -I$tmp -I$root/include -c $f -o $tmp/obj/$(basename $f .hip).o &
 done
 wait
 /opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $pkg/lib/variants/$name.so $tmp/obj/*.o

@@ -184,8 +184,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
         // phase 1: does entry j reach this lane's pixel of quadrant p?
         const v2f d = d0 - v2f{8.f * (p & 1), 8.f * (p >> 1)};  // (dx, dy) = mean - pixel
-        const v2f q2 = cd * d * d;  // log2(e) x (-conic_xx dx^2 / 2, -conic_yy dy^2 / 2)
-        const float power = q2.x + q2.y + (cxy * d.x) * d.y;  // log2(e) x upstream's power
+        const float power = splat_power(cd, cxy, d);  // log2(e) x upstream's power
         const float G = __builtin_amdgcn_exp2f(power);
         const float av = fminf(kMaxAlpha, op * G);
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
@@ -360,8 +359,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
       const float cxy = B.x, op = B.y;
       const v2f d = mxy - p0;
-      const v2f q2 = cd * d * d;
-      const float power = q2.x + q2.y + (cxy * d.x) * d.y;
+      const float power = splat_power(cd, cxy, d);
       const float G = __builtin_amdgcn_exp2f(power);
       const float av = fminf(kMaxAlpha, op * G);
       const bool v = cidx < last && power <= 0.0f && av >= kMinAlpha;

@@ -703,8 +703,7 @@ __device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const u
     const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
     const float4 Cc = sC[j];
     const v2f d = v2f{A.x, A.y} - pxy;                     // (dx, dy) = mean - pixel
-    const v2f q2 = v2f{A.z, A.w} * d * d;                  // log2(e) x (-conic_xx dx^2/2, -conic_yy dy^2/2)
-    const float power = q2.x + q2.y + (B.x * d.x) * d.y;  // log2(e) x upstream's power
+    const float power = splat_power(v2f{A.z, A.w}, B.x, d);  // log2(e) x upstream's power
     const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
     const float test_T = fmaf(-T, alpha, T);  // T (1 - alpha)
     const uint64_t live = wave_ballot(power <= 0.0f) & wave_ballot(alpha >= kMinAlpha) & ~dm;

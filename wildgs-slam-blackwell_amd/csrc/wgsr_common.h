@@ -423,6 +423,24 @@ __device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B,
 // Two packed floats: arithmetic on these lowers to v_pk_*_f32 on gfx950.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// log2(e) x upstream's power at (dx, dy) = mean - pixel, from the pre-scaled
+// conic (cd = (A.z, A.w), cxy = B.x): A.z dx^2 + A.w dy^2 + B.x dx dy
+// evaluated as dx (A.z dx + B.x dy) + A.w dy^2 -- one packed multiply and
+// three scalar ops.  The forward and both backwards call this one helper, so
+// the backward recomputes exactly the forward's alpha.
+#ifndef WGSR_POWER_FMA
+#define WGSR_POWER_FMA 1
+#endif
+__device__ __forceinline__ float splat_power(v2f cd, float cxy, v2f d) {
+#if WGSR_POWER_FMA
+  const v2f t = cd * d;
+  return fmaf(d.x, fmaf(cxy, d.y, t.x), t.y * d.y);
+#else
+  const v2f q2 = cd * d * d;
+  return q2.x + q2.y + (cxy * d.x) * d.y;
+#endif
+}
+
 // Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
 
 // ---------------------------------------------------------------------------
