@@ -25,6 +25,11 @@ namespace wgsr {
 namespace {
 
 constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
+// the quad backward keeps its "entry left a partial" flags as one SGPR mask
+// instead of an LDS array (one VALU move and one LDS store fewer per entry)
+#ifndef WGSR_BWD_HITMASK
+#define WGSR_BWD_HITMASK 1
+#endif
 // below this many tiles the backward runs k_render_bwd_split (four waves per
 // tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
 constexpr int kBwdSplitBelowTiles = 3072;
@@ -119,6 +124,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   // flags stay 0 (zeroed before the launch), and so does every entry no pixel
   // of the tile receives gradient from -- typically > 90 % of all pairs
   const uint32_t end = range.x + m;
+  float* const sPm = &sP[0][0] + sum10_slot(lane);  // this lane's store slot in an entry's row
 
   // prefetch pipeline (back to front): records of the next batch in
   // registers, ids one batch further
@@ -139,7 +145,9 @@ __device__ __forceinline__ void render_bwd_quad_tile(
     sB[lane] = nB;
     sC[lane] = nC;
     sG[lane] = gcur;
+#if !WGSR_BWD_HITMASK
     sHit[lane] = 0;
+#endif
     __syncthreads();
     gcur = gnext;
     if (b_end >= range.x + 1 + kBatch + lane) {
@@ -163,6 +171,9 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       }
     }
     uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
+#if WGSR_BWD_HITMASK
+    uint64_t hitm = 0;  // entries that left a partial (wave-uniform: SGPRs)
+#endif
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;
@@ -218,11 +229,19 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       }
       if (!hit) continue;  // no pixel of the tile: no partial
       const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
-      wave_sum10_store(gv, &sP[j][0]);
+      wave_sum10_store_m(gv, sPm + 11 * j);
+#if WGSR_BWD_HITMASK
+      hitm |= 1ull << j;
+#else
       if (lane == 0) sHit[j] = 1;
+#endif
     }
     __syncthreads();
+#if WGSR_BWD_HITMASK
+    if (lane < cnt && ((hitm >> lane) & 1)) {
+#else
     if (lane < cnt && sHit[lane]) {
+#endif
       // duplicate slot of (Gaussian, this tile): its first slot plus the
       // tile's index in the Gaussian's exact tile list (k_duplicate)
       const uint32_t gid = sG[lane];

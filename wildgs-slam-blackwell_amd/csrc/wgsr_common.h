@@ -69,33 +69,62 @@ __device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
 //   v_permlane32_swap pairs values (lanes 0-31 keep value 2k, 32-63 value
 //   2k+1): 5 swaps + 5 adds; v_permlane16_swap pairs those by rows: 3 swaps
 //   + 3 adds; then 3 x 4 DPP row adds.  ~30 VALU ops instead of 60 shuffles.
-__device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
+#ifndef WGSR_SUM10_V2
+#define WGSR_SUM10_V2 1
+#endif
+// Lane 15 of row r holds, after wave_sum10, value m of S[0], 4 + m of S[1]
+// and (even rows only, where m = r / 2) 8 + m of S[2], m = sum10_slot(lane).
+__device__ __forceinline__ int sum10_slot(int lane) {
+  const int row = lane >> 4;
+  return (row & 1) * 2 + (row >> 1);
+}
+__device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) {
   float R[5];
+  uint32_t R4b = 0u;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * k]), __float_as_uint(v[2 * k + 1]), false,
                                               false);
     R[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    if (k == 4) R4b = r[1];
   }
-  float S[3];
   {
     auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[0]), __float_as_uint(R[1]), false, false);
     S[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v0 v2 v1 v3
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[2]), __float_as_uint(R[3]), false, false);
     S[1] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v4 v6 v5 v7
+#if WGSR_SUM10_V2
+    // the partner register's rows only reach S[2]'s odd rows, which are never
+    // stored: pass a dead register (no zero move)
+    r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), R4b, false, false);
+    S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 - v9 -
+#else
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), 0u, false, false);
     S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 0 v9 0
+#endif
   }
 #pragma unroll
   for (int i = 0; i < 3; ++i) S[i] = dpp_row_sum16(S[i]);
+#if WGSR_SUM10_V2
+  // materialise the sums before the store branch, so the last DPP step folds
+  // into one v_add_f32_dpp instead of a DPP move + an add inside the branch
+  asm volatile("" ::"v"(S[0]), "v"(S[1]), "v"(S[2]));
+#endif
+}
+// dstm = the entry's 10 floats + sum10_slot(lane): the lane part of the
+// address computed once by the caller, one address register for all stores
+__device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], float* dstm) {
+  float S[3];
+  wave_sum10(v, S);
   const int lane = __lane_id();
   if ((lane & 15) == 15) {
-    const int row = lane >> 4;
-    const int m = (row & 1) * 2 + (row >> 1);
-    dst[m] = S[0];
-    dst[4 + m] = S[1];
-    if (!(row & 1)) dst[8 + (row >> 1)] = S[2];
+    dstm[0] = S[0];
+    dstm[4] = S[1];
+    if (!((lane >> 4) & 1)) dstm[8] = S[2];
   }
+}
+__device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
+  wave_sum10_store_m(v, dst + sum10_slot(__lane_id()));
 }
 
 // inclusive prefix sum across the wave
