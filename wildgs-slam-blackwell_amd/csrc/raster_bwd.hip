@@ -27,6 +27,11 @@ namespace {
 constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 // the quad backward keeps its "entry left a partial" flags as one SGPR mask
 // instead of an LDS array (one VALU move and one LDS store fewer per entry)
+// the render backward's per-pixel gradient body under the pixel's exec mask
+// instead of branch-free with alpha = 0 and dL/dalpha = 0 selects
+#ifndef WGSR_BWD_MASKED
+#define WGSR_BWD_MASKED 1
+#endif
 #ifndef WGSR_BWD_HITMASK
 #define WGSR_BWD_HITMASK 1
 #endif
@@ -201,6 +206,34 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
         if (!wave_any(v)) continue;
         hit = true;
+#if WGSR_BWD_MASKED
+        // phase 2 on the lanes whose pixel the entry reaches (exec mask): the
+        // others keep T, the accumulated colour and their sums as they are.
+        // Constant factors of the mean2D (0.5 W, 0.5 H) and conic (-0.5)
+        // gradients are applied once per Gaussian in k_gauss_bwd.
+        if (v) {
+          const float alpha = av;
+          const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);  // alpha <= 0.99
+          const float Tn = T[p] * rinv;
+          T[p] = Tn;
+          const float dch = alpha * Tn;
+          // colour / depth behind this contributor: upstream's accum_rec enters
+          // dL/dalpha only through its dot product with dL/d(colour, depth),
+          // which follows the same recurrence (accd += alpha (c.dp - accd))
+          const v2f cp = c01 * dp01[p] + c2d * dp2d[p];
+          const float sd = (cp.x + cp.y) - accd[p];
+          const float dLda = kBg ? sd * Tn + tb[p] * rinv : sd * Tn;
+          accd[p] += alpha * sd;
+          const float gl = G * dLda;   // dL/dG / opacity
+          const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
+          g01 += u;
+          g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG / opacity
+          g4 += u.y * d.y;
+          g5 += gl;
+          g67 += dch * dp01[p];
+          g89 += dch * dp2d[p];
+        }
+#else
         // phase 2: branch-free; a lane whose pixel the entry misses runs with
         // alpha = 0 (T and the accumulated colour pass through exactly) and
         // dL/dalpha = 0.  Constant factors of the mean2D (0.5 W, 0.5 H) and
@@ -226,6 +259,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         g5 += gl;
         g67 += dch * dp01[p];
         g89 += dch * dp2d[p];
+#endif
       }
       if (!hit) continue;  // no pixel of the tile: no partial
       const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
