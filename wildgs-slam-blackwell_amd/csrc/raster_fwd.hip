@@ -688,14 +688,18 @@ constexpr int kFwdBatch = 64;
 // front to back.  Contributor number of entry j: cbase + j, or (bin lists)
 // sIdx[j] + 1, its position in the bin's list.  n_touched increments are
 // staged per entry in sTouch and leave as one atomic wave instruction.
-template <bool kIdx>
-__device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const uint32_t* sIdx, const float4* sA,
-                                                const float4* sB, const float4* sC, const uint32_t* sG,
-                                                uint32_t* sTouch, int wx0, int wx1, int wy0, int wy1, v2f pxy,
-                                                int lane, int32_t* __restrict__ n_touched, float& T, v2f& c01,
-                                                v2f& c2d, uint32_t& last, uint64_t& dm) {
-  uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-  sTouch[lane] = 0;
+// WGSR_FWD_HALF: a batch whose wave has no pixel left with T > 0.5 runs the
+// entry loop without the n_touched bookkeeping (T only falls, so none of its
+// entries can touch a pixel): one compare, two VALU moves and one LDS store
+// fewer per entry, with no per-entry branch
+#ifndef WGSR_FWD_HALF
+#define WGSR_FWD_HALF 1
+#endif
+template <bool kIdx, bool kTouch>
+__device__ __forceinline__ void fwd_blend_loop(uint64_t todo, uint32_t cbase, const uint32_t* sIdx,
+                                               const float4* sA, const float4* sB, const float4* sC,
+                                               uint32_t* sTouch, v2f pxy, float& T, v2f& c01, v2f& c2d,
+                                               uint32_t& last, uint64_t& dm) {
   while (todo != 0 && dm != ~0ull) {
     const int j = __builtin_ctzll(todo);
     todo &= ~(1ull << j);
@@ -714,12 +718,30 @@ __device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const u
     c01 += wgt * v2f{Cc.x, Cc.y};
     c2d += wgt * v2f{Cc.z, Cc.w};
     // upstream n_touched: pixels whose T stays above 0.5 after this blend
-    const uint32_t tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
+    uint32_t tot = 0;
+    if (kTouch) tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
     T = bl ? test_T : T;
     last = bl ? (kIdx ? sIdx[j] + 1u : cbase + j) : last;
     dm |= live & low;
-    sTouch[j] = tot;  // (every lane stores the same value: no branch)
+    if (kTouch) sTouch[j] = tot;  // (every lane stores the same value: no branch)
   }
+}
+
+template <bool kIdx>
+__device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const uint32_t* sIdx, const float4* sA,
+                                                const float4* sB, const float4* sC, const uint32_t* sG,
+                                                uint32_t* sTouch, int wx0, int wx1, int wy0, int wy1, v2f pxy,
+                                                int lane, int32_t* __restrict__ n_touched, float& T, v2f& c01,
+                                                v2f& c2d, uint32_t& last, uint64_t& dm) {
+  const uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
+#if WGSR_FWD_HALF
+  if ((wave_ballot(T > 0.5f) & ~dm) == 0) {  // (uniform)
+    fwd_blend_loop<kIdx, false>(todo, cbase, sIdx, sA, sB, sC, sTouch, pxy, T, c01, c2d, last, dm);
+    return;
+  }
+#endif
+  sTouch[lane] = 0;
+  fwd_blend_loop<kIdx, true>(todo, cbase, sIdx, sA, sB, sC, sTouch, pxy, T, c01, c2d, last, dm);
   // one atomic per touched entry, all of the batch's in one wave instruction
   const uint32_t tv = sTouch[lane];
   if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
