@@ -327,6 +327,38 @@ def test_repeated_backward_of_one_forward_is_identical():
         assert torch.equal(c[0], c[1])
 
 
+def test_forwards_back_to_back_on_two_streams():
+    """The forward's pair counters live in two persistent blocks per host
+    thread (one accumulates, k_preprocess zeroes the other for the next
+    call): forwards of different scenes alternating between two streams,
+    without synchronising, give the counts and images of a lone forward."""
+    C = _c()
+    scenes = []
+    for P, seed in ((10_000, 0), (3_000, 1), (20_000, 2)):
+        inputs, st, _ = _synthetic(P, 320, 240, 3, 1, seed=seed)
+        d = lambda x: x.to(DEV)  # noqa: E731
+        e = torch.empty(0, device=DEV)
+        scenes.append((d(st["bg"]), d(inputs["means3D"]), e, d(inputs["opacities"]), d(inputs["scales"]),
+                       d(inputs["rotations"]), 1.0, e, d(st["viewmatrix"]), d(st["projmatrix"]),
+                       d(st["projmatrix_raw"]), st["tanfovx"], st["tanfovy"], st["H"], st["W"], d(inputs["shs"]), 3,
+                       d(st["campos"]), False, False))
+    alone = []
+    for a in scenes:
+        out = C.rasterize_gaussians(*a)
+        torch.cuda.synchronize()
+        alone.append((out[0], out[1].clone(), out[2].clone()))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for k in range(9):
+        with torch.cuda.stream(streams[k % 2]):
+            out = C.rasterize_gaussians(*scenes[k % 3])
+            got.append((k % 3, out[0], out[1], out[2]))
+    torch.cuda.synchronize()
+    for i, nr, color, radii in got:
+        assert nr == alone[i][0]
+        assert torch.equal(color, alone[i][1]) and torch.equal(radii, alone[i][2])
+
+
 def test_exact_tile_lists_elongated_splats():
     """Stress the exact tile lists (row_span) and the per-wave ellipse culling:
     needle-like rotated splats (per-axis scales over 2.6 decades) and opacities

@@ -42,6 +42,40 @@ HostCounters& host_counters() {
   return hc;
 }
 
+// The forward's counter block without a memset launch per call: two blocks
+// per (host thread, device) in device memory.  A forward accumulates into one
+// and its k_preprocess zeroes the other for the next forward on this thread.
+// The previous forward's block was last touched by its D->H copy, which the
+// host waited for before that call returned, so no stream (ours or another)
+// can still be reading it.  WGSR_COUNTER_MEMSET=1 keeps the memset of the
+// geometry buffer's counter block.
+struct DevCounters {
+  uint32_t* buf = nullptr;  // 2 x kCounterBytes, zeroed once
+  int parity = 0;
+  bool failed = false;
+};
+DevCounters* dev_counters() {
+  static const bool off = [] {
+    const char* e = getenv("WGSR_COUNTER_MEMSET");
+    return e && strcmp(e, "1") == 0;
+  }();
+  if (off) return nullptr;
+  thread_local DevCounters per_dev[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  DevCounters& dc = per_dev[dev];
+  if (!dc.buf && !dc.failed) {
+    void* p = nullptr;
+    if (hipMalloc(&p, 2 * kCounterBytes) != hipSuccess || hipMemset(p, 0, 2 * kCounterBytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      dc.failed = true;  // fall back to the per-call memset
+      return nullptr;
+    }
+    dc.buf = static_cast<uint32_t*>(p);
+  }
+  return dc.buf ? &dc : nullptr;
+}
+
 }
 
 int set_error(int code, const char* fmt, ...) {
@@ -244,15 +278,20 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // counter block (kCounterBytes): error flags and the partial sums of
   // upstream's num_rendered and of the exact list lengths, all produced by
   // k_preprocess
-  uint32_t* counter = at<uint32_t>(geom, GL.counter);
-  HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
+  DevCounters* dc = dev_counters();
+  uint32_t* counter = dc ? dc->buf + (size_t)dc->parity * (kCounterBytes / 4) : at<uint32_t>(geom, GL.counter);
+  if (!dc) HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
   const int bshift = bin_shift(a);
   const Bins bins(grid.gx, grid.gy, bshift);
   // the depth sort's superblock sums are zeroed by k_preprocess's workgroups
-  // (no memset launch)
+  // (no memset launch), and so is the next forward's counter block
   size_t sup_off = 0;
   const size_t sup_words = sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off);
   ZeroJob zj{};
+  if (dc) {
+    zj.p[zj.count] = reinterpret_cast<float*>(dc->buf + (size_t)(dc->parity ^ 1) * (kCounterBytes / 4));
+    zj.n[zj.count++] = kCounterBytes / 4;
+  }
   if (sup_words) {
     zj.p[zj.count] = reinterpret_cast<float*>(at<uint32_t>(geom, GL.hist) + sup_off);
     zj.n[zj.count++] = sup_words;
@@ -264,8 +303,10 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
   }
   { StageTimer T(0, s);
-  STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
-                                reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s)); }
+  const hipError_t pe = launch_preprocess(a, geom, radii, n_touched, counter + 1,
+                                          reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s);
+  if (pe == hipSuccess && dc) dc->parity ^= 1;  // k_preprocess, which zeroes the other block, is queued
+  STAGE(a, s, pe); }
 
   // The pair counts are known once k_preprocess is done: copy them to pinned
   // host memory behind it and let the depth sort + scan run while the host
@@ -293,7 +334,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   } else {
     STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
                                       at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
-                                      at<uint32_t>(geom, GL.bsum), counter, s, sizeof(ListRec) / 4));
+                                      at<uint32_t>(geom, GL.bsum), at<uint32_t>(geom, GL.counter), s,
+                                      sizeof(ListRec) / 4));
   }
   delete scan_timer;
   HIPCHK(hipEventSynchronize(hc.ev));
