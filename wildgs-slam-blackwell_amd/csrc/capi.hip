@@ -54,7 +54,7 @@ struct DevCounters {
   int parity = 0;
   bool failed = false;
 };
-DevCounters* dev_counters() {
+DevCounters* dev_counters(hipStream_t s) {
   static const bool off = [] {
     const char* e = getenv("WGSR_COUNTER_MEMSET");
     return e && strcmp(e, "1") == 0;
@@ -66,8 +66,9 @@ DevCounters* dev_counters() {
   DevCounters& dc = per_dev[dev];
   if (!dc.buf && !dc.failed) {
     void* p = nullptr;
-    if (hipMalloc(&p, 2 * kCounterBytes) != hipSuccess || hipMemset(p, 0, 2 * kCounterBytes) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
+    // zeroed on the first forward's stream (ahead of its k_preprocess; any
+    // later forward of this thread starts after this one's host wait)
+    if (hipMalloc(&p, 2 * kCounterBytes) != hipSuccess || hipMemsetAsync(p, 0, 2 * kCounterBytes, s) != hipSuccess) {
       dc.failed = true;  // fall back to the per-call memset
       return nullptr;
     }
@@ -278,7 +279,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // counter block (kCounterBytes): error flags and the partial sums of
   // upstream's num_rendered and of the exact list lengths, all produced by
   // k_preprocess
-  DevCounters* dc = dev_counters();
+  DevCounters* dc = dev_counters(s);
   uint32_t* counter = dc ? dc->buf + (size_t)dc->parity * (kCounterBytes / 4) : at<uint32_t>(geom, GL.counter);
   if (!dc) HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
   const int bshift = bin_shift(a);
