@@ -359,6 +359,47 @@ def test_forwards_back_to_back_on_two_streams():
         assert torch.equal(color, alone[i][1]) and torch.equal(radii, alone[i][2])
 
 
+_MEMSET_CHILD = r"""
+import sys, torch
+sys.path[:0] = sys.argv[1:4]
+import test_gpu_raster as T
+inputs, st, _ = T._synthetic(20_000, 320, 240, 3, 1, seed=4)
+d = lambda x: x.to("cuda")
+e = torch.empty(0, device="cuda")
+a = (d(st["bg"]), d(inputs["means3D"]), e, d(inputs["opacities"]), d(inputs["scales"]), d(inputs["rotations"]),
+     1.0, e, d(st["viewmatrix"]), d(st["projmatrix"]), d(st["projmatrix_raw"]), st["tanfovx"], st["tanfovy"],
+     st["H"], st["W"], d(inputs["shs"]), 3, d(st["campos"]), False, False)
+outs = [T._c().rasterize_gaussians(*a) for _ in range(3)]
+torch.save({"nr": [o[0] for o in outs], "color": outs[-1][1].cpu(), "radii": outs[-1][2].cpu()}, sys.argv[4])
+"""
+
+
+@pytest.mark.parametrize("memset", ["0", "1"])
+def test_counter_blocks_match_memset_mode(tmp_path, memset):
+    """WGSR_COUNTER_MEMSET=1 (the geometry buffer's counter block zeroed by a
+    memset per forward; read once per process, hence a child process) and the
+    default persistent blocks give the same counts and images."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, WGSR_COUNTER_MEMSET=memset)
+    out = tmp_path / "o.pt"
+    subprocess.run([sys.executable, "-c", _MEMSET_CHILD, here, os.path.join(root, "wildgs-slam-blackwell_amd", "python"),
+                    root, str(out)], env=env, check=True, timeout=300)
+    got = torch.load(out, weights_only=True)
+    inputs, st, _ = _synthetic(20_000, 320, 240, 3, 1, seed=4)
+    d = lambda x: x.to(DEV)  # noqa: E731
+    e = torch.empty(0, device=DEV)
+    a = (d(st["bg"]), d(inputs["means3D"]), e, d(inputs["opacities"]), d(inputs["scales"]), d(inputs["rotations"]),
+         1.0, e, d(st["viewmatrix"]), d(st["projmatrix"]), d(st["projmatrix_raw"]), st["tanfovx"], st["tanfovy"],
+         st["H"], st["W"], d(inputs["shs"]), 3, d(st["campos"]), False, False)
+    ref = _c().rasterize_gaussians(*a)
+    assert got["nr"] == [ref[0]] * 3
+    assert torch.equal(got["color"], ref[1].cpu()) and torch.equal(got["radii"], ref[2].cpu())
+
+
 def test_exact_tile_lists_elongated_splats():
     """Stress the exact tile lists (row_span) and the per-wave ellipse culling:
     needle-like rotated splats (per-axis scales over 2.6 decades) and opacities
