@@ -35,7 +35,7 @@ def lib():
         L.cr_forward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _f, _f, _f, _f, _f,
                                  ctypes.c_float, _f, _f, _f, _f, ctypes.c_float, ctypes.c_float,
                                  ctypes.c_int, ctypes.c_int, _f, _f, _f, _f, _f, _i, _i,
-                                 ctypes.POINTER(ctypes.c_longlong)]
+                                 ctypes.POINTER(ctypes.c_longlong), _i, _i]
         L.cr_backward.restype = None
         L.cr_backward.argtypes = [ctypes.c_void_p] + [_f] * 11
         L.cr_free.restype = None
@@ -80,13 +80,19 @@ class CpuRaster:
         self.opacity = np.zeros((1, H, W), np.float32)
         self.radii = np.zeros(P, np.int32)
         self.n_touched = np.zeros(P, np.int32)
+        # blends whose T > 0.5 decision is clear (firm) or within rounding
+        # slack of a threshold (soft), cpu_raster.cpp: any correct count lies
+        # in [firm, firm + soft] and equals n_touched where soft == 0
+        self.n_touched_firm = np.zeros(P, np.int32)
+        self.n_touched_soft = np.zeros(P, np.int32)
         nr = ctypes.c_longlong(0)
         self._h = L.cr_forward(P, int(sh_degree), M, _p(bgn), _p(m), _p(col), _p(o), _p(sc), _p(rot),
                                float(scale_modifier), _p(cov), _p(vm), _p(pm), _p(pr), float(tanfovx),
                                float(tanfovy), int(H), int(W), _p(sh), _p(cp), _p(self.color),
                                _p(self.depth), _p(self.opacity),
                                self.radii.ctypes.data_as(_i), self.n_touched.ctypes.data_as(_i),
-                               ctypes.byref(nr))
+                               ctypes.byref(nr), self.n_touched_firm.ctypes.data_as(_i),
+                               self.n_touched_soft.ctypes.data_as(_i))
         self.num_rendered = int(nr.value)
 
     def backward(self, dL_dcolor, dL_ddepth):

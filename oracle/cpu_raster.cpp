@@ -232,7 +232,7 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
                  const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
                  const float* projmatrix_raw, float tan_fovx, float tan_fovy, int H, int W, const float* sh,
                  const float* campos, float* out_color, float* out_depth, float* out_opacity, int* radii,
-                 int* n_touched, long long* num_rendered) {
+                 int* n_touched, long long* num_rendered, int* n_touched_firm, int* n_touched_soft) {
   State* s = new State();
   s->P = P; s->D = D; s->M = M; s->W = W; s->H = H;
   s->gx = (W + BX - 1) / BX; s->gy = (H + BY - 1) / BY;
@@ -365,10 +365,18 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
   // ---- render (A.3)
   s->final_T.assign((size_t)W * H, 0.f);
   s->n_contrib.assign((size_t)W * H, 0);
-  std::vector<int> touched(P, 0);
+  std::vector<int> touched(P, 0), firm(P, 0), soft(P, 0);
+  // n_touched counts blends with T > 0.5 after the blend.  Besides the plain
+  // count, each decision is classified: FIRM when the oracle's T is away from
+  // 0.5 by more than the slack rounding could explain, SOFT otherwise.  The
+  // slack starts at 1e-5 (relative) and grows by the opacity of every entry
+  // whose inclusion itself sits on a threshold (power ~ 0, alpha ~ 1/255):
+  // another exp() rounding may include or skip it, moving T by that factor.
+  // Such an ambiguous entry is a SOFT candidate itself.  A correct
+  // implementation therefore has firm <= n_touched <= firm + soft, and equals
+  // the oracle exactly wherever soft == 0 (then n_touched == firm).
 #pragma omp parallel
   {
-    std::vector<int> my_touched;  // lazily sized
 #pragma omp for schedule(dynamic, 4)
     for (int tl = 0; tl < ntiles; ++tl) {
       int tx = tl % gx, ty = tl / gx;
@@ -376,6 +384,7 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
       for (int py = ty * BY; py < std::min(H, ty * BY + BY); ++py)
         for (int px = tx * BX; px < std::min(W, tx * BX + BX); ++px) {
           float T = 1.f, C[3] = {0, 0, 0}, Dp = 0.f;
+          float slack = 1e-5f;
           uint32_t contributor = 0, last = 0;
           for (uint32_t j = b; j < e; ++j) {
             contributor++;
@@ -383,6 +392,16 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
             float dx = s->xy[2 * g] - (float)px, dy = s->xy[2 * g + 1] - (float)py;
             const float* co = &s->conic_o[4 * (size_t)g];
             float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+            float a_any = std::min(0.99f, co[3] * std::exp(std::min(power, 0.0f)));
+            bool amb = std::fabs(power) < 1e-5f ||
+                       std::fabs(a_any - 1.0f / 255.0f) <= 1e-4f * (1.0f / 255.0f);
+            if (amb) {
+              slack += std::max(a_any, 1.0f / 255.0f);
+              if (T * (1 - a_any) > 0.5f * (1.0f - 1.02f * slack)) {
+#pragma omp atomic
+                soft[g]++;
+              }
+            }
             if (power > 0.0f) continue;
             float alpha = std::min(0.99f, co[3] * std::exp(power));
             if (alpha < 1.0f / 255.0f) continue;
@@ -393,6 +412,15 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
             if (test_T > 0.5f) {
 #pragma omp atomic
               touched[g]++;
+            }
+            if (!amb) {
+              if (std::fabs(test_T - 0.5f) <= 0.5f * 1.02f * slack) {
+#pragma omp atomic
+                soft[g]++;
+              } else if (test_T > 0.5f) {
+#pragma omp atomic
+                firm[g]++;
+              }
             }
             T = test_T;
             last = contributor;
@@ -405,9 +433,12 @@ void* cr_forward(int P, int D, int M, const float* bg, const float* means3D, con
           out_opacity[pid] = 1 - T;
         }
     }
-    (void)my_touched;
   }
   for (int i = 0; i < P; ++i) { radii[i] = s->radii[i]; n_touched[i] = touched[i]; }
+  if (n_touched_firm)
+    for (int i = 0; i < P; ++i) n_touched_firm[i] = firm[i];
+  if (n_touched_soft)
+    for (int i = 0; i < P; ++i) n_touched_soft[i] = soft[i];
   *num_rendered = (long long)N;
   return s;
 }

@@ -118,7 +118,7 @@ def se3_exp(tau: torch.Tensor) -> torch.Tensor:
 
 def rasterize_dense(means3D, means2D, opacities, shs, colors_precomp, scales, rotations,
                     cov3D_precomp, tau, *, H, W, tanfovx, tanfovy, bg, scale_modifier,
-                    viewmatrix, projmatrix, projmatrix_raw, sh_degree, campos):
+                    viewmatrix, projmatrix, projmatrix_raw, sh_degree, campos, touch_threshold=0.5):
     """Dense forward.  All tensor arguments float64 (leaf tensors may require
     grad).  ``tau`` = [rho(3), theta(3)] (pose delta, zero in every caller).
 
@@ -273,7 +273,7 @@ def rasterize_dense(means3D, means2D, opacities, shs, colors_precomp, scales, ro
             Dd = w @ depth[L][:, None]            # [npx,1]
             Tf = torch.prod(torch.where(keep, one_m, torch.ones_like(one_m)), dim=1, keepdim=True)
             with torch.no_grad():
-                touched = keep & valid & (Tinc > 0.5)
+                touched = keep & valid & (Tinc > touch_threshold)
                 n_touched.index_add_(0, L, touched.sum(0))
             out_c[ty_][tx_] = (Cc + Tf * bgd[None, :]).T
             out_d[ty_][tx_] = Dd.T

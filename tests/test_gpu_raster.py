@@ -5,13 +5,16 @@ Tolerances (written here, SURVEY.md 8(c), north_star "<= 1e-4 rel L1"):
   images (colour, depth, opacity)      rel-L1 <= 1e-4
   radii, num_rendered                  exact (the preprocess arithmetic is
                                        bit-identical to the CPU restatement)
-  n_touched                            exact on the golden scenes; on large
-                                       random scenes <= 1e-4 of the Gaussians
-                                       may differ (it counts pixels whose T
-                                       after blending exceeds 0.5, and T goes
-                                       through exp(), which no two math
-                                       libraries round identically -- the
-                                       upstream CUDA expf included)
+  n_touched                            exact on the golden scenes; against
+                                       the fp32 CPU restatement exact for
+                                       every Gaussian none of whose blend
+                                       decisions sits within rounding slack
+                                       of a threshold (T vs 0.5, alpha vs
+                                       1/255, power vs 0: exp() rounds
+                                       differently in every math library, the
+                                       upstream CUDA expf included), and
+                                       within [firm, firm + soft] for the
+                                       rest (oracle/cpu_raster.cpp)
   per-tensor gradients                 rel-L1 <= 1e-4
   pose gradient (summed over P)        rel-L1 <= 1e-3
   distCUDA2                            bit-exact vs the CPU restatement
@@ -71,7 +74,6 @@ def run_c(inputs, settings, grads, debug=False):
     return out
 
 
-N_TOUCHED_MISMATCH_TOL = 1e-4
 PIX_TOL = 1e-4       # per-pixel abs error (relative to the image's max magnitude) ...
 PIX_BAD_FRAC = 1e-5  # ... exceeded by at most this fraction of pixels (threshold flips)
 PIX_FLIP_TOL = 1e-2  # and never by more than a couple of 1/255 threshold flips
@@ -80,11 +82,13 @@ PIX_FLIP_TOL = 1e-2  # and never by more than a couple of 1/255 threshold flips
 def check_against(out, expect, grad_keys=GRAD_KEYS, exact_touched=False):
     assert out["num_rendered"] == expect["num_rendered"]
     np.testing.assert_array_equal(out["radii"], expect["radii"])
-    if exact_touched:
+    if exact_touched or "n_touched_soft" not in expect:
         np.testing.assert_array_equal(out["n_touched"], expect["n_touched"])
     else:
-        bad = np.count_nonzero(out["n_touched"] != expect["n_touched"])
-        assert bad <= max(1.0, N_TOUCHED_MISMATCH_TOL * len(out["n_touched"])), bad
+        got, firm, soft = out["n_touched"], expect["n_touched_firm"], expect["n_touched_soft"]
+        clear = soft == 0
+        np.testing.assert_array_equal(got[clear], expect["n_touched"][clear])
+        assert np.all((got >= firm) & (got <= firm + soft)), int(np.count_nonzero((got < firm) | (got > firm + soft)))
     for k in ("color", "depth", "opacity"):
         r = rel_l1(out[k], expect[k])
         assert r <= IMG_TOL, (k, r)
@@ -145,7 +149,8 @@ def _cpu_expect(inputs, settings, grads):
     cr = cpu_oracle.CpuRaster(**inputs, **settings)
     g = cr.backward(*grads)
     exp = dict(num_rendered=cr.num_rendered, color=cr.color, depth=cr.depth, opacity=cr.opacity,
-               radii=cr.radii, n_touched=cr.n_touched)
+               radii=cr.radii, n_touched=cr.n_touched, n_touched_firm=cr.n_touched_firm,
+               n_touched_soft=cr.n_touched_soft)
     exp.update(g)
     return exp
 

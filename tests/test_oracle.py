@@ -156,3 +156,27 @@ def test_config0_cpu_plumbing_10k_640x480():
     for k in ("dL_dmeans3D", "dL_dmeans2D", "dL_dopacity", "dL_dscales", "dL_drotations"):
         assert rel_l1(g[k], ref[k].numpy()) <= GRAD_TOL, k
     assert rel_l1(g["dL_dtau"].sum(0), ref["dL_dtau"].numpy()) <= TAU_TOL
+
+
+def test_n_touched_firm_soft_band_is_consistent():
+    """The CPU restatement's n_touched classification (cpu_raster.cpp): its
+    own count lies in [firm, firm + soft], equals firm wherever no decision is
+    soft, and only a small fraction of Gaussians carry a soft decision; on the
+    golden scenes (dense float64 oracle) every firm count matches too."""
+    W, H = 320, 240
+    sc = make_scene(8000, W, H, 3, seed=9)
+    f = wcam.synthetic_camera(W, H, 1).raster_fields()
+    cr = cpu_oracle.CpuRaster(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales,
+                              rotations=sc.rotations, H=H, W=W, tanfovx=f["tanfovx"], tanfovy=f["tanfovy"],
+                              bg=np.zeros(3, np.float32), scale_modifier=1.0, viewmatrix=f["viewmatrix"],
+                              projmatrix=f["projmatrix"], projmatrix_raw=f["projmatrix_raw"], sh_degree=3,
+                              campos=f["campos"])
+    n, firm, soft = cr.n_touched, cr.n_touched_firm, cr.n_touched_soft
+    assert np.all((n >= firm) & (n <= firm + soft))
+    np.testing.assert_array_equal(n[soft == 0], firm[soft == 0])
+    assert np.count_nonzero(soft) <= 0.02 * len(n) and n.sum() > 0
+    for name in scene_names():
+        inputs, settings, expect, grads = load_scene(name)
+        c = cpu_oracle.CpuRaster(**inputs, **settings)
+        clear = c.n_touched_soft == 0
+        np.testing.assert_array_equal(c.n_touched_firm[clear], expect["n_touched"][clear])
