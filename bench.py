@@ -55,9 +55,19 @@ TILE = 16
 
 
 def byte_model(P, N, W, H, K, M):
-    """Algorithmic bytes per stage (SURVEY.md 8(d) per-unit figures)."""
+    """Algorithmic bytes per stage (SURVEY.md 8(d) per-unit figures).
+
+    The gradient outputs' write, P (12 + 12 + 12 M + 4 + 12 + 16 + 24), is
+    booked to render_bwd: the render backward streams every output row's zero
+    fill, and gauss_bwd then writes only the ~8 % of rows that received
+    gradient (so gauss_bwd's figure is its read side only).  The total is
+    SURVEY's.  N is upstream's num_rendered (rectangle pairs), as SURVEY
+    defines it; the build lists fewer pairs (exact tile lists) and sorts
+    (Gaussian, bin) pairs -- the counter bytes (pass_roofline.counter_bytes)
+    are what it actually moves."""
     npix = W * H
     ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
+    grad_write = P * (12 + 12 + 12 * M + 4 + 12 + 16 + 24)
     return {
         "preprocess": P * (44 + 12 * K) + 76 * P,
         "depth_sort": 16 * P,
@@ -66,9 +76,17 @@ def byte_model(P, N, W, H, K, M):
         "tile_sort": 24 * N,
         "ranges": 8 * N + 8 * ntile,
         "render_fwd": 44 * N + 28 * npix + 4 * P,
-        "render_bwd": 48 * N + 24 * npix + 40 * P,
-        "gauss_bwd": P * (44 + 12 * K + 24 + 40) + P * (12 + 12 + 12 * M + 4 + 12 + 16 + 24),
+        "render_bwd": 48 * N + 24 * npix + 40 * P + grad_write,
+        "gauss_bwd": P * (44 + 12 * K + 24 + 40),
     }
+
+
+def workload_label(P, W, H, deg, world):
+    """BASELINE.json config index of this run's workload, or 'custom'."""
+    if world > 1:
+        return "configs[3]" if (P, W, H, deg) == (1_000_000, 1920, 1080, 3) else "custom (multi-GPU)"
+    return {(1_000_000, 1920, 1080, 3): "configs[2]", (200_000, 1920, 1080, 3): "configs[1]",
+            (10_000, 640, 480, 0): "configs[0] (on the GPU)"}.get((P, W, H, deg), "custom")
 
 
 def n_contrib_sum(img_buffer, W, H):
@@ -76,37 +94,26 @@ def n_contrib_sum(img_buffer, W, H):
     def a256(x):
         return (x + 255) & ~255
     ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
-    # ImageLayout (csrc/wgsr_common.h): ranges, tile_len, tile_m, order_fwd,
-    # order_bwd, final_T, n_contrib -- each region 256-byte aligned
+    # ImageLayout (csrc/wgsr_common.h): ranges, tile_len, tile_m, order_bwd,
+    # meta, final_T, n_contrib -- each region 256-byte aligned
     off = 0
-    for nbytes in (8 * ntile, 4 * ntile, 16 * ntile, 4 * ntile, 4 * ntile, 4 * W * H):
+    for nbytes in (8 * ntile, 4 * ntile, 16 * ntile, 4 * ntile, 16, 4 * W * H):
         off += a256(nbytes)
     nc = img_buffer[off: off + 4 * W * H].view(torch.int32)
     return int(nc.sum().item())
 
 
-def load_pmc_stage(stage):
-    """The committed PMC summary's record for ``stage`` (or None)."""
+def load_pmc(P, W, H, sh):
+    """The committed PMC summary (profiles/pmc_summary.json) if it was taken
+    on this workload, else None: counters are never quoted across configs."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        return json.load(open(path)).get("stages", {}).get(stage)
-    except Exception:
-        return None
-
-
-def load_pmc_traffic(stage):
-    """HBM bytes per launch of ``stage`` from the committed PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
-        return None, None
     try:
         d = json.load(open(path))
-        rec = d.get("stages", {}).get(stage)
-        if rec:
-            return float(rec["hbm_bytes_per_launch"]), d.get("source")
     except Exception:
-        pass
-    return None, None
+        return None
+    if d.get("config") != {"P": P, "W": W, "H": H, "sh": sh}:
+        return None
+    return d
 
 
 def main():
@@ -140,12 +147,19 @@ def main():
     backend = os.environ.get("WGSR_BENCH_BACKEND", "nccl")
     if os.environ.get("WGSR_BENCH_SHARE_GPU") == "1":
         local_rank = 0
+    ctrl = None
     if world > 1:
+        from datetime import timedelta
+        # a hung collective ends the run (watchdog timeout -> non-zero exit)
+        # instead of holding the node; the gloo control group decides the
+        # exchange fallback even when an RCCL collective failed
+        tmo = timedelta(seconds=float(os.environ.get("WGSR_BENCH_PG_TIMEOUT", "300")))
         torch.cuda.set_device(local_rank)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+        ctrl = dist.new_group(backend="gloo", timeout=tmo)
     dev = torch.device("cuda", local_rank)
 
     from diff_gaussian_rasterization import _C
@@ -199,32 +213,47 @@ def main():
     exchange_check = None
     if vsb is not None:
         # the views exchange's summed gradients against the plain backward +
-        # RCCL all-reduce of the same views, once before timing; every rank
-        # falls back to the all-reduce exchange if any rank disagrees
-        nr, color, radii, geom, binning, img, depth, opacity, nt = _C.rasterize_gaussians(
-            bg, means, e, opac, scales, rots, 1.0, e, view, proj, praw, tanx, tany, H, W, shs, deg,
-            campos, False, False)
-        got, _, _ = vsb.backward((means, scales, rots, shs, deg, camd, nr, radii, geom, binning, img), gc, gd)
-        ref = GradBuffer.allocate(P, M, dev)
-        _C.rasterize_gaussians_backward(
-            bg, means, radii, e, scales, rots, 1.0, e, view, proj, praw, tanx, tany, gc, gd, shs,
-            deg, campos, geom, nr, binning, img, False, out=ref.views)
+        # RCCL all-reduce of the same views, once before timing.  Every rank
+        # falls back to the all-reduce exchange if any rank disagrees OR any
+        # rank's exchange raised (decided over the gloo control group, which
+        # does not depend on RCCL); if the all-reduce itself fails the run
+        # exits non-zero.
+        err, reason = float("inf"), None
+        try:
+            nr, color, radii, geom, binning, img, depth, opacity, nt = _C.rasterize_gaussians(
+                bg, means, e, opac, scales, rots, 1.0, e, view, proj, praw, tanx, tany, H, W, shs, deg,
+                campos, False, False)
+            got, _, _ = vsb.backward((means, scales, rots, shs, deg, camd, nr, radii, geom, binning, img), gc, gd)
+            ref = GradBuffer.allocate(P, M, dev)
+            _C.rasterize_gaussians_backward(
+                bg, means, radii, e, scales, rots, 1.0, e, view, proj, praw, tanx, tany, gc, gd, shs,
+                deg, campos, geom, nr, binning, img, False, out=ref.views)
+            if world > 1:
+                allreduce_grads(ref)
+            err = 0.0
+            for k, v in ref.views.items():
+                den = float(v.abs().sum())
+                err = max(err, float((got[k] - v).abs().sum()) / max(den, 1e-30))
+            del ref
+            torch.cuda.synchronize()
+        except Exception as ex:  # noqa: BLE001 -- any failure of the exchange: fall back
+            reason = f"{type(ex).__name__}: {ex}"[:400]
+        ok = torch.tensor([1.0 if (reason is None and err <= 1e-5) else 0.0], dtype=torch.float64)
         if world > 1:
-            allreduce_grads(ref)
-        err = 0.0
-        for k, v in ref.views.items():
-            den = float(v.abs().sum())
-            err = max(err, float((got[k] - v).abs().sum()) / max(den, 1e-30))
-        ok = torch.tensor([1.0 if err <= 1e-5 else 0.0], dtype=torch.float64,
-                          device=dev if backend == "nccl" else "cpu")
-        if world > 1:
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=ctrl)
         exchange_check = {"rel_l1_vs_allreduce": err, "ok": bool(ok.item() > 0.5)}
+        if reason is not None:
+            exchange_check["error"] = reason
         if not exchange_check["ok"]:
             exchange, vsb = "allreduce", None
             exchange_check["fallback"] = "allreduce"
-        del ref
-        torch.cuda.synchronize()
+            try:  # the fallback's own collective must work, else stop here
+                allreduce_grads(gbuf)
+                torch.cuda.synchronize()
+            except Exception as ex:  # noqa: BLE001
+                print(json.dumps({"error": f"all-reduce fallback failed: {type(ex).__name__}: {ex}"[:600],
+                                  "exchange_check": exchange_check}), file=sys.stderr)
+                sys.exit(1)
 
     prof = _lib.StageProfile() if not args.no_profile else None
     if world > 1:
@@ -248,6 +277,7 @@ def main():
         dt = float(t.item())
 
     value = P * world * args.steps / dt
+    label = workload_label(P, W, H, deg, world)
     ms_per_step = 1e3 * dt / args.steps
     N = state["nr"]
     out = {
@@ -256,9 +286,9 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": (f"configs[2]: {P} Gaussians, {W}x{H}, SH{deg}, single-view fwd+bwd, pose grad on"
+            "workload": (f"{label}: {P} Gaussians, {W}x{H}, SH{deg}, single-view fwd+bwd, pose grad on"
                          if world == 1 else
-                         f"configs[3]: {P} Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
+                         f"{label}: {P} Gaussians x {world} keyframe views (one per GPU), fwd+bwd "
                          "+ the SUM over views of the per-Gaussian gradients on every rank "
                          f"(RCCL, exchange: {exchange})"),
             "gaussians": P, "image": f"{W}x{H}", "sh_degree": deg, "num_rendered": N,
@@ -288,19 +318,15 @@ def main():
         dom = max(timed, key=lambda k: timed[k][0])
         ms_avg = timed[dom][0] / timed[dom][1]
         achieved = model[dom] / (ms_avg * 1e-3) / 1e9
-        traffic, src = load_pmc_traffic(dom)
+        pmc = load_pmc(P, W, H, deg) if world == 1 else None
+        pst = pmc["stages"] if pmc else {}
+        traffic = pst.get(dom, {}).get("hbm_bytes_per_step") if pmc else None
         out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": achieved,
                            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                            "traffic": traffic, "algorithmic_bytes": model[dom],
                            "avg_launch_ms": ms_avg}
         if traffic is not None:
-            out["roofline"]["traffic_source"] = src
-            if dom == "render_bwd":
-                # the render backward also streams the zero fill of the nine
-                # per-Gaussian gradient outputs (P x 77 floats at SH3), which
-                # the byte model counts under gauss_bwd
-                out["roofline"]["traffic_note"] = ("includes the per-Gaussian gradient zero fill "
-                                                   f"({P * 4 * (3 + 3 + 1 + 3 + 6 + 3 * M + 3 + 4 + 6)} B)")
+            out["roofline"]["traffic_source"] = pmc.get("source")
         # whole fwd+bwd pass against HBM (the north-star roofline) and the
         # render kernels' pair arithmetic against the fp32 VALU peak
         kernel_ms = sum(v[0] for k, v in timed.items()) / max(1, args.steps)
@@ -311,6 +337,15 @@ def main():
             "achieved_GBps_kernels": total_bytes / (kernel_ms * 1e-3) / 1e9,
             "achieved_GBps_step": total_bytes / (ms_per_step * 1e-3) / 1e9,
             "frac_step": total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        if pmc:
+            # what the kernels actually moved (PMC HBM bytes of this workload),
+            # per step, beside the algorithmic figure
+            cb = {k: v["hbm_bytes_per_step"] for k, v in pst.items() if k in model}
+            out["pass_roofline"]["counter_bytes"] = sum(cb.values())
+            out["pass_roofline"]["counter_bytes_by_stage"] = cb
+            out["pass_roofline"]["frac_step_counter"] = (sum(cb.values()) / (ms_per_step * 1e-3) / 1e9
+                                                         / HBM_PEAK_GBPS)
+            out["pass_roofline"]["counter_source"] = pmc.get("source")
         rf = timed.get("render_fwd", (0, 1))
         rb = timed.get("render_bwd", (0, 1))
         out["render_valu"] = {
@@ -319,19 +354,25 @@ def main():
             "bwd_TFLOPs": 60 * pairs / (rb[0] / rb[1] * 1e-3) / 1e12 if rb[0] else None,
             "peak_TFLOPs": VALU_PEAK_TFLOPS}
         # the render kernels' actual bound: VALU issue.  Wave-level VALU
-        # instructions per launch (rocprofv3 SQ_INSTS_VALU, profiles/) over
-        # the live launch time, against 1 wave-instruction / 4 cycles / SIMD
+        # instructions per step (rocprofv3 SQ_INSTS_VALU of THIS workload,
+        # profiles/pmc_summary.json) over the live per-step stage time,
+        # against 1 wave-instruction / 4 cycles / SIMD.  This is the primary
+        # roofline of the two render kernels; their HBM fraction is not.
         issue = {}
         for st in ("render_fwd", "render_bwd"):
-            rec = load_pmc_stage(st)
+            rec = pst.get(st)
             t = timed.get(st)
-            if rec and rec.get("valu_insts_per_launch") and t and t[0]:
-                rate = rec["valu_insts_per_launch"] / (t[0] / t[1] * 1e-3)
-                issue[st] = {"valu_wave_insts": rec["valu_insts_per_launch"],
+            if rec and rec.get("valu_insts_per_step") and t and t[0]:
+                rate = rec["valu_insts_per_step"] / (t[0] / max(1, args.steps) * 1e-3)
+                issue[st] = {"valu_wave_insts_per_step": rec["valu_insts_per_step"],
                              "achieved_Ginst_s": rate / 1e9, "peak_Ginst_s": VALU_ISSUE_PEAK / 1e9,
                              "frac": rate / VALU_ISSUE_PEAK}
         if issue:
             out["render_valu_issue"] = issue
+            if dom in issue:
+                out["roofline"]["valu_issue_frac"] = issue[dom]["frac"]
+                out["roofline"]["bound_note"] = (f"{dom} is VALU-issue bound: valu_issue_frac is its "
+                                                 "primary roofline, frac its HBM fraction")
 
     if rank == 0 and world == 1 and not args.no_knn:
         # simple_knn.distCUDA2 over the scene's points

@@ -162,19 +162,39 @@ int wgsr_gauss_backward_views(const wgsr_raster_args* params, int lo, int hi, in
  * dL/dopacity, dL/dscales (3), dL/drotations (4). */
 int wgsr_sparse_grad_row_floats(int M);
 
+/* 32-bit mask words per owner segment of S rows: ceil(S / 32). */
+int64_t wgsr_sparse_mask_words(int64_t S);
+
 /* records [P_pad, 12] of one view -> per owner o (segment [o S, (o+1) S)),
  * the rows with a non-zero partial sum compacted to packed + o S * 12, field
  * 10 replaced by the row's index inside the segment (uint32 bits).
- * counts[P_pad / S] (zeroed by the caller) receive the rows per owner.
- * Row order inside a segment is unspecified. */
+ * counts[P_pad / S] (zeroed by the caller) receive the rows per owner; with
+ * nzmask (zeroed, [P_pad / S][wgsr_sparse_mask_words(S)], may be null) bit j
+ * of owner o's words is set for each packed row j.  Row order inside a
+ * segment is unspecified. */
 int wgsr_sparse_pack_records(const float* records, int64_t P_pad, int64_t S, uint32_t* counts,
-                             float* packed, void* stream);
+                             float* packed, uint32_t* nzmask, void* stream);
 
-/* Owner side: received [n_views][S][12] (view v's counts[v] packed rows at
- * v S) scattered into records [n_views][S][12] (zeroed by the caller) and
- * mask[S] (zeroed) set for every received row.  keep_radius: keep the
- * radius field already in `records` (wgsr_sparse_fill_radius), else 1. */
-int wgsr_sparse_unpack_records(const float* received, const uint32_t* counts, int n_views, int64_t S,
+/* uint32 words of one rank's block in the exchange's small all-gather:
+ * WGSR_VIEW_CAMERA_FLOATS (the camera row's float bits) + world (rows sent to
+ * each owner) + world x wgsr_sparse_mask_words(S) (non-zero row masks). */
+int64_t wgsr_sparse_summary_block_words(int world, int64_t S);
+
+/* blocks [world][wgsr_sparse_summary_block_words] (every rank's block,
+ * gathered) -> summary [world * world + world]: count[v][o] (rows view v sends
+ * owner o) then owner o's union row count (rows some view gives gradient);
+ * offsets [world + 1]: exclusive prefix over v of count[v][rank] (where view
+ * v's rows land in this rank's all_to_all output) and the total; cams
+ * [world][WGSR_VIEW_CAMERA_FLOATS]. */
+int wgsr_sparse_exchange_summary(const uint32_t* blocks, int world, int rank, int64_t S, uint32_t* summary,
+                                 uint32_t* offsets, float* cams, void* stream);
+
+/* Owner side: received [offsets[n_views]][12], view v's packed rows at
+ * [offsets[v], offsets[v + 1]), scattered into records [n_views][S][12]
+ * (zeroed by the caller) and mask[S] (zeroed) set for every received row.
+ * keep_radius: keep the radius field already in `records`
+ * (wgsr_sparse_fill_radius), else 1. */
+int wgsr_sparse_unpack_records(const float* received, const uint32_t* offsets, int n_views, int64_t S,
                                int keep_radius, float* records, uint8_t* mask, void* stream);
 
 /* records[j].radius = radii[j] for j < n (rows of WGSR_VIEW_RECORD_FLOATS). */
@@ -186,12 +206,15 @@ int wgsr_sparse_pack_grads(int64_t lo, int64_t hi, int M, const uint8_t* mask, c
                            const float* dL_dsh, const float* dL_dopacity, const float* dL_dscales,
                            const float* dL_drotations, uint32_t* count, float* packed, void* stream);
 
-/* gathered [world][cap][row floats]: owner r's counts[r] rows, indices into
- * shard r (rows r S + index).  Scatters every owner's rows except `rank`'s
- * into the [P, ...] gradient tensors (zeroed by the caller). */
-int wgsr_sparse_unpack_grads(const float* gathered, const uint32_t* counts, int world, int rank, int64_t cap,
-                             int64_t S, int64_t P, int M, float* dL_dmeans3D, float* dL_dsh,
-                             float* dL_dopacity, float* dL_dscales, float* dL_drotations, void* stream);
+/* gathered: owner r's packed rows at gathered + r * block_stride floats,
+ * counts[r] (<= cap) rows, indices into shard r (rows r S + index).  Scatters
+ * every owner's rows except `rank`'s into the [P, ...] gradient tensors
+ * (zeroed by the caller), or with clear != 0 writes zeros at those rows
+ * (undoes an earlier call's scatter, so the tensors need no full re-zeroing). */
+int wgsr_sparse_unpack_grads(const float* gathered, int64_t block_stride, const uint32_t* counts, int world,
+                             int rank, int64_t cap, int64_t S, int64_t P, int M, float* dL_dmeans3D,
+                             float* dL_dsh, float* dL_dopacity, float* dL_dscales, float* dL_drotations,
+                             int clear, void* stream);
 
 /* ---- the mapping iteration around the path ----
  * src/mapper.py:1083-1219 per iteration, as fused launches (csrc/mapping.hip;

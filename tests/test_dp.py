@@ -134,7 +134,7 @@ def test_views_for_rank_round_robin():
 # gathered into place (ragged P: padding rows), and the pose / statistics
 # reductions.  Stand-in: view v's record of Gaussian i is rec(v, i); the
 # owner's "backward" of view v scales it by (camera id + 1).
-VP, VWORLD, VM = 37, 3, 4
+VP, VM = 37, 4
 
 
 def _mock_rec(view, P_pad):
@@ -144,7 +144,9 @@ def _mock_rec(view, P_pad):
     r[:, 10] = ((torch.arange(P_pad) + view) % 3).float()  # radius 0 -> not visible
     # visible but no gradient (every pixel saturated before it): an all-zero
     # record apart from the radius -- the rows the sparse exchange skips
-    quiet = (torch.arange(P_pad) + view) % 4 == 0
+    # (views >= 100 have none: their rows must be cleared again afterwards)
+    i = torch.arange(P_pad)
+    quiet = (((i + view) % 4 == 1) | (i % 4 == 0)) & (view < 100)
     r[quiet, :10] = 0
     r[quiet, 11] = 0
     r[VP:] = 0
@@ -193,7 +195,14 @@ class _MockKernels:
     def grad_row_floats(self, M):
         return 12 + 3 * M
 
-    def sparse_pack_records(self, send, S, counts, packed):
+    def mask_words(self, S):
+        return (S + 31) // 32
+
+    def summary_block_words(self, world, S):
+        return 64 + world + world * self.mask_words(S)
+
+    def sparse_pack_records(self, send, S, counts, packed, nzmask):
+        W32 = self.mask_words(S)
         for o in range(send.size(0) // S):
             seg = send[o * S:(o + 1) * S]
             idx = (seg[:, :10] != 0).any(1).nonzero().flatten()
@@ -201,10 +210,30 @@ class _MockKernels:
             rows[:, 10] = idx.to(torch.int32).view(torch.float32)
             packed[o * S:o * S + idx.numel()] = rows.flip(0)
             counts[o] = idx.numel()
+            words = [0] * W32
+            for j in idx.tolist():
+                words[j // 32] |= 1 << (j % 32)
+            nzmask[o * W32:(o + 1) * W32] = torch.tensor([w - (1 << 32) if w >= 1 << 31 else w for w in words],
+                                                         dtype=torch.int32)
 
-    def sparse_unpack_records(self, recvp, counts, S, keep_radius, recv, mask):
+    def sparse_exchange_summary(self, blocks, world, rank, S, summary, offsets, cams):
+        W32 = self.mask_words(S)
+        b = blocks.long() & 0xFFFFFFFF
+        for o in range(world):
+            acc = [0] * W32
+            for v in range(world):
+                for w in range(W32):
+                    acc[w] |= int(b[v, 64 + world + o * W32 + w])
+            summary[world * world + o] = sum(bin(a).count("1") for a in acc)
+        summary[:world * world] = blocks[:, 64:64 + world].reshape(-1)
+        cams.copy_(blocks[:, :64].contiguous().view(torch.float32))
+        col = blocks[:, 64 + rank].long()
+        offsets[0] = 0
+        offsets[1:] = torch.cumsum(col, 0).to(torch.int32)
+
+    def sparse_unpack_records(self, received, offsets, S, keep_radius, recv, mask):
         for v in range(recv.size(0)):
-            rows = recvp[v, :int(counts[v])]
+            rows = received[int(offsets[v]):int(offsets[v + 1])]
             idx = rows[:, 10].contiguous().view(torch.int32).long()
             rad = recv[v, idx, 10].clone() if keep_radius else torch.ones(idx.numel())
             recv[v, idx] = rows
@@ -216,33 +245,38 @@ class _MockKernels:
 
     def sparse_pack_grads(self, grads, lo, hi, mask, count, packed):
         n = hi - lo
+        F = self.grad_row_floats(grads["shs"].size(1))
         idx = mask[:n].nonzero().flatten()
         rows = torch.cat([grads["means3D"][lo:hi], grads["shs"][lo:hi].reshape(n, -1), grads["opacities"][lo:hi],
                           grads["scales"][lo:hi], grads["rotations"][lo:hi]], 1)[idx].flip(0)
-        packed[:idx.numel(), 0] = idx.flip(0).to(torch.int32).view(torch.float32)
-        packed[:idx.numel(), 1:] = rows
+        out = packed[:idx.numel() * F].view(-1, F)
+        out[:, 0] = idx.flip(0).to(torch.int32).view(torch.float32)
+        out[:, 1:] = rows
         count[0] = idx.numel()
 
-    def sparse_unpack_grads(self, gathered, counts, rank, cap, S, P, grads):
+    def sparse_unpack_grads(self, gathered, block_stride, counts, rank, cap, S, P, grads, clear=False):
         M = grads["shs"].size(1)
+        F = self.grad_row_floats(M)
         for r in range(counts.numel()):
             if r == rank:
                 continue
-            rows = gathered[r, :int(counts[r])]
+            n = min(int(counts[r]), cap)
+            rows = gathered[r * block_stride:r * block_stride + n * F].view(n, F)
             i = r * S + rows[:, 0].contiguous().view(torch.int32).long()
-            grads["means3D"][i] = rows[:, 1:4]
-            grads["shs"][i] = rows[:, 4:4 + 3 * M].reshape(-1, M, 3)
-            grads["opacities"][i] = rows[:, 4 + 3 * M:5 + 3 * M]
-            grads["scales"][i] = rows[:, 5 + 3 * M:8 + 3 * M]
-            grads["rotations"][i] = rows[:, 8 + 3 * M:12 + 3 * M]
+            z = 0.0 if clear else 1.0
+            grads["means3D"][i] = rows[:, 1:4] * z
+            grads["shs"][i] = rows[:, 4:4 + 3 * M].reshape(-1, M, 3) * z
+            grads["opacities"][i] = rows[:, 4 + 3 * M:5 + 3 * M] * z
+            grads["scales"][i] = rows[:, 5 + 3 * M:8 + 3 * M] * z
+            grads["rotations"][i] = rows[:, 8 + 3 * M:12 + 3 * M] * z
 
 
-def _mock_expected():
+def _mock_expected(world):
     P_pad = VP + 5
     out = {"means3D": torch.zeros(VP, 3), "shs": torch.zeros(VP, VM, 3), "opacities": torch.zeros(VP, 1),
            "scales": torch.zeros(VP, 3), "rotations": torch.zeros(VP, 4)}
     taus, st = [], torch.zeros(VP, 3)
-    for v in range(VWORLD):
+    for v in range(world):
         r = _mock_rec(v, P_pad)[:VP]
         vis = r[:, 10] > 0
         w = torch.where(vis, torch.tensor(v + 1.0), torch.zeros(()))[:, None]
@@ -258,24 +292,33 @@ def _mock_expected():
     return out, taus, st
 
 
-def _vsb_worker(rank, port, out_dir, sparse=True):
+def _vsb_worker(rank, world, port, out_dir, sparse=True):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     for p in (os.path.join(root, "wildgs-slam-blackwell_amd", "python"), root):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=VWORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     from wgsr.dp import ViewShardedBackward
     vsb = ViewShardedBackward(VP, VM, "cpu", stats=True, kernels=_MockKernels(), sparse=sparse)
     assert vsb.sparse == sparse
-    assert vsb.P_pad == 39 and vsb.S == 13
+    S = -(-VP // world)
+    assert vsb.S == S and vsb.P_pad == S * world
     e = torch.zeros(3, 4, 5)
     fwd = (torch.zeros(VP, 3), None, None, None, 0, {"id": rank})
-    for _ in range(2):  # repeated steps reuse (and must re-zero) the buffers
+    for step in range(3):  # repeated steps reuse (and must re-zero) the buffers
+        # a different view per step: the rows scattered by the previous step
+        # must be cleared where this step has none
+        fwd = (torch.zeros(VP, 3), None, None, None, 0, {"id": rank if step != 1 else 100 + rank})
         grads, tau, stats = vsb.backward(fwd, e, e[:1])
+        if step == 0:
+            first = {k: v.clone() for k, v in grads.items()}
     if sparse:
         # rows with a non-zero record only: a quarter of the visible rows stay home
-        assert 0 < vsb.last_exchange["record_rows_in"] < (VWORLD - 1) * vsb.S
+        assert 0 < vsb.last_exchange["record_rows_in"] < (world - 1) * vsb.S
+    for k, v in grads.items():  # step 3 = step 1's views again: the same sums
+        assert torch.equal(v, first[k]), k
+    assert (grads["means3D"][torch.arange(VP) % 4 == 0] == 0).all()  # step 2's extra rows cleared
     torch.save({"grads": {k: v.clone() for k, v in grads.items()}, "tau": tau.clone(), "stats": stats.clone()},
                os.path.join(out_dir, f"vsb{rank}.pt"))
     dist.barrier()
@@ -283,10 +326,11 @@ def _vsb_worker(rank, port, out_dir, sparse=True):
 
 
 @pytest.mark.parametrize("sparse", [True, False])
-def test_view_sharded_exchange_routes_records_to_owners(tmp_path, sparse):
-    mp.spawn(_vsb_worker, args=(_free_port(), str(tmp_path), sparse), nprocs=VWORLD, join=True)
-    exp, taus, st = _mock_expected()
-    for r in range(VWORLD):
+@pytest.mark.parametrize("world", [2, 3])
+def test_view_sharded_exchange_routes_records_to_owners(tmp_path, sparse, world):
+    mp.spawn(_vsb_worker, args=(world, _free_port(), str(tmp_path), sparse), nprocs=world, join=True)
+    exp, taus, st = _mock_expected(world)
+    for r in range(world):
         o = torch.load(tmp_path / f"vsb{r}.pt", weights_only=True)
         for k, t in exp.items():
             assert torch.allclose(o["grads"][k], t, rtol=1e-6, atol=1e-6), (r, k)

@@ -195,14 +195,21 @@ def test_two_ranks_gloo_match_sum_of_views(tmp_path, sparse):
 
 @pytest.mark.parametrize("world,S", [(3, 1000), (4, 777), (1, 64)])
 def test_sparse_record_and_gradient_round_trip(world, S):
-    """csrc/dp_sparse.hip: records packed per owner and scattered back equal
-    the dense records of the non-zero rows (radius kept or set to 1), the
-    mask is their union, and packed gradient rows land at their indices."""
+    """csrc/dp_sparse.hip: records packed per owner (+ non-zero row masks),
+    the exchange summary of the gathered small blocks (count matrix, union row
+    counts, receive offsets, camera table), records scattered back from one
+    contiguous all_to_all-shaped buffer equal the dense records of the
+    non-zero rows (radius kept or set to 1), the mask is their union, and
+    packed gradient rows land at their indices -- and a clear pass puts zeros
+    back at exactly those rows."""
     from wgsr.dp import GradBuffer, _HipViewKernels
     dev = torch.device("cuda:0")
     k = _HipViewKernels()
     g = torch.Generator().manual_seed(7)
     P_pad = world * S
+    W32 = k.mask_words(S)
+    BW = k.summary_block_words(world, S)
+    assert W32 == (S + 31) // 32 and BW == 64 + world + world * W32
     views = []
     for v in range(world):
         r = torch.randn(P_pad, 12, generator=g)
@@ -210,25 +217,40 @@ def test_sparse_record_and_gradient_round_trip(world, S):
         r[quiet, :10] = 0
         r[:, 10] = torch.randint(0, 5, (P_pad,), generator=g).float()
         views.append(r.to(dev))
-    for keep_radius in (False, True):
-        for owner in range(world):
-            recvp = torch.zeros(world, S, 12, device=dev)
-            counts = torch.zeros(world, dtype=torch.int32, device=dev)
-            for v, r in enumerate(views):
-                c = torch.zeros(world, dtype=torch.int32, device=dev)
-                packed = torch.full((P_pad, 12), float("nan"), device=dev)
-                k.sparse_pack_records(r, S, c, packed)
-                n = int(c[owner])
-                recvp[v, :n] = packed[owner * S:owner * S + n]
-                counts[v] = n
-                seg = r[owner * S:(owner + 1) * S]
-                assert n == int((seg[:, :10] != 0).any(1).sum())
+    # every view (= rank) packs; the small blocks are "gathered" by stacking
+    blocks = torch.zeros(world, BW, dtype=torch.int32, device=dev)
+    packs = []
+    for v, r in enumerate(views):
+        blocks[v, :64] = (torch.arange(64, device=dev, dtype=torch.float32) + 100 * v).view(torch.int32)
+        packed = torch.full((P_pad, 12), float("nan"), device=dev)
+        k.sparse_pack_records(r, S, blocks[v, 64:64 + world], packed, blocks[v, 64 + world:])
+        packs.append(packed)
+        for o in range(world):
+            seg = r[o * S:(o + 1) * S]
+            assert int(blocks[v, 64 + o]) == int((seg[:, :10] != 0).any(1).sum())
+    for owner in range(world):
+        summary = torch.zeros(world * world + world, dtype=torch.int32, device=dev)
+        offsets = torch.zeros(world + 1, dtype=torch.int32, device=dev)
+        cams = torch.zeros(world, 64, device=dev)
+        k.sparse_exchange_summary(blocks, world, owner, S, summary, offsets, cams)
+        cnt = blocks[:, 64:64 + world].cpu()
+        assert torch.equal(summary[:world * world].cpu().view(world, world), cnt)
+        assert torch.equal(cams.view(torch.int32), blocks[:, :64])
+        assert offsets.tolist() == [0] + torch.cumsum(cnt[:, owner], 0).tolist()
+        for o in range(world):
+            union = torch.zeros(S, dtype=torch.bool, device=dev)
+            for r in views:
+                union |= (r[o * S:(o + 1) * S, :10] != 0).any(1)
+            assert int(summary[world * world + o]) == int(union.sum())
+        # the owner's all_to_all output: view v's rows for this owner, contiguous
+        received = torch.cat([packs[v][owner * S:owner * S + int(cnt[v, owner])] for v in range(world)])
+        for keep_radius in (False, True):
             dense = torch.zeros(world, S, 12, device=dev)
             if keep_radius:
                 k.sparse_fill_radius(torch.stack([r[owner * S:(owner + 1) * S, 10] for r in views]).reshape(-1),
                                      dense.view(-1, 12))
             mask = torch.zeros(S, dtype=torch.uint8, device=dev)
-            k.sparse_unpack_records(recvp, counts, S, keep_radius, dense, mask)
+            k.sparse_unpack_records(received, offsets, S, keep_radius, dense, mask)
             union = torch.zeros(S, dtype=torch.bool, device=dev)
             for v, r in enumerate(views):
                 seg = r[owner * S:(owner + 1) * S]
@@ -238,25 +260,34 @@ def test_sparse_record_and_gradient_round_trip(world, S):
                 exp[:, 10] = seg[:, 10] if keep_radius else nz.float()
                 assert torch.equal(dense[v], exp), (owner, v, keep_radius)
             assert torch.equal(mask.bool(), union)
-    # gradient rows: every owner packs its masked rows, rank 0 unpacks the others
+    # gradient rows: every owner packs its masked rows into its block's row
+    # region (after a `head` of other data), rank 0 unpacks the others
     M = 16
     src = GradBuffer.allocate(P_pad, M, dev)
     src.flat.copy_(torch.randn(src.flat.numel(), generator=g).to(dev))
     F = k.grad_row_floats(M)
     assert F == 12 + 3 * M
+    head, cap = 7, S
+    blk = head + cap * F
     masks = [(torch.rand(S, generator=g) < 0.3).to(torch.uint8).to(dev) for _ in range(world)]
     counts = torch.zeros(world, dtype=torch.int32, device=dev)
-    gathered = torch.full((world, S, F), float("nan"), device=dev)
+    gathered = torch.full((world, blk), float("nan"), device=dev)
     for r in range(world):
         c = torch.zeros(1, dtype=torch.int32, device=dev)
-        k.sparse_pack_grads(src.views, r * S, (r + 1) * S, masks[r], c, gathered[r])
+        k.sparse_pack_grads(src.views, r * S, (r + 1) * S, masks[r], c, gathered[r, head:])
         counts[r] = c[0]
         assert int(c[0]) == int(masks[r].sum())
     dst = GradBuffer.allocate(P_pad, M, dev)
     dst.flat.zero_()
-    k.sparse_unpack_grads(gathered, counts, 0, S, S, P_pad, dst.views)
+    flat = gathered.view(-1)
+    k.sparse_unpack_grads(flat[head:], blk, counts, 0, cap, S, P_pad, dst.views)
     keep = torch.cat([torch.zeros(S, dtype=torch.bool, device=dev)] + [m.bool() for m in masks[1:]])
     for name in src.views:
         exp = src.views[name].clone()
         exp[~keep] = 0
         assert torch.equal(dst.views[name], exp), name
+    dst.flat[:3 * S].fill_(5.0)  # rank 0's own shard rows are never touched by the clear
+    k.sparse_unpack_grads(flat[head:], blk, counts, 0, cap, S, P_pad, dst.views, clear=True)
+    assert torch.equal(dst.views["means3D"][:S], torch.full((S, 3), 5.0, device=dev))
+    for name in src.views:
+        assert not dst.views[name][S:].any(), name

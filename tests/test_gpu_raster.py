@@ -41,8 +41,9 @@ def _c():
     return _C
 
 
-def run_c(inputs, settings, grads, debug=False):
-    """Forward + backward through the exact upstream ``_C`` ABI."""
+def run_c(inputs, settings, grads, debug=False, between=None):
+    """Forward + backward through the exact upstream ``_C`` ABI
+    (``between()`` runs after the forward, before the backward)."""
     C = _c()
     d = lambda x: None if x is None else x.to(DEV)  # noqa: E731
     e = torch.empty(0, device=DEV)
@@ -57,6 +58,8 @@ def run_c(inputs, settings, grads, debug=False):
             d(st["projmatrix"]), d(st["projmatrix_raw"]), st["tanfovx"], st["tanfovy"], st["H"],
             st["W"], shs if shs is not None else e, st["sh_degree"], d(st["campos"]), False, debug)
     (nr, color, radii, geom, binning, img, depth, opac, ntouch) = C.rasterize_gaussians(*args)
+    if between is not None:
+        between()
     bargs = (d(st["bg"]), means, radii, colors if colors is not None else e,
              scales if scales is not None else e, rots if rots is not None else e,
              st["scale_modifier"], cov if cov is not None else e, d(st["viewmatrix"]),
@@ -241,6 +244,19 @@ def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):
                 assert outs[sh][k] == v
             else:
                 np.testing.assert_array_equal(outs[sh][k], v, err_msg=f"shift {sh} {k}")
+
+
+@pytest.mark.parametrize("fwd_shift,bwd_shift", [("2", "0"), ("0", "2")])
+def test_backward_finds_lists_whatever_bin_shift(fwd_shift, bwd_shift, monkeypatch):
+    """The backward locates the forward's tile lists through the image
+    buffer's meta word, not by recomputing the bin shift: a WGSR_BIN_SHIFT
+    change between the two calls does not change any result."""
+    inputs, settings, grads = _synthetic(20_000, 640, 480, 3, 1)
+    monkeypatch.setenv("WGSR_BIN_SHIFT", fwd_shift)
+    ref = run_c(inputs, settings, grads)
+    out = run_c(inputs, settings, grads, between=lambda: monkeypatch.setenv("WGSR_BIN_SHIFT", bwd_shift))
+    for k, v in ref.items():
+        np.testing.assert_array_equal(np.asarray(out[k]), np.asarray(v), err_msg=k)
 
 
 def test_wide_radix_pass_matches_8bit_passes(monkeypatch):

@@ -70,6 +70,12 @@ for s in $STEPS; do
     pmc_custom)
       # PMC_COUNTERS="A B C" PMC_NAME=name: one extra counter pass (SQ block: at most 8 counters)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom}.err); rc=$? ;;
+    dp2)
+      # N = 2 rehearsal of the multi-GPU bench path on the box's one GPU: two
+      # ranks share cuda:0 over gloo (device tensors staged through host memory)
+      WGSR_BENCH_BACKEND=gloo WGSR_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 \
+        --no-profile ${BENCH_ARGS:-} > $OUT/bench_dp2.json 2> $OUT/bench_dp2.err; rc=$? ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   echo "$s rc=$rc" | tee -a $OUT/steps.log

@@ -7,7 +7,13 @@ coalesced reads, so the corrected read bytes are 2 x FETCH_SIZE (reported
 next to the raw value; other access widths are uncalibrated).  Counters come
 from separate passes (FETCH_SIZE and WRITE_SIZE do not fit one pass).
 
-usage: python tools/pmc_summary.py gpurun_out [out.json [source-label]]
+Per-step figures: each kernel's per-dispatch average times its dispatches per
+step (dispatch count over the run / --steps-run, the warmup + timed steps of
+the profiled bench.py command); a stage's bytes and VALU instructions are
+summed over its kernels.  The config the counters were taken on is recorded
+(--config P,W,H,SH) so that bench.py only quotes them for the same workload.
+
+usage: python tools/pmc_summary.py gpurun_out out.json --config 1000000,1920,1080,3 --steps-run 7 [--source label]
 """
 import csv
 import json
@@ -54,9 +60,16 @@ def stage_for(kernel, grid, P_grid):
 
 
 def main():
-    root = sys.argv[1]
-    out_path = sys.argv[2] if len(sys.argv) > 2 else None
-    source = sys.argv[3] if len(sys.argv) > 3 else "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes of bench.py"
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("out", nargs="?")
+    ap.add_argument("--config", required=True, help="P,W,H,SH of the profiled bench.py run")
+    ap.add_argument("--steps-run", type=int, required=True, help="warmup + timed steps of the profiled run")
+    ap.add_argument("--source", default="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ passes of bench.py")
+    args = ap.parse_args()
+    root, out_path, source = args.root, args.out, args.source
+    cP, cW, cH, cS = (int(x) for x in args.config.split(","))
     fetch = load(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"))
     write = load(os.path.join(root, "pmc_write", "run_counter_collection.csv"))
     sq = load(os.path.join(root, "pmc_sq", "run_counter_collection.csv"))
@@ -64,8 +77,8 @@ def main():
     # grid size of the depth-sort radix kernels: the smallest radix scatter grid
     rg = [g for (k, g) in keys if k == "k_radix_scatter"]
     P_grid = min(rg) if rg else 0
-    rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_launch": 0.0, "valu_insts_per_launch": 0.0,
-                                            "launch_kinds": []})
+    rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_step": 0.0, "valu_insts_per_step": 0.0,
+                                            "launches_per_step": 0.0, "launch_kinds": []})
     hdr = (f"{'kernel':18s} {'grid':>9s} {'FETCH_KB':>10s} {'WRITE_KB':>10s} {'HBM_MB*':>9s} "
            f"{'VALU/wave':>9s} {'VMEM/wave':>9s} {'LDS/wave':>8s} {'wait%':>6s}")
     print(hdr)
@@ -80,6 +93,9 @@ def main():
         lds = avg(sq, "SQ_INSTS_LDS")
         cyc, wait = avg(sq, "SQ_WAVE_CYCLES"), avg(sq, "SQ_WAIT_ANY")
         hbm = ((2 * f if f is not None else 0) + (w or 0)) * 1024
+        nd = max(len(d[key].get(c, [])) for d, c in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE"),
+                                                     (sq, "SQ_WAVES")))
+        per_step = nd / args.steps_run
         per = lambda x: (x / waves) if (x is not None and waves) else float("nan")  # noqa: E731
         print(f"{k:18s} {g:9d} {f if f is not None else float('nan'):10.0f} "
               f"{w if w is not None else float('nan'):10.0f} {hbm / 1e6:9.1f} {per(valu):9.0f} "
@@ -87,17 +103,22 @@ def main():
               f"{100 * wait / cyc if (wait and cyc) else float('nan'):6.1f}")
         rows.append(dict(kernel=k, grid=g, fetch_kib=f, write_kib=w, hbm_bytes=hbm, waves=waves,
                          valu_per_wave=per(valu), vmem_per_wave=per((vrd or 0) + (vwr or 0)),
-                         lds_per_wave=per(lds), wait_frac=(wait / cyc) if (wait and cyc) else None))
+                         lds_per_wave=per(lds), wait_frac=(wait / cyc) if (wait and cyc) else None,
+                         dispatches_per_step=per_step))
         st = stage_for(k, g, P_grid)
         if st:
-            stages[st]["hbm_bytes_per_launch"] += hbm
+            stages[st]["hbm_bytes_per_step"] += hbm * per_step
+            stages[st]["launches_per_step"] += per_step
             if valu is not None and waves:
-                stages[st]["valu_insts_per_launch"] += valu  # wave-level VALU instructions
-            stages[st]["launch_kinds"].append(k)
+                stages[st]["valu_insts_per_step"] += valu * per_step  # wave-level VALU instructions
+            if k not in stages[st]["launch_kinds"]:
+                stages[st]["launch_kinds"].append(k)
     print("* HBM_MB = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch (gfx950 FETCH correction)")
     if out_path:
-        json.dump({"source": source, "note": "per-dispatch averages; radix stage bytes summed over "
-                   "one pass's kernels (multiply by passes for the stage)",
+        json.dump({"source": source, "config": {"P": cP, "W": cW, "H": cH, "sh": cS},
+                   "steps_run": args.steps_run,
+                   "note": "kernels: per-dispatch averages; stages: per bench step (every dispatch of the "
+                           "stage's kernels in one step)",
                    "kernels": rows, "stages": stages}, open(out_path, "w"), indent=1)
 
 

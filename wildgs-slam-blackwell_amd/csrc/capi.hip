@@ -161,8 +161,8 @@ int tile_sort_bits(const Grid& g) { return num_bits((uint32_t)g.nt) > 0 ? num_bi
 // bin lists into the exact per-tile lists (the pair key carries the
 // Gaussian's exact tile mask inside the bin).  Default 4 x 4 tiles: at 1080p
 // 510 bins, ~1.3 sorted pairs per visible Gaussian instead of ~9.
-// WGSR_BIN_SHIFT overrides; the forward and its backward must see the same
-// value (the backward recomputes it to find the lists).
+// WGSR_BIN_SHIFT overrides (the backward finds the lists through the image
+// buffer's meta word, so it never depends on the setting).
 // Small frames (<= kSmallFrameTiles tiles) default to 2 x 2-tile bins: their
 // expand step is launch-latency bound and finer bins shorten it (A/B, 100k
 // Gaussians: 512x384 0.328 -> 0.324 ms, 640x480 0.342 -> 0.335 ms).
@@ -307,10 +307,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     zj.p[zj.count] = at<float>(geom, GL.bsup);
     zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
   }
+  // Once k_preprocess is queued it zeroes the thread's other counter block;
+  // the next forward may only reuse that block after this call's host wait.
+  // Any error return before that wait synchronises the stream instead.
+  struct SyncOnError {
+    hipStream_t s;
+    bool armed = false;
+    ~SyncOnError() { if (armed) (void)hipStreamSynchronize(s); }
+  } sync_on_error{s};
   { StageTimer T(0, s);
   const hipError_t pe = launch_preprocess(a, geom, radii, n_touched, counter + 1,
                                           reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s);
   if (pe == hipSuccess && dc) dc->parity ^= 1;  // k_preprocess, which zeroes the other block, is queued
+  sync_on_error.armed = true;
   STAGE(a, s, pe); }
 
   // The pair counts are known once k_preprocess is done: copy them to pinned
@@ -344,6 +353,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   }
   delete scan_timer;
   HIPCHK(hipEventSynchronize(hc.ev));
+  sync_on_error.armed = false;
   const uint32_t* host_counter = hc.buf;
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
@@ -402,19 +412,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bshift) {
       STAGE(a, s, launch_expand_bins(a, sorted_keys, at<uint32_t>(binning, BL.point_g), (uint32_t)NL, bshift,
                                      at<uint2>(image, IL.tile_m), bounds_done, lists, ranges,
-                                     at<uint32_t>(image, IL.tile_len), s));
+                                     at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta), s));
     } else {
       STAGE(a, s, launch_ranges(sorted_keys, (uint32_t)NL, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
-                                at<uint32_t>(image, IL.order_fwd), s));
+                                at<uint32_t>(image, IL.meta), s));
     }
   } else {
     StageTimer T(5, s);  // every list is empty
     STAGE(a, s, launch_ranges(nullptr, 0u, grid.nt, ranges, at<uint32_t>(image, IL.tile_len),
-                              at<uint32_t>(image, IL.order_fwd), s));
+                              at<uint32_t>(image, IL.meta), s));
   }
   const uint32_t* sorted_g = lists;
   { StageTimer T(6, s);
-  STAGE(a, s, launch_render_fwd(a, ranges, at<uint32_t>(image, IL.order_fwd), sorted_g, geom,
+  STAGE(a, s, launch_render_fwd(a, ranges, sorted_g, geom,
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, at<uint32_t>(image, IL.tile_m), s)); }
   *num_rendered = (int64_t)N_rect;
@@ -452,10 +462,11 @@ int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* bin
     StageTimer T(7, s);
     uint32_t* order = at<uint32_t>(image, IL.order_bwd);
     STAGE(a, s, launch_tile_order(at<uint32_t>(image, IL.tile_m), grid.nt, order, s));
-    // the tile lists: after the sized layout with sort bins (same shift as
-    // the forward: bin_shift is a function of the arguments and WGSR_BIN_SHIFT)
-    const uint32_t* lists = bin_shift(a) ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
-    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order, lists, geom, at<float>(image, IL.final_T),
+    // the tile lists: point_g, or with sort bins the region after the sized
+    // layout -- the forward records which in the image buffer's meta word
+    STAGE(a, s, launch_render_bwd(a, at<uint2>(image, IL.ranges), order, at<uint32_t>(image, IL.meta),
+                                  at<uint32_t>(binning, BL.point_g), at<uint32_t>(binning, BL.total), geom,
+                                  at<float>(image, IL.final_T),
                                   at<uint32_t>(image, IL.n_contrib), dL_dcolor, dL_ddepth, partial, pflag, zero,
                                   s));
   } else {

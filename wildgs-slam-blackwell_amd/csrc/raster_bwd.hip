@@ -297,7 +297,8 @@ __device__ __forceinline__ void render_bwd_quad_tile(
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
-    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ lists_exact,
+    const uint32_t* __restrict__ lists_bins, const float4* __restrict__ splat,
     const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W, int H, int gx, int ntiles,
     const float* __restrict__ bg, const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib,
     const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep, float4* __restrict__ partial,
@@ -306,6 +307,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __shared__ uint32_t sG[kBatch];
   __shared__ float sP[kBatch][11];
   __shared__ uint32_t sHit[kBatch];
+  // where the forward left the tile lists (ImageLayout::meta)
+  const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
   if (bg0 == 0.f && bg1 == 0.f && bg2 == 0.f)  // (uniform)
@@ -329,7 +332,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // pixel; only the order of the final cross-quadrant sum differs.
 __global__ __launch_bounds__(256) void k_render_bwd_split(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
-    const uint32_t* __restrict__ point_g, const float4* __restrict__ splat,
+    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ lists_exact,
+    const uint32_t* __restrict__ lists_bins, const float4* __restrict__ splat,
     const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
     int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
@@ -339,6 +343,8 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
   __shared__ float sP[4][kBatch][11];
   __shared__ uint64_t sHitW[4];
   __shared__ uint32_t sEnd[4];
+  // where the forward left the tile lists (ImageLayout::meta)
+  const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tx = (int)(tile % gx), ty = (int)(tile / gx);
@@ -1413,7 +1419,8 @@ __global__ __launch_bounds__(kGbWave) void k_gauss_bwd_views(
 }  // namespace
 
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
-                             const uint32_t* point_g, const void* geom, const float* final_T,
+                             const uint32_t* meta, const uint32_t* lists_exact, const uint32_t* lists_bins,
+                             const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, const ZeroJob& zero, hipStream_t s) {
   const GeomLayout L(a.P);
@@ -1423,13 +1430,15 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const char* env = getenv("WGSR_BWD_SPLIT_BELOW");  // read per launch: tests switch kernels
   const int split_below = env ? atoi(env) : kBwdSplitBelowTiles;
   if (nt < split_below) {
-    hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), point_g,
+    hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), meta,
+                       lists_exact, lists_bins,
                        at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
                        dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), point_g,
+  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), meta,
+                     lists_exact, lists_bins,
                      at<float4>(geom, L.splat),
                      at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.slot_start), a.W,
                      a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor, dL_ddepth, partial, pflag,

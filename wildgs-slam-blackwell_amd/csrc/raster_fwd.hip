@@ -528,10 +528,12 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
                                                              const uint2* __restrict__ bounds, int gx, int gy,
                                                              int bshift, int gbx, uint32_t* __restrict__ lists,
                                                              uint2* __restrict__ ranges,
-                                                             uint32_t* __restrict__ tile_len) {
+                                                             uint32_t* __restrict__ tile_len,
+                                                             uint32_t* __restrict__ meta) {
   constexpr int NW = kExpThreads / 64;
   __shared__ uint32_t s_wc[NW][4];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (blockIdx.x == 0 && t == 0) meta[0] = 1u;  // the lists are the sort-bin region
   const int B = 1 << bshift;
   const uint32_t bin = blockIdx.x >> bshift;
   const int r = (int)(blockIdx.x & (uint32_t)(B - 1));
@@ -649,8 +651,10 @@ __device__ __forceinline__ void order_chunk(uint32_t c0, uint32_t c1, const uint
 // ranges[tile] = [first, end) of the tile's run in the sorted pair keys
 // (binary search); len[tile] = its list length.
 __global__ __launch_bounds__(256) void k_ranges(const uint32_t* __restrict__ keys, uint32_t N, int ntiles,
-                                                uint2* __restrict__ ranges, uint32_t* __restrict__ len) {
+                                                uint2* __restrict__ ranges, uint32_t* __restrict__ len,
+                                                uint32_t* __restrict__ meta) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) meta[0] = 0u;  // the lists are point_g
   if (t >= ntiles) return;
   auto lower = [&](uint32_t v) {
     uint32_t lo = 0, hi = N;
@@ -879,7 +883,7 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
 
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
                               uint32_t NB, int bshift, uint2* bounds, bool bounds_done, uint32_t* lists, uint2* ranges,
-                              uint32_t* tile_len, hipStream_t s) {
+                              uint32_t* tile_len, uint32_t* meta, hipStream_t s) {
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const Bins B(gx, gy, bshift);
   if (!bounds_done) {  // (a one-pass sort already wrote them)
@@ -888,7 +892,7 @@ hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_
     hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
   }
   hipLaunchKernelGGL(k_expand_bins, dim3((uint32_t)B.n << bshift), dim3(kExpThreads), 0, s, sorted_keys, sorted_g, bounds, gx,
-                     gy, bshift, B.bx, lists, ranges, tile_len);
+                     gy, bshift, B.bx, lists, ranges, tile_len, meta);
   return hipGetLastError();
 }
 
@@ -903,20 +907,9 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
   return hipGetLastError();
 }
 
-// WGSR_FWD_LPT=1: order the forward's tiles by list length too (measured no
-// gain on the bench scene: its per-tile forward work is nearly uniform)
-static bool fwd_lpt() {
-  static const bool v = [] {
-    const char* e = getenv("WGSR_FWD_LPT");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
-
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
-                         uint32_t* order, hipStream_t s) {
-  hipLaunchKernelGGL(k_ranges, dim3((ntiles + 255) / 256), dim3(256), 0, s, sorted_keys, N, ntiles, ranges, len);
-  if (fwd_lpt()) hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, len, false, false, (uint32_t)ntiles, order);
+                         uint32_t* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_ranges, dim3((ntiles + 255) / 256), dim3(256), 0, s, sorted_keys, N, ntiles, ranges, len, meta);
   return hipGetLastError();
 }
 
@@ -936,14 +929,13 @@ hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* o
   return hipGetLastError();
 }
 
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
-                             const uint32_t* point_g, const void* geom, float* out_color, float* out_depth,
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g, const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
                              uint32_t* tile_m, hipStream_t s) {
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, fwd_lpt() ? order : nullptr, point_g,
+  hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, nullptr, point_g,
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T,
                      n_contrib, n_touched, tile_m);
   return hipGetLastError();

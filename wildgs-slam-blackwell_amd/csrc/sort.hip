@@ -92,7 +92,7 @@ __device__ __forceinline__ void add_runs(uint32_t* h, const uint32_t (&k)[I], in
 // With `sup` (superblock mode), each block also adds its counts into its
 // superblock's (kSupBlocks consecutive blocks) per-digit sums, so the scatter
 // can find its offsets without a row-scan kernel in between.
-constexpr uint32_t kSupBlocks = 16;
+constexpr uint32_t kSupBlocks = kSortSupBlocks;
 template <int I>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     int bits, uint32_t nb, uint32_t* __restrict__ hist,
@@ -713,7 +713,7 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
   const uint32_t nsup = (nb + kSupBlocks - 1) / kSupBlocks;
   uint32_t* sup = nullptr;
   if (!onesweep && sup_mode()) {
-    sup = status + 256 * (size_t)nb;  // (status holds kMaxSortPasses x 256 x nb words; passes x 256 x nsup fit after one)
+    sup = status + 256 * (size_t)nb;  // (sort_status_bytes reserves 256 nb + kMaxSortPasses x 256 nsup words)
     if (!sup_zeroed) {
       hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
       if (e != hipSuccess) return e;

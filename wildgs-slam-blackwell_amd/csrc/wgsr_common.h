@@ -645,11 +645,17 @@ struct Bins {
 constexpr int kMaxSortPasses = 4;
 // Sized so that any sort of n' <= n keys fits (buffers sized for an upper
 // bound, e.g. upstream's rectangle pair count, sort the exact count).
+// Superblock mode keeps the per-block histogram [256][nb] followed by every
+// pass's [256][nsup] superblock sums (nsup = ceil(nb / kSortSupBlocks)).
+constexpr uint32_t kSortSupBlocks = 16;
 __host__ __device__ inline size_t sort_status_bytes(size_t n) {
   const size_t small = n < kSmallSortN ? n : kSmallSortN;
   const size_t b_small = (small + 256 * kSmallSortItems - 1) / (256 * kSmallSortItems);
   const size_t b_large = (n + 256 * kSortItems - 1) / (256 * kSortItems);
-  return 4ull * 256 * (b_small > b_large ? b_small : b_large) * kMaxSortPasses;
+  const size_t nb = b_small > b_large ? b_small : b_large;
+  const size_t nsup = (nb + kSortSupBlocks - 1) / kSortSupBlocks;
+  const size_t onesweep = 256 * nb * kMaxSortPasses, sup = 256 * nb + 256 * nsup * kMaxSortPasses;
+  return 4ull * (onesweep > sup ? onesweep : sup);
 }
 constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
 
@@ -710,7 +716,7 @@ struct BinLayout {
 
 // Per-pixel state (image buffer).
 struct ImageLayout {
-  size_t ranges, tile_len, tile_m, order_fwd, order_bwd, final_T, n_contrib, total;
+  size_t ranges, tile_len, tile_m, order_bwd, meta, final_T, n_contrib, total;
   __host__ __device__ ImageLayout(int W, int H) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o = align256(o + bytes); return r; };
@@ -718,8 +724,9 @@ struct ImageLayout {
     ranges = take(8 * nt);     // list [start, end) per tile
     tile_len = take(4 * nt);   // list length per tile (forward work)
     tile_m = take(16 * nt);    // deepest contributor per tile quadrant (backward work)
-    order_fwd = take(4 * nt);  // launch orders (heaviest first per XCD chunk)
-    order_bwd = take(4 * nt);
+    order_bwd = take(4 * nt);  // the backward's launch order (heaviest first per XCD chunk)
+    meta = take(16);           // [0]: where the forward left the tile lists (1: sort-bin region
+                               // after the binning layout, 0: point_g) -- read by the backward
     final_T = take(4 * (size_t)W * H);
     n_contrib = take(4 * (size_t)W * H);
     total = o;

@@ -69,23 +69,25 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
 // tile, the lists in bin-sized regions of `lists` (2^2s x NB entries)
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
                               uint32_t NB, int bshift, uint2* bounds, bool bounds_done, uint32_t* lists, uint2* ranges,
-                              uint32_t* tile_len, hipStream_t s);
-// tile ranges + the forward's launch order (tiles by list length, per XCD chunk)
+                              uint32_t* tile_len, uint32_t* meta, hipStream_t s);
+// tile ranges of the exact (Gaussian, tile) pair sort
 hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, uint2* ranges, uint32_t* len,
-                         uint32_t* order, hipStream_t s);
+                         uint32_t* meta, hipStream_t s);
 // the backward's launch order (tiles by deepest contributor, per XCD chunk)
 hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* order, hipStream_t s);
 bool bwd_order_global();
-hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
-                             const uint32_t* point_g, const void* geom, float* out_color, float* out_depth,
+hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
+                             const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
                              uint32_t* tile_m4, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                                hipStream_t s);
 
 // backward stages (raster_bwd.hip)
+// the tile lists: lists_bins when the forward's ImageLayout::meta word says so, else lists_exact
 hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* order,
-                             const uint32_t* point_g, const void* geom, const float* final_T,
+                             const uint32_t* meta, const uint32_t* lists_exact, const uint32_t* lists_bins,
+                             const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, const ZeroJob& zero, hipStream_t s);
 // Per-Gaussian backward.  GbMode:

@@ -148,8 +148,14 @@ def load():
                                                                                           c_int, _fp])
         L.wgsr_sparse_grad_row_floats.restype = c_int
         L.wgsr_sparse_grad_row_floats.argtypes = [c_int]
+        L.wgsr_sparse_mask_words.restype = c_i64
+        L.wgsr_sparse_mask_words.argtypes = [c_i64]
         L.wgsr_sparse_pack_records.restype = c_int
-        L.wgsr_sparse_pack_records.argtypes = [_fp, c_i64, c_i64, _fp, _fp, _fp]
+        L.wgsr_sparse_pack_records.argtypes = [_fp, c_i64, c_i64, _fp, _fp, _fp, _fp]
+        L.wgsr_sparse_summary_block_words.restype = c_i64
+        L.wgsr_sparse_summary_block_words.argtypes = [c_int, c_i64]
+        L.wgsr_sparse_exchange_summary.restype = c_int
+        L.wgsr_sparse_exchange_summary.argtypes = [_fp, c_int, c_int, c_i64, _fp, _fp, _fp, _fp]
         L.wgsr_sparse_unpack_records.restype = c_int
         L.wgsr_sparse_unpack_records.argtypes = [_fp, _fp, c_int, c_i64, c_int, _fp, _fp, _fp]
         L.wgsr_sparse_fill_radius.restype = c_int
@@ -157,7 +163,8 @@ def load():
         L.wgsr_sparse_pack_grads.restype = c_int
         L.wgsr_sparse_pack_grads.argtypes = [c_i64, c_i64, c_int] + [_fp] * 8 + [_fp]
         L.wgsr_sparse_unpack_grads.restype = c_int
-        L.wgsr_sparse_unpack_grads.argtypes = [_fp, _fp, c_int, c_int, c_i64, c_i64, c_i64, c_int] + [_fp] * 5 + [_fp]
+        L.wgsr_sparse_unpack_grads.argtypes = ([_fp, c_i64, _fp, c_int, c_int, c_i64, c_i64, c_i64, c_int] + [_fp] * 5
+                                               + [c_int, _fp])
         L.wgsr_grad_mask.restype = c_int
         L.wgsr_grad_mask.argtypes = [c_int, c_int, _fp, ctypes.c_float, _fp, _fp]
         L.wgsr_mlp_scratch_bytes.restype = c_sz
@@ -229,7 +236,8 @@ EXPORTED_SYMBOLS = (
     "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
     "wgsr_pose_state_floats", "wgsr_pose_step",
     "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
-    "wgsr_sparse_grad_row_floats", "wgsr_sparse_pack_records", "wgsr_sparse_unpack_records",
+    "wgsr_sparse_grad_row_floats", "wgsr_sparse_mask_words", "wgsr_sparse_pack_records",
+    "wgsr_sparse_summary_block_words", "wgsr_sparse_exchange_summary", "wgsr_sparse_unpack_records",
     "wgsr_sparse_fill_radius", "wgsr_sparse_pack_grads", "wgsr_sparse_unpack_grads",
 )
 

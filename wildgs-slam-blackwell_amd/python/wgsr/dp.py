@@ -213,15 +213,30 @@ class _HipViewKernels:
         from wgsr import _lib
         return int(_lib.load().wgsr_sparse_grad_row_floats(int(M)))
 
-    def sparse_pack_records(self, send, S, counts, packed):
+    def mask_words(self, S):
+        from wgsr import _lib
+        return int(_lib.load().wgsr_sparse_mask_words(int(S)))
+
+    def summary_block_words(self, world, S):
+        from wgsr import _lib
+        return int(_lib.load().wgsr_sparse_summary_block_words(int(world), int(S)))
+
+    def sparse_pack_records(self, send, S, counts, packed, nzmask):
         from wgsr import _lib
         _lib.check(_lib.load().wgsr_sparse_pack_records(send.data_ptr(), send.size(0), int(S), counts.data_ptr(),
-                                                        packed.data_ptr(), _lib.stream_handle(send.device)))
+                                                        packed.data_ptr(), _lib.ptr(nzmask),
+                                                        _lib.stream_handle(send.device)))
 
-    def sparse_unpack_records(self, recvp, counts, S, keep_radius, recv, mask):
+    def sparse_exchange_summary(self, blocks, world, rank, S, summary, offsets, cams):
         from wgsr import _lib
-        _lib.check(_lib.load().wgsr_sparse_unpack_records(recvp.data_ptr(), counts.data_ptr(), recv.size(0), int(S),
-                                                          int(keep_radius), recv.data_ptr(), mask.data_ptr(),
+        _lib.check(_lib.load().wgsr_sparse_exchange_summary(blocks.data_ptr(), int(world), int(rank), int(S),
+                                                            summary.data_ptr(), offsets.data_ptr(), cams.data_ptr(),
+                                                            _lib.stream_handle(blocks.device)))
+
+    def sparse_unpack_records(self, received, offsets, S, keep_radius, recv, mask):
+        from wgsr import _lib
+        _lib.check(_lib.load().wgsr_sparse_unpack_records(received.data_ptr(), offsets.data_ptr(), recv.size(0),
+                                                          int(S), int(keep_radius), recv.data_ptr(), mask.data_ptr(),
                                                           _lib.stream_handle(recv.device)))
 
     def sparse_fill_radius(self, radii, recv):
@@ -237,109 +252,57 @@ class _HipViewKernels:
             grads["opacities"].data_ptr(), grads["scales"].data_ptr(), grads["rotations"].data_ptr(),
             count.data_ptr(), packed.data_ptr(), _lib.stream_handle(packed.device)))
 
-    def sparse_unpack_grads(self, gathered, counts, rank, cap, S, P, grads):
+    def sparse_unpack_grads(self, gathered, block_stride, counts, rank, cap, S, P, grads, clear=False):
+        """gathered: flat tensor whose element 0 is owner 0's first packed row;
+        owner r's rows start block_stride floats later per owner."""
         from wgsr import _lib
         M = grads["shs"].size(1)
         _lib.check(_lib.load().wgsr_sparse_unpack_grads(
-            gathered.data_ptr(), counts.data_ptr(), counts.numel(), int(rank), int(cap), int(S), int(P), int(M),
-            grads["means3D"].data_ptr(), grads["shs"].data_ptr(), grads["opacities"].data_ptr(),
-            grads["scales"].data_ptr(), grads["rotations"].data_ptr(), _lib.stream_handle(gathered.device)))
+            gathered.data_ptr(), int(block_stride), counts.data_ptr(), counts.numel(), int(rank), int(cap), int(S),
+            int(P), int(M), grads["means3D"].data_ptr(), grads["shs"].data_ptr(), grads["opacities"].data_ptr(),
+            grads["scales"].data_ptr(), grads["rotations"].data_ptr(), int(bool(clear)),
+            _lib.stream_handle(gathered.device)))
 
 
-def _gloo_cuda(group):
-    """gloo has no device collectives for every op: stage device tensors
-    through host memory (test rigs only -- RCCL is the product backend)."""
-    return dist.get_backend(group) == "gloo"
+# ---- collectives ------------------------------------------------------------
+# Exactly two collective shapes carry the exchange on every backend: equal-block
+# all_gather_into_tensor and all_to_all_single (equal, or with split sizes in
+# rows).  gloo has no device collectives, so on gloo device tensors are staged
+# through host memory with the SAME call (test rigs only: RCCL is the product
+# backend); the CPU and one-GPU tests therefore run the call shapes the RCCL
+# branch runs.
+
+def _staged(group, *ts):
+    return dist.get_backend(group) == "gloo" and any(t.is_cuda for t in ts)
 
 
-def _all_to_all_equal(out, inp, group):
-    if _gloo_cuda(group) and inp.is_cuda:
-        o = torch.empty_like(out, device="cpu")
-        dist.all_to_all_single(o, inp.cpu(), group=group)
-        out.copy_(o)
-        return None
-    return dist.all_to_all_single(out, inp, group=group, async_op=True)
-
-
-def _all_gather_into(out_flat, inp, group):
-    if _gloo_cuda(group) and inp.is_cuda:
+def _all_gather_into(out_flat, inp, group, async_op=True):
+    """all_gather_into_tensor(out_flat, inp): equal blocks, rank order."""
+    if _staged(group, out_flat, inp):
         h = torch.empty(out_flat.shape, dtype=out_flat.dtype)
         dist.all_gather_into_tensor(h, inp.cpu(), group=group)
         out_flat.copy_(h)
         return None
-    return dist.all_gather_into_tensor(out_flat, inp, group=group, async_op=True)
+    return dist.all_gather_into_tensor(out_flat, inp, group=group, async_op=async_op)
 
 
-def _all_gather_inplace(full, rank, group):
-    """full [world * S, ...]: rank's block holds its shard; gather the rest."""
-    world = dist.get_world_size(group)
-    S = full.size(0) // world
-    if _gloo_cuda(group) and full.is_cuda:
-        h = full.cpu()
-        dist.all_gather_into_tensor(h.view(-1), h[rank * S:(rank + 1) * S].reshape(-1).clone(), group=group)
-        full.copy_(h)
+def _all_to_all(out, inp, group, out_splits=None, in_splits=None, async_op=True):
+    """all_to_all_single(out, inp[, output_split_sizes, input_split_sizes])
+    (split sizes along dim 0; None = equal blocks)."""
+    if _staged(group, out, inp):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        out.copy_(o)
         return None
-    return dist.all_gather_into_tensor(full.view(-1), full[rank * S:(rank + 1) * S].view(-1), group=group,
-                                       async_op=True)
+    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group,
+                                  async_op=async_op)
 
 
-def _all_to_all_var(outs, ins, group):
-    """outs[v] <- rank v's ins[me]: uneven row blocks, one collective."""
-    if dist.get_backend(group) == "gloo":  # test rigs: one alltoallv through host memory
-        flat = [t.reshape(t.size(0), -1) for t in ins]
-        inp = torch.cat(flat).cpu()
-        out = torch.empty((sum(o.size(0) for o in outs),) + tuple(inp.shape[1:]), dtype=inp.dtype)
-        dist.all_to_all_single(out, inp, output_split_sizes=[o.size(0) for o in outs],
-                               input_split_sizes=[t.size(0) for t in ins], group=group)
-        off = 0
-        for o in outs:
-            n = o.size(0)
-            o.copy_(out[off:off + n].view_as(o))
-            off += n
-        return None
-    return dist.all_to_all(outs, ins, group=group, async_op=True)
-
-
-def _all_gather_many(pairs, group):
-    """all_gather_into_tensor of several (out_flat, in_flat) pairs as ONE
-    coalesced RCCL group (a single grouped launch, one collective latency)."""
-    if any(_gloo_cuda(group) and i.is_cuda for _, i in pairs):
-        for o, i in pairs:
-            _all_gather_into(o, i, group)
-        return None
-    try:
-        with dist._coalescing_manager(group, async_ops=True) as cm:
-            for o, i in pairs:
-                dist.all_gather_into_tensor(o, i, group=group)
-        return cm
-    except (RuntimeError, AttributeError, NotImplementedError):
-        # a backend / torch build without the coalesced fast path: every rank
-        # takes this branch alike (same code, same backend), so the collectives
-        # still pair up -- one gather per buffer
-        return _WaitAll([_all_gather_into(o, i, group) for o, i in pairs])
-
-
-def _all_gather_inplace_many(fulls, rank, group):
-    """In-place all-gathers of several [world * S, ...] buffers (each rank's
-    block holds its shard) as ONE coalesced collective: RCCL runs the group
-    as a single launch, so the small buffers ride along with the SH block
-    instead of paying a collective's latency each."""
-    world = dist.get_world_size(group)
-    pairs = []
-    for f in fulls:
-        S = f.size(0) // world
-        pairs.append((f.view(-1), f[rank * S:(rank + 1) * S].view(-1)))
-    return _all_gather_many(pairs, group)
-
-
-class _WaitAll:
-    def __init__(self, works):
-        self.works = works
-
-    def wait(self):
-        for w in self.works:
-            if w is not None:
-                w.wait()
+def _wait(*works):
+    for w in works:
+        if w is not None:
+            w.wait()
 
 
 class ViewShardedBackward:
@@ -387,14 +350,28 @@ class ViewShardedBackward:
         self.last_exchange = None
         if self.sparse:
             i32 = dict(dtype=torch.int32, device=dev)
+            world, S = self.world, self.S
             self.F = self.k.grad_row_floats(M)
+            self.BW = self.k.summary_block_words(world, S)
+            # this rank's small block: [camera row | rows sent per owner | non-zero row masks]
+            self.small = torch.zeros(self.BW, **i32)
+            self.small_all = torch.zeros(world, self.BW, **i32)
             self.packed = torch.empty(self.P_pad, 12, **f32)
             self.recvp = torch.empty(self.P_pad, 12, **f32)
-            self.mask = torch.zeros(self.S, dtype=torch.uint8, device=dev)
-            self.cbuf = torch.zeros(2, self.world, **i32)  # [rows sent to each owner, rows got from each view]
+            self.mask = torch.zeros(S, dtype=torch.uint8, device=dev)
+            self.offsets = torch.zeros(world + 1, **i32)
             self.gcount = torch.zeros(1, **i32)
-            self.gcounts = torch.zeros(self.world, **i32)
-            self.gpack = torch.empty(self.S, self.F, **f32)
+            # gradient block per rank: [stats S x 3 | tau world x 6 | cap x F packed rows]
+            self.st_n = 3 * S if stats else 0
+            self.head = self.st_n + 6 * world
+            self.gsend = torch.empty(self.head + S * self.F, **f32)
+            # two generations (step parity): the next step first clears, on
+            # every rank, the rows this step's gather scattered (instead of
+            # zeroing the whole gradient buffer)
+            self.summary = [torch.zeros(world * world + world, **i32) for _ in range(2)]
+            self.gall = [None, None]
+            self.gen = 0
+            self.prev = None  # (gathered flat, block, counts, cap) of the last step
             if stats:
                 self.rad_send = torch.empty(self.P_pad, **f32)
                 self.rad_recv = torch.empty(self.P_pad, **f32)
@@ -412,21 +389,18 @@ class ViewShardedBackward:
         g = self.group
         # this view's camera row -> every owner (tiny; overlaps the records)
         self.k.pack_camera(cam, W, H, self.cam_row)
+        w_cam = None
         if self.world > 1:
             w_cam = _all_gather_into(self.cams.view(-1), self.cam_row, g)
         else:
             self.cams.copy_(self.cam_row[None])
-            w_cam = None
         # this view's screen-space records of every Gaussian -> owners
         self.k.records(fwd, dL_dcolor, dL_ddepth, self.P_pad, self.send)
         if self.world > 1:
-            w = _all_to_all_equal(self.recv.view(self.P_pad, 12), self.send, g)
-            if w is not None:
-                w.wait()
+            _wait(_all_to_all(self.recv.view(self.P_pad, 12), self.send, g))
         else:
             self.recv.view(self.P_pad, 12).copy_(self.send)
-        if w_cam is not None:
-            w_cam.wait()
+        _wait(w_cam)
         # owner: all views of the shard, summed
         st = self.stats[self.lo:self.hi] if self.stats is not None else None
         self.k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
@@ -437,93 +411,112 @@ class ViewShardedBackward:
         else:
             mine.zero_()
         if self.world > 1:
+            # every buffer's shard gathered in place: one equal-block
+            # all_gather_into_tensor each, issued back to back, waited once
             fulls = [v.view(self.P_pad, -1) for v in self.buf.views.values()]
             if self.stats is not None:
                 fulls.append(self.stats)
             fulls.append(self.tau_own)
-            w = _all_gather_inplace_many(fulls, self.rank, g)
-            if w is not None:
-                w.wait()
+            works = []
+            for f in fulls:
+                n = f.size(0) // self.world
+                works.append(_all_gather_into(f.view(-1), f[self.rank * n:(self.rank + 1) * n].reshape(-1).clone(),
+                                              g))
+            _wait(*works)
         torch.sum(self.tau_own, dim=0, out=self.tau)
         stats = self.stats[:self.P] if self.stats is not None else None
         return self.grads, self.tau[self.rank], stats
 
     def _backward_sparse(self, fwd, dL_dcolor, dL_ddepth, scale_modifier):
-        """The same result as the dense exchange, moving only non-zero rows:
-        each view's records with a non-zero partial sum go to their owners
-        (uneven all-to-all), and each owner gathers only the gradient rows of
-        Gaussians some view gave gradient to (padded to the largest owner's
-        count).  Two host reads of row counts per step size the collectives."""
+        """The same result as the dense exchange, moving only non-zero rows.
+
+        Collectives per step: one small equal-block all-gather (camera rows,
+        rows sent per owner, non-zero row masks), the records as ONE
+        all_to_all_single with split sizes, and ONE equal-block all-gather of
+        [statistics | pose sums | packed gradient rows] per owner (padded to
+        the largest owner's union count); with statistics also the dense
+        radius column (equal all_to_all_single).  ONE host read per step: the
+        count matrix and every owner's union row count, both computed on the
+        device from the small all-gather (csrc/dp_sparse.hip)."""
         means3D, scales, rotations, shs, D, cam = fwd[:6]
         H, W = dL_dcolor.size(1), dL_dcolor.size(2)
-        g, S, world, rank = self.group, self.S, self.world, self.rank
+        g, S, world, rank, F = self.group, self.S, self.world, self.rank, self.F
+        k = self.k
+        small = self.small
+        small.zero_()
         self.k.pack_camera(cam, W, H, self.cam_row)
-        w_cam = _all_gather_into(self.cams.view(-1), self.cam_row, g)
-        self.k.records(fwd, dL_dcolor, dL_ddepth, self.P_pad, self.send)
-        cb = self.cbuf
-        cb.zero_()
-        self.k.sparse_pack_records(self.send, S, cb[0], self.packed)
+        small[:64].copy_(self.cam_row.view(torch.int32))
+        k.records(fwd, dL_dcolor, dL_ddepth, self.P_pad, self.send)
+        k.sparse_pack_records(self.send, S, small[64:64 + world], self.packed, small[64 + world:])
         w_rad = None
         if self.stats is not None:  # the statistics need every visible Gaussian's radius
             self.rad_send.copy_(self.send[:, 10])
-            w_rad = _all_to_all_equal(self.rad_recv, self.rad_send, g)
-        w = _all_to_all_equal(cb[1], cb[0], g)
-        if w is not None:
-            w.wait()
-        sent, got = cb.tolist()  # host read 1: the row counts
-        ins = [self.packed[o * S:o * S + sent[o]] for o in range(world)]
-        outs = [self.recvp[v * S:v * S + got[v]] for v in range(world)]
-        w = _all_to_all_var(outs, ins, g)
+            w_rad = _all_to_all(self.rad_recv, self.rad_send, g)
+        _wait(_all_gather_into(self.small_all.view(-1), small, g))
+        p = self.gen & 1
+        summary = self.summary[p]
+        k.sparse_exchange_summary(self.small_all, world, rank, S, summary, self.offsets, self.cams)
+        host = summary.tolist()  # the step's one host read
+        cmat = [host[v * world:(v + 1) * world] for v in range(world)]
+        union = host[world * world:]
+        sent = cmat[rank]
+        got = [cmat[v][rank] for v in range(world)]
+        cap = max(union)
+        # records: this rank's per-owner segments, packed contiguously -> owners
+        ins = torch.cat([self.packed[o * S:o * S + sent[o]] for o in range(world)])
+        received = self.recvp[:sum(got)]
+        w = _all_to_all(received, ins, g, out_splits=got, in_splits=sent)
         self.recv.zero_()
         self.mask.zero_()
         if self.stats is not None:
-            if w_rad is not None:
-                w_rad.wait()
-            self.k.sparse_fill_radius(self.rad_recv, self.recv.view(-1, 12))
-        if w is not None:
-            w.wait()
-        self.k.sparse_unpack_records(self.recvp.view(world, S, 12), cb[1], S, self.stats is not None, self.recv,
-                                     self.mask)
-        if w_cam is not None:
-            w_cam.wait()
-        # rows no owner writes stay zero: the sparse gather leaves them alone
-        self.buf.flat.zero_()
-        st = self.stats[self.lo:self.hi] if self.stats is not None else None
-        self.k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
-                           self.recv, self.buf.views, self.tau_blk if self.hi > self.lo else None, st)
-        mine = self.tau_own[rank]
+            _wait(w_rad)
+            k.sparse_fill_radius(self.rad_recv, self.recv.view(-1, 12))
+        _wait(w)
+        k.sparse_unpack_records(received, self.offsets, S, self.stats is not None, self.recv, self.mask)
+        # owner: all views of the shard, summed; statistics and pose sums go
+        # straight into this rank's gradient block
+        blk = self.head + cap * F
+        send = self.gsend[:blk]
+        st = send[:self.st_n].view(S, 3)[:self.hi - self.lo] if self.stats is not None else None
+        tau_mine = send[self.st_n:self.head].view(world, 6)
+        k.gauss_views((means3D, scales, rotations, shs, D, scale_modifier), self.lo, self.hi, self.cams,
+                      self.recv, self.buf.views, self.tau_blk if self.hi > self.lo else None, st)
         if self.hi > self.lo:
-            torch.sum(self.tau_blk, dim=0, out=mine)
+            torch.sum(self.tau_blk, dim=0, out=tau_mine)
         else:
-            mine.zero_()
+            tau_mine.zero_()
+        if self.stats is not None and self.hi - self.lo < S:
+            send[:self.st_n].view(S, 3)[self.hi - self.lo:].zero_()
         self.gcount.zero_()
-        self.k.sparse_pack_grads(self.buf.views, self.lo, self.hi, self.mask, self.gcount, self.gpack)
-        w = _all_gather_into(self.gcounts, self.gcount, g)
-        if w is not None:
-            w.wait()
-        counts = self.gcounts.tolist()  # host read 2: gradient rows per owner
-        cap = max(counts)
-        pairs = []
-        gathered = None
-        if cap > 0:
-            gathered = torch.empty(world * cap * self.F, dtype=torch.float32, device=self.gpack.device)
-            pairs.append((gathered, self.gpack[:cap].reshape(-1)))
-        fulls = ([self.stats] if self.stats is not None else []) + [self.tau_own]
-        for f in fulls:
-            n = f.size(0) // world
-            pairs.append((f.view(-1), f[rank * n:(rank + 1) * n].reshape(-1)))
-        w = _all_gather_many(pairs, g)
-        if w is not None:
-            w.wait()
-        if gathered is not None:
-            self.k.sparse_unpack_grads(gathered.view(world, cap, self.F), self.gcounts, rank, cap, S, self.P,
-                                       self.buf.views)
+        k.sparse_pack_grads(self.buf.views, self.lo, self.hi, self.mask, self.gcount, send[self.head:])
+        gathered = torch.empty(world * blk, dtype=torch.float32, device=send.device)
+        _wait(_all_gather_into(gathered, send, g))
+        gv = gathered.view(world, blk)
+        if self.stats is not None:
+            self.stats.view(world, S * 3).copy_(gv[:, :self.st_n])
+        self.tau_own.copy_(gv[:, self.st_n:self.head].reshape(world, world, 6))
+        counts = summary[world * world:]
+        # the rows the previous step scattered from other owners go back to
+        # zero (this rank's own shard is rewritten whole by the owner kernel)
+        if self.prev is not None:
+            pg, pblk, pcounts, pcap = self.prev
+            self._unpack_grads(pg, pblk, pcounts, pcap, clear=True)
+        self._unpack_grads(gathered, blk, counts, cap, clear=False)
+        self.prev = (gathered, blk, counts, cap)
+        self.gen += 1
         torch.sum(self.tau_own, dim=0, out=self.tau)
         others = sum(got) - got[rank]
         self.last_exchange = {
-            "record_rows_in": others, "grad_rows_per_owner": counts, "grad_rows_cap": cap,
-            "bytes_in": int(others * 48 + (world - 1) * cap * self.F * 4 +
-                            ((world - 1) * S * 16 if self.stats is not None else 0) + (world - 1) * world * 24),
+            "record_rows_in": others, "grad_rows_per_owner": union, "grad_rows_cap": cap,
+            "bytes_in": int(others * 48 + (world - 1) * blk * 4 +
+                            ((world - 1) * S * 4 if self.stats is not None else 0) +
+                            (world - 1) * self.BW * 4),
         }
         stats = self.stats[:self.P] if self.stats is not None else None
         return self.grads, self.tau[rank], stats
+
+    def _unpack_grads(self, gathered, blk, counts, cap, clear):
+        if cap == 0:
+            return
+        self.k.sparse_unpack_grads(gathered[self.head:], blk, counts, self.rank, cap, self.S, self.P, self.buf.views,
+                                   clear=clear)
