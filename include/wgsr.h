@@ -445,6 +445,60 @@ typedef struct wgsr_row_tensor {
 int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,
                       wgsr_alloc_fn scratch_alloc, void* alloc_ctx, void* stream);
 
+/* ---- densification on the device (csrc/densify.hip, wgsr/store.py) -------
+ * The GaussianModel state lives in a capacity-preallocated SoA of two banks;
+ * one bank = the five parameter tensors (xyz [C,3], features [C,M,3],
+ * opacity [C,1], scaling [C,3], rotation [C,4]; raw, as GaussianModel's
+ * _xyz ... _rotation), their Adam moments in that order, and per-row
+ * keyframe ids / observation counts (optional).  Rows are addressed by
+ * index; a densify reads one bank and writes the other. */
+typedef struct wgsr_gaussian_bank {
+  float* xyz;
+  float* features;
+  float* opacity;
+  float* scaling;
+  float* rotation;
+  float* exp_avg[5];
+  float* exp_avg_sq[5];
+  int32_t* kf_id;
+  int32_t* n_obs;
+} wgsr_gaussian_bank;
+
+/* Workgroups of the select / emit kernels over P rows; block_counts holds
+ * 4 x (wgsr_densify_blocks(P) + 1) uint32. */
+int64_t wgsr_densify_blocks(int64_t P);
+
+/* Replaces the selection of GaussianModel.densify_and_prune(max_grad,
+ * min_opacity, extent, max_screen_size) (gaussian_model.py:646-743):
+ * grad_threshold = max_grad (> 0), dense_threshold = percent_dense * extent,
+ * world_threshold = 0.1 * extent, use_screen_size = bool(max_screen_size).
+ * Per row a flag byte (kept original, kept clone, kept split pair, split
+ * selected) and, after the built-in scan, block_counts = exclusive per-block
+ * offsets of the four regions with the totals (kept originals Ko, kept
+ * clones Kc, kept split rows per copy Ks, selected split rows Ns) at
+ * [4 * wgsr_densify_blocks(P)].  New row count: Ko + Kc + 2 Ks.
+ * With prune_mask (bytes, 1 = prune) instead: prune_points(mask)
+ * (gaussian_model.py:548-564) -- only kept originals. */
+int wgsr_densify_select(int64_t P, const float* accum, const float* denom, const float* opacity,
+                        const float* scaling, const uint8_t* prune_mask, float grad_threshold,
+                        float dense_threshold, float min_opacity, float world_threshold, int use_screen_size,
+                        float max_screen_size, uint8_t* flags, uint32_t* block_counts, void* stream);
+
+/* Writes the densified / pruned table into bank dst (capacity >= the new row
+ * count): kept originals with their moments, then kept clones, kept split
+ * copies A and B (zero moments): split xyz = R(q) (z * exp(s)) + xyz with z
+ * [2 Ns, 3] standard-normal samples (copy A rows first, by selection rank),
+ * split scaling = log(exp(s) / 1.6). */
+int wgsr_densify_emit(int64_t P, int M, const uint8_t* flags, const uint32_t* block_counts, const float* z,
+                      const wgsr_gaussian_bank* src, const wgsr_gaussian_bank* dst, void* stream);
+
+/* reset_opacity (visible = null, value = inverse_sigmoid(0.01)) and
+ * reset_opacity_nonvisible (value = inverse_sigmoid(0.4); visible rows get
+ * sigmoid(raw): the reference writes get_opacity[filter] into the raw
+ * tensor) (gaussian_model.py:389-402); the opacity moments -> 0. */
+int wgsr_reset_opacity(int64_t P, float* opacity_raw, const uint8_t* visible, float value, float* exp_avg,
+                       float* exp_avg_sq, void* stream);
+
 /* ---- SSIM for the mapping loss -------------------
  * Images are `planes` contiguous H x W fp32 planes (any leading dims
  * flattened; zero padding at the borders, as F.conv2d(padding=ws//2)).

@@ -1,0 +1,161 @@
+#!/usr/bin/env python
+"""configs[4]-shaped online mapping run on synthetic keyframes (wgsr.online).
+
+BASELINE.json configs[4] is the TUM fr3/walking_xyz end-to-end mapper loop;
+the dataset, droid.pth and the Metric3D / DINOv2 weights are absent offline
+(SURVEY.md 8(f) f4), so this runs the same mapper loop -- initialisation,
+per-keyframe insertion (distCUDA2 point init), map_opt_online with the
+uncertainty-aware loss, the DINO regulariser, densify / prune and the
+opacity reset -- on keyframes rendered from a synthetic room at the product
+operating point: 512x384, SH degree 0, TUM-like intrinsics.
+
+Ground truth: a dense synthetic room (textured floor, ceiling and walls of
+Gaussians) rendered by the same rasteriser from a camera trajectory; depth =
+rendered depth / opacity where the opacity exceeds 0.5 (else invalid, 0);
+features: a fixed random [h, w, 384] map per keyframe (h, w = H/14, W/14).
+
+Prints one JSON line: ms per mapping iteration (wall clock over
+map_opt_online, synchronised), ms per keyframe insertion (visibility render
++ window update + back-projection + distCUDA2 + append), the Gaussian count,
+the densify / reset events and the PSNR of the final map's renders against
+the keyframes' ground truth.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+for p in (os.path.join(ROOT, "wildgs-slam-blackwell_amd", "python"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+
+def room(P, seed=0, dev="cuda"):
+    """Gaussians on the inside of a 6 x 3 x 10 m box, textured."""
+    g = torch.Generator().manual_seed(seed)
+    face = torch.randint(0, 5, (P,), generator=g)
+    a, b = torch.rand(P, generator=g), torch.rand(P, generator=g)
+    x = torch.empty(P)
+    y = torch.empty(P)
+    z = torch.empty(P)
+    # 0 floor (y = 1.5), 1 ceiling (y = -1.5), 2 back (z = 8), 3 left (x = -3), 4 right (x = 3)
+    sel = face == 0
+    x[sel], y[sel], z[sel] = -3 + 6 * a[sel], 1.5, -2 + 10 * b[sel]
+    sel = face == 1
+    x[sel], y[sel], z[sel] = -3 + 6 * a[sel], -1.5, -2 + 10 * b[sel]
+    sel = face == 2
+    x[sel], y[sel], z[sel] = -3 + 6 * a[sel], -1.5 + 3 * b[sel], 8.0
+    sel = face == 3
+    x[sel], y[sel], z[sel] = -3.0, -1.5 + 3 * a[sel], -2 + 10 * b[sel]
+    sel = face == 4
+    x[sel], y[sel], z[sel] = 3.0, -1.5 + 3 * a[sel], -2 + 10 * b[sel]
+    xyz = torch.stack([x, y, z], 1)
+    u, v = a * 8, b * 8
+    col = torch.stack([0.5 + 0.4 * torch.sin(3.1 * u + face), 0.5 + 0.4 * torch.cos(2.3 * v + 2 * face),
+                       0.5 + 0.4 * torch.sin(1.7 * (u + v))], 1)
+    col = torch.where(((u.floor() + v.floor()) % 2 == 0)[:, None], col, col * 0.6)
+    scales = torch.full((P, 3), 0.03)
+    rots = torch.zeros(P, 4)
+    rots[:, 0] = 1
+    opac = torch.full((P, 1), 0.95)
+    shs = ((col - 0.5) / 0.28209479177387814)[:, None, :]
+    return [t.contiguous().to(dev) for t in (xyz, opac, scales, rots, shs)]
+
+
+def pose(k):
+    ang = math.radians(1.5 * k)
+    c, s = math.cos(ang), math.sin(ang)
+    R = torch.tensor([[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]])
+    T = torch.tensor([-0.08 * k, 0.0, 0.0])
+    return R, T
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--keyframes", type=int, default=12)
+    ap.add_argument("--init-keyframes", type=int, default=2)
+    ap.add_argument("--init-iters", type=int, default=1050)
+    ap.add_argument("--iters", type=int, default=450)
+    ap.add_argument("--gt-gaussians", type=int, default=400_000)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+    from diff_gaussian_rasterization import _C
+    from wgsr.camera import PinholeCamera
+    from wgsr.online import Keyframe, OnlineMapper
+
+    dev = torch.device("cuda:0")
+    W, H = a.width, a.height
+    fx = fy = 517.3 * W / 512.0
+    cx, cy = W / 2.0, H / 2.0
+    gt = room(a.gt_gaussians, dev=dev)
+    e = torch.empty(0, device=dev)
+    kfs = []
+    g = torch.Generator().manual_seed(a.seed + 1)
+    for k in range(a.keyframes):
+        R, T = pose(k)
+        f = PinholeCamera(R=R, T=T, fx=fx, fy=fy, cx=cx, cy=cy, W=W, H=H).raster_fields()
+        d = {kk: (v.to(dev) if torch.is_tensor(v) else v) for kk, v in f.items()}
+        out = _C.rasterize_gaussians(torch.zeros(3, device=dev), gt[0], e, gt[1], gt[2], gt[3], 1.0, e,
+                                     d["viewmatrix"], d["projmatrix"], d["projmatrix_raw"], d["tanfovx"],
+                                     d["tanfovy"], H, W, gt[4], 0, d["campos"], False, False)
+        img, depth, opac = out[1], out[6], out[7]
+        dep = torch.where(opac > 0.5, depth / opac.clamp_min(1e-6), torch.zeros_like(depth))
+        feats = torch.randn(H // 14, W // 14, 384, generator=g).to(dev)
+        kfs.append(Keyframe(k, R, T, fx, fy, cx, cy, img.clamp(0, 1).contiguous(), dep.contiguous(), feats))
+    torch.cuda.synchronize()
+
+    m = OnlineMapper(sh_degree=0, device=dev, seed=a.seed)
+    t0 = time.perf_counter()
+    m.initialize(kfs[:a.init_keyframes], iters=a.init_iters)
+    torch.cuda.synchronize()
+    t_init = time.perf_counter() - t0
+    ins_ms, it_ms, its = [], 0.0, 0
+    for kf in kfs[a.init_keyframes:]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vis = m.visibility(kf)
+        m.keyframes[kf.uid] = kf
+        m.window = m._add_to_window(kf.uid, vis, m.window)
+        m._add_points(kf, init=False)
+        m._new_exposure_optimizer()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        split = m.map_opt_online(m.window, a.iters)
+        n = a.iters
+        if split:
+            m.map_opt_online(m.window, 1)
+            n += 1
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ins_ms.append(1e3 * (t1 - t0))
+        it_ms += 1e3 * (t2 - t1)
+        its += n
+    # PSNR of the final map against every keyframe's ground truth
+    ps = []
+    for kf in kfs:
+        img, _ = m.render_image(kf)
+        mse = float(((img.clamp(0, 1) - kf.image) ** 2).mean())
+        ps.append(10 * math.log10(1.0 / max(mse, 1e-12)))
+    print(json.dumps({
+        "workload": f"configs[4]-shaped online mapping: synthetic room, {W}x{H}, SH0, {a.keyframes} keyframes "
+                    f"({a.init_keyframes} init x {a.init_iters} its, then {a.iters} its per keyframe)",
+        "ms_per_mapping_iteration": it_ms / max(its, 1), "mapping_iterations": its,
+        "ms_per_keyframe_insertion": sum(ins_ms) / max(len(ins_ms), 1),
+        "init_seconds": t_init, "gaussians_final": m.ms.P,
+        "events": [(i, k, v) for i, k, v in m.events][:40],
+        "psnr_db_mean": sum(ps) / len(ps), "psnr_db_per_keyframe": ps,
+        "note": "uncertainty-aware loss + DINO regulariser + isotropic term, densify/prune, opacity reset, "
+                "Adam (Gaussians, exposures, MLP); wall clock with a device sync per keyframe"}))
+
+
+if __name__ == "__main__":
+    main()

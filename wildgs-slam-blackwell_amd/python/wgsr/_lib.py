@@ -72,6 +72,13 @@ class UncerParams(ctypes.Structure):
 PLY_MAX_TENSORS = 8
 PLY_MAX_COLS = 128
 ADAM_MAX_TENSORS = 16
+class GaussianBank(ctypes.Structure):
+    """Mirror of ``wgsr_gaussian_bank`` (one bank of the densification SoA)."""
+
+    _fields_ = [("xyz", _fp), ("features", _fp), ("opacity", _fp), ("scaling", _fp), ("rotation", _fp),
+                ("exp_avg", _fp * 5), ("exp_avg_sq", _fp * 5), ("kf_id", _fp), ("n_obs", _fp)]
+
+
 COMPACT_MAX_TENSORS = 32
 
 _lib = None
@@ -146,6 +153,16 @@ def load():
         L.wgsr_pose_step.restype = c_int
         L.wgsr_pose_step.argtypes = ([_fp] * 3 + [c_int, _fp] + [ctypes.c_float] * 6 + [c_int, ctypes.c_float, _fp,
                                                                                           c_int, _fp])
+        L.wgsr_densify_blocks.restype = c_i64
+        L.wgsr_densify_blocks.argtypes = [c_i64]
+        L.wgsr_densify_select.restype = c_int
+        L.wgsr_densify_select.argtypes = ([c_i64] + [_fp] * 5 + [ctypes.c_float] * 4 + [c_int, ctypes.c_float]
+                                          + [_fp, _fp, _fp])
+        L.wgsr_densify_emit.restype = c_int
+        L.wgsr_densify_emit.argtypes = [c_i64, c_int, _fp, _fp, _fp, ctypes.POINTER(GaussianBank),
+                                        ctypes.POINTER(GaussianBank), _fp]
+        L.wgsr_reset_opacity.restype = c_int
+        L.wgsr_reset_opacity.argtypes = [c_i64, _fp, _fp, ctypes.c_float, _fp, _fp, _fp]
         L.wgsr_sparse_grad_row_floats.restype = c_int
         L.wgsr_sparse_grad_row_floats.argtypes = [c_int]
         L.wgsr_sparse_mask_words.restype = c_i64
@@ -236,6 +253,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
     "wgsr_pose_state_floats", "wgsr_pose_step",
     "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
+    "wgsr_densify_blocks", "wgsr_densify_select", "wgsr_densify_emit", "wgsr_reset_opacity",
     "wgsr_sparse_grad_row_floats", "wgsr_sparse_mask_words", "wgsr_sparse_pack_records",
     "wgsr_sparse_summary_block_words", "wgsr_sparse_exchange_summary", "wgsr_sparse_unpack_records",
     "wgsr_sparse_fill_radius", "wgsr_sparse_pack_grads", "wgsr_sparse_unpack_grads",

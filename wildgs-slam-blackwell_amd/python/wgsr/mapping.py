@@ -40,36 +40,102 @@ def _blocks(n):
 
 
 class MappingStep:
-    """GaussianModel state in the fused layout + one-call mapping iterations."""
+    """GaussianModel state in the fused layout + one-call mapping iterations.
+
+    The state lives in a ``GaussianStore`` (capacity-preallocated banks,
+    wgsr/store.py): keyframe insertion (``extend``), ``densify_and_prune`` and
+    the opacity resets change the row count without re-allocating, and every
+    view below (``xyz``, ``grad``, ``exp_avg`` ...) is re-taken from the
+    current bank."""
+
+    GROUPS = ("xyz", "features", "opacity", "scaling", "rotation")
 
     def __init__(self, xyz, features_dc, features_rest, opacity, scaling, rotation, sh_degree: int,
-                 lr: dict | None = None, betas=(0.9, 0.999), eps: float = 1e-15):
+                 lr: dict | None = None, betas=(0.9, 0.999), eps: float = 1e-15, capacity: int | None = None):
+        from .store import GaussianStore
         dev = xyz.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.P = P = xyz.shape[0]
+        P = xyz.shape[0]
         self.D = int(sh_degree)
-        self.xyz = xyz.detach().to(**f32).contiguous().clone()
-        self.features = torch.cat([features_dc, features_rest], dim=1).detach().to(**f32).contiguous()
-        self.M = self.features.shape[1]
-        self.opacity = opacity.detach().to(**f32).reshape(P, 1).contiguous().clone()
-        self.scaling = scaling.detach().to(**f32).contiguous().clone()
-        self.rotation = rotation.detach().to(**f32).contiguous().clone()
+        features = torch.cat([features_dc, features_rest], dim=1).detach().to(**f32).contiguous()
+        self.M = features.shape[1]
+        self.store = GaussianStore(xyz.detach().to(**f32), features, opacity.detach().to(**f32).reshape(P, 1),
+                                   scaling.detach().to(**f32), rotation.detach().to(**f32), capacity=capacity)
         self.lr = dict(DEFAULT_LR, **(lr or {}))
         self.betas, self.eps = betas, eps
-        self.step_count = 0
-        names = ("xyz", "features", "opacity", "scaling", "rotation")
-        self.grad = {n: torch.zeros_like(getattr(self, n)) for n in names}
-        self.exp_avg = {n: torch.zeros_like(getattr(self, n)) for n in names}
-        self.exp_avg_sq = {n: torch.zeros_like(getattr(self, n)) for n in names}
-        # densification state (gaussian_model.py: max_radii2D, xyz_gradient_accum, denom)
-        self.max_radii2D = torch.zeros(P, **f32)
-        self.xyz_gradient_accum = torch.zeros(P, 1, **f32)
-        self.denom = torch.zeros(P, 1, **f32)
-        # activated parameters and their gradients (scratch)
-        self.act = {"opacity": torch.empty(P, 1, **f32), "scales": torch.empty(P, 3, **f32),
-                    "rotations": torch.empty(P, 4, **f32)}
-        self.act_grad = {k: torch.empty_like(v) for k, v in self.act.items()}
-        self.iso_part = torch.empty(max(1, _blocks(P)), **f32)
+        # torch.optim.Adam keeps a step count per parameter; a group whose
+        # parameter was replaced without a gradient (densify, opacity reset)
+        # skips its update and its count (f_dc and f_rest always move together)
+        self.steps = {g: 0 for g in self.GROUPS}
+        self._iso = None
+
+    # storage views (current bank, [:P]) --------------------------------------
+    @property
+    def P(self):
+        return self.store.P
+
+    @property
+    def step_count(self):
+        return self.steps["xyz"]
+
+    @property
+    def xyz(self):
+        return self.store.param("xyz")
+
+    @property
+    def features(self):
+        return self.store.param("features")
+
+    @property
+    def opacity(self):
+        return self.store.param("opacity")
+
+    @property
+    def scaling(self):
+        return self.store.param("scaling")
+
+    @property
+    def rotation(self):
+        return self.store.param("rotation")
+
+    @property
+    def grad(self):
+        return {n: self.store.grad(n) for n in self.GROUPS}
+
+    @property
+    def exp_avg(self):
+        return {n: self.store.exp_avg(n) for n in self.GROUPS}
+
+    @property
+    def exp_avg_sq(self):
+        return {n: self.store.exp_avg_sq(n) for n in self.GROUPS}
+
+    @property
+    def max_radii2D(self):
+        return self.store.stat("max_radii2D")
+
+    @property
+    def xyz_gradient_accum(self):
+        return self.store.stat("xyz_gradient_accum")
+
+    @property
+    def denom(self):
+        return self.store.stat("denom")
+
+    @property
+    def act(self):
+        return {k: self.store.scratch("act_" + k) for k in ("opacity", "scales", "rotations")}
+
+    @property
+    def act_grad(self):
+        return {k: self.store.scratch("actg_" + k) for k in ("opacity", "scales", "rotations")}
+
+    @property
+    def iso_part(self):
+        n = max(1, _blocks(self.P))
+        if self._iso is None or self._iso.numel() != n:
+            self._iso = torch.empty(n, dtype=torch.float32, device=self.store.device)
+        return self._iso
 
     # reference-style views -------------------------------------------------
     @property
@@ -91,6 +157,30 @@ class MappingStep:
     @property
     def get_rotation(self):
         return torch.nn.functional.normalize(self.rotation)
+
+    # densification (GaussianModel, gaussian_model.py:231-269, 389-402, 646-743)
+    def extend(self, xyz, features, scaling, rotation, opacity, kf_id=None):
+        """extend_from_pcd (gaussian_model.py:231-259): features [n, M, 3]."""
+        n = xyz.shape[0]
+        kf = None if kf_id is None else torch.full((n,), int(kf_id), dtype=torch.int32)
+        self.store.append(xyz, features, opacity, scaling, rotation, kf_id=kf)
+
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, percent_dense=0.01, z=None,
+                          generator=None):
+        """Every parameter is replaced: the reference's optimizer.step() that
+        follows skips them all (their new nn.Parameters carry no gradient)."""
+        out = self.store.densify_and_prune(max_grad, min_opacity, extent, max_screen_size, percent_dense, z=z,
+                                           generator=generator)
+        self._skip = set(self.GROUPS)
+        return out
+
+    def reset_opacity_nonvisible(self, visibility_filters):
+        self.store.reset_opacity_nonvisible(visibility_filters)
+        self._skip = getattr(self, "_skip", set()) | {"opacity"}
+
+    def reset_opacity(self):
+        self.store.reset_opacity()
+        self._skip = getattr(self, "_skip", set()) | {"opacity"}
 
     # -----------------------------------------------------------------------
     def _render(self, cam: dict, H: int, W: int, bg):
@@ -244,27 +334,38 @@ class MappingStep:
                 "uncertainty_loss": state.uncertainty_loss}
 
     @torch.no_grad()
-    def optimizer_step(self):
+    def optimizer_step(self, skip=()):
         """torch.optim.Adam(param_groups, lr=0.0, eps=1e-15).step() over the six
-        reference groups, ONE launch (f_dc / f_rest as a two-rate split)."""
+        reference groups, ONE launch (f_dc / f_rest as a two-rate split).
+        Groups in ``skip`` -- and those whose parameter a densify / opacity
+        reset replaced since the last step -- take no update and keep their
+        step count, as torch's Adam does for a parameter without a gradient."""
         L = _lib.load()
-        self.step_count += 1
+        skip = set(skip) | getattr(self, "_skip", set())
+        self._skip = set()
         b1, b2 = self.betas
-        bc1 = 1.0 - b1 ** self.step_count
-        bc2s = math.sqrt(1.0 - b2 ** self.step_count)
         lr = self.lr
         ts = []
         for name, step, tail in (("xyz", lr["xyz"], None), ("features", lr["f_dc"], lr["f_rest"]),
                                  ("opacity", lr["opacity"], None), ("scaling", lr["scaling"], None),
                                  ("rotation", lr["rotation"], None)):
-            prm = getattr(self, name)
-            t = _lib.AdamTensor(prm.data_ptr(), self.grad[name].data_ptr(), self.exp_avg[name].data_ptr(),
-                                self.exp_avg_sq[name].data_ptr(), prm.numel(), step / bc1, bc2s)
+            if name in skip:
+                continue
+            self.steps[name] += 1
+            n = self.steps[name]
+            bc1 = 1.0 - b1 ** n
+            bc2s = math.sqrt(1.0 - b2 ** n)
+            prm = self.store.param(name)
+            t = _lib.AdamTensor(prm.data_ptr(), self.store.grad(name).data_ptr(),
+                                self.store.exp_avg(name).data_ptr(), self.store.exp_avg_sq(name).data_ptr(),
+                                prm.numel(), step / bc1, bc2s)
             if tail is not None:
                 t.split_period, t.split_len, t.step_size_tail = 3 * self.M, 3, tail / bc1
             ts.append(t)
+        if not ts or self.P == 0:
+            return
         arr = (_lib.AdamTensor * len(ts))(*ts)
-        dev = self.xyz.device
+        dev = self.store.device
         with torch.cuda.device(dev):
             _lib.check(L.wgsr_adam_step(arr, len(ts), b1, b2, self.eps, _lib.stream_handle(dev)))
 

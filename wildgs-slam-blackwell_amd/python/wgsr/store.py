@@ -1,0 +1,244 @@
+"""The GaussianModel state in a capacity-preallocated SoA.
+
+The reference grows and shrinks its six parameter tensors and their Adam
+moments with ``torch.cat`` / boolean indexing on every keyframe insertion,
+densification and prune (thirdparty/gaussian_splatting/scene/gaussian_model.py:
+231-269, 526-743): each re-allocates ~18 tensors.  ``GaussianStore`` keeps
+them in two preallocated banks of ``capacity`` rows:
+
+* parameters (raw, as ``_xyz``, ``_features_dc|_features_rest`` fused into one
+  [C, M, 3] SH storage, ``_opacity``, ``_scaling``, ``_rotation``), their Adam
+  moments (``exp_avg`` / ``exp_avg_sq``), keyframe ids and observation counts
+  (``unique_kfIDs`` / ``n_obs``) -- per bank;
+* gradients, densification statistics (``xyz_gradient_accum``, ``denom``,
+  ``max_radii2D``) and activation scratch -- one copy.
+
+A densify / prune reads the current bank and writes the other
+(csrc/densify.hip: select + scan + emit, one host read of the four region
+sizes); a keyframe insertion writes the new rows after the last one.  Only
+when the row count outgrows the capacity are both banks re-allocated
+(geometric growth).  Views ``[:P]`` of the current bank are what the
+rasteriser and the optimizer see.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+
+PARAMS = ("xyz", "features", "opacity", "scaling", "rotation")
+
+
+def inverse_sigmoid(x: torch.Tensor) -> torch.Tensor:
+    """general_utils.inverse_sigmoid (general_utils.py:21-22)."""
+    return torch.log(x / (1 - x))
+
+
+class GaussianStore:
+    def __init__(self, xyz, features, opacity, scaling, rotation, capacity: int | None = None,
+                 kf_id=None, n_obs=None, growth: float = 1.5):
+        dev = xyz.device
+        self.device = dev
+        self.P = P = int(xyz.shape[0])
+        self.M = int(features.shape[1])
+        self.growth = float(growth)
+        self.capacity = max(int(capacity or 0), P, 1)
+        self.banks = [self._new_bank(self.capacity), self._new_bank(self.capacity)]
+        self.cur = 0
+        self.single = self._new_single(self.capacity)
+        b = self.banks[0]
+        for name, t in zip(PARAMS, (xyz, features, opacity, scaling, rotation)):
+            b[name][:P].copy_(t.detach().reshape(b[name][:P].shape))
+            b["m_" + name][:P].zero_()
+            b["v_" + name][:P].zero_()
+        b["kf_id"][:P].copy_(kf_id if kf_id is not None else torch.full((P,), -1, dtype=torch.int32))
+        b["n_obs"][:P].copy_(n_obs if n_obs is not None else torch.zeros(P, dtype=torch.int32))
+        self.zero_stats()
+
+    # ---- storage -------------------------------------------------------------
+    def _shape(self, name, n):
+        return {"xyz": (n, 3), "features": (n, self.M, 3), "opacity": (n, 1), "scaling": (n, 3),
+                "rotation": (n, 4)}[name]
+
+    def _new_bank(self, cap):
+        f32 = dict(dtype=torch.float32, device=self.device)
+        b = {}
+        for name in PARAMS:
+            b[name] = torch.empty(self._shape(name, cap), **f32)
+            b["m_" + name] = torch.empty(self._shape(name, cap), **f32)
+            b["v_" + name] = torch.empty(self._shape(name, cap), **f32)
+        b["kf_id"] = torch.empty(cap, dtype=torch.int32, device=self.device)
+        b["n_obs"] = torch.empty(cap, dtype=torch.int32, device=self.device)
+        return b
+
+    def _new_single(self, cap):
+        f32 = dict(dtype=torch.float32, device=self.device)
+        s = {"grad_" + n: torch.zeros(self._shape(n, cap), **f32) for n in PARAMS}
+        s["xyz_gradient_accum"] = torch.zeros(cap, 1, **f32)
+        s["denom"] = torch.zeros(cap, 1, **f32)
+        s["max_radii2D"] = torch.zeros(cap, **f32)
+        s["act_opacity"] = torch.empty(cap, 1, **f32)
+        s["act_scales"] = torch.empty(cap, 3, **f32)
+        s["act_rotations"] = torch.empty(cap, 4, **f32)
+        for k in ("opacity", "scales", "rotations"):
+            s["actg_" + k] = torch.empty_like(s["act_" + k])
+        return s
+
+    def reserve(self, n: int):
+        """Room for n rows (both banks); keeps the current rows, moments and
+        statistics.  Growth is geometric, so inserts stay amortised O(1)."""
+        if n <= self.capacity:
+            return
+        cap = max(int(n), int(math.ceil(self.capacity * self.growth)))
+        P = self.P
+        nb = [self._new_bank(cap), self._new_bank(cap)]
+        for k, t in self.banks[self.cur].items():
+            nb[0][k][:P].copy_(t[:P])
+        ns = self._new_single(cap)
+        for k, t in self.single.items():
+            ns[k][:P].copy_(t[:P])
+        self.banks, self.single, self.cur, self.capacity = nb, ns, 0, cap
+
+    # ---- views [:P] ---------------------------------------------------------
+    def param(self, name):
+        return self.banks[self.cur][name][:self.P]
+
+    def exp_avg(self, name):
+        return self.banks[self.cur]["m_" + name][:self.P]
+
+    def exp_avg_sq(self, name):
+        return self.banks[self.cur]["v_" + name][:self.P]
+
+    def grad(self, name):
+        return self.single["grad_" + name][:self.P]
+
+    def stat(self, name):
+        return self.single[name][:self.P]
+
+    def scratch(self, name):
+        return self.single[name][:self.P]
+
+    @property
+    def kf_id(self):
+        return self.banks[self.cur]["kf_id"][:self.P]
+
+    @property
+    def n_obs(self):
+        return self.banks[self.cur]["n_obs"][:self.P]
+
+    def zero_stats(self):
+        """densification_postfix's reset (gaussian_model.py:635-637)."""
+        for k in ("xyz_gradient_accum", "denom", "max_radii2D"):
+            self.single[k][:self.P].zero_()
+
+    def _bank_struct(self, b):
+        bank = self.banks[b]
+        s = _lib.GaussianBank()
+        for name in PARAMS:
+            setattr(s, name, bank[name].data_ptr())
+        for k, name in enumerate(PARAMS):
+            s.exp_avg[k] = bank["m_" + name].data_ptr()
+            s.exp_avg_sq[k] = bank["v_" + name].data_ptr()
+        s.kf_id = bank["kf_id"].data_ptr()
+        s.n_obs = bank["n_obs"].data_ptr()
+        return s
+
+    # ---- reference operations ------------------------------------------------
+    def append(self, xyz, features, opacity, scaling, rotation, kf_id=None, n_obs=None):
+        """densification_postfix / extend_from_pcd (gaussian_model.py:231-259,
+        602-644): new rows after the last one with zero Adam moments; the
+        statistics of ALL rows reset to zero."""
+        n = int(xyz.shape[0])
+        P = self.P
+        self.reserve(P + n)
+        b = self.banks[self.cur]
+        for name, t in zip(PARAMS, (xyz, features, opacity, scaling, rotation)):
+            b[name][P:P + n].copy_(t.detach().reshape(self._shape(name, n)))
+            b["m_" + name][P:P + n].zero_()
+            b["v_" + name][P:P + n].zero_()
+        b["kf_id"][P:P + n].copy_(kf_id if kf_id is not None else torch.full((n,), -1, dtype=torch.int32))
+        b["n_obs"][P:P + n].copy_(n_obs if n_obs is not None else torch.zeros(n, dtype=torch.int32))
+        self.P = P + n
+        self.zero_stats()
+
+    def _select_emit(self, prune_mask=None, max_grad=0.0, min_opacity=0.0, extent=0.0, max_screen_size=None,
+                     percent_dense=0.0, z=None, generator=None):
+        L = _lib.load()
+        P, dev = self.P, self.device
+        nb = int(L.wgsr_densify_blocks(P))
+        flags = torch.empty(max(P, 1), dtype=torch.uint8, device=dev)
+        bc = torch.empty(4 * (nb + 1), dtype=torch.int32, device=dev)
+        st = _lib.stream_handle(dev)
+        pm = prune_mask.to(torch.uint8).contiguous() if prune_mask is not None else None
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_densify_select(
+                P, _lib.ptr(self.stat("xyz_gradient_accum")), _lib.ptr(self.stat("denom")),
+                _lib.ptr(self.param("opacity")), _lib.ptr(self.param("scaling")), _lib.ptr(pm), float(max_grad),
+                float(percent_dense * extent), float(min_opacity), float(0.1 * extent),
+                int(bool(max_screen_size)), float(max_screen_size or 0.0), flags.data_ptr(), bc.data_ptr(), st))
+        Ko, Kc, Ks, Ns = bc[4 * nb:4 * nb + 4].tolist()  # the one host read
+        P_new = Ko + Kc + 2 * Ks
+        if Ns and z is None:
+            z = torch.randn(2 * Ns, 3, device=dev, generator=generator)
+        if z is not None:
+            z = z.to(device=dev, dtype=torch.float32).contiguous()
+            if Ns and z.numel() < 6 * Ns:
+                raise ValueError(f"densify: need z of [{2 * Ns}, 3] standard-normal samples, got {tuple(z.shape)}")
+        self.reserve(P_new)
+        src, dst = self._bank_struct(self.cur), self._bank_struct(self.cur ^ 1)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_densify_emit(P, self.M, flags.data_ptr(), bc.data_ptr(), _lib.ptr(z),
+                                           ctypes.byref(src), ctypes.byref(dst), st))
+        self.cur ^= 1
+        self.P = P_new
+        self.zero_stats()
+        return {"kept": Ko, "cloned": Kc, "split_selected": Ns, "split_kept": Ks, "P": P_new}
+
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, percent_dense, z=None,
+                          generator=None):
+        """GaussianModel.densify_and_prune (gaussian_model.py:646-743) in one
+        select + scan + emit.  ``z``: the split's standard-normal samples
+        [2 Ns, 3] (copy A rows, then copy B; drawn with ``generator`` when
+        absent), i.e. the reference's torch.normal(0, stds) = z * stds."""
+        return self._select_emit(None, max_grad, min_opacity, extent, max_screen_size, percent_dense, z, generator)
+
+    def prune_points(self, mask):
+        """GaussianModel.prune_points (gaussian_model.py:548-564): rows with
+        mask set go, the rest keep their order and moments.  (Unlike
+        densification_postfix, prune keeps the statistics of the kept rows.)"""
+        keep_stats = {k: self.stat(k)[~mask.bool()].clone() for k in ("xyz_gradient_accum", "denom", "max_radii2D")}
+        out = self._select_emit(prune_mask=mask)
+        for k, v in keep_stats.items():
+            self.single[k][:self.P].copy_(v)
+        return out
+
+    def reset_opacity(self):
+        """GaussianModel.reset_opacity (gaussian_model.py:389-392)."""
+        self._reset_opacity(None, self._inv_sigmoid_const(0.01))
+
+    def reset_opacity_nonvisible(self, visibility_filters):
+        """GaussianModel.reset_opacity_nonvisible (gaussian_model.py:394-402):
+        invisible rows -> inverse_sigmoid(0.4); rows visible in any filter keep
+        get_opacity (the activated value, written into the raw tensor as the
+        reference does); opacity moments -> 0."""
+        vis = None
+        for f in visibility_filters:
+            f = f.to(device=self.device, dtype=torch.bool)
+            vis = f if vis is None else (vis | f)
+        self._reset_opacity(vis, self._inv_sigmoid_const(0.4))
+
+    def _inv_sigmoid_const(self, c):
+        """inverse_sigmoid(torch.ones_like(opacity) * c), evaluated on the
+        device as the reference does (one element: the value is per row)."""
+        return float(inverse_sigmoid(torch.ones(1, device=self.device) * c).item())
+
+    def _reset_opacity(self, vis, value):
+        L = _lib.load()
+        v8 = vis.to(torch.uint8).contiguous() if vis is not None else None
+        with torch.cuda.device(self.device):
+            _lib.check(L.wgsr_reset_opacity(self.P, self.param("opacity").data_ptr(), _lib.ptr(v8), value,
+                                            self.exp_avg("opacity").data_ptr(), self.exp_avg_sq("opacity").data_ptr(),
+                                            _lib.stream_handle(self.device)))

@@ -269,3 +269,36 @@ def get_loss_mapping_uncertainty(config, rendered_img, rendered_depth, viewpoint
                                     viewpoint.exposure_a, viewpoint.exposure_b, uncertainty, train_frac, ssim_frac,
                                     config, initialization, freeze_uncertainty_loss)
     return uncertainty, loss
+
+
+# ---- DINO feature-similarity regulariser (mapping_utils.py:325-389) --------
+DINO_TOP_K = 128
+DINO_SIMILARITY_THRESHOLD = 0.75
+DINO_EPS = float(torch.finfo(torch.float32).eps)
+
+
+def dino_regularization_loss(uncertainty, features):
+    """compute_dino_regularization_loss (mapping_utils.py:332-389): the mean
+    over samples of the variance of the uncertainty over each sample's (up
+    to) 128 most similar features with cosine similarity > 0.75 (NeRF-on-the-
+    Go eqs. 2-3).  ``uncertainty`` [.., 1] or a list of tensors, ``features``
+    [.., C] (or a list) with the same sample count; differentiable in the
+    uncertainty.  torch ops (an N x N GEMM + top-k on a few thousand samples:
+    hipBLASLt + rocPRIM), the same arithmetic as the reference's."""
+    unc = torch.stack(uncertainty) if isinstance(uncertainty, (list, tuple)) else uncertainty
+    feat = torch.stack(features) if isinstance(features, (list, tuple)) else features
+    C = feat.shape[-1]
+    u = unc.reshape(-1, 1)
+    fn = torch.nn.functional.normalize(feat.contiguous().view(-1, C), p=2, dim=-1)
+    if u.shape[0] != fn.shape[0]:
+        raise ValueError("Uncertainty and feature buffers must have same number of samples"
+                         + f"but got {u.shape[0]} and {fn.shape[0]}")
+    sim = fn @ fn.T
+    k = min(DINO_TOP_K, sim.shape[-1])
+    top, idx = torch.topk(sim, k=k, dim=-1)
+    mask = (top > DINO_SIMILARITY_THRESHOLD).float()
+    nb = u[idx] * mask.unsqueeze(-1)
+    cnt = mask.sum(dim=-1, keepdim=True) + DINO_EPS
+    mean = nb.sum(dim=1) / cnt
+    var = (((nb - mean.unsqueeze(-1)) ** 2) * mask.unsqueeze(-1)).sum(dim=1) / cnt
+    return var.mean()
