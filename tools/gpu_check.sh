@@ -70,6 +70,14 @@ for s in $STEPS; do
     pmc_custom)
       # PMC_COUNTERS="A B C" PMC_NAME=name: one extra counter pass (SQ block: at most 8 counters)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_${PMC_NAME:-custom}.err); rc=$? ;;
+    pmcab)
+      # one PMC_COUNTERS pass per AB_LIBS entry (bench.py, 3 steps) -> pmc_ab_<name>/
+      rc=0
+      for v in ${AB_LIBS}; do
+        if [ "$v" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$v.so; fi
+        (cd /tmp && WGSR_LIB=$GRAFT_REPO_ROOT/$lib timeout -k 10 300 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_ab_$v -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_ab_$v.err); rc=$?
+        if [ $rc -ne 0 ]; then break; fi
+      done ;;
     dp2)
       # N = 2 rehearsal of the multi-GPU bench path on the box's one GPU: two
       # ranks share cuda:0 over gloo (device tensors staged through host memory)

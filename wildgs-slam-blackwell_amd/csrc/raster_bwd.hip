@@ -35,6 +35,14 @@ constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 #ifndef WGSR_BWD_HITMASK
 #define WGSR_BWD_HITMASK 1
 #endif
+// diagnostic build: histogram of (quadrants reached, quadrants evaluated in
+// phase 2) per entry over the quad backward (wgsr_debug_bwd_stats)
+#ifndef WGSR_BWD_STATS
+#define WGSR_BWD_STATS 0
+#endif
+#if WGSR_BWD_STATS
+__device__ unsigned long long g_bwd_stats[32];
+#endif
 // below this many tiles the backward runs k_render_bwd_split (four waves per
 // tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
 constexpr int kBwdSplitBelowTiles = 3072;
@@ -85,6 +93,11 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
+#if WGSR_BWD_STATS
+  uint32_t* const sStat = sHit;
+  if (lane < 32) sStat[lane] = 0;
+  __syncthreads();
+#endif
 
   // per-quadrant pixel state; pairs are packed for v_pk_* math.  Pixel
   // positions are not kept per quadrant: quadrant p's pixel is this lane's
@@ -195,9 +208,15 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
       float g4 = 0.f, g5 = 0.f;
       bool hit = false;
+#if WGSR_BWD_STATS
+      uint32_t st_reach = 0, st_p2 = 0;
+#endif
 #pragma unroll
       for (int p = 0; p < Q; ++p) {
         if (!((qb[p] >> j) & 1)) continue;  // wave-uniform: the splat cannot reach quadrant p
+#if WGSR_BWD_STATS
+        st_reach |= 1u << p;
+#endif
         // phase 1: does entry j reach this lane's pixel of quadrant p?
         const v2f d = d0 - v2f{8.f * (p & 1), 8.f * (p >> 1)};  // (dx, dy) = mean - pixel
         const float power = splat_power(cd, cxy, d);  // log2(e) x upstream's power
@@ -206,6 +225,9 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
         if (!wave_any(v)) continue;
         hit = true;
+#if WGSR_BWD_STATS
+        st_p2 |= 1u << p;
+#endif
 #if WGSR_BWD_MASKED
         // phase 2 on the lanes whose pixel the entry reaches (exec mask): the
         // others keep T, the accumulated colour and their sums as they are.
@@ -261,6 +283,12 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         g89 += dch * dp2d[p];
 #endif
       }
+#if WGSR_BWD_STATS
+      if (lane == 0) {
+        atomicAdd(&sStat[st_reach], 1u);
+        atomicAdd(&sStat[16 + st_p2], 1u);
+      }
+#endif
       if (!hit) continue;  // no pixel of the tile: no partial
       const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
       wave_sum10_store_m(gv, sPm + 11 * j);
@@ -293,6 +321,256 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       gflag[gid] = 1;  // same value from every tile: a benign race
     }
   }
+#if WGSR_BWD_STATS
+  __syncthreads();
+  if (lane < 32) atomicAdd(&g_bwd_stats[lane], (unsigned long long)sStat[lane]);
+#endif
+}
+
+// Pixel-pair variant of render_bwd_quad_tile (WGSR_BWD_PAIR=1; off by
+// default: measured 340 vs 306 us at 1M / 1080p -- 18.5k vs 17.6k VALU per
+// wave, since an entry reaching one quadrant of a row pair still pays both
+// pixels' exp2 and a row pair runs phase 2 whenever any lane of the tile
+// took the entry):
+// the same wave per tile and per-quadrant culling, but the lane's pixels of
+// horizontally adjacent quadrants (0, 1) and (2, 3) -- same row, x and x + 8
+// -- are evaluated TOGETHER in packed-FP32 math whenever the entry reaches
+// both (most entries reach 3-4 quadrants): every per-pixel operation of the
+// two evaluations except the transcendentals and compares is one v_pk_*
+// instruction, and the two pixels share dy.  The per-pixel arithmetic is the
+// forward's own operation sequence (dx = mean - (x0 + 8), power =
+// dx (A.z dx + B.x dy) + (A.w dy) dy), so alpha is bitwise the forward's.
+// A pair runs branch-free: a pixel the entry misses gets G = 0 and alpha = 0
+// (T, the accumulated colour and every sum pass through exactly).  An entry
+// reaching only one quadrant of a row pair evaluates that pixel alone
+// (exec-masked, as the quad tile).  Per-entry sums are pairs (one half per
+// pixel of the pair), added together once before the wave reduction; the
+// first evaluation of an entry writes them, later ones accumulate.
+// The background enters as the accumulated colour's starting value: upstream's
+// dL/dalpha term -T_final / (1 - alpha) (bg . dL/dpix) equals
+// -T (prod of (1 - alpha) behind the entry) (bg . dL/dpix), which is what the
+// accum_rec recurrence adds when it starts from bg instead of 0 -- so one
+// code path serves every background (a black one starts from 0).
+#ifndef WGSR_BWD_PAIR
+#define WGSR_BWD_PAIR 0
+#endif
+
+// phase 1 of one row pair (the lane's pixels at x and x + 8, same y) for
+// one entry: the forward's power / alpha and the per-pixel contribution tests
+// (reach: the entry reaches that quadrant at all, wave-uniform)
+struct PairP1 {
+  v2f G, av;
+  uint64_t mA, mB;  // lanes whose pixel takes this entry (SGPR lane masks)
+};
+__device__ __forceinline__ PairP1 bwd_pair_p1(v2f dX, v2f tX, float dy, float w, float cxy, float op, uint32_t cidx,
+                                              uint32_t lastA, uint32_t lastB, bool reachA, bool reachB) {
+  PairP1 r;
+  const v2f in = pfma(v2f{cxy, cxy}, v2f{dy, dy}, tX);
+  const v2f pw = pfma(dX, in, v2f{w, w});
+  r.G = v2f{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
+  const v2f ag = v2f{op, op} * r.G;
+  r.av = v2f{fminf(kMaxAlpha, ag.x), fminf(kMaxAlpha, ag.y)};
+  // each test its own ballot, combined by scalar ops (a ballot of the
+  // compound predicate would go through a VGPR)
+  const uint64_t mA = wave_ballot(cidx < lastA) & wave_ballot(pw.x <= 0.0f) & wave_ballot(r.av.x >= kMinAlpha);
+  const uint64_t mB = wave_ballot(cidx < lastB) & wave_ballot(pw.y <= 0.0f) & wave_ballot(r.av.y >= kMinAlpha);
+  r.mA = reachA ? mA : 0ull;
+  r.mB = reachB ? mB : 0ull;
+  return r;
+}
+
+// phase 2 of one row pair, branch-free: a pixel the entry does not reach
+// (v false) runs with alpha = 0 and G = 0, which passes T and the
+// accumulated colour through exactly (1 / (1 - 0) = 1) and adds 0 to every
+// sum.  kInit: write the sums instead of adding to them.
+template <bool kInit>
+__device__ __forceinline__ void bwd_pair_p2(const PairP1& q, v2f dX, float dy, v2f c01, v2f c2d, v2f& T, v2f& acc,
+                                            const v2f (&dp)[4], v2f (&S)[10]) {
+  const bool vA = __builtin_amdgcn_inverse_ballot_w64(q.mA), vB = __builtin_amdgcn_inverse_ballot_w64(q.mB);
+  const v2f a{vA ? q.av.x : 0.f, vB ? q.av.y : 0.f};
+  const v2f Ge{vA ? q.G.x : 0.f, vB ? q.G.y : 0.f};
+  const v2f om = v2f{1.f, 1.f} - a;
+  const v2f rinv{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};  // alpha <= 0.99
+  const v2f Tn = T * rinv;
+  T = Tn;
+  const v2f dch = a * Tn;
+  // c . dL/d(colour, depth) per pixel: upstream's accum_rec recurrence, dotted
+  const v2f cp = pfma(v2f{c2d.y, c2d.y}, dp[3],
+                      pfma(v2f{c2d.x, c2d.x}, dp[2], pfma(v2f{c01.y, c01.y}, dp[1], v2f{c01.x, c01.x} * dp[0])));
+  const v2f sd = cp - acc;
+  const v2f dLda = sd * Tn;
+  acc = pfma(a, sd, acc);
+  const v2f gl = Ge * dLda;
+  const v2f dyy{dy, dy};
+  const v2f ux = gl * dX, uy = gl * dyy;
+  if (kInit) {
+    S[0] = ux; S[1] = uy; S[2] = ux * dX; S[3] = ux * dyy; S[4] = uy * dyy; S[5] = gl;
+    S[6] = dch * dp[0]; S[7] = dch * dp[1]; S[8] = dch * dp[2]; S[9] = dch * dp[3];
+  } else {
+    S[0] += ux; S[1] += uy;
+    S[2] = pfma(ux, dX, S[2]); S[3] = pfma(ux, dyy, S[3]); S[4] = pfma(uy, dyy, S[4]);
+    S[5] += gl;
+    S[6] = pfma(dch, dp[0], S[6]); S[7] = pfma(dch, dp[1], S[7]);
+    S[8] = pfma(dch, dp[2], S[8]); S[9] = pfma(dch, dp[3], S[9]);
+  }
+}
+
+__device__ __forceinline__ void render_bwd_pair_tile(
+    const uint32_t tile, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g,
+    const float4* __restrict__ splat, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
+    int H, int gx, float bg0, float bg1, float bg2, const float* __restrict__ final_Ts,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, float4 (*sA2)[kBatch],
+    float4 (*sB2)[kBatch], float4 (*sC2)[kBatch], float (*sP)[11]) {
+  constexpr int Q = 4;
+  const int lane = threadIdx.x;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
+  const size_t HW = (size_t)H * W;
+  const uint2 range = ranges[tile];
+  // pixel x of the lane in quadrants (0 | 2) and (1 | 3); rows y and y + 8
+  const v2f PX{(float)(tx0 + (lane & 7)), (float)(tx0 + 8 + (lane & 7))};
+  const float PY0 = (float)(ty0 + (lane >> 3)), PY1 = (float)(ty0 + 8 + (lane >> 3));
+  // row pair r: T, accd, dL/dpix channels as (pixel of quadrant 2r, of 2r + 1)
+  v2f T[2], acc[2], dp[2][4];
+  uint32_t last[Q];
+  uint32_t m = 0, mq[Q];
+  {
+    float Tq[Q], dq[Q][4];
+    bool inside[Q];
+#pragma unroll
+    for (int p = 0; p < Q; ++p) {
+      const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
+      inside[p] = px < W && py < H;
+      const size_t pid = inside[p] ? (size_t)py * W + px : 0;
+      Tq[p] = final_Ts[pid];
+      last[p] = n_contrib[pid];
+      dq[p][0] = dL_dpix[pid];
+      dq[p][1] = dL_dpix[HW + pid];
+      dq[p][2] = dL_dpix[2 * HW + pid];
+      dq[p][3] = dL_ddep[pid];
+    }
+#pragma unroll
+    for (int p = 0; p < Q; ++p) {
+      Tq[p] = inside[p] ? Tq[p] : 0.f;
+      last[p] = inside[p] ? last[p] : 0u;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dq[p][c] = inside[p] ? dq[p][c] : 0.f;
+      uint32_t x = last[p];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
+      mq[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);  // wave-uniform: an SGPR
+      m = max(m, mq[p]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      T[r] = v2f{Tq[2 * r], Tq[2 * r + 1]};
+      // the background as the colour behind the last contributor (see above)
+      acc[r] = v2f{bg0 * dq[2 * r][0] + bg1 * dq[2 * r][1] + bg2 * dq[2 * r][2],
+                   bg0 * dq[2 * r + 1][0] + bg1 * dq[2 * r + 1][1] + bg2 * dq[2 * r + 1][2]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dp[r][c] = v2f{dq[2 * r][c], dq[2 * r + 1][c]};
+    }
+  }
+  const uint32_t end = range.x + m;
+  float* const sPm = &sP[0][0] + sum10_slot(lane);
+
+  // records stream straight into LDS (global_load_lds_dwordx4: no VGPRs held
+  // for the prefetch), double buffered; Gaussian ids one batch ahead
+  auto fetch = [&](uint32_t g, int buf) {
+    const float4* src = splat + 3 * (size_t)g;
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)&sA2[buf][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 1), (__attribute__((address_space(3))) void*)&sB2[buf][0], 16,
+                                     0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 2), (__attribute__((address_space(3))) void*)&sC2[buf][0], 16,
+                                     0, 0);
+  };
+  uint32_t gcur = 0, gnext = 0;
+  int buf = 0;
+  if (end >= range.x + 1 + lane) {
+    gcur = point_g[end - 1 - lane];
+    fetch(gcur, 0);
+  }
+  if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
+
+  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
+    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
+    __builtin_amdgcn_s_waitcnt(0);  // this batch's records (and the next ids) have landed
+    __syncthreads();
+    const float4* sA = sA2[buf];
+    const float4* sB = sB2[buf];
+    const float4* sC = sC2[buf];
+    const uint32_t gmine = gcur;  // this lane's entry of the batch
+    gcur = gnext;
+    if (b_end >= range.x + 1 + kBatch + lane) fetch(gcur, buf ^ 1);
+    if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
+
+    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
+    uint64_t qb[Q];
+    {
+      const uint32_t myidx = cfirst - (uint32_t)lane;
+      const float4 a = sA[lane], b = sB[lane];
+#pragma unroll
+      for (int p = 0; p < Q; ++p) {
+        const int x0 = tx0 + (p & 1) * 8, y0 = ty0 + (p >> 1) * 8;
+        qb[p] = wave_ballot(lane < cnt && myidx < mq[p] && ellipse_hits(a, b, x0, x0 + 7, y0, y0 + 7));
+      }
+    }
+    uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
+    uint64_t hitm = 0;
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t cidx = cfirst - j;
+      const float4 A = sA[j];
+      const float4 B = sB[j];
+      const float4 Cc = sC[j];
+      const v2f c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
+      const float cxy = B.x, op = B.y;
+      const v2f dX = v2f{A.x, A.x} - PX;     // mean.x - pixel x, both quadrant columns
+      const v2f tX = v2f{A.z, A.z} * dX;     // (A.z dx) of both
+      const bool r0 = (qb[0] >> j) & 1, r1 = (qb[1] >> j) & 1, r2 = (qb[2] >> j) & 1, r3 = (qb[3] >> j) & 1;
+      const float dy0 = A.y - PY0, w0 = (A.w * dy0) * dy0;
+      const float dy1 = A.y - PY1, w1 = (A.w * dy1) * dy1;
+      v2f S[10];
+      // straight-line code per case (wave-uniform): both row pairs, or one
+      if ((r0 || r1) && (r2 || r3)) {
+        const PairP1 q0 = bwd_pair_p1(dX, tX, dy0, w0, cxy, op, cidx, last[0], last[1], r0, r1);
+        const PairP1 q1 = bwd_pair_p1(dX, tX, dy1, w1, cxy, op, cidx, last[2], last[3], r2, r3);
+        if ((q0.mA | q0.mB | q1.mA | q1.mB) == 0) continue;  // no pixel of the tile: no partial
+        bwd_pair_p2<true>(q0, dX, dy0, c01, c2d, T[0], acc[0], dp[0], S);
+        bwd_pair_p2<false>(q1, dX, dy1, c01, c2d, T[1], acc[1], dp[1], S);
+      } else if (r0 || r1) {
+        const PairP1 q0 = bwd_pair_p1(dX, tX, dy0, w0, cxy, op, cidx, last[0], last[1], r0, r1);
+        if ((q0.mA | q0.mB) == 0) continue;
+        bwd_pair_p2<true>(q0, dX, dy0, c01, c2d, T[0], acc[0], dp[0], S);
+      } else {
+        const PairP1 q1 = bwd_pair_p1(dX, tX, dy1, w1, cxy, op, cidx, last[2], last[3], r2, r3);
+        if ((q1.mA | q1.mB) == 0) continue;
+        bwd_pair_p2<true>(q1, dX, dy1, c01, c2d, T[1], acc[1], dp[1], S);
+      }
+      float gv[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) gv[k] = S[k].x + S[k].y;
+      wave_sum10_store_m(gv, sPm + 11 * j);
+      hitm |= 1ull << j;
+    }
+    if (lane < cnt && ((hitm >> lane) & 1)) {
+      const uint32_t gid = gmine;
+      const float4 A = sA[lane], B = sB[lane];
+      const size_t k =
+          slot_start[gid] + pair_local(A, B, lr_rect(lrec[gid].w), lrec[gid].tab, (int)(tile % gx), (int)(tile / gx));
+      float sv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
+      record_sums(A, B, sv);
+      partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+      partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+      partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
+      pflag[k] = 1;
+      gflag[gid] = 1;  // same value from every tile: a benign race
+    }
+    buf ^= 1;
+  }
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
@@ -311,12 +589,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+#if WGSR_BWD_PAIR
+  (void)sHit; (void)sA; (void)sB; (void)sC; (void)sG;
+  __shared__ float4 sA2[2][kBatch], sB2[2][kBatch], sC2[2][kBatch];
+  render_bwd_pair_tile(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts, n_contrib,
+                       dL_dpix, dL_ddep, partial, pflag, gflag, sA2, sB2, sC2, sP);
+#else
   if (bg0 == 0.f && bg1 == 0.f && bg2 == 0.f)  // (uniform)
     render_bwd_quad_tile<false>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
                                 n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
   else
     render_bwd_quad_tile<true>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
                                n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
+#endif
   // this tile's share of the per-Gaussian outputs' zero fill (HBM is idle
   // here; measured at 1M/1080p: render_bwd +2 % with the fill after the walk,
   // +4.5 % before it, while k_gauss_bwd drops from 86 to 49 us)
@@ -1538,3 +1823,13 @@ hipError_t launch_gauss_bwd_views(const wgsr_raster_args& a, int lo, int hi, int
 }
 
 }  // namespace wgsr
+
+#if WGSR_BWD_STATS
+// diagnostic build only: read and clear the quad backward's entry histogram
+extern "C" int wgsr_debug_bwd_stats(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_bwd_stats), sizeof(unsigned long long) * 32) != hipSuccess)
+    return 1;
+  unsigned long long z[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_bwd_stats), z, sizeof(z)) != hipSuccess;
+}
+#endif

@@ -451,6 +451,8 @@ __device__ __forceinline__ uint32_t pair_local(const float4& A, const float4& B,
 
 // Two packed floats: arithmetic on these lowers to v_pk_*_f32 on gfx950.
 typedef float v2f __attribute__((ext_vector_type(2)));
+// packed fused multiply-add (v_pk_fma_f32): per element exactly fmaf
+__device__ __forceinline__ v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
 
 // log2(e) x upstream's power at (dx, dy) = mean - pixel, from the pre-scaled
 // conic (cd = (A.z, A.w), cxy = B.x): A.z dx^2 + A.w dy^2 + B.x dx dy
