@@ -145,7 +145,11 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   float* const sPm = &sP[0][0] + sum10_slot(lane);  // this lane's store slot in an entry's row
 
   // prefetch pipeline (back to front): records of the next batch in
-  // registers, ids one batch further
+  // registers, ids one batch further.  A batch's partial records are written
+  // at the top of the NEXT batch, from the sums left in sP, with each hit
+  // entry's slot_start / ListRec loaded one batch early: the stores then sit
+  // in the memory queue behind loads that are waited for only a batch later,
+  // and no dependent load stands between the walk and the stores.
   uint32_t gcur = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
   if (end >= range.x + 1 + lane) {
@@ -155,18 +159,69 @@ __device__ __forceinline__ void render_bwd_quad_tile(
     nC = splat[3 * (size_t)gcur + 2];
   }
   if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
+  uint64_t hit_prev = 0;             // entries of the previous batch that left sums in sP
+  uint32_t gid_prev = 0, ss_prev = 0;
+  uint2 rw_prev = make_uint2(0u, 0u);
+  uint4 tab_prev = make_uint4(0u, 0u, 0u, 0u);
+  auto write_records = [&]() {
+    if ((hit_prev >> lane) & 1) {
+      // duplicate slot of (Gaussian, this tile): its first slot plus the
+      // tile's index in the Gaussian's exact tile list (k_duplicate)
+      const float4 A = sA[lane], B = sB[lane];
+      const size_t k = ss_prev + pair_local(A, B, lr_rect(make_uint4(rw_prev.x, rw_prev.y, 0u, 0u)), tab_prev,
+                                            (int)(tile % gx), (int)(tile / gx));
+      float sv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
+      record_sums(A, B, sv);
+      partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+      partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+      partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
+      pflag[k] = 1;
+      gflag[gid_prev] = 1;  // same value from every tile: a benign race
+    }
+  };
 
   for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
     const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
+    // (one wave per workgroup: LDS accesses of the wave stay in order, and
+    // the barriers compile to wave barriers)
+    // the previous batch's records and sums, before this batch overwrites them
+    float4 pA = make_float4(0, 0, 0, 0), pB = pA;
+    float psv[10];
+    const bool phit = (hit_prev >> lane) & 1;
+    if (phit) {
+      pA = sA[lane];
+      pB = sB[lane];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) psv[q] = sP[lane][q];
+    }
     __syncthreads();
     sA[lane] = nA;
     sB[lane] = nB;
     sC[lane] = nC;
-    sG[lane] = gcur;
 #if !WGSR_BWD_HITMASK
     sHit[lane] = 0;
 #endif
     __syncthreads();
+    if (phit) {
+      const size_t k = ss_prev + pair_local(pA, pB, lr_rect(make_uint4(rw_prev.x, rw_prev.y, 0u, 0u)), tab_prev,
+                                            (int)(tile % gx), (int)(tile / gx));
+      record_sums(pA, pB, psv);
+      partial[3 * k] = make_float4(psv[0], psv[1], psv[2], psv[3]);
+      partial[3 * k + 1] = make_float4(psv[4], psv[5], psv[6], psv[7]);
+      partial[3 * k + 2] = make_float4(psv[8], psv[9], 0.f, 0.f);
+      pflag[k] = 1;
+      gflag[gid_prev] = 1;  // same value from every tile: a benign race
+    }
+    // this batch's entry of this lane: its slot data, for the write one batch on
+    // (every lane loads: lanes past the batch hold id 0 or an earlier id, a
+    // valid row, and a conditional load would cost register copies that wait
+    // for it)
+    gid_prev = gcur;
+    ss_prev = slot_start[gcur];
+    rw_prev = *reinterpret_cast<const uint2*>(&lrec[gcur].w);
+    tab_prev = lrec[gcur].tab;
     gcur = gnext;
     if (b_end >= range.x + 1 + kBatch + lane) {
       nA = splat[3 * (size_t)gcur];
@@ -298,29 +353,14 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       if (lane == 0) sHit[j] = 1;
 #endif
     }
-    __syncthreads();
 #if WGSR_BWD_HITMASK
-    if (lane < cnt && ((hitm >> lane) & 1)) {
+    hit_prev = hitm & (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull));
 #else
-    if (lane < cnt && sHit[lane]) {
+    __syncthreads();
+    hit_prev = wave_ballot(lane < cnt && sHit[lane]);
 #endif
-      // duplicate slot of (Gaussian, this tile): its first slot plus the
-      // tile's index in the Gaussian's exact tile list (k_duplicate)
-      const uint32_t gid = sG[lane];
-      const float4 A = sA[lane], B = sB[lane];
-      const size_t k =
-          slot_start[gid] + pair_local(A, B, lr_rect(lrec[gid].w), lrec[gid].tab, (int)(tile % gx), (int)(tile / gx));
-      float sv[10];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
-      record_sums(A, B, sv);
-      partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-      partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
-      partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
-      pflag[k] = 1;
-      gflag[gid] = 1;  // same value from every tile: a benign race
-    }
   }
+  write_records();  // the last batch's
 #if WGSR_BWD_STATS
   __syncthreads();
   if (lane < 32) atomicAdd(&g_bwd_stats[lane], (unsigned long long)sStat[lane]);
@@ -590,8 +630,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 #if WGSR_BWD_PAIR
-  (void)sHit; (void)sA; (void)sB; (void)sC; (void)sG;
   __shared__ float4 sA2[2][kBatch], sB2[2][kBatch], sC2[2][kBatch];
+  (void)sHit; (void)sA; (void)sB; (void)sC; (void)sG;
   render_bwd_pair_tile(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts, n_contrib,
                        dL_dpix, dL_ddep, partial, pflag, gflag, sA2, sB2, sC2, sP);
 #else

@@ -751,6 +751,113 @@ __device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const u
   if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
 }
 
+// Entry-pair blend (WGSR_FWD_EPAIR, the default): the batch's entries that
+// survive the wave's culling are first compacted into the wave's own LDS area
+// with two consecutive survivors interleaved per field (sQ: {x1, x2, y1, y2},
+// {A.z1, A.z2, A.w1, A.w2}, {B.x1, B.x2, o1, o2}), so that one ds_read_b128
+// hands two entries' operands to packed-FP32 math: the power, exp2 argument
+// and opacity product of BOTH entries cost one v_pk_* instruction each (the
+// forward's own operation sequence per lane, so alpha is bitwise that of
+// fwd_blend_loop and of the backward's recomputation).  Only the
+// transmittance recurrence, the compares and the colour accumulation stay
+// per entry.  n_touched increments are staged per compact slot.
+#ifndef WGSR_FWD_EPAIR
+#define WGSR_FWD_EPAIR 1
+#endif
+// wave 0 streams the next batch's records into a second LDS buffer with
+// global_load_lds instead of holding them in registers (every wave of the
+// kernel would allocate those VGPRs)
+#ifndef WGSR_FWD_LDSPF
+#define WGSR_FWD_LDSPF 1
+#endif
+struct FwdPairRec {   // two consecutive survivors (one LDS address per pair)
+  float4 q[3];       // {x, x', y, y'}, {A.z, A.z', A.w, A.w'}, {B.x, B.x', o, o'}
+  float4 c[2];       // colour (c0, c1, c2, depth) of each
+  uint32_t n[2];     // contributor numbers
+  uint32_t pad[2];
+};
+struct FwdPairLds {
+  FwdPairRec p[kFwdBatch / 2];
+  uint32_t touch[kFwdBatch];  // n_touched increment per compact slot
+};
+
+template <bool kTouch>
+__device__ __forceinline__ void fwd_blend_one(float a, float pw, const float4& C, uint32_t cn, uint32_t* touch_slot,
+                                              float& T, v2f& c01, v2f& c2d, uint32_t& last, uint64_t& dm,
+                                              uint64_t valid) {
+  const float test_T = fmaf(-T, a, T);  // T (1 - alpha)
+  const uint64_t live = wave_ballot(pw <= 0.0f) & wave_ballot(a >= kMinAlpha) & ~dm & valid;
+  const uint64_t low = wave_ballot(test_T < kMinT);
+  const uint64_t blend = live & ~low;
+  const bool bl = __builtin_amdgcn_inverse_ballot_w64(blend);
+  const float wgt = bl ? a * T : 0.f;
+  c01 += wgt * v2f{C.x, C.y};
+  c2d += wgt * v2f{C.z, C.w};
+  uint32_t tot = 0;
+  if (kTouch) tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
+  T = bl ? test_T : T;
+  last = bl ? cn : last;
+  dm |= live & low;
+  if (kTouch) *touch_slot = tot;
+}
+
+template <bool kTouch>
+__device__ __forceinline__ void fwd_blend_pairs(int n, const FwdPairLds& L, uint32_t* touch, v2f pxy, float& T,
+                                                v2f& c01, v2f& c2d, uint32_t& last, uint64_t& dm) {
+  for (int i = 0; i < n && dm != ~0ull; i += 2) {
+    const FwdPairRec& R = L.p[i >> 1];
+    const float4 q0 = R.q[0], q1 = R.q[1], q2 = R.q[2];
+    const float4 C1 = R.c[0], C2 = R.c[1];
+    const uint2 cn = *reinterpret_cast<const uint2*>(&R.n[0]);
+    const v2f DX = v2f{q0.x, q0.y} - v2f{pxy.x, pxy.x}, DY = v2f{q0.z, q0.w} - v2f{pxy.y, pxy.y};
+    // splat_power per lane: fma(dx, fma(B.x, dy, A.z dx), (A.w dy) dy)
+    const v2f tz = v2f{q1.x, q1.y} * DX, tw = v2f{q1.z, q1.w} * DY;
+    const v2f PW = pfma(DX, pfma(v2f{q2.x, q2.y}, DY, tz), tw * DY);
+    const v2f ag = v2f{q2.z, q2.w} * v2f{__builtin_amdgcn_exp2f(PW.x), __builtin_amdgcn_exp2f(PW.y)};
+    const float a1 = fminf(kMaxAlpha, ag.x), a2 = fminf(kMaxAlpha, ag.y);
+    fwd_blend_one<kTouch>(a1, PW.x, C1, cn.x, touch + i, T, c01, c2d, last, dm, ~0ull);
+    // (an odd survivor count leaves the last pair's second half unused)
+    fwd_blend_one<kTouch>(a2, PW.y, C2, cn.y, touch + i + 1, T, c01, c2d, last, dm, i + 1 < n ? ~0ull : 0ull);
+  }
+}
+
+// cull the staged batch against the wave's pixel box, compact the survivors
+// into L, blend them front to back in pairs, flush n_touched
+__device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, const float4* sA, const float4* sB,
+                                                      const float4* sC, const uint32_t* sG, FwdPairLds& L, int wx0,
+                                                      int wx1, int wy0, int wy1, v2f pxy, int lane,
+                                                      int32_t* __restrict__ n_touched, float& T, v2f& c01, v2f& c2d,
+                                                      uint32_t& last, uint64_t& dm) {
+  const float4 A = sA[lane], B = sB[lane];
+  const bool mine = lane < cnt && ellipse_hits(A, B, wx0, wx1, wy0, wy1);
+  const uint64_t todo = wave_ballot(mine);
+  const int n = __popcll(todo);
+  const uint32_t k = lanes_below(todo);
+  const bool touch = (wave_ballot(T > 0.5f) & ~dm) != 0;  // (uniform) see WGSR_FWD_HALF
+  if (mine) {
+    FwdPairRec& R = L.p[k >> 1];
+    float* q = &R.q[0].x + (k & 1);
+    q[0] = A.x; q[2] = A.y; q[4] = A.z; q[6] = A.w; q[8] = B.x; q[10] = B.y;
+    R.c[k & 1] = sC[lane];
+    R.n[k & 1] = cbase + (uint32_t)lane;
+  }
+  if (touch) L.touch[lane] = 0;
+  if (lane == 63 && (n & 1)) {  // the unused half of an odd last pair: finite operands
+    FwdPairRec& R = L.p[n >> 1];
+    float* q = &R.q[0].x + 1;
+    q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
+    R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // (a wave's own LDS writes are visible to its later reads: no barrier)
+  if (touch) {
+    fwd_blend_pairs<true>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
+    const uint32_t tv = mine ? L.touch[k] : 0u;
+    if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
+  } else {
+    fwd_blend_pairs<false>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
+  }
+}
+
 // One 16x16 tile per workgroup of 4 waves; wave w owns the 8x8 quadrant w,
 // one pixel per lane.  Every per-pixel predicate (done, live, low, blend) is
 // an explicit SGPR lane mask combined by scalar ops: the per-entry update is
@@ -763,9 +870,18 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     float* __restrict__ out_color, float* __restrict__ out_depth, float* __restrict__ out_opac,
     float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ tile_m4) {
+#if WGSR_FWD_LDSPF
+  __shared__ float4 sA2[2][kFwdBatch], sB2[2][kFwdBatch], sC2[2][kFwdBatch];
+  __shared__ uint32_t sG2[2][kFwdBatch];
+#else
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
+#endif
+#if WGSR_FWD_EPAIR
+  __shared__ FwdPairLds sPair[4];  // per wave: the batch's surviving entries, compacted
+#else
   __shared__ uint32_t sTouch[4][kFwdBatch];  // per wave: n_touched increments of the batch's entries
+#endif
   const uint32_t slot = xcd_remap(blockIdx.x, (uint32_t)ntiles);
   const uint32_t tile = order ? order[slot] : slot;  // null: xcd_remap's order as it is
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -784,6 +900,46 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
   v2f c01{0.f, 0.f}, c2d{0.f, 0.f};  // (colour 0, colour 1), (colour 2, depth)
   uint32_t last = 0;
 
+#if WGSR_FWD_LDSPF
+  // prefetch pipeline (wave 0): batch b+1's records stream straight into the
+  // other LDS buffer (global_load_lds_dwordx4, no VGPRs held), ids of b+2 in
+  // registers; one barrier per batch
+  auto fetch = [&](uint32_t g, int buf) {
+    const float4* src = splat + 3 * (size_t)g;
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)&sA2[buf][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 1), (__attribute__((address_space(3))) void*)&sB2[buf][0], 16,
+                                     0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 2), (__attribute__((address_space(3))) void*)&sC2[buf][0], 16,
+                                     0, 0);
+  };
+  uint32_t gcur = 0, gnext = 0;
+  if (t < kFwdBatch) {
+    if (range.x + t < range.y) {
+      gcur = point_g[range.x + t];
+      fetch(gcur, 0);
+    }
+    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
+  }
+  int buf = 0;
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch, buf ^= 1) {
+    if (t < kFwdBatch) {
+      sG2[buf][t] = gcur;
+      __builtin_amdgcn_s_waitcnt(0);  // this batch's records have landed
+    }
+    // (also: every wave is done with the other buffer)
+    if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(dm)) == (int)blockDim.x) break;
+    if (t < kFwdBatch) {
+      gcur = gnext;
+      if (b0 + kFwdBatch + t < range.y) fetch(gcur, buf ^ 1);
+      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
+    }
+    if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
+    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+    const float4* sA = sA2[buf];
+    const float4* sB = sB2[buf];
+    const float4* sC = sC2[buf];
+    const uint32_t* sG = sG2[buf];
+#else
   // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
   uint32_t gcur = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
@@ -817,8 +973,14 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     }
     if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+#endif
+#if WGSR_FWD_EPAIR
+    fwd_blend_batch_pairs(cnt, b0 - range.x + 1, sA, sB, sC, sG, sPair[w], wx0, wx1, wy0, wy1, pxy, lane, n_touched, T,
+                          c01, c2d, last, dm);
+#else
     fwd_blend_batch<false>(cnt, b0 - range.x + 1, nullptr, sA, sB, sC, sG, sTouch[w], wx0, wx1, wy0, wy1, pxy, lane,
                            n_touched, T, c01, c2d, last, dm);
+#endif
   }
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
     uint32_t mx = last;

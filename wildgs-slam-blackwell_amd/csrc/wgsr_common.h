@@ -72,12 +72,47 @@ __device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
 #ifndef WGSR_SUM10_V2
 #define WGSR_SUM10_V2 1
 #endif
+// WGSR_SUM10_V3 (default): the 8- and 4-lane stages are transposed too, with
+// bank-masked DPP adds (a bank = 4 lanes of a row): 3 + 2 adds instead of
+// 3 x 2 row adds, then one quad butterfly on a single register, and each
+// sum leaves from its own lane by ONE store (23 VALU + 1 LDS store per call
+// instead of 28 + 3).  The stages' lane layouts:
+//   after the 16-lane swap: row r of S0 holds value m, of S1 value 4 + m,
+//   of S2 (even rows) value 8 + m, m = (r & 1) 2 + (r >> 1);
+//   8-lane stage: S0's lanes 0-7 of a row += lanes 8-15, lanes 8-15 take
+//   S1's lanes 0-7 + 8-15; S2's lanes 8-15 += lanes 0-7;
+//   4-lane stage: S0's banks 0, 2 += banks 1, 3; bank 3 takes S2's banks 2 + 3;
+//   quad butterfly: lanes 0-3 of row r end with value m, lanes 8-11 with
+//   4 + m, lanes 12-15 (even rows) with 8 + m.
+#ifndef WGSR_SUM10_V3
+#define WGSR_SUM10_V3 1
+#endif
+#if WGSR_SUM10_V3
+// value index whose sum this lane stores (-1: none)
+__device__ __forceinline__ int sum10_value(int lane) {
+  const int row = lane >> 4, pos = lane & 15, m = (row & 1) * 2 + (row >> 1);
+  if (pos == 0) return m;
+  if (pos == 8) return 4 + m;
+  if (pos == 12 && !(row & 1)) return 8 + m;
+  return -1;
+}
+// the lanes sum10_value names (a constant lane mask: no per-call compare)
+constexpr uint64_t kSum10StoreLanes = (1ull << 0) | (1ull << 8) | (1ull << 12) | (1ull << 16) | (1ull << 24) |
+                                      (1ull << 32) | (1ull << 40) | (1ull << 44) | (1ull << 48) | (1ull << 56);
+// the lane part of a store address (callers add it once; lanes that store
+// nothing get slot 0 and never write)
+__device__ __forceinline__ int sum10_slot(int lane) {
+  const int v = sum10_value(lane);
+  return v < 0 ? 0 : v;
+}
+#else
 // Lane 15 of row r holds, after wave_sum10, value m of S[0], 4 + m of S[1]
 // and (even rows only, where m = r / 2) 8 + m of S[2], m = sum10_slot(lane).
 __device__ __forceinline__ int sum10_slot(int lane) {
   const int row = lane >> 4;
   return (row & 1) * 2 + (row >> 1);
 }
+#endif
 __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) {
   float R[5];
   uint32_t R4b = 0u;
@@ -93,7 +128,7 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) 
     S[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v0 v2 v1 v3
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[2]), __float_as_uint(R[3]), false, false);
     S[1] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v4 v6 v5 v7
-#if WGSR_SUM10_V2
+#if WGSR_SUM10_V2 || WGSR_SUM10_V3
     // the partner register's rows only reach S[2]'s odd rows, which are never
     // stored: pass a dead register (no zero move)
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), R4b, false, false);
@@ -103,12 +138,27 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) 
     S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 0 v9 0
 #endif
   }
+#if WGSR_SUM10_V3
+  // bank-masked DPP adds write only the named banks; the rest of the tied
+  // destination keeps its value.  Each asm opens with the 2 wait states a DPP
+  // read of a just-written VGPR needs (the hazard check does not look inside
+  // inline asm).
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shl:8 row_mask:0xf bank_mask:0x3" : "+v"(S[0]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xc" : "+v"(S[0]) : "v"(S[1]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xc" : "+v"(S[2]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5" : "+v"(S[0]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa" : "+v"(S[0]) : "v"(S[2]));
+  S[0] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(S[0]), 0xB1, 0xf, 0xf, true));
+  S[0] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(S[0]), 0x4E, 0xf, 0xf, true));
+  asm volatile("" ::"v"(S[0]));
+#else
 #pragma unroll
   for (int i = 0; i < 3; ++i) S[i] = dpp_row_sum16(S[i]);
 #if WGSR_SUM10_V2
   // materialise the sums before the store branch, so the last DPP step folds
   // into one v_add_f32_dpp instead of a DPP move + an add inside the branch
   asm volatile("" ::"v"(S[0]), "v"(S[1]), "v"(S[2]));
+#endif
 #endif
 }
 // dstm = the entry's 10 floats + sum10_slot(lane): the lane part of the
@@ -117,11 +167,16 @@ __device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], float* 
   float S[3];
   wave_sum10(v, S);
   const int lane = __lane_id();
+#if WGSR_SUM10_V3
+  (void)lane;
+  if (__builtin_amdgcn_inverse_ballot_w64(kSum10StoreLanes)) dstm[0] = S[0];
+#else
   if ((lane & 15) == 15) {
     dstm[0] = S[0];
     dstm[4] = S[1];
     if (!((lane >> 4) & 1)) dstm[8] = S[2];
   }
+#endif
 }
 __device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
   wave_sum10_store_m(v, dst + sum10_slot(__lane_id()));
