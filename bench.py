@@ -104,16 +104,17 @@ def n_contrib_sum(img_buffer, W, H):
 
 
 def load_pmc(P, W, H, sh):
-    """The committed PMC summary (profiles/pmc_summary.json) if it was taken
-    on this workload, else None: counters are never quoted across configs."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        d = json.load(open(path))
-    except Exception:
-        return None
-    if d.get("config") != {"P": P, "W": W, "H": H, "sh": sh}:
-        return None
-    return d
+    """The committed PMC summary (profiles/pmc_summary*.json) taken on this
+    workload, else None: counters are never quoted across configs."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_summary*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("config") == {"P": P, "W": W, "H": H, "sh": sh}:
+            return d
+    return None
 
 
 def main():
@@ -367,12 +368,27 @@ def main():
                 issue[st] = {"valu_wave_insts_per_step": rec["valu_insts_per_step"],
                              "achieved_Ginst_s": rate / 1e9, "peak_Ginst_s": VALU_ISSUE_PEAK / 1e9,
                              "frac": rate / VALU_ISSUE_PEAK}
+        # VALU pipe occupancy measured by the counters (SQ_ACTIVE_INST_VALU
+        # quad-cycles incl. 8-cycle ops over SQ_BUSY_CYCLES: at the clock the
+        # kernel actually ran, tools/pmc_summary.py)
+        for st in ("render_fwd", "render_bwd"):
+            rec = pst.get(st)
+            if rec and rec.get("valu_busy_frac") is not None:
+                issue.setdefault(st, {})
+                issue[st]["valu_busy_frac_counters"] = rec["valu_busy_frac"]
+                issue[st]["clock_ghz_counters"] = rec.get("clock_ghz")
         if issue:
             out["render_valu_issue"] = issue
             if dom in issue:
-                out["roofline"]["valu_issue_frac"] = issue[dom]["frac"]
-                out["roofline"]["bound_note"] = (f"{dom} is VALU-issue bound: valu_issue_frac is its "
-                                                 "primary roofline, frac its HBM fraction")
+                if "frac" in issue[dom]:
+                    out["roofline"]["valu_issue_frac"] = issue[dom]["frac"]
+                if "valu_busy_frac_counters" in issue[dom]:
+                    out["roofline"]["valu_busy_frac"] = issue[dom]["valu_busy_frac_counters"]
+                    out["roofline"]["clock_ghz"] = issue[dom]["clock_ghz_counters"]
+                out["roofline"]["bound_note"] = (
+                    f"{dom} is VALU-issue bound: valu_busy_frac (the VALU pipe's busy share of the kernel's "
+                    "SQ clocks, PMC) is its primary roofline; valu_issue_frac = wave-instructions per second "
+                    "against 1 per 4 cycles per SIMD at 2.4 GHz; frac is its HBM fraction")
 
     if rank == 0 and world == 1 and not args.no_knn:
         # simple_knn.distCUDA2 over the scene's points

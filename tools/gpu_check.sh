@@ -18,9 +18,9 @@ for s in $STEPS; do
       timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1; rc=$?
       if [ $rc -ge 2 ] && [ $rc -le 5 ]; then rc=0; fi ;;  # pytest usage/collection codes are not GPU faults
     bench)
-      timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err; rc=$? ;;
+      timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench${SFX:-}.json 2> $OUT/bench${SFX:-}.err; rc=$? ;;
     prof)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-knn > $GRAFT_REPO_ROOT/$OUT/prof_bench.json 2> $GRAFT_REPO_ROOT/$OUT/prof.err); rc=$? ;;
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/prof_bench${SFX:-}.json 2> $GRAFT_REPO_ROOT/$OUT/prof${SFX:-}.err); rc=$? ;;
     f1)
       timeout -k 10 300 python tools/bench_f1.py > $OUT/bench_f1.json 2> $OUT/bench_f1.err; rc=$? ;;
     f2)
@@ -38,11 +38,14 @@ for s in $STEPS; do
     f1prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f1prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f1.py --iters 20 > $GRAFT_REPO_ROOT/$OUT/f1prof.json 2> $GRAFT_REPO_ROOT/$OUT/f1prof.err); rc=$? ;;
     pmc_fetch)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_fetch -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_fetch.err); rc=$? ;;
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_fetch${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_fetch${SFX:-}.err); rc=$? ;;
     pmc_write)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_write -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_write.err); rc=$? ;;
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_write${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_write${SFX:-}.err); rc=$? ;;
     pmc_sq)
-      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq.err); rc=$? ;;
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq${SFX:-}.err); rc=$? ;;
+    pmc_sq2)
+      # VALU pipe occupancy (SQ_ACTIVE_INST_VALU, quad-cycles incl. multi-cycle ops) and the SQ clock (SQ_BUSY_CYCLES per SE)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_INSTS_VALU_TRANS_F32 SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq2${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq2${SFX:-}.err); rc=$? ;;
     ab)
       # AB_LIBS="name ...": bench each lib/variants/<name>.so ("base" = lib/libwgsr.so), twice, interleaved
       rc=0

@@ -20,6 +20,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -770,6 +772,9 @@ __device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const u
 #ifndef WGSR_FWD_LDSPF
 #define WGSR_FWD_LDSPF 1
 #endif
+#if WGSR_FWD_LDSPF && !WGSR_FWD_EPAIR
+#error "WGSR_FWD_LDSPF needs WGSR_FWD_EPAIR"
+#endif
 struct FwdPairRec {   // two consecutive survivors (one LDS address per pair)
   float4 q[3];       // {x, x', y, y'}, {A.z, A.z', A.w, A.w'}, {B.x, B.x', o, o'}
   float4 c[2];       // colour (c0, c1, c2, depth) of each
@@ -823,12 +828,17 @@ __device__ __forceinline__ void fwd_blend_pairs(int n, const FwdPairLds& L, uint
 
 // cull the staged batch against the wave's pixel box, compact the survivors
 // into L, blend them front to back in pairs, flush n_touched
+// after(): called once the survivors are compacted (the LDS-DMA of the next
+// batch is queued there, behind every LDS write of this batch)
+template <class F>
 __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, const float4* sA, const float4* sB,
                                                       const float4* sC, const uint32_t* sG, FwdPairLds& L, int wx0,
                                                       int wx1, int wy0, int wy1, v2f pxy, int lane,
                                                       int32_t* __restrict__ n_touched, float& T, v2f& c01, v2f& c2d,
-                                                      uint32_t& last, uint64_t& dm) {
-  const float4 A = sA[lane], B = sB[lane];
+                                                      uint32_t& last, uint64_t& dm, uint32_t* fl_gid,
+                                                      uint32_t* fl_tv, const float4* pre, uint32_t pre_gid, F after) {
+  // (pre: this lane's records, read by the caller before it queued an LDS DMA)
+  const float4 A = pre ? pre[0] : sA[lane], B = pre ? pre[1] : sB[lane];
   const bool mine = lane < cnt && ellipse_hits(A, B, wx0, wx1, wy0, wy1);
   const uint64_t todo = wave_ballot(mine);
   const int n = __popcll(todo);
@@ -838,7 +848,7 @@ __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, c
     FwdPairRec& R = L.p[k >> 1];
     float* q = &R.q[0].x + (k & 1);
     q[0] = A.x; q[2] = A.y; q[4] = A.z; q[6] = A.w; q[8] = B.x; q[10] = B.y;
-    R.c[k & 1] = sC[lane];
+    R.c[k & 1] = pre ? pre[2] : sC[lane];
     R.n[k & 1] = cbase + (uint32_t)lane;
   }
   if (touch) L.touch[lane] = 0;
@@ -849,10 +859,16 @@ __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, c
     R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // (a wave's own LDS writes are visible to its later reads: no barrier)
+  after();
   if (touch) {
     fwd_blend_pairs<true>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
     const uint32_t tv = mine ? L.touch[k] : 0u;
-    if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
+    if (fl_tv) {  // the caller issues the atomic later
+      *fl_gid = pre_gid;
+      *fl_tv = tv;
+    } else if (tv != 0) {
+      atomicAdd(&n_touched[sG[lane]], (int)tv);
+    }
   } else {
     fwd_blend_pairs<false>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
   }
@@ -871,8 +887,12 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ tile_m4) {
 #if WGSR_FWD_LDSPF
-  __shared__ float4 sA2[2][kFwdBatch], sB2[2][kFwdBatch], sC2[2][kFwdBatch];
-  __shared__ uint32_t sG2[2][kFwdBatch];
+  // two batch buffers as separate objects, so that the compiler can tell the
+  // LDS-DMA into one from the reads of the other (no vmcnt wait before them)
+  __shared__ float4 sA_0[kFwdBatch], sB_0[kFwdBatch], sC_0[kFwdBatch];
+  __shared__ float4 sA_1[kFwdBatch], sB_1[kFwdBatch], sC_1[kFwdBatch];
+  __shared__ uint32_t sG_0[kFwdBatch], sG_1[kFwdBatch];
+  __shared__ uint32_t sDone[2][4];  // per batch parity: wave w has no pixel left
 #else
   __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
   __shared__ uint32_t sG[kFwdBatch];
@@ -903,42 +923,78 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
 #if WGSR_FWD_LDSPF
   // prefetch pipeline (wave 0): batch b+1's records stream straight into the
   // other LDS buffer (global_load_lds_dwordx4, no VGPRs held), ids of b+2 in
-  // registers; one barrier per batch
-  auto fetch = [&](uint32_t g, int buf) {
+  // registers.  ONE barrier per batch, which waits for LDS only: wave 0's
+  // vmcnt wait before it finds every load a batch old, and the n_touched
+  // atomics of a batch are issued right after the next batch's barrier, so
+  // no wave ever waits for an atomic.  Loads past the list re-read its last
+  // entry (valid; culled by lane < cnt), so they need no branch.
+  const uint32_t last_i = range.y > range.x ? range.y - 1 : range.x;
+  auto fetch = [&](uint32_t g, float4* dA, float4* dB, float4* dC) {
     const float4* src = splat + 3 * (size_t)g;
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)&sA2[buf][0], 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + 1), (__attribute__((address_space(3))) void*)&sB2[buf][0], 16,
-                                     0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + 2), (__attribute__((address_space(3))) void*)&sC2[buf][0], 16,
-                                     0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dA, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 1), (__attribute__((address_space(3))) void*)dB, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 2), (__attribute__((address_space(3))) void*)dC, 16, 0, 0);
   };
   uint32_t gcur = 0, gnext = 0;
-  if (t < kFwdBatch) {
-    if (range.x + t < range.y) {
-      gcur = point_g[range.x + t];
-      fetch(gcur, 0);
-    }
-    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
+  if (w == 0 && range.x < range.y) {
+    gcur = point_g[min(range.x + t, last_i)];
+    fetch(gcur, sA_0, sB_0, sC_0);
+    if (range.x + kFwdBatch < range.y) gnext = point_g[min(range.x + kFwdBatch + t, last_i)];
   }
-  int buf = 0;
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch, buf ^= 1) {
-    if (t < kFwdBatch) {
-      sG2[buf][t] = gcur;
+  uint32_t fl_gid = 0, fl_tv = 0;  // this lane's n_touched increment of the previous batch
+  // one batch: read buffer (cA..cG), DMA target (nA..nC) as restrict
+  // parameters, so that the compiler's LDS-DMA wait tracking sees that the
+  // reads cannot alias the DMA in flight
+  auto body = [&](uint32_t b0, uint32_t* __restrict__ done, float4* __restrict__ cA, float4* __restrict__ cB,
+                  float4* __restrict__ cC, uint32_t* __restrict__ cG, float4* __restrict__ nA_,
+                  float4* __restrict__ nB_, float4* __restrict__ nC_) -> bool {
+    if (w == 0) {
+      cG[t] = gcur;
       __builtin_amdgcn_s_waitcnt(0);  // this batch's records have landed
     }
-    // (also: every wave is done with the other buffer)
-    if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(dm)) == (int)blockDim.x) break;
-    if (t < kFwdBatch) {
-      gcur = gnext;
-      if (b0 + kFwdBatch + t < range.y) fetch(gcur, buf ^ 1);
-      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
+    if (lane == 0) done[w] = dm == ~0ull ? 1u : 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (every wave is done with the other buffer)
+    const uint4 dn = *reinterpret_cast<const uint4*>(done);
+    // this lane's entry, read before the DMA is queued: the compiler would
+    // otherwise wait for the DMA before reading the other buffer
+    const float4 pre[3] = {cA[lane], cB[lane], cC[lane]};
+    const uint32_t gme = cG[lane];
+    // wave 0 queues the next batch's DMA after this batch's LDS writes (the
+    // compiler orders LDS writes behind a DMA in flight), its id loads, then
+    // the previous batch's n_touched atomics (a wait the compiler places for
+    // the loads then never covers an atomic)
+    bool queued = false;
+    auto queue_next = [&]() {
+      if (queued) return;
+      queued = true;
+      if (w == 0 && b0 + kFwdBatch < range.y) {
+        gcur = gnext;
+        fetch(gcur, nA_, nB_, nC_);
+        if (b0 + 2 * kFwdBatch < range.y) gnext = point_g[min(b0 + 2 * kFwdBatch + t, last_i)];
+      }
+      if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
+      fl_tv = 0;
+    };
+    if (dn.x & dn.y & dn.z & dn.w) return false;
+    if (dm != ~0ull) {
+      const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+      fwd_blend_batch_pairs(cnt, b0 - range.x + 1, cA, cB, cC, cG, sPair[w], wx0, wx1, wy0, wy1, pxy, lane, n_touched,
+                            T, c01, c2d, last, dm, &fl_gid, &fl_tv, pre, gme, queue_next);
     }
-    if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
-    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-    const float4* sA = sA2[buf];
-    const float4* sB = sB2[buf];
-    const float4* sC = sC2[buf];
-    const uint32_t* sG = sG2[buf];
+    queue_next();  // (a finished wave: keeps the barriers and the pipeline)
+    return true;
+  };
+  auto step = [&](auto par, uint32_t b0) -> bool {
+    if constexpr (decltype(par)::value == 0)
+      return body(b0, sDone[0], sA_0, sB_0, sC_0, sG_0, sA_1, sB_1, sC_1);
+    else
+      return body(b0, sDone[1], sA_1, sB_1, sC_1, sG_1, sA_0, sB_0, sC_0);
+  };
+  for (uint32_t b0 = range.x; b0 < range.y; b0 += 2 * kFwdBatch) {
+    if (!step(std::integral_constant<int, 0>{}, b0)) break;
+    if (b0 + kFwdBatch >= range.y || !step(std::integral_constant<int, 1>{}, b0 + kFwdBatch)) break;
+  }
+  if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
 #else
   // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
   uint32_t gcur = 0, gnext = 0;
@@ -973,15 +1029,15 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     }
     if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
     const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-#endif
 #if WGSR_FWD_EPAIR
     fwd_blend_batch_pairs(cnt, b0 - range.x + 1, sA, sB, sC, sG, sPair[w], wx0, wx1, wy0, wy1, pxy, lane, n_touched, T,
-                          c01, c2d, last, dm);
+                          c01, c2d, last, dm, nullptr, nullptr, nullptr, 0u, [] {});
 #else
     fwd_blend_batch<false>(cnt, b0 - range.x + 1, nullptr, sA, sB, sC, sG, sTouch[w], wx0, wx1, wy0, wy1, pxy, lane,
                            n_touched, T, c01, c2d, last, dm);
 #endif
   }
+#endif
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
     uint32_t mx = last;
 #pragma unroll
