@@ -557,6 +557,9 @@ size_t wgsr_image_bytes(int W, int H);
  * accumulated milliseconds and launch counts per stage (returns the number
  * of stages).  Not thread-safe; meant for benchmarks. */
 #define WGSR_NUM_STAGES 10
+/* on = 0: off; 1: every stage; (mask << 1) for mask != 0: only the stages
+ * whose bit is set (bit i = stage i), e.g. (1 << 7) << 1 times render_bwd
+ * alone -- each timed stage adds two event records to the stream. */
 void wgsr_profile_enable(int on);
 int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset);
 const char* wgsr_profile_stage_name(int i);

@@ -106,7 +106,7 @@ const char* const kStageNames[WGSR_NUM_STAGES] = {"preprocess", "depth_sort", "o
                                                   "tile_sort", "ranges", "render_fwd", "render_bwd",
                                                   "gauss_bwd", "dist_cuda2"};
 struct Prof {
-  bool on = false;
+  uint32_t mask = 0;  // stages timed (bit i: stage i)
   struct Rec { int stage; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -138,7 +138,7 @@ struct StageTimer {
   hipStream_t s;
   hipEvent_t a = nullptr;
   StageTimer(int st, hipStream_t str) : stage(st), s(str) {
-    if (g_prof.on && (a = g_prof.get()) && hipEventRecord(a, s) != hipSuccess) a = nullptr;
+    if (((g_prof.mask >> st) & 1u) && (a = g_prof.get()) && hipEventRecord(a, s) != hipSuccess) a = nullptr;
   }
   ~StageTimer() {
     if (!a) return;
@@ -227,7 +227,9 @@ const char* wgsr_last_error(void) { return g_err; }
 
 void wgsr_profile_enable(int on) {
   g_prof.flush();
-  g_prof.on = on != 0;
+  // 1: every stage (each timed stage adds two event records to the stream);
+  // otherwise on is the mask of stages to time, as (mask << 1) | 0 ... see wgsr.h
+  g_prof.mask = on == 1 ? ((1u << WGSR_NUM_STAGES) - 1u) : (on > 1 ? ((uint32_t)on >> 1) : 0u);
 }
 
 int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset) {

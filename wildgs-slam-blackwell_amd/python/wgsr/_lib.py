@@ -264,12 +264,26 @@ VIEW_CAMERA_FLOATS = 64   # WGSR_VIEW_CAMERA_FLOATS
 
 
 class StageProfile:
-    """Per-stage device time (HIP events on the launch stream) inside a block."""
+    """Per-stage device time (HIP events on the launch stream) inside a block.
+
+    stages: names of the stages to time (None: all).  Each timed stage adds
+    two event records per launch to the stream, which the GPU serialises, so
+    a timed loop should time only what it reports."""
+
+    def __init__(self, stages=None):
+        self.only = stages
 
     def __enter__(self):
         L = load()
         L.wgsr_profile_read(None, None, 0, 1)
-        L.wgsr_profile_enable(1)
+        if self.only is None:
+            L.wgsr_profile_enable(1)
+        else:
+            names = [L.wgsr_profile_stage_name(i).decode() for i in range(16)]
+            mask = 0
+            for st in self.only:
+                mask |= 1 << names.index(st)
+            L.wgsr_profile_enable(mask << 1)
         return self
 
     def __exit__(self, *exc):
