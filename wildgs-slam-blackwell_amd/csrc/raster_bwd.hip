@@ -648,6 +648,125 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
 }
 
+// Entry pairs in the four-wave backward (WGSR_BWD_SPLIT_EPAIR, the default):
+// a wave owns one 8x8 quadrant, so the batch's entries that reach it are
+// compacted (two consecutive survivors interleaved per field, as the
+// forward's FwdPairRec) and walked in pairs: both entries' power, alpha,
+// 1 / (1 - alpha), colour dot products and gradient terms in packed-FP32
+// math, only the T / accumulated-colour recurrence per entry, and the two
+// entries' 10 sums reduced together (wave_sum20: two independent chains in
+// flight, 42 instead of 46 VALU).  A pixel an entry does not reach runs it
+// with alpha = 0 and G = 0 (pass-through, zero sums).  The background enters
+// as the accumulated colour's starting value (render_bwd_pair_tile).
+#ifndef WGSR_BWD_SPLIT_EPAIR
+#define WGSR_BWD_SPLIT_EPAIR 1
+#endif
+struct BwdPairRec {
+  float4 q[3];   // {x, x', y, y'}, {A.z, A.z', A.w, A.w'}, {B.x, B.x', o, o'}
+  float4 c[2];   // {c0, c0', c1, c1'}, {c2, c2', depth, depth'}
+  uint32_t j[2]; // batch slots
+  uint32_t pad[2];
+};
+
+__device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cfirst, const float4* sA, const float4* sB,
+                                                      const float4* sC, BwdPairRec* R, float (*sPw)[11], v2f p0,
+                                                      uint32_t last, const v2f& dp01, const v2f& dp2d, float& T,
+                                                      float& accd, int lane) {
+  const int n = __popcll(todo);
+  const uint32_t k = lanes_below(todo);
+  if ((todo >> lane) & 1) {
+    const float4 A = sA[lane], B = sB[lane], C = sC[lane];
+    BwdPairRec& r = R[k >> 1];
+    float* q = &r.q[0].x + (k & 1);
+    q[0] = A.x; q[2] = A.y; q[4] = A.z; q[6] = A.w; q[8] = B.x; q[10] = B.y;
+    float* c = &r.c[0].x + (k & 1);
+    c[0] = C.x; c[2] = C.y; c[4] = C.z; c[6] = C.w;
+    r.j[k & 1] = (uint32_t)lane;
+  }
+  if (lane == 63 && (n & 1)) {  // the unused half of an odd last pair: finite operands
+    BwdPairRec& r = R[n >> 1];
+    float* q = &r.q[0].x + 1;
+    q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
+    float* c = &r.c[0].x + 1;
+    c[0] = 0.f; c[2] = 0.f; c[4] = 0.f; c[6] = 0.f;
+    r.j[1] = 0u;
+  }
+  // per-lane targets of the two-entry sums (constants of the lane)
+  const int yv = sum20_y_value(lane), zv = sum20_z_value(lane);
+  const int yk = yv >> 1, ye = yv & 1, zk = zv >> 1, ze = zv & 1;
+  const v2f px{p0.x, p0.x}, py{p0.y, p0.y};
+  uint64_t hits = 0;
+  for (int i = 0; i < n; i += 2) {
+    const BwdPairRec& r = R[i >> 1];
+    const float4 q0 = r.q[0], q1 = r.q[1], q2 = r.q[2], c0 = r.c[0], c1 = r.c[1];
+    const uint2 jj = *reinterpret_cast<const uint2*>(&r.j[0]);
+    const v2f DX = v2f{q0.x, q0.y} - px, DY = v2f{q0.z, q0.w} - py;
+    // splat_power per lane: fma(dx, fma(B.x, dy, A.z dx), (A.w dy) dy)
+    const v2f tz = v2f{q1.x, q1.y} * DX, tw = v2f{q1.z, q1.w} * DY;
+    const v2f PW = pfma(DX, pfma(v2f{q2.x, q2.y}, DY, tz), tw * DY);
+    const v2f G = v2f{__builtin_amdgcn_exp2f(PW.x), __builtin_amdgcn_exp2f(PW.y)};
+    const v2f ag = v2f{q2.z, q2.w} * G;
+    const v2f av{fminf(kMaxAlpha, ag.x), fminf(kMaxAlpha, ag.y)};
+    const uint32_t ci1 = cfirst - jj.x, ci2 = cfirst - jj.y;
+    const uint64_t m1 = wave_ballot(ci1 < last) & wave_ballot(PW.x <= 0.0f) & wave_ballot(av.x >= kMinAlpha);
+    const uint64_t m2 = (i + 1 < n) ? (wave_ballot(ci2 < last) & wave_ballot(PW.y <= 0.0f) &
+                                       wave_ballot(av.y >= kMinAlpha))
+                                    : 0ull;
+    if ((m1 | m2) == 0) continue;
+    const bool v1 = __builtin_amdgcn_inverse_ballot_w64(m1), v2 = __builtin_amdgcn_inverse_ballot_w64(m2);
+    const v2f a{v1 ? av.x : 0.f, v2 ? av.y : 0.f};
+    const v2f Ge{v1 ? G.x : 0.f, v2 ? G.y : 0.f};
+    const v2f om = v2f{1.f, 1.f} - a;
+    const float r1 = __builtin_amdgcn_rcpf(om.x), r2 = __builtin_amdgcn_rcpf(om.y);  // alpha <= 0.99
+    const float Tn1 = T * r1, Tn2 = Tn1 * r2;
+    T = Tn2;
+    const v2f Tn{Tn1, Tn2};
+    const v2f dch = a * Tn;
+    // c . dL/d(colour, depth) of both entries
+    const v2f cp = pfma(v2f{c1.z, c1.w}, v2f{dp2d.y, dp2d.y},
+                        pfma(v2f{c1.x, c1.y}, v2f{dp2d.x, dp2d.x},
+                             pfma(v2f{c0.z, c0.w}, v2f{dp01.y, dp01.y}, v2f{c0.x, c0.y} * v2f{dp01.x, dp01.x})));
+    const float sd1 = cp.x - accd;
+    accd = fmaf(a.x, sd1, accd);
+    const float sd2 = cp.y - accd;
+    accd = fmaf(a.y, sd2, accd);
+    const v2f gl = Ge * (v2f{sd1, sd2} * Tn);  // dL/dG / opacity of each entry
+    v2f S[10];
+    S[0] = gl * DX;
+    S[1] = gl * DY;
+    S[2] = S[0] * DX;
+    S[3] = S[0] * DY;
+    S[4] = S[1] * DY;
+    S[5] = gl;
+    S[6] = dch * v2f{dp01.x, dp01.x};
+    S[7] = dch * v2f{dp01.y, dp01.y};
+    S[8] = dch * v2f{dp2d.x, dp2d.x};
+    S[9] = dch * v2f{dp2d.y, dp2d.y};
+    if (m1 && m2) {
+      float Y, Z;
+      wave_sum20(S, Y, Z);
+      float* const rowy = &sPw[ye ? jj.y : jj.x][0];
+      float* const rowz = &sPw[ze ? jj.y : jj.x][0];
+      if (__builtin_amdgcn_inverse_ballot_w64(kSum20StoreY)) rowy[yk] = Y;
+      if (__builtin_amdgcn_inverse_ballot_w64(kSum20StoreZ)) rowz[zk] = Z;
+      hits |= (1ull << jj.x) | (1ull << jj.y);
+    } else if (m1) {
+      float gv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) gv[q] = S[q].x;
+      wave_sum10_store(gv, &sPw[jj.x][0]);
+      hits |= 1ull << jj.x;
+    } else {
+      float gv[10];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) gv[q] = S[q].y;
+      wave_sum10_store(gv, &sPw[jj.y][0]);
+      hits |= 1ull << jj.y;
+    }
+  }
+  return hits;
+}
+
 // Small images (few tiles: TUM's 512x384 has 768) leave most SIMDs without a
 // wave under k_render_bwd_quad, and each tile's serial walk sets the time.
 // This variant gives a tile FOUR waves, one per 8x8 quadrant: wave 0 stages
@@ -668,6 +787,9 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
   __shared__ float sP[4][kBatch][11];
   __shared__ uint64_t sHitW[4];
   __shared__ uint32_t sEnd[4];
+#if WGSR_BWD_SPLIT_EPAIR
+  __shared__ BwdPairRec sPairs[4][kBatch / 2];
+#endif
   // where the forward left the tile lists (ImageLayout::meta)
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
@@ -687,9 +809,15 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
   const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
   const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
   const v2f dp01{d0, d1}, dp2d{d2, dd};
+#if WGSR_BWD_SPLIT_EPAIR
+  // the background as the colour behind the last contributor (see render_bwd_pair_tile)
+  float accd = bg0 * d0 + bg1 * d1 + bg2 * d2;
+  (void)Tf;
+#else
   const float tb = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);
-  float T = Tf;
   float accd = 0.f;  // accum_rec . dL/d(colour, depth), as k_render_bwd_quad
+#endif
+  float T = Tf;
   uint32_t x = last;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
@@ -732,6 +860,10 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
     const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
     uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < mq &&
                                 ellipse_hits(sA[lane], sB[lane], qx0, qx0 + 7, qy0, qy0 + 7));
+#if WGSR_BWD_SPLIT_EPAIR
+    const uint64_t hits = split_batch_pairs(todo, cfirst, sA, sB, sC, sPairs[w], sP[w], p0, last, dp01, dp2d, T,
+                                            accd, lane);
+#else
     uint64_t hits = 0;
     while (todo) {
       const int j = __builtin_ctzll(todo);
@@ -766,6 +898,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       wave_sum10_store(gv, &sP[w][j][0]);
       hits |= 1ull << j;
     }
+#endif
     if (lane == 0) sHitW[w] = hits;
     __syncthreads();
     if (w == 0 && lane < cnt) {

@@ -25,6 +25,8 @@ constexpr float kConicSq = -0.5f * kL2E;  // A.z = kConicSq conic_xx, A.w = kCon
 constexpr float kConicXY = -kL2E;         // B.x = kConicXY conic_xy
 constexpr float kUnConicSq = -2.0f / kL2E, kUnConicXY = -1.0f / kL2E;
 
+typedef float v2f __attribute__((ext_vector_type(2)));  // packed-FP32 pair (v_pk_*)
+
 // ---------------------------------------------------------------------------
 // Wave-level primitives (wave64)
 // ---------------------------------------------------------------------------
@@ -181,6 +183,57 @@ __device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], float* 
 __device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
   wave_sum10_store_m(v, dst + sum10_slot(__lane_id()));
 }
+
+// Wave-wide sums of TWO entries' 10 per-lane values (pair k = (entry 0's
+// value k, entry 1's value k) in one v2f), transposed through every stage
+// (32- and 16-lane swaps, bank-masked 8- and 4-lane DPP adds, one quad
+// butterfly on two registers): 42 VALU instead of 2 x 23.  Value index
+// v = 2k + e ends in (lane-quad) positions: register Y, row r, bank b holds
+// v = m + 4 (b >> 1) + 8 (b & 1); register Z, bank 3 of row r holds 16 + m;
+// m = (r & 1) 2 + (r >> 1) (derived and checked by a lane-level simulation of
+// these instructions; tests/test_gpu_raster.py checks the sums).
+__device__ __forceinline__ void wave_sum20(const v2f (&S)[10], float& Y, float& Z) {
+  float R[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(S[k].x), __float_as_uint(S[k].y), false, false);
+    R[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  float Q[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[2 * m]), __float_as_uint(R[2 * m + 1]), false, false);
+    Q[m] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  // 8-lane stage: pairs (Q0, Q1), (Q2, Q3); Q4 alone (lanes 8-15 of each row)
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shl:8 row_mask:0xf bank_mask:0x3" : "+v"(Q[0]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xc" : "+v"(Q[0]) : "v"(Q[1]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shl:8 row_mask:0xf bank_mask:0x3" : "+v"(Q[2]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xc" : "+v"(Q[2]) : "v"(Q[3]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xc" : "+v"(Q[4]));
+  // 4-lane stage: pair (Q0, Q2); Q4 bank 3 += bank 2
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shl:4 row_mask:0xf bank_mask:0x5" : "+v"(Q[0]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa" : "+v"(Q[0]) : "v"(Q[2]));
+  asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0x8" : "+v"(Q[4]));
+  Y = Q[0] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(Q[0]), 0xB1, 0xf, 0xf, true));
+  Y += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(Y), 0x4E, 0xf, 0xf, true));
+  Z = Q[4] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(Q[4]), 0xB1, 0xf, 0xf, true));
+  Z += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(Z), 0x4E, 0xf, 0xf, true));
+  asm volatile("" ::"v"(Y), "v"(Z));
+}
+// per lane: the value index wave_sum20 leaves in Y (all lanes) and in Z
+// (lanes of bank 3; -1 elsewhere)
+__device__ __forceinline__ int sum20_y_value(int lane) {
+  const int r = lane >> 4, b = (lane >> 2) & 3, m = (r & 1) * 2 + (r >> 1);
+  return m + 4 * (b >> 1) + 8 * (b & 1);
+}
+__device__ __forceinline__ int sum20_z_value(int lane) {
+  const int r = lane >> 4, b = (lane >> 2) & 3, m = (r & 1) * 2 + (r >> 1);
+  return b == 3 ? 16 + m : -1;
+}
+// one storing lane per quad (position 0) for Y, per row (bank 3, position 0) for Z
+constexpr uint64_t kSum20StoreY = 0x1111111111111111ull;
+constexpr uint64_t kSum20StoreZ = (1ull << 12) | (1ull << 28) | (1ull << 44) | (1ull << 60);
 
 // inclusive prefix sum across the wave
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
