@@ -632,58 +632,30 @@ size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words
   return 256 * (size_t)((nb + kSupBlocks - 1) / kSupBlocks) * ((bits + 7) / 8);
 }
 
-hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
-                            size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
-                            hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done,
-                            bool sup_zeroed) {
-  *result_in_alt = false;
-  if (bounds_done) *bounds_done = false;
-  if (n == 0 || end_bit <= begin_bit) {
-    if (vals_iota && n > 0) {
-      // a zero-pass sort still has to materialise the identity permutation
-      return hipErrorInvalidValue;
-    }
-    return hipSuccess;
-  }
+// one sort with I keys per thread (workgroup tile 256 I)
+template <int I>
+static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt,
+                                   bool vals_iota, size_t n, int begin_bit, int end_bit, uint32_t* status,
+                                   uint32_t* totals, hipStream_t stream, bool* result_in_alt, uint2* digit_bounds,
+                                   bool* bounds_done, bool sup_zeroed) {
+  const uint32_t nb = sort_blocks(n);
   if (wide_pass(end_bit - begin_bit) && n <= (size_t)kStCount) {
     const int bits = end_bit - begin_bit;
-    const uint32_t nb = sort_blocks(n);
-    const bool small = sort_items(n) == kSmallSortItems;
     // status doubles as the [DIG][nb] per-block histogram (DIG <= 1024 <= 256 x kMaxSortPasses rows)
     if (bits <= 9) {
-      if (small) {
-        hipLaunchKernelGGL((k_radix_hist_wide<512, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys,
-                           (uint32_t)n, begin_bit, bits, nb, status);
-      } else {
-        hipLaunchKernelGGL((k_radix_hist_wide<512, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
-                           begin_bit, bits, nb, status);
-      }
+      hipLaunchKernelGGL((k_radix_hist_wide<512, I>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
+                         bits, nb, status);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(512), dim3(256), 0, stream, status, nb, totals);
-      if (small)
-        hipLaunchKernelGGL((k_radix_scatter_wide<512, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                           begin_bit == 0 ? digit_bounds : nullptr);
-      else
-        hipLaunchKernelGGL((k_radix_scatter_wide<512, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                           begin_bit == 0 ? digit_bounds : nullptr);
+      hipLaunchKernelGGL((k_radix_scatter_wide<512, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                         vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                         begin_bit == 0 ? digit_bounds : nullptr);
     } else {
-      if (small) {
-        hipLaunchKernelGGL((k_radix_hist_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys,
-                           (uint32_t)n, begin_bit, bits, nb, status);
-      } else {
-        hipLaunchKernelGGL((k_radix_hist_wide<1024, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
-                           begin_bit, bits, nb, status);
-      }
+      hipLaunchKernelGGL((k_radix_hist_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
+                         bits, nb, status);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(1024), dim3(256), 0, stream, status, nb, totals);
-      if (small)
-        hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                           begin_bit == 0 ? digit_bounds : nullptr);
-      else
-        hipLaunchKernelGGL((k_radix_scatter_wide<1024, kSortItems>), dim3(nb), dim3(256), 0, stream, keys, vals,
-                           vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                           begin_bit == 0 ? digit_bounds : nullptr);
+      hipLaunchKernelGGL((k_radix_scatter_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
+                         vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
+                         begin_bit == 0 ? digit_bounds : nullptr);
     }
     *result_in_alt = true;
     if (bounds_done) *bounds_done = digit_bounds && begin_bit == 0;
@@ -691,21 +663,15 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
   }
   const int passes = (end_bit - begin_bit + 7) / 8;
   if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;
-  const uint32_t nb = sort_blocks(n);
-  const bool small = sort_items(n) == kSmallSortItems;
-  const bool onesweep = sort_mode() == 1 || (sort_mode() == 2 && small);
+  const bool onesweep = sort_mode() == 1 || (sort_mode() == 2 && n <= kSmallSortN);
   uint32_t* ghist = totals;                          // onesweep: [passes][256]; rts: digit totals
   uint32_t* vcount = totals + kMaxSortPasses * 256;  // onesweep: virtual block counters [passes]
   if (onesweep) {
     hipError_t e = hipMemsetAsync(totals, 0, kSortTotalsBytes, stream);
     if (e == hipSuccess) e = hipMemsetAsync(status, 0, 4 * 256 * (size_t)nb * passes, stream);
     if (e != hipSuccess) return e;
-    if (small)
-      hipLaunchKernelGGL(k_onesweep_hist<kSmallSortItems>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n,
-                         begin_bit, end_bit, ghist);
-    else
-      hipLaunchKernelGGL(k_onesweep_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
-                         end_bit, ghist);
+    hipLaunchKernelGGL(k_onesweep_hist<I>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit, end_bit,
+                       ghist);
   }
   // superblock mode (default for reduce-then-scan; WGSR_SORT_SUP=0 keeps the
   // row-scan kernel): one memset of every pass's superblock sums replaces a
@@ -728,33 +694,18 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     const int shift = begin_bit + per * p;
     const int bits = min(per, end_bit - shift);
     if (onesweep) {
-      if (small)
-        hipLaunchKernelGGL((k_radix_scatter<true, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
-                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                           status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
-      else
-        hipLaunchKernelGGL((k_radix_scatter<true, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                           (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                           status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
+      hipLaunchKernelGGL((k_radix_scatter<true, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
+                         (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
+                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
     } else {
       // status doubles as the [256][nb] per-block histogram (and, in
       // superblock mode, holds the passes' [256][nsup] superblock sums after it)
       uint32_t* sp = sup ? sup + (size_t)p * 256 * nsup : nullptr;
-      if (small)
-        hipLaunchKernelGGL(k_radix_hist<kSmallSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift,
-                           bits, nb, status, sp, nsup);
-      else
-        hipLaunchKernelGGL(k_radix_hist<kSortItems>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits,
-                           nb, status, sp, nsup);
+      hipLaunchKernelGGL(k_radix_hist<I>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status,
+                         sp, nsup);
       if (!sp) hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
-      if (small)
-        hipLaunchKernelGGL((k_radix_scatter<false, kSmallSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
-                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp,
-                           nsup);
-      else
-        hipLaunchKernelGGL((k_radix_scatter<false, kSortItems>), dim3(nb), dim3(256), 0, stream, ki, vi,
-                           iota ? 1 : 0, (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp,
-                           nsup);
+      hipLaunchKernelGGL((k_radix_scatter<false, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
+                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup);
     }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
@@ -762,6 +713,33 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     *result_in_alt = !*result_in_alt;
   }
   return hipGetLastError();
+}
+
+hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
+                            size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
+                            hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done,
+                            bool sup_zeroed) {
+  *result_in_alt = false;
+  if (bounds_done) *bounds_done = false;
+  if (n == 0 || end_bit <= begin_bit) {
+    if (vals_iota && n > 0) {
+      // a zero-pass sort still has to materialise the identity permutation
+      return hipErrorInvalidValue;
+    }
+    return hipSuccess;
+  }
+  switch (sort_items(n)) {
+    case kTinySortItems:
+      return radix_sort_tiled<kTinySortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
+                                              totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed);
+    case kSmallSortItems:
+      return radix_sort_tiled<kSmallSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit,
+                                               status, totals, stream, result_in_alt, digit_bounds, bounds_done,
+                                               sup_zeroed);
+    default:
+      return radix_sort_tiled<kSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
+                                          totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed);
+  }
 }
 
 hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
