@@ -32,7 +32,7 @@ for s in $STEPS; do
     f3prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/f3prof -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_f3.py > $GRAFT_REPO_ROOT/$OUT/f3prof.json 2> $GRAFT_REPO_ROOT/$OUT/f3prof.err); rc=$? ;;
     trace)
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/trace -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-profile --no-knn > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/trace.err); rc=$? ;;
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $GRAFT_REPO_ROOT/$OUT/trace${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/trace${SFX:-}.err); rc=$? ;;
     listpmc)
       (cd /tmp && timeout -k 10 120 rocprofv3 -L > $GRAFT_REPO_ROOT/$OUT/pmc_list.txt 2>&1); rc=$? ;;
     f1prof)
