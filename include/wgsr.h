@@ -379,6 +379,18 @@ int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float
                       const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
                       float* scratch, float* grad, void* stream);
 
+/* DINO feature-similarity regulariser: compute_dino_regularization_loss
+ * (src/utils/dyn_uncertainty/mapping_utils.py:332-389, replaces its
+ * normalize / N x N matmul / topk / gathers on the mapper's uncertainty
+ * branch, mapper.py:986-997, 1122-1140).  u [N] uncertainty samples, feat
+ * [N, C] features (row-major).  Writes loss[0] = mean_i var_i over the
+ * min(top_k, N) most similar samples with cosine similarity > thresh, and
+ * grad_u [N] = d loss / d u (zeroed by the call; float atomics, so the
+ * order of its adds is not fixed).  Scratch: fn [N, C], sim [N, N], row_var
+ * [N].  N <= 16384, thresh > 0. */
+int wgsr_dino_reg(const float* u, const float* feat, int N, int C, int top_k, float thresh, float eps,
+                  float* fn_scratch, float* sim_scratch, float* row_var, float* grad_u, float* loss, void* stream);
+
 /* One view's densification bookkeeping (mapper.py:1177-1183,
  * gaussian_model.py:745-749) for Gaussians with radii > 0:
  * max_radii2D = max(max_radii2D, radii); grad_accum += ||dL_dmeans2D[:2]||;

@@ -192,6 +192,9 @@ def load():
         L.wgsr_mlp_forward.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float, ctypes.c_uint32] + [_fp] * 4 + [_fp]
         L.wgsr_mlp_backward.restype = c_int
         L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
+        L.wgsr_dino_reg.restype = c_int
+        L.wgsr_dino_reg.argtypes = ([_fp, _fp, c_int, c_int, c_int, ctypes.c_float, ctypes.c_float] + [_fp] * 5
+                                    + [_fp])
         L.wgsr_densification_stats.restype = c_int
         L.wgsr_densification_stats.argtypes = [c_int] + [_fp] * 5 + [_fp]
         L.wgsr_mark_visible.restype = c_int
@@ -252,7 +255,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_uncer_blocks", "wgsr_uncer_loss_forward", "wgsr_uncer_small_maps", "wgsr_uncer_loss_small",
     "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
     "wgsr_pose_state_floats", "wgsr_pose_step",
-    "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward",
+    "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward", "wgsr_dino_reg",
     "wgsr_densify_blocks", "wgsr_densify_select", "wgsr_densify_emit", "wgsr_reset_opacity",
     "wgsr_sparse_grad_row_floats", "wgsr_sparse_mask_words", "wgsr_sparse_pack_records",
     "wgsr_sparse_summary_block_words", "wgsr_sparse_exchange_summary", "wgsr_sparse_unpack_records",

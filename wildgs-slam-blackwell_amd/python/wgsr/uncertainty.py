@@ -277,22 +277,56 @@ DINO_SIMILARITY_THRESHOLD = 0.75
 DINO_EPS = float(torch.finfo(torch.float32).eps)
 
 
+class _DinoReg(torch.autograd.Function):
+    """wgsr_dino_reg (csrc/dino.hip): the whole regulariser in four launches;
+    d loss / d u is produced by the forward and scaled in the backward."""
+
+    @staticmethod
+    def forward(ctx, u, feat):
+        from . import _lib
+        L = _lib.load()
+        N, C = feat.shape
+        dev = feat.device
+        fn = torch.empty(N, C, device=dev)
+        sim = torch.empty(N, N, device=dev)
+        row_var = torch.empty(N, device=dev)
+        grad_u = torch.empty(N, device=dev)
+        loss = torch.empty((), device=dev)
+        pt = _lib.ptr
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_dino_reg(pt(u), pt(feat), N, C, DINO_TOP_K, DINO_SIMILARITY_THRESHOLD, DINO_EPS,
+                                       pt(fn), pt(sim), pt(row_var), pt(grad_u), pt(loss),
+                                       _lib.stream_handle(dev)))
+        ctx.save_for_backward(grad_u)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad_u,) = ctx.saved_tensors
+        return grad_u * g, None
+
+
 def dino_regularization_loss(uncertainty, features):
     """compute_dino_regularization_loss (mapping_utils.py:332-389): the mean
     over samples of the variance of the uncertainty over each sample's (up
     to) 128 most similar features with cosine similarity > 0.75 (NeRF-on-the-
     Go eqs. 2-3).  ``uncertainty`` [.., 1] or a list of tensors, ``features``
     [.., C] (or a list) with the same sample count; differentiable in the
-    uncertainty.  torch ops (an N x N GEMM + top-k on a few thousand samples:
-    hipBLASLt + rocPRIM), the same arithmetic as the reference's."""
+    uncertainty.  Device tensors run the HIP kernels (csrc/dino.hip; fails
+    loudly without the library); CPU tensors run the torch restatement with
+    the reference's own arithmetic (the CPU parity tests' path)."""
     unc = torch.stack(uncertainty) if isinstance(uncertainty, (list, tuple)) else uncertainty
     feat = torch.stack(features) if isinstance(features, (list, tuple)) else features
     C = feat.shape[-1]
     u = unc.reshape(-1, 1)
-    fn = torch.nn.functional.normalize(feat.contiguous().view(-1, C), p=2, dim=-1)
-    if u.shape[0] != fn.shape[0]:
+    if u.shape[0] != feat.numel() // C:
         raise ValueError("Uncertainty and feature buffers must have same number of samples"
-                         + f"but got {u.shape[0]} and {fn.shape[0]}")
+                         + f"but got {u.shape[0]} and {feat.numel() // C}")
+    if feat.is_cuda:
+        if feat.dtype != torch.float32 or unc.dtype != torch.float32:
+            raise RuntimeError("dino_regularization_loss: fp32 device tensors only (the HIP path has no fallback)")
+        return _DinoReg.apply(u.reshape(-1).contiguous(), feat.detach().contiguous().view(-1, C))
+    fn = torch.nn.functional.normalize(feat.contiguous().view(-1, C), p=2, dim=-1)
     sim = fn @ fn.T
     k = min(DINO_TOP_K, sim.shape[-1])
     top, idx = torch.topk(sim, k=k, dim=-1)
