@@ -579,6 +579,14 @@ const char* wgsr_profile_stage_name(int i);
 const char* wgsr_last_error(void);
 const char* wgsr_version(void);
 
+/* Byte offset, inside the geometry buffer of this thread's last
+ * wgsr_rasterize_forward call, of its depth order: P uint32 Gaussian ids by
+ * ascending view-space depth (ties in index order, culled Gaussians last) --
+ * the order upstream's (tile | depth) key sort gives every tile list.  The
+ * depth sort runs three passes over the visible key range (WGSR_DEPTH_SORT=
+ * full: four 8-bit passes over the whole keys), so where it lands varies. */
+int64_t wgsr_depth_order_offset(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,140 @@
+"""The depth sort over the visible key range (csrc/sort.hip launch_depth_sort,
+DepthKeyPlan in csrc/wgsr_common.h) against the four 8-bit passes over the
+whole 32-bit keys (WGSR_DEPTH_SORT=full).
+
+Both are stable sorts of the same keys, so the depth order (rank -> Gaussian,
+read from the geometry buffer at wgsr_depth_order_offset()) and every raster
+output must be bit-identical.  The scenes cover each branch of the plan:
+depth ranges giving 24 key bits (three 8-bit passes), 26 and 28 bits (9- and
+10-bit digit passes), 29+ bits (far Gaussians: the host-queued fix-up pass and
+the re-run scan), equal depths (ties keep index order), Gaussians behind the
+camera (culled: last), nothing visible, a single Gaussian, and the three
+workgroup-tile tiers (<= 256k, <= 2M, more keys).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+W, H = 512, 384
+
+
+def _scene(P, zlo, zhi, seed=0, far=0, behind=0, ties=0, log_z=False):
+    g = torch.Generator().manual_seed(seed)
+    tanx = 1.0 / (2.0 * 0.9)
+    tany = H / (2.0 * 0.9 * W)
+    r = torch.rand(P, generator=g)
+    z = torch.exp(math.log(zlo) + (math.log(zhi) - math.log(zlo)) * r) if log_z else zlo + (zhi - zlo) * r
+    u = torch.rand(P, generator=g) * 2 - 1
+    v = torch.rand(P, generator=g) * 2 - 1
+    if far:
+        z[:far] = 1e12 * (1.0 + torch.rand(far, generator=g))
+    if behind:
+        z[far:far + behind] = -1.0 - torch.rand(behind, generator=g)
+    means = torch.stack([u * z * tanx * 0.9, v * z * tany * 0.9, z], dim=1)
+    if ties:  # identical means (e.g. clones after densification): equal depth keys
+        means[P - ties:] = means[far + behind:far + behind + ties]
+    scales = torch.exp(math.log(0.004) + (math.log(0.03) - math.log(0.004)) * torch.rand(P, 3, generator=g))
+    q = torch.randn(P, 4, generator=g)
+    q = q / q.norm(dim=1, keepdim=True)
+    opac = 0.05 + 0.9 * torch.rand(P, 1, generator=g)
+    shs = torch.randn(P, 1, 3, generator=g) * 0.5
+    return means, scales, q, opac, shs
+
+
+def _forward(scene):
+    from diff_gaussian_rasterization import _C
+    from wgsr import _lib
+    from wgsr.camera import synthetic_camera
+    f = synthetic_camera(W, H, 0).raster_fields()
+    d = lambda x: x.to(DEV).contiguous()  # noqa: E731
+    means, scales, q, opac, shs = (d(x) for x in scene)
+    e = torch.empty(0, device=DEV)
+    out = _C.rasterize_gaussians(d(torch.zeros(3)), means, e, opac, scales, q, 1.0, e, d(f["viewmatrix"]),
+                                 d(f["projmatrix"]), d(f["projmatrix_raw"]), f["tanfovx"], f["tanfovy"], H, W,
+                                 shs, 0, d(f["campos"]), False, False)
+    torch.cuda.synchronize()
+    off = int(_lib.load().wgsr_depth_order_offset())
+    geom = out[3]
+    P = means.shape[0]
+    order = geom[off:off + 4 * P].cpu().numpy().view(np.uint32).copy()
+    res = dict(num_rendered=out[0], color=out[1].cpu().numpy(), radii=out[2].cpu().numpy(),
+               depth=out[6].cpu().numpy(), opacity=out[7].cpu().numpy(), n_touched=out[8].cpu().numpy())
+    return order, res
+
+
+def _compare(scene, monkeypatch):
+    outs = {}
+    for mode in ("full", "range"):
+        monkeypatch.setenv("WGSR_DEPTH_SORT", mode)
+        outs[mode] = _forward(scene)
+    (o_full, r_full), (o_rng, r_rng) = outs["full"], outs["range"]
+    P = scene[0].shape[0]
+    assert np.array_equal(np.sort(o_rng), np.arange(P, dtype=np.uint32))  # a permutation
+    np.testing.assert_array_equal(o_rng, o_full)
+    for k, v in r_full.items():
+        if k == "num_rendered":
+            assert r_rng[k] == v
+        else:
+            np.testing.assert_array_equal(r_rng[k], v, err_msg=k)
+    return o_rng, r_full
+
+
+@pytest.mark.parametrize("P,zlo,zhi,log_z", [
+    (100_000, 2.0, 8.0, False),      # 24 key bits: three 8-bit passes
+    (60_000, 0.25, 60.0, True),      # 26 bits: 8 + 9 + 9
+    (60_000, 0.21, 3.0e4, True),     # 28 bits: 8 + 10 + 10
+    (300_000, 0.5, 5.0, False),      # 2048-key tiles
+])
+def test_depth_sort_matches_full_key_sort(P, zlo, zhi, log_z, monkeypatch):
+    _compare(_scene(P, zlo, zhi, log_z=log_z, behind=P // 50, ties=P // 20), monkeypatch)
+
+
+def test_far_gaussians_take_the_fixup_pass(monkeypatch):
+    """Visible Gaussians at 1e12 m next to ones at 0.3 m: the key range needs
+    29+ bits, so the host queues one more pass after reading the range."""
+    scene = _scene(20_000, 0.3, 10.0, far=40, behind=100, ties=500, log_z=True)
+    order, res = _compare(scene, monkeypatch)
+    radii = res["radii"]
+    far_visible = np.nonzero(radii[:40] > 0)[0]
+    assert far_visible.size > 0  # the far ones are on screen, so the range really is that wide
+    ranks = np.empty_like(order)
+    ranks[order] = np.arange(order.size, dtype=np.uint32)
+    visible = np.nonzero(radii > 0)[0]
+    # the far ones come right before the culled ones
+    assert set(order[visible.size - far_visible.size:visible.size].tolist()) == set(far_visible.tolist())
+
+
+def test_nothing_visible_and_tiny_inputs(monkeypatch):
+    s = _scene(5_000, 1.0, 4.0, behind=5_000)
+    order, res = _compare(s, monkeypatch)
+    np.testing.assert_array_equal(order, np.arange(5_000, dtype=np.uint32))  # all culled: index order
+    assert res["num_rendered"] == 0
+    _compare(_scene(1, 1.0, 4.0), monkeypatch)
+    _compare(_scene(7, 1.0, 1.0 + 1e-6), monkeypatch)  # all depths within a few ulps: R <= 8
+
+
+def test_large_tile_tier(monkeypatch):
+    """More than 2M keys: 4096-key workgroup tiles."""
+    _compare(_scene(2_200_000, 1.0, 12.0, behind=10_000, ties=50_000), monkeypatch)
+
+
+def test_depth_order_is_by_depth_then_index(monkeypatch):
+    """Independently of the full-key sort: the visible Gaussians come first,
+    by non-decreasing view depth (the splat's depth word), equal depths in
+    index order."""
+    monkeypatch.setenv("WGSR_DEPTH_SORT", "range")
+    scene = _scene(50_000, 0.4, 20.0, behind=500, ties=3_000, log_z=True)
+    order, res = _forward(scene)
+    z = scene[0][:, 2].numpy().astype(np.float32)
+    vis = res["radii"] > 0
+    nv = int(vis.sum())
+    assert vis[order[:nv]].all() and not vis[order[nv:]].any()
+    zs = z[order[:nv]]  # view depth = z for the identity camera (view 0)
+    assert np.all(np.diff(zs) >= 0)
+    same = np.diff(zs) == 0
+    assert np.all(np.diff(order[:nv].astype(np.int64))[same] > 0)
+    np.testing.assert_array_equal(order[nv:], np.sort(order[nv:]))

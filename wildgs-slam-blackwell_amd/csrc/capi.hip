@@ -24,6 +24,13 @@ thread_local char g_err[1024] = "";
 struct HostCounters {
   uint32_t* buf = nullptr;
   hipEvent_t ev = nullptr;
+  // the D->H copy runs on a side stream behind `pre` (recorded after
+  // k_preprocess), so the forward's stream goes straight on to the depth
+  // sort instead of waiting out the copy and its host-visible release
+  // (~10 us of the stream's time per forward); WGSR_COUNTER_SIDE=0 keeps
+  // the copy on the forward's stream
+  hipStream_t side = nullptr;
+  hipEvent_t pre = nullptr;
 };
 // one pinned block + event per (host thread, device): an event recorded on a
 // stream must belong to that stream's device
@@ -38,6 +45,15 @@ HostCounters& host_counters() {
     if (hipHostMalloc(&p, kCounterBytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
     hc.buf = static_cast<uint32_t*>(p);
     if (hipEventCreateWithFlags(&hc.ev, hipEventDisableTiming) != hipSuccess) hc.ev = nullptr;
+    static const bool side_off = [] {
+      const char* e = getenv("WGSR_COUNTER_SIDE");
+      return e && strcmp(e, "0") == 0;
+    }();
+    if (!side_off) {
+      if (hipStreamCreateWithFlags(&hc.side, hipStreamNonBlocking) != hipSuccess) hc.side = nullptr;
+      if (hc.side && hipEventCreateWithFlags(&hc.pre, hipEventDisableTiming) != hipSuccess) hc.pre = nullptr;
+      if (!hc.pre) hc.side = nullptr;
+    }
   }
   return hc;
 }
@@ -176,8 +192,18 @@ int bin_shift(const wgsr_raster_args& a) {
   // bin ids fit the key's low 16 bits, list lengths the packed scan's 16 bits
   return sh > 0 && g.nt > 65535 ? 0 : sh;
 }
+// WGSR_DEPTH_SORT=full: the depth sort as four 8-bit passes over the whole
+// 32-bit keys (the reference schedule for A/B runs and the parity tests);
+// default: three passes over the visible key range (launch_depth_sort)
+bool depth_sort_full() {
+  const char* e = getenv("WGSR_DEPTH_SORT");  // read per call: tests compare both
+  return e && strcmp(e, "full") == 0;
+}
 constexpr int kDepthBits = 32;
-constexpr bool kDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;
+constexpr bool kFullDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;
+// byte offset of the last forward's depth order (rank -> Gaussian) in its
+// geometry buffer (wgsr_depth_order_offset)
+thread_local size_t g_depth_order_off = 0;
 
 int validate(const wgsr_raster_args* a) {
   if (!a) return set_error(WGSR_EINVAL, "null args");
@@ -246,6 +272,7 @@ int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset) {
 
 const char* wgsr_profile_stage_name(int i) { return (i >= 0 && i < WGSR_NUM_STAGES) ? kStageNames[i] : ""; }
 const char* wgsr_version(void) { return "wgsr 0.1 gfx950"; }
+int64_t wgsr_depth_order_offset(void) { return (int64_t)g_depth_order_off; }
 
 size_t wgsr_geometry_bytes(int P) { return GeomLayout((size_t)(P > 0 ? P : 0)).total; }
 size_t wgsr_binning_bytes(int64_t N, int W, int H) {
@@ -292,8 +319,11 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   const Bins bins(grid.gx, grid.gy, bshift);
   // the depth sort's superblock sums are zeroed by k_preprocess's workgroups
   // (no memset launch), and so is the next forward's counter block
+  const bool full_depth = depth_sort_full();
   size_t sup_off = 0;
-  const size_t sup_words = sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off);
+  const size_t sup_words = full_depth ? sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off)
+                                      : depth_sort_sup_words((size_t)a.P);
+  if (!full_depth) sup_off = depth_sort_sup_offset_words((size_t)a.P);
   ZeroJob zj{};
   if (dc) {
     zj.p[zj.count] = reinterpret_cast<float*>(dc->buf + (size_t)(dc->parity ^ 1) * (kCounterBytes / 4));
@@ -329,34 +359,78 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // waits for them, allocates the binning buffer and queues the rest.
   HostCounters& hc = host_counters();
   if (!hc.buf || !hc.ev) return set_error(WGSR_EHIP, "pinned counter buffer / event allocation failed");
-  HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipEventRecord(hc.ev, s));
+  if (hc.side) {
+    HIPCHK(hipEventRecord(hc.pre, s));
+    HIPCHK(hipStreamWaitEvent(hc.side, hc.pre, 0));
+    HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, hc.side));
+    HIPCHK(hipEventRecord(hc.ev, hc.side));
+  } else {
+    HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(hc.ev, s));
+  }
   // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
-  bool in_alt = false;
+  const uint32_t* depth_order = nullptr;
   { StageTimer T(1, s);
-  STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
-                               at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
-                               kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt,
-                               nullptr, nullptr, sup_words != 0)); }
-  const uint32_t* depth_order = at<uint32_t>(geom, kDepthInAlt ? GL.dval_alt : GL.dval);
+  if (full_depth) {
+    bool in_alt = false;
+    STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
+                                 at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), true, (size_t)a.P, 0,
+                                 kDepthBits, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals), s, &in_alt,
+                                 nullptr, nullptr, sup_words != 0));
+    if (in_alt != kFullDepthInAlt) return set_error(WGSR_EHIP, "internal: depth sort parity");
+    depth_order = at<uint32_t>(geom, kFullDepthInAlt ? GL.dval_alt : GL.dval);
+  } else {
+    STAGE(a, s, launch_depth_sort(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
+                                  at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), (size_t)a.P,
+                                  counter + kDepthRangeOffset / 4, counter + 2, at<uint32_t>(geom, GL.hist), s));
+    depth_order = at<uint32_t>(geom, GL.dval_alt);
+  } }
   // in depth order: duplicate-slot offsets of the exact tile lists (the
   // backward's record slots; Gaussian -> first slot), and with sort bins the
   // bin-pair offsets -- their down-sweep writes the pairs, after the binning
   // buffer exists
-  StageTimer* scan_timer = new StageTimer(2, s);
-  if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
-    STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, depth_order, (size_t)a.P,
-                                   at<uint32_t>(geom, GL.bsum), s, scan_sup ? at<uint2>(geom, GL.bsup) : nullptr));
-  } else {
-    STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
-                                      at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
-                                      at<uint32_t>(geom, GL.bsum), at<uint32_t>(geom, GL.counter), s,
-                                      sizeof(ListRec) / 4));
-  }
-  delete scan_timer;
+  auto queue_scan = [&]() -> int {
+    StageTimer T(2, s);
+    if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
+      STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, depth_order, (size_t)a.P,
+                                     at<uint32_t>(geom, GL.bsum), s, scan_sup ? at<uint2>(geom, GL.bsup) : nullptr));
+    } else {
+      STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
+                                        at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
+                                        at<uint32_t>(geom, GL.bsum), at<uint32_t>(geom, GL.counter), s,
+                                        sizeof(ListRec) / 4));
+    }
+    return WGSR_OK;
+  };
+  if (int e = queue_scan()) return e;
   HIPCHK(hipEventSynchronize(hc.ev));
   sync_on_error.armed = false;
   const uint32_t* host_counter = hc.buf;
+  if (!full_depth) {
+    // depths spanning more than the three passes' bits: one more stable pass
+    // over the bits above them, then the scan again in the final order
+    const uint32_t* rw = host_counter + kDepthRangeOffset / 4;
+    uint32_t hi = 0, nlo = 0;
+    for (int i = 0; i < kRectPairLanes; ++i) {
+      hi = rw[i] > hi ? rw[i] : hi;
+      nlo = rw[kRectPairLanes + i] > nlo ? rw[kRectPairLanes + i] : nlo;
+    }
+    const DepthKeyPlan pl = depth_key_plan(hi, ~nlo);
+    if (pl.extra_bits > 0) {
+      bool alt = false;
+      StageTimer T(1, s);
+      STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey_alt), at<uint32_t>(geom, GL.dkey),
+                                   at<uint32_t>(geom, GL.dval_alt), at<uint32_t>(geom, GL.dval), false, (size_t)a.P,
+                                   pl.extra_shift, pl.R, at<uint32_t>(geom, GL.hist), at<uint32_t>(geom, GL.totals),
+                                   s, &alt));
+      depth_order = at<uint32_t>(geom, alt ? GL.dval : GL.dval_alt);
+      if (scan_sup)
+        HIPCHK(hipMemsetAsync(at<uint2>(geom, GL.bsup), 0,
+                              sizeof(uint2) * kScanSupStride * packed_scan_supers((size_t)a.P), s));
+      if (int e = queue_scan()) return e;
+    }
+  }
+  g_depth_order_off = (size_t)(reinterpret_cast<const uint8_t*>(depth_order) - static_cast<const uint8_t*>(geom));
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
   const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
@@ -389,11 +463,20 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     const bool odd = radix_passes(0, bits) % 2 == 1;
     uint32_t* vin = at<uint32_t>(binning, odd ? BL.slot_g : BL.point_g);
     uint32_t* valt = at<uint32_t>(binning, odd ? BL.point_g : BL.slot_g);
+    // the bin sort's superblock sums are zeroed by k_duplicate_bins (no memset launch)
+    size_t bs_off = 0;
+    const size_t bs_words = bshift ? sort_sup_words(NL, 0, bits, &bs_off) : 0;
+    ZeroJob zb{};
+    if (bs_words) {
+      zb.p[0] = reinterpret_cast<float*>(at<uint32_t>(binning, BL.hist) + bs_off);
+      zb.n[0] = bs_words;
+      zb.count = 1;
+    }
     { StageTimer T(3, s);
     if (bshift) {
       // (the backward's record flags live on the exact slots: zeroed here too)
       STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
-                                        at<uint32_t>(binning, BL.key), vin, scan_sup, s));
+                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
@@ -405,7 +488,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false,
                                  NL, 0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s,
-                                 &talt, bin_bounds, &bounds_done)); }
+                                 &talt, bin_bounds, &bounds_done, bs_words != 0)); }
     // the Gaussian ids are the payload; the backward recomputes each pair's
     // record slot from (Gaussian, tile) instead of carrying it through the sort
     if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");

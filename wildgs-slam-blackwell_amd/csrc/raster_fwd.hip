@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, const ZeroJob zero) {
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero) {
 
   extern __shared__ float s_sh[];  // kPreRows x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
@@ -233,6 +233,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     }
   }
   uint3 ac = make_uint3(0u, 0u, 0u);
+  uint32_t khi = 0u, knlo = 0u;  // this lane's visible depth key and its complement (0: culled)
   if (i < P) {
     uint4 w;
     uint2 rcw;
@@ -244,6 +245,10 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);  // rect, tb, exact list length
     if (bshift) tb[i] = w.z;
     dkey[i] = w.w;
+    if (w.w != 0xFFFFFFFFu) {
+      khi = w.w;
+      knlo = ~w.w;
+    }
     n_touched[i] = 0;
     gflag[i] = 0;  // the backward's "received gradient" flag
   }
@@ -255,11 +260,16 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     area += __shfl_xor(area, off, 64);
     cnt += __shfl_xor(cnt, off, 64);
     nbin += __shfl_xor(nbin, off, 64);
+    khi = max(khi, (uint32_t)__shfl_xor((int)khi, off, 64));
+    knlo = max(knlo, (uint32_t)__shfl_xor((int)knlo, off, 64));
   }
   if (lane == 0) {
     atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
     atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
     atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
+    // the depth sort's key range (DepthKeyPlan): max key, max complement
+    if (khi) atomicMax(&drange[blockIdx.x % kRectPairLanes], khi);
+    if (knlo) atomicMax(&drange[kRectPairLanes + blockIdx.x % kRectPairLanes], knlo);
   }
   // scratch the next kernels need zeroed (the depth sort's superblock sums)
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
@@ -393,7 +403,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     uint32_t P, int bshift, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
-    uint32_t* __restrict__ vals) {
+    uint32_t* __restrict__ vals, const ZeroJob zero) {
   constexpr int NW = kDupScanThreads / 64;
   __shared__ uint2 s_w[NW], s_p[NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -460,6 +470,8 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   if (in) slot_start[g] = wb.x + ic - cnt;
   // the wave's slots are contiguous: one byte store per lane per 64 slots
   for (uint32_t k = lane; k < wt.x; k += 64) pflag[wb.x + k] = 0;
+  // scratch the bin sort needs zeroed (its superblock sums)
+  zero_share(zero, blockIdx.x, gridDim.x, t, kDupScanThreads);
   if (wt.y == 0) return;  // wave-uniform; no barrier below
   const uint32_t my_off = wb.y + ib - nb;  // first bin pair of this rank
   const uint32_t start = wb.y, end = wb.y + wt.y;
@@ -1073,6 +1085,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                              hipStream_t s) {
   unsigned long long* list_pairs = rect_pairs + kRectPairLanes;
   unsigned long long* bin_pairs = rect_pairs + 2 * kRectPairLanes;
+  uint32_t* drange = reinterpret_cast<uint32_t*>(rect_pairs + 3 * kRectPairLanes);  // kDepthRangeOffset
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
@@ -1082,12 +1095,13 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                      at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs, bshift,
-                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), zero);
+                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero);
   return hipGetLastError();
 }
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
-                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, hipStream_t s) {
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
+                                 hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
@@ -1095,7 +1109,7 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
                      s, (uint32_t)a.P, bshift, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
-                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals);
+                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero);
   return hipGetLastError();
 }
 

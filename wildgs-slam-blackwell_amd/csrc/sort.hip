@@ -120,7 +120,8 @@ __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__
 // (block-major layouts: thread t's loads are coalesced across the block).
 __device__ __forceinline__ uint32_t sup_digit_base(const uint32_t* __restrict__ hist,
                                                    const uint32_t* __restrict__ sup, uint32_t nb, uint32_t nsup,
-                                                   uint32_t bid, int t, uint32_t* s_tmp) {
+                                                   uint32_t bid, int t, uint32_t* s_tmp, uint2* bounds,
+                                                   uint32_t mask) {
   const uint32_t sb = bid / kSupBlocks;
   // every load of a 32-superblock chunk (and the own superblock's earlier
   // blocks) is issued before the first add: one round trip per chunk
@@ -144,7 +145,10 @@ __device__ __forceinline__ uint32_t sup_digit_base(const uint32_t* __restrict__ 
   uint32_t intra = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kSupBlocks - 1; ++k) intra += h[k];
-  return block_excl_scan256(total, s_tmp, nullptr) + pre + intra;
+  const uint32_t start = block_excl_scan256(total, s_tmp, nullptr);
+  // a one-pass sort hands back every digit's [start, end) of the output
+  if (bounds && bid == 0 && (uint32_t)t <= mask) bounds[t] = make_uint2(start, start + total);
+  return start + pre + intra;
 }
 
 // Reduce-then-scan mode, step 2: exclusive scan of hist row d (over blocks)
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup) {
+    uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup, uint2* __restrict__ bounds) {
   constexpr int kTile = 256 * I;
   __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16)
   __shared__ uint32_t s_wcnt[4][256];
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   uint32_t gdig = 0;  // reduce-then-scan: this block's global base of digit t
   if (!kOnesweep) {  // (the scans' barriers publish s_wcnt = 0)
     if (sup) {
-      gdig = sup_digit_base(hist, sup, nb, nsup, bid, t, s_tmp);
+      gdig = sup_digit_base(hist, sup, nb, nsup, bid, t, s_tmp, bounds, mask);
     } else {
       const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);
       gdig = ex + hist[(size_t)t * nb + bid];
@@ -439,6 +443,242 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
       const uint32_t d = (kv.x >> shift) & mask;
       const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
       kout[dst] = kv.x;
+      vout[dst] = kv.y;
+    }
+  }
+}
+
+// ---- depth sort over the visible key range (DepthKeyPlan, wgsr_common.h) -----
+// Three stable passes over key'' (the first maps the raw keys); each kernel
+// derives the passes' digit widths from the range words k_preprocess left in
+// the counter block, so the host queues the passes before it knows the range.
+// Same reduce-then-scan structure as the 8-bit passes (superblock sums, no
+// row-scan launch), with up to 1024 digits: thread t owns digits
+// [t dpt, t dpt + dpt), dpt = ceil(digits / 256).
+static_assert(kRectPairLanes == 64, "one range word per lane");
+__device__ __forceinline__ int bitlen32(uint32_t x) {
+  return x ? 32 - __clz((int)x) : 0;
+}
+// The range words: one per lane, max-reduced across the wave.  Every kernel
+// issues its key loads (and the scatter its first digit-sum loads) before it
+// needs the plan, so this adds no round trip of its own.
+// wave max into a scalar: DPP within each 16-lane row (shifted-in lanes
+// read 0), then the four rows' lane 15 by readlane
+__device__ __forceinline__ uint32_t wave_max_u32_uniform(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));  // row_shr:4
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));  // row_shr:8
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 15), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 47), d = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+  return max(max(a, b), max(c, d));
+}
+// The first kernel (pass 0's histogram) reduces k_preprocess's 2 x 64 range
+// words and its workgroup 0 leaves the result in two words (the counter
+// block's pad words) that every later kernel reads with one scalar load,
+// whose wait does not hold up the vector loads issued before the plan is
+// needed.
+__device__ __forceinline__ uint2 depth_range_reduce(const uint32_t* __restrict__ range) {
+  const int lane = threadIdx.x & 63;
+  return make_uint2(wave_max_u32_uniform(range[lane]), wave_max_u32_uniform(range[kRectPairLanes + lane]));
+}
+__device__ __forceinline__ DepthKeyPlan depth_plan_from2(const uint32_t* __restrict__ range2) {
+  return depth_key_plan(range2[0], ~range2[1]);
+}
+
+template <int I, int PASS>
+__global__ __launch_bounds__(256) void k_depth_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                    const uint32_t* __restrict__ range, uint32_t* __restrict__ range2,
+                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ sup) {
+  __shared__ uint32_t s_h[kDepthMaxDigits];
+  const int t = threadIdx.x;
+  uint32_t k[I];
+  const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, k);
+#pragma unroll
+  for (int q = 0; q < kDepthMaxDigits / 256; ++q) s_h[t + 256 * q] = 0;
+  DepthKeyPlan pl;
+  if (PASS == 0) {
+    const uint2 r = depth_range_reduce(range);
+    if (blockIdx.x == 0 && t == 0) {
+      range2[0] = r.x;
+      range2[1] = r.y;
+    }
+    pl = depth_key_plan(r.x, ~r.y);
+  } else {
+    pl = depth_plan_from2(range2);
+  }
+  const int shift = pl.shift[PASS], bits = pl.bits[PASS];
+  const uint32_t ndig = 1u << bits;
+  if (PASS == 0) {
+#pragma unroll
+    for (int j = 0; j < I; ++j) k[j] = depth_key_xform(pl, k[j]);
+  }
+  __syncthreads();
+  add_runs(s_h, k, nv, shift, ndig - 1u);
+  __syncthreads();
+  uint32_t* hrow = hist + (size_t)blockIdx.x * kDepthMaxDigits;
+  uint32_t* srow = sup + (size_t)(blockIdx.x / kSupBlocks) * kDepthMaxDigits;
+  for (uint32_t d = t; d < ndig; d += 256) {
+    const uint32_t c = s_h[d];
+    hrow[d] = c;
+    if (c) atomicAdd(&srow[d], c);
+  }
+}
+
+// digit d: its total over all blocks, over the superblocks before block
+// bid's, and over the blocks before bid in its own superblock (every load
+// of a 32-superblock chunk issued before the first add)
+__device__ __forceinline__ void depth_digit_sums(const uint32_t* __restrict__ hist, const uint32_t* __restrict__ sup,
+                                                 uint32_t nsup, uint32_t bid, uint32_t d, uint32_t& total,
+                                                 uint32_t& pre, uint32_t& intra) {
+  const uint32_t sb = bid / kSupBlocks;
+  uint32_t h[kSupBlocks - 1];
+#pragma unroll
+  for (uint32_t k = 0; k < kSupBlocks - 1; ++k) {
+    const uint32_t b = sb * kSupBlocks + k;
+    h[k] = b < bid ? hist[(size_t)b * kDepthMaxDigits + d] : 0u;
+  }
+  // the first 32 superblocks' loads go out with the row loads (no loop in
+  // between to wait at)
+  uint32_t v0[32];
+#pragma unroll
+  for (uint32_t k = 0; k < 32; ++k) v0[k] = k < nsup ? sup[(size_t)k * kDepthMaxDigits + d] : 0u;
+  total = 0;
+  pre = 0;
+  for (uint32_t q0 = 32; q0 < nsup; q0 += 32) {
+    uint32_t v[32];
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k) v[k] = q0 + k < nsup ? sup[(size_t)(q0 + k) * kDepthMaxDigits + d] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k) {
+      total += v[k];
+      pre += q0 + k < sb ? v[k] : 0u;
+    }
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 32; ++k) {
+    total += v0[k];
+    pre += k < sb ? v0[k] : 0u;
+  }
+  intra = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kSupBlocks - 1; ++k) intra += h[k];
+}
+
+// Thread t owns digits t + 256 q (q < dpt = ceil(digits / 256)), so the
+// q = 0 sums are loaded before the plan is known: a column beyond this
+// pass's digits holds zeros (superblock sums) or stale counts (block rows)
+// and only ever feeds the bases of digits no key has.
+template <int I, int PASS>
+__global__ __launch_bounds__(256) void k_depth_scatter(const uint32_t* __restrict__ kin,
+                                                       const uint32_t* __restrict__ vin, uint32_t n,
+                                                       const uint32_t* __restrict__ range2,
+                                                       const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ sup, uint32_t nsup,
+                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+  constexpr int kTile = 256 * I, kQ = kDepthMaxDigits / 256;
+  __shared__ uint2 s_buf[kTile];
+  __shared__ uint32_t s_wcnt[4][kDepthMaxDigits];
+  __shared__ uint32_t s_lbase[kDepthMaxDigits];
+  __shared__ uint32_t s_gbase[kDepthMaxDigits];
+  __shared__ uint32_t s_tmp[4];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t bid = blockIdx.x;
+  const size_t blk0 = (size_t)bid * kTile;
+  const size_t base = blk0 + (size_t)w * (64 * I);
+  uint32_t key[I], val[I], rank[I];
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    key[j] = valid ? kin[e] : 0u;
+    val[j] = PASS == 0 ? (uint32_t)e : (valid ? vin[e] : 0u);
+  }
+  uint32_t tot[kQ], pre[kQ], intra[kQ];
+  depth_digit_sums(hist, sup, nsup, bid, (uint32_t)t, tot[0], pre[0], intra[0]);
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    s_wcnt[0][t + 256 * q] = 0;
+    s_wcnt[1][t + 256 * q] = 0;
+    s_wcnt[2][t + 256 * q] = 0;
+    s_wcnt[3][t + 256 * q] = 0;
+  }
+  const DepthKeyPlan pl = depth_plan_from2(range2);
+  const int shift = pl.shift[PASS], bits = pl.bits[PASS];
+  const uint32_t ndig = 1u << bits, mask = ndig - 1u;
+  const int dpt = (int)((ndig + 255u) >> 8);
+#pragma unroll
+  for (int q = 1; q < kQ; ++q) {
+    tot[q] = pre[q] = intra[q] = 0u;
+    if (q < dpt) depth_digit_sums(hist, sup, nsup, bid, (uint32_t)t + 256u * q, tot[q], pre[q], intra[q]);
+  }
+  if (PASS == 0) {
+#pragma unroll
+    for (int j = 0; j < I; ++j) key[j] = depth_key_xform(pl, key[j]);
+  }
+  {  // global base of this block's digits (the scans' barriers publish s_wcnt = 0)
+    uint32_t carry = 0;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      if (q < dpt) {
+        uint32_t all;
+        const uint32_t ex = block_excl_scan256(tot[q], s_tmp, &all);
+        s_gbase[t + 256 * q] = carry + ex + pre[q] + intra[q];
+        carry += all;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const bool valid = e < n;
+    const uint32_t d = (key[j] >> shift) & mask;
+    const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    uint32_t old = 0;
+    if (valid && lane == leader) old = atomicAdd(&s_wcnt[w][d], (uint32_t)__popcll(peers));
+    old = (uint32_t)__shfl((int)old, leader & 63, 64);
+    rank[j] = old + lanes_below(peers);
+  }
+  __syncthreads();
+  {  // per digit: exclusive prefix over waves, then over digits (block-local)
+    uint32_t carry = 0;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      if (q < dpt) {
+        const uint32_t d = (uint32_t)t + 256u * q;
+        const uint32_t c0 = s_wcnt[0][d], c1 = s_wcnt[1][d], c2 = s_wcnt[2][d], c3 = s_wcnt[3][d];
+        s_wcnt[0][d] = 0;
+        s_wcnt[1][d] = c0;
+        s_wcnt[2][d] = c0 + c1;
+        s_wcnt[3][d] = c0 + c1 + c2;
+        uint32_t all;
+        const uint32_t ex = block_excl_scan256(c0 + c1 + c2 + c3, s_tmp, &all);
+        s_lbase[d] = carry + ex;
+        carry += all;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < I; ++j) {
+    const size_t e = base + (size_t)j * 64 + lane;
+    const uint32_t d = (key[j] >> shift) & mask;
+    const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];
+    if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
+  }
+  __syncthreads();
+  // the last pass writes keys only when a fix-up pass over extra_bits follows
+  const bool wkeys = PASS < kDepthPasses - 1 || pl.extra_bits > 0;
+  const uint32_t cnt = (uint32_t)min((size_t)kTile, (size_t)n - blk0);
+#pragma unroll
+  for (int r = 0; r < I; ++r) {
+    const uint32_t i = (uint32_t)t + 256u * r;
+    if (i < cnt) {
+      const uint2 kv = s_buf[i];
+      const uint32_t d = (kv.x >> shift) & mask;
+      const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
+      if (wkeys) kout[dst] = kv.x;
       vout[dst] = kv.y;
     }
   }
@@ -696,7 +936,7 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
     if (onesweep) {
       hipLaunchKernelGGL((k_radix_scatter<true, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
                          (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u);
+                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u, nullptr);
     } else {
       // status doubles as the [256][nb] per-block histogram (and, in
       // superblock mode, holds the passes' [256][nsup] superblock sums after it)
@@ -704,8 +944,11 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
       hipLaunchKernelGGL(k_radix_hist<I>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status,
                          sp, nsup);
       if (!sp) hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
+      // a single superblock pass over bits [0, end_bit) also writes the digit bounds
+      uint2* db = (sp && passes == 1 && begin_bit == 0) ? digit_bounds : nullptr;
       hipLaunchKernelGGL((k_radix_scatter<false, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup);
+                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup, db);
+      if (db && bounds_done) *bounds_done = true;
     }
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
@@ -739,6 +982,48 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     default:
       return radix_sort_tiled<kSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
                                           totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed);
+  }
+}
+
+template <int I>
+static hipError_t depth_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, size_t n,
+                                   const uint32_t* range, uint32_t* range2, uint32_t* scratch, hipStream_t s) {
+  const uint32_t nb = (uint32_t)((n + 256 * I - 1) / (256 * I)), nsup = (nb + kSupBlocks - 1) / kSupBlocks;
+  uint32_t* hist = scratch;
+  uint32_t* sup = scratch + depth_sort_sup_offset_words(n);
+  const size_t sup_pass = (size_t)kDepthMaxDigits * nsup;
+  const uint32_t un = (uint32_t)n;
+  hipLaunchKernelGGL((k_depth_hist<I, 0>), dim3(nb), dim3(256), 0, s, keys, un, range, range2, hist, sup);
+  hipLaunchKernelGGL((k_depth_scatter<I, 0>), dim3(nb), dim3(256), 0, s, keys, vals, un, range2, hist, sup, nsup,
+                     keys_alt, vals_alt);
+  hipLaunchKernelGGL((k_depth_hist<I, 1>), dim3(nb), dim3(256), 0, s, keys_alt, un, range, range2, hist,
+                     sup + sup_pass);
+  hipLaunchKernelGGL((k_depth_scatter<I, 1>), dim3(nb), dim3(256), 0, s, keys_alt, vals_alt, un, range2, hist,
+                     sup + sup_pass, nsup, keys, vals);
+  hipLaunchKernelGGL((k_depth_hist<I, 2>), dim3(nb), dim3(256), 0, s, keys, un, range, range2, hist,
+                     sup + 2 * sup_pass);
+  hipLaunchKernelGGL((k_depth_scatter<I, 2>), dim3(nb), dim3(256), 0, s, keys, vals, un, range2, hist,
+                     sup + 2 * sup_pass, nsup, keys_alt, vals_alt);
+  return hipGetLastError();
+}
+
+hipError_t launch_depth_sort(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, size_t n,
+                             const uint32_t* range, uint32_t* range2, uint32_t* scratch, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > (size_t)kStCount) return hipErrorInvalidValue;
+  // WGSR_DEPTH_ITEMS=4|8|16 overrides the keys per thread (A/B runs)
+  static const int items = [] {
+    const char* e = getenv("WGSR_DEPTH_ITEMS");
+    const int v = e ? atoi(e) : 0;
+    return (v == kTinySortItems || v == kSmallSortItems || v == kSortItems) ? v : 0;
+  }();
+  switch (items ? items : sort_items(n)) {
+    case kTinySortItems:
+      return depth_sort_tiled<kTinySortItems>(keys, keys_alt, vals, vals_alt, n, range, range2, scratch, s);
+    case kSmallSortItems:
+      return depth_sort_tiled<kSmallSortItems>(keys, keys_alt, vals, vals_alt, n, range, range2, scratch, s);
+    default:
+      return depth_sort_tiled<kSortItems>(keys, keys_alt, vals, vals_alt, n, range, range2, scratch, s);
   }
 }
 

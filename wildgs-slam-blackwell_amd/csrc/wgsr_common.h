@@ -743,10 +743,72 @@ __host__ __device__ inline uint32_t sort_blocks(size_t n) {
 // upstream num_rendered is accumulated in this many u64 partial sums (spread
 // so that the per-wave atomics of k_preprocess do not serialise on one word)
 constexpr int kRectPairLanes = 64;
-// geometry counter block: u32 [0] scan total, [1] error flags, [2..3] pad,
+// geometry counter block: u32 [0] scan total, [1] error flags, [2..3] the depth
+// sort's reduced key range (launch_depth_sort),
 // then u64 rect-pair partials [kRectPairLanes], u64 listed-pair partials
-// [kRectPairLanes], u64 bin-pair partials [kRectPairLanes]
-constexpr size_t kCounterBytes = 16 + 3 * 8 * kRectPairLanes;
+// [kRectPairLanes], u64 bin-pair partials [kRectPairLanes], then u32 maxima
+// of the visible Gaussians' depth keys [kRectPairLanes] and of their
+// complements [kRectPairLanes] (the depth sort's key range, DepthKeyPlan)
+constexpr size_t kDepthRangeOffset = 16 + 3 * 8 * kRectPairLanes;
+constexpr size_t kCounterBytes = kDepthRangeOffset + 2 * 4 * kRectPairLanes;
+
+// ---- depth sort over the visible key range -------------------------------------
+// Depth keys are the float bits of view-space depth (> 0.2 for a visible
+// Gaussian, so the bits order like the floats; culled Gaussians carry
+// 0xFFFFFFFF).  The sort (sort.hip, launch_depth_sort) works on
+//   key'' = key - lo_r   (visible; lo_r = the smallest visible key, low byte cleared)
+//   key'' = 2^R - 1      (culled)
+// with R = bits of (hi - lo_r + 1): an order-preserving map of the visible
+// keys into [0, 2^R - 2] that puts the culled ones last, so a stable sort of
+// key'' IS the stable sort of the keys.  Depths within [2, 8) (the bench
+// scene) give R = 24: three 8-bit passes instead of four.  Pass 0 sorts the
+// low byte (the raw key's low byte: lo_r has none), passes 1 and 2 split the
+// remaining R - 8 bits (<= 10 each, so up to 1024 digits); R > 28 (the
+// visible depths spanning more than ~32 octaves, e.g. 0.2 m .. 1e9 m) leaves
+// extra_bits for one more stable pass that the host queues after it has
+// read the range back with the pair counts.
+constexpr int kDepthPasses = 3;
+constexpr int kDepthMaxDigitBits = 10;
+constexpr int kDepthMaxDigits = 1 << kDepthMaxDigitBits;
+struct DepthKeyPlan {
+  uint32_t lo_r, cul;
+  int R;
+  int shift[kDepthPasses], bits[kDepthPasses];
+  int extra_shift, extra_bits;
+};
+__host__ __device__ inline DepthKeyPlan depth_key_plan(uint32_t hi, uint32_t lo) {
+  DepthKeyPlan p;
+  if (hi < lo) {  // nothing visible: every key'' is 0
+    p.lo_r = 0u;
+    p.cul = 0u;
+    p.R = 0;
+  } else {
+    p.lo_r = lo & ~0xFFu;
+    const uint32_t span = hi - p.lo_r + 1u;  // visible keys < 0x7F800001: no wrap
+    int r = 0;
+    while (r < 32 && (span >> r) != 0u) ++r;
+    p.R = r;
+    p.cul = r >= 32 ? 0xFFFFFFFFu : (1u << r) - 1u;
+  }
+  const int b0 = p.R < 8 ? p.R : 8;
+  const int rest = p.R - b0;
+  int b1 = (rest + 1) / 2;
+  b1 = b1 > kDepthMaxDigitBits ? kDepthMaxDigitBits : b1;
+  int b2 = rest - b1;
+  b2 = b2 > kDepthMaxDigitBits ? kDepthMaxDigitBits : b2;
+  p.shift[0] = 0;
+  p.bits[0] = b0;
+  p.shift[1] = b0;
+  p.bits[1] = b1;
+  p.shift[2] = b0 + b1;
+  p.bits[2] = b2;
+  p.extra_shift = b0 + b1 + b2;
+  p.extra_bits = p.R - p.extra_shift;
+  return p;
+}
+__host__ __device__ inline uint32_t depth_key_xform(const DepthKeyPlan& p, uint32_t key) {
+  return key == 0xFFFFFFFFu ? p.cul : key - p.lo_r;
+}
 
 // ---- sort bins ----------------------------------------------------------------
 // The (Gaussian, tile) lists are sorted as (Gaussian, BIN) pairs of 2^s x 2^s
@@ -781,6 +843,24 @@ __host__ __device__ inline size_t sort_status_bytes(size_t n) {
   return 4ull * (onesweep > sup ? onesweep : sup);
 }
 constexpr size_t kSortTotalsBytes = 4 * (kMaxSortPasses * 256 + kMaxSortPasses);
+// Depth sort scratch (launch_depth_sort): per-block digit counts [nb][1024]
+// followed by the three passes' superblock sums [3][nsup][1024] (zeroed by
+// k_preprocess), in words.
+// (sized for the smallest workgroup tile, so that any tile choice fits)
+__host__ __device__ inline size_t depth_sort_blocks(size_t n) {
+  return (n + 256 * (size_t)kTinySortItems - 1) / (256 * (size_t)kTinySortItems);
+}
+__host__ __device__ inline size_t depth_sort_sup_offset_words(size_t n) {
+  return (size_t)kDepthMaxDigits * depth_sort_blocks(n);
+}
+__host__ __device__ inline size_t depth_sort_sup_words(size_t n) {
+  const size_t nsup = (depth_sort_blocks(n) + kSortSupBlocks - 1) / kSortSupBlocks;
+  return (size_t)kDepthPasses * kDepthMaxDigits * nsup;
+}
+__host__ __device__ inline size_t depth_sort_status_bytes(size_t n) {
+  const size_t a = 4 * (depth_sort_sup_offset_words(n) + depth_sort_sup_words(n)), b = sort_status_bytes(n);
+  return a > b ? a : b;
+}
 
 // Per-Gaussian state (geometry buffer).
 // The dual scan's block sums are also summed per kScanSupBlocks consecutive
@@ -809,7 +889,7 @@ struct GeomLayout {
     offs = take(4 * (P + 1));      // rank -> first duplicate slot
     slot_start = take(4 * P);      // Gaussian -> first duplicate slot
     tb = take(4 * P);              // sort bins: the list records' tb words, dense (the scan's gather stays in L2)
-    hist = take(sort_status_bytes(P));    // radix sort look-back status
+    hist = take(depth_sort_status_bytes(P));  // radix sort scratch (depth sort; the fix-up pass)
     totals = take(kSortTotalsBytes);
     bsum = take(8 * ((P + kPackedScanTile - 1) / kPackedScanTile + 1));  // uint2 block sums of the (dual) scans
     bsup = take(8 * kScanSupStride * (packed_scan_supers(P) + 1));  // uint2 sums of kScanSupBlocks block sums

@@ -25,6 +25,16 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
 // (zero before the sort; 0 = none), at *offset_words
 size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words);
 
+// Depth sort (DepthKeyPlan): three stable passes over key'' of the depth keys
+// in `keys` (values = input positions); range = the counter block's range
+// words (kDepthRangeOffset), range2 = two words for their reduction, scratch = depth_sort_status_bytes(n) bytes whose
+// superblock sums (depth_sort_sup_offset_words / depth_sort_sup_words) are
+// zero.  Result: rank -> position in vals_alt; keys_alt holds key'' when the
+// plan leaves extra_bits (the caller's fix-up pass sorts those), else
+// garbage.  keys and vals are clobbered.
+hipError_t launch_depth_sort(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, size_t n,
+                             const uint32_t* range, uint32_t* range2, uint32_t* scratch, hipStream_t s);
+
 // out[i] = sum_{j<i} vals[idx ? idx[j] : j]  (i in [0, n]; out has n + 1
 // entries), optional scatter_out[idx[i]] = out[i]; *total_out = out[n].
 hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size_t n, uint32_t* out,
@@ -62,7 +72,8 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 // the slot flags zeroed) fused with the (bin | exact tile mask << 16,
 // Gaussian) pair expansion.
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
-                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, hipStream_t s);
+                                 uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
+                                 hipStream_t s);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per

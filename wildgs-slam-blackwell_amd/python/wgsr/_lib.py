@@ -231,6 +231,8 @@ def load():
         L.wgsr_last_error.argtypes = []
         L.wgsr_version.restype = ctypes.c_char_p
         L.wgsr_version.argtypes = []
+        L.wgsr_depth_order_offset.restype = ctypes.c_int64
+        L.wgsr_depth_order_offset.argtypes = []
         L.wgsr_profile_enable.restype = None
         L.wgsr_profile_enable.argtypes = [c_int]
         L.wgsr_profile_read.restype = c_int
@@ -244,7 +246,7 @@ def load():
 EXPORTED_SYMBOLS = (
     "wgsr_rasterize_forward", "wgsr_rasterize_backward", "wgsr_mark_visible", "wgsr_dist_cuda2",
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
-    "wgsr_version", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
+    "wgsr_version", "wgsr_depth_order_offset", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_compact_rows",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
