@@ -27,11 +27,6 @@ namespace {
 constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 // the quad backward keeps its "entry left a partial" flags as one SGPR mask
 // instead of an LDS array (one VALU move and one LDS store fewer per entry)
-// the render backward's per-pixel gradient body under the pixel's exec mask
-// instead of branch-free with alpha = 0 and dL/dalpha = 0 selects
-#ifndef WGSR_BWD_MASKED
-#define WGSR_BWD_MASKED 1
-#endif
 #ifndef WGSR_BWD_HITMASK
 #define WGSR_BWD_HITMASK 1
 #endif
@@ -105,7 +100,11 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   // (mean - p0) minus an immediate (fewer live VGPRs: no spills)
   const v2f p0{(float)(tx0 + (lane & 7)), (float)(ty0 + (lane >> 3))};
   v2f dp01[Q], dp2d[Q];
-  float accd[Q];  // upstream's accum_rec (colour, depth) dotted with this pixel's dL/d(colour, depth)
+  // upstream's accum_rec (colour, depth) dotted with this pixel's dL/d(colour,
+  // depth), held negated as a pair (-accd = na.x + na.y, na.y stays 0): the
+  // pair rides in the packed dot product, c.dp - accd = sum of
+  // fma(c2d, dp2d, fma(c01, dp01, na)) -- one instruction fewer per evaluation
+  v2f na[Q];
   float T[Q], tb[Q];
   uint32_t last[Q], mq[Q];
   uint32_t m = 0;
@@ -130,7 +129,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
     dp2d[p] = inside[p] ? dp2d[p] : v2f{0.f, 0.f};
     const float Tf = T[p], d0 = dp01[p].x, d1 = dp01[p].y, d2 = dp2d[p].x;
     tb[p] = kBg ? -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2) : 0.f;  // background: dL/dalpha += tb / (1 - alpha)
-    accd[p] = 0.f;
+    na[p] = v2f{0.f, 0.f};
     // quadrant p takes gradient from list indices < mq[p] only
     uint32_t x = last[p];
 #pragma unroll
@@ -260,8 +259,8 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       // pixel sums of u = G dL/dalpha (dx, dy) and of its moments; the
       // entry's constants (opacity, conic) multiply the sums afterwards
       // (record_sums)
-      v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
-      float g4 = 0.f, g5 = 0.f;
+      // (five zero pairs: one 64-bit move each per entry)
+      v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g45{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
       bool hit = false;
 #if WGSR_BWD_STATS
       uint32_t st_reach = 0, st_p2 = 0;
@@ -279,64 +278,36 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         const float av = fminf(kMaxAlpha, op * G);
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
         if (!wave_any(v)) continue;
-        hit = true;
 #if WGSR_BWD_STATS
         st_p2 |= 1u << p;
 #endif
-#if WGSR_BWD_MASKED
         // phase 2 on the lanes whose pixel the entry reaches (exec mask): the
         // others keep T, the accumulated colour and their sums as they are.
         // Constant factors of the mean2D (0.5 W, 0.5 H) and conic (-0.5)
         // gradients are applied once per Gaussian in k_gauss_bwd.
+        // colour / depth behind this contributor: upstream's accum_rec enters
+        // dL/dalpha only through its dot product with dL/d(colour, depth),
+        // which follows the same recurrence (accd += alpha (c.dp - accd))
+        hit = true;
         if (v) {
           const float alpha = av;
           const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);  // alpha <= 0.99
           const float Tn = T[p] * rinv;
           T[p] = Tn;
           const float dch = alpha * Tn;
-          // colour / depth behind this contributor: upstream's accum_rec enters
-          // dL/dalpha only through its dot product with dL/d(colour, depth),
-          // which follows the same recurrence (accd += alpha (c.dp - accd))
-          const v2f cp = c01 * dp01[p] + c2d * dp2d[p];
-          const float sd = (cp.x + cp.y) - accd[p];
+          const v2f cp = pfma(c2d, dp2d[p], pfma(c01, dp01[p], na[p]));
+          const float sd = cp.x + cp.y;
           const float dLda = kBg ? sd * Tn + tb[p] * rinv : sd * Tn;
-          accd[p] += alpha * sd;
+          na[p].x = fmaf(-alpha, sd, na[p].x);
           const float gl = G * dLda;   // dL/dG / opacity
           const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
           g01 += u;
           g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG / opacity
-          g4 += u.y * d.y;
-          g5 += gl;
+          g45.x += u.y * d.y;
+          g45.y += gl;
           g67 += dch * dp01[p];
           g89 += dch * dp2d[p];
         }
-#else
-        // phase 2: branch-free; a lane whose pixel the entry misses runs with
-        // alpha = 0 (T and the accumulated colour pass through exactly) and
-        // dL/dalpha = 0.  Constant factors of the mean2D (0.5 W, 0.5 H) and
-        // conic (-0.5) gradients are applied once per Gaussian in k_gauss_bwd.
-        const float alpha = v ? av : 0.f;
-        const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);  // alpha <= 0.99
-        const float Tn = T[p] * rinv;
-        T[p] = Tn;
-        const float dch = alpha * Tn;
-        // colour / depth behind this contributor: upstream's accum_rec enters
-        // dL/dalpha only through its dot product with dL/d(colour, depth),
-        // which follows the same recurrence (accd += alpha (c.dp - accd))
-        const v2f cp = c01 * dp01[p] + c2d * dp2d[p];
-        const float sd = (cp.x + cp.y) - accd[p];
-        float dLda = kBg ? sd * Tn + tb[p] * rinv : sd * Tn;
-        dLda = v ? dLda : 0.f;
-        accd[p] += alpha * sd;
-        const float gl = G * dLda;   // dL/dG / opacity
-        const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
-        g01 += u;
-        g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG / opacity
-        g4 += u.y * d.y;
-        g5 += gl;
-        g67 += dch * dp01[p];
-        g89 += dch * dp2d[p];
-#endif
       }
 #if WGSR_BWD_STATS
       if (lane == 0) {
@@ -345,7 +316,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       }
 #endif
       if (!hit) continue;  // no pixel of the tile: no partial
-      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
+      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g45.x, g45.y, g67.x, g67.y, g89.x, g89.y};
       wave_sum10_store_m(gv, sPm + 11 * j);
 #if WGSR_BWD_HITMASK
       hitm |= 1ull << j;

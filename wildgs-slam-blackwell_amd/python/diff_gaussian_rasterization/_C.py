@@ -5,16 +5,52 @@ pybind module (rasterize_points.cu of the diff-gaussian-rasterization-w-pose
 submodule, absent from the reference snapshot: .gitmodules:7-9; contract in
 SURVEY.md 8(b)), implemented by calls into libwgsr.so's C ABI
 (include/wgsr.h).  Tensors must be float32 (int32 radii) on one HIP device.
+
+When the compiled host wrapper ``_native`` (csrc_py/wgsr_torch.cpp, built
+in-tree by ``make``) is present, each function hands its arguments to it:
+the same checks, messages, allocations and C-ABI calls without the Python
+per-call cost.  The bodies below are the reference for that module and the
+path taken without it (WGSR_NATIVE_WRAPPER=0 forces them).  Both drive the
+libwgsr.so that ``wgsr._lib`` loaded.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from wgsr import _lib
 
+try:
+    from . import _native as _native_module
+except ImportError:  # not built: the ctypes bodies below
+    _native_module = None
+
 NUM_CHANNELS = 3
+_NATIVE = None  # the bound _native module, False when absent or disabled
+
+
+def _native():
+    global _NATIVE
+    if _NATIVE is None:
+        n = _native_module if os.environ.get("WGSR_NATIVE_WRAPPER", "1") != "0" else None
+        if n is not None:
+            L = _lib.load()
+            addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+            n.bind(addr(L.wgsr_rasterize_forward), addr(L.wgsr_rasterize_backward), addr(L.wgsr_mark_visible),
+                   addr(L.wgsr_last_error))
+        _NATIVE = n if n is not None else False
+    return _NATIVE
+
+
+def use_native(on: bool) -> bool:
+    """Select the compiled wrapper (True, when built) or the ctypes bodies
+    (False); returns whether the compiled one is now in use."""
+    global _NATIVE
+    os.environ["WGSR_NATIVE_WRAPPER"] = "1" if on else "0"
+    _NATIVE = None
+    return bool(_native())
 
 
 def _on(t, dev, dtype, name):
@@ -55,6 +91,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                         image_height, image_width, sh, degree, campos, prefiltered, debug):
     """-> (num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer,
     imgBuffer, depth[1,H,W], opacity[1,H,W], n_touched[P] int32)."""
+    n = _native()
+    if n:
+        return n.rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                                     cov3D_precomp, viewmatrix, projmatrix, projmatrix_raw, tan_fovx, tan_fovy,
+                                     image_height, image_width, sh, degree, campos, prefiltered, debug)
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     L = _lib.load()
@@ -103,6 +144,14 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     ``out`` (extension, keyword-only): dict of preallocated contiguous float32
     tensors for "means3D", "shs", "opacities", "scales", "rotations" (e.g. the
     views of a wgsr.dp.GradBuffer) that the kernels write directly."""
+    n = _native()
+    if n:
+        o = out.get if out is not None else (lambda _k: None)
+        return n.rasterize_gaussians_backward(
+            background, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+            projmatrix, projmatrix_raw, tan_fovx, tan_fovy, dL_dout_color, dL_dout_depth, sh, degree, campos,
+            geomBuffer, R, binningBuffer, imageBuffer, debug, o("means3D"), o("shs"), o("opacities"), o("scales"),
+            o("rotations"))
     L = _lib.load()
     dev = means3D.device
     P = means3D.size(0)
@@ -170,6 +219,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 
 def mark_visible(means3D, viewmatrix, projmatrix):
     """-> bool[P]: view-space depth > 0.2 (upstream checkFrustum)."""
+    n = _native()
+    if n:
+        return n.mark_visible(means3D, viewmatrix, projmatrix)
     L = _lib.load()
     dev = means3D.device
     P = means3D.size(0)
