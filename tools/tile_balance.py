@@ -14,7 +14,7 @@ from diff_gaussian_rasterization import _C  # noqa: E402
 from wgsr.camera import synthetic_camera  # noqa: E402
 from wgsr.scene import make_scene  # noqa: E402
 
-P, W, H, deg = 1_000_000, 1920, 1080, 3
+P, W, H, deg = (int(a) for a in sys.argv[1:5]) if len(sys.argv) >= 5 else (1_000_000, 1920, 1080, 3)
 dev = torch.device("cuda")
 sc = make_scene(P, W, H, deg, seed=0)
 f = synthetic_camera(W, H, view=0).raster_fields()
@@ -28,14 +28,12 @@ torch.cuda.synchronize()
 gx, gy = (W + 15) // 16, (H + 15) // 16
 ntl = gx * gy
 b = img.cpu().numpy().view(np.uint8)
-ranges = b[:8 * ntl].view(np.uint32).reshape(ntl, 2)
 a256 = lambda x: (x + 255) // 256 * 256  # noqa: E731
-off_T = a256(8 * ntl)
-off_nc = off_T + a256(4 * W * H)
-ncon = b[off_nc:off_nc + 4 * W * H].view(np.uint32).reshape(H, W)
-pad = np.zeros((gy * 16, gx * 16), np.uint32)
-pad[:H, :W] = ncon
-m = pad.reshape(gy, 16, gx, 16).max(axis=(1, 3)).reshape(-1)
+# ImageLayout (csrc/wgsr_common.h): ranges 8 nt, tile_len 4 nt, tile_m 16 nt, ...
+ranges = b[:8 * ntl].view(np.uint32).reshape(ntl, 2)
+off_m = a256(8 * ntl) + a256(4 * ntl)
+m4 = b[off_m:off_m + 16 * ntl].view(np.uint32).reshape(ntl, 4)
+m = m4.max(axis=1)
 os.makedirs("gpurun_out", exist_ok=True)
 np.savez("gpurun_out/tile_work.npz", length=(ranges[:, 1] - ranges[:, 0]).astype(np.int64), m=m.astype(np.int64),
          gx=gx, gy=gy)
