@@ -582,9 +582,11 @@ const char* wgsr_version(void);
 /* Byte offset, inside the geometry buffer of this thread's last
  * wgsr_rasterize_forward call, of its depth order: P uint32 Gaussian ids by
  * ascending view-space depth (ties in index order, culled Gaussians last) --
- * the order upstream's (tile | depth) key sort gives every tile list.  The
- * depth sort runs three passes over the visible key range (WGSR_DEPTH_SORT=
- * full: four 8-bit passes over the whole keys), so where it lands varies. */
+ * the order upstream's (tile | depth) key sort gives every tile list.  Only
+ * WGSR_DEPTH_SORT=global (three passes over the visible key range) or =full
+ * (four 8-bit passes over the whole keys), or sort bins off, produce one;
+ * where it lands varies.  -1 when the last forward had none: by default the
+ * entries of every sort bin are ordered by depth after the bin sort. */
 int64_t wgsr_depth_order_offset(void);
 
 #ifdef __cplusplus

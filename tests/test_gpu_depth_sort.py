@@ -1,6 +1,14 @@
-"""The depth sort over the visible key range (csrc/sort.hip launch_depth_sort,
-DepthKeyPlan in csrc/wgsr_common.h) against the four 8-bit passes over the
-whole 32-bit keys (WGSR_DEPTH_SORT=full).
+"""The depth orderings of the forward against each other:
+
+* the Gaussian-level depth sort over the visible key range (csrc/sort.hip
+  launch_depth_sort, DepthKeyPlan in csrc/wgsr_common.h; WGSR_DEPTH_SORT=
+  global) against the four 8-bit passes over the whole 32-bit keys
+  (WGSR_DEPTH_SORT=full): identical depth order and outputs;
+* the default, per-bin depth sort after the bin sort (csrc/raster_fwd.hip
+  k_bin_depth_sort: pairs duplicated in index order, every sort bin ordered by
+  depth key, ties by index), which has no Gaussian-level order: every raster
+  output bit-identical to the global schedules, incl. bins larger than one
+  LDS tile (the chunked pass through global scratch).
 
 Both are stable sorts of the same keys, so the depth order (rank -> Gaussian,
 read from the geometry buffer at wgsr_depth_order_offset()) and every raster
@@ -45,41 +53,49 @@ def _scene(P, zlo, zhi, seed=0, far=0, behind=0, ties=0, log_z=False):
     return means, scales, q, opac, shs
 
 
-def _forward(scene):
+def _forward(scene, w=W, h=H):
     from diff_gaussian_rasterization import _C
     from wgsr import _lib
     from wgsr.camera import synthetic_camera
-    f = synthetic_camera(W, H, 0).raster_fields()
+    f = synthetic_camera(w, h, 0).raster_fields()
     d = lambda x: x.to(DEV).contiguous()  # noqa: E731
     means, scales, q, opac, shs = (d(x) for x in scene)
     e = torch.empty(0, device=DEV)
     out = _C.rasterize_gaussians(d(torch.zeros(3)), means, e, opac, scales, q, 1.0, e, d(f["viewmatrix"]),
-                                 d(f["projmatrix"]), d(f["projmatrix_raw"]), f["tanfovx"], f["tanfovy"], H, W,
+                                 d(f["projmatrix"]), d(f["projmatrix_raw"]), f["tanfovx"], f["tanfovy"], h, w,
                                  shs, 0, d(f["campos"]), False, False)
     torch.cuda.synchronize()
     off = int(_lib.load().wgsr_depth_order_offset())
     geom = out[3]
     P = means.shape[0]
-    order = geom[off:off + 4 * P].cpu().numpy().view(np.uint32).copy()
+    order = geom[off:off + 4 * P].cpu().numpy().view(np.uint32).copy() if off >= 0 else None
     res = dict(num_rendered=out[0], color=out[1].cpu().numpy(), radii=out[2].cpu().numpy(),
                depth=out[6].cpu().numpy(), opacity=out[7].cpu().numpy(), n_touched=out[8].cpu().numpy())
     return order, res
 
 
-def _compare(scene, monkeypatch):
+def _same_outputs(ra, rb, tag):
+    for k, v in ra.items():
+        if k == "num_rendered":
+            assert rb[k] == v, tag
+        else:
+            np.testing.assert_array_equal(rb[k], v, err_msg=f"{tag}: {k}")
+
+
+def _compare(scene, monkeypatch, w=W, h=H):
     outs = {}
-    for mode in ("full", "range"):
+    # (bins: the per-bin sort whatever the bins' load -- no fallback)
+    monkeypatch.setenv("WGSR_BIN_DEPTH_MAX_AVG", str(1 << 40))
+    for mode in ("full", "global", "bins"):
         monkeypatch.setenv("WGSR_DEPTH_SORT", mode)
-        outs[mode] = _forward(scene)
-    (o_full, r_full), (o_rng, r_rng) = outs["full"], outs["range"]
+        outs[mode] = _forward(scene, w, h)
+    (o_full, r_full), (o_rng, r_rng), (o_bins, r_bins) = outs["full"], outs["global"], outs["bins"]
     P = scene[0].shape[0]
     assert np.array_equal(np.sort(o_rng), np.arange(P, dtype=np.uint32))  # a permutation
     np.testing.assert_array_equal(o_rng, o_full)
-    for k, v in r_full.items():
-        if k == "num_rendered":
-            assert r_rng[k] == v
-        else:
-            np.testing.assert_array_equal(r_rng[k], v, err_msg=k)
+    assert o_bins is None  # (per-bin ordering: no Gaussian-level depth order)
+    _same_outputs(r_full, r_rng, "global vs full")
+    _same_outputs(r_full, r_bins, "bins vs full")
     return o_rng, r_full
 
 
@@ -126,7 +142,7 @@ def test_depth_order_is_by_depth_then_index(monkeypatch):
     """Independently of the full-key sort: the visible Gaussians come first,
     by non-decreasing view depth (the splat's depth word), equal depths in
     index order."""
-    monkeypatch.setenv("WGSR_DEPTH_SORT", "range")
+    monkeypatch.setenv("WGSR_DEPTH_SORT", "global")
     scene = _scene(50_000, 0.4, 20.0, behind=500, ties=3_000, log_z=True)
     order, res = _forward(scene)
     z = scene[0][:, 2].numpy().astype(np.float32)
@@ -138,3 +154,48 @@ def test_depth_order_is_by_depth_then_index(monkeypatch):
     same = np.diff(zs) == 0
     assert np.all(np.diff(order[:nv].astype(np.int64))[same] > 0)
     np.testing.assert_array_equal(order[nv:], np.sort(order[nv:]))
+
+
+def _clustered(P, cx, cy, spread, seed=3):
+    """P small Gaussians whose centres fall inside a few pixels around
+    (cx, cy) of the W x H view: one sort bin holds (nearly) all of them."""
+    means, scales, q, opac, shs = _scene(P, 1.0, 6.0, seed=seed, ties=P // 10, log_z=True)
+    z = means[:, 2]
+    tanx = 1.0 / (2.0 * 0.9)
+    tany = H / (2.0 * 0.9 * W)
+    g = torch.Generator().manual_seed(seed + 1)
+    u = (cx + spread * (torch.rand(P, generator=g) - 0.5)) / W * 2 - 1
+    v = (cy + spread * (torch.rand(P, generator=g) - 0.5)) / H * 2 - 1
+    means = torch.stack([u * z * tanx, v * z * tany, z], dim=1)
+    means[P - P // 10:] = means[:P // 10]  # exact ties
+    return means, scales * 0.05, q, opac, shs
+
+
+@pytest.mark.parametrize("P", [9_000, 40_000])
+def test_bin_beyond_one_lds_tile(P, monkeypatch):
+    """A bin with more entries than k_bin_depth_sort sorts in LDS (8192):
+    the chunked passes through global scratch give the same images."""
+    _compare(_clustered(P, 200.0, 150.0, 6.0), monkeypatch)
+
+
+def test_bin_sort_1080p_bins(monkeypatch):
+    """4 x 4-tile bins (frames beyond 2048 tiles), with one crowded bin."""
+    a = _scene(150_000, 0.5, 9.0, behind=1_000, ties=5_000, log_z=True)
+    b = _clustered(20_000, 300.0, 200.0, 10.0, seed=9)
+    scene = tuple(torch.cat([x, y]) for x, y in zip(a, b))
+    _compare(scene, monkeypatch, 1920, 1080)
+
+
+def test_bins_too_full_fall_back_to_the_gaussian_sort(monkeypatch):
+    """Above WGSR_BIN_DEPTH_MAX_AVG entries per bin the host, at its one wait,
+    queues the Gaussian-level depth sort and redoes the scan in depth order:
+    the same outputs as the global schedule (and a depth order again)."""
+    scene = _scene(60_000, 0.3, 12.0, behind=600, ties=2_000, log_z=True)
+    monkeypatch.setenv("WGSR_DEPTH_SORT", "global")
+    o_glob, r_glob = _forward(scene)
+    monkeypatch.setenv("WGSR_DEPTH_SORT", "bins")
+    monkeypatch.setenv("WGSR_BIN_DEPTH_MAX_AVG", "0")
+    o_fb, r_fb = _forward(scene)
+    assert o_fb is not None
+    np.testing.assert_array_equal(o_fb, o_glob)
+    _same_outputs(r_glob, r_fb, "fallback vs global")

@@ -54,7 +54,7 @@ for s in $STEPS; do
         lname=${v%%:*}; envset=""; tag=$lname
         if [ "$v" != "$lname" ]; then envset=${v#*:}; tag=${lname}_${envset//=/_}; fi
         if [ "$lname" = base ]; then lib=wildgs-slam-blackwell_amd/lib/libwgsr.so; else lib=wildgs-slam-blackwell_amd/lib/variants/$lname.so; fi
-        env WGSR_LIB=$lib $envset timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${tag}_$rep.json 2> $OUT/ab_${tag}_$rep.err; rc=$?
+        env WGSR_LIB=$lib $envset timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/ab_${tag}${SFX:-}_$rep.json 2> $OUT/ab_${tag}${SFX:-}_$rep.err; rc=$?
         if [ $rc -ne 0 ]; then break 2; fi
       done; done ;;
     knnab)

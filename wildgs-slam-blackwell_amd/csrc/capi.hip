@@ -196,14 +196,38 @@ int bin_shift(const wgsr_raster_args& a) {
 // 32-bit keys (the reference schedule for A/B runs and the parity tests);
 // default: three passes over the visible key range (launch_depth_sort)
 bool depth_sort_full() {
-  const char* e = getenv("WGSR_DEPTH_SORT");  // read per call: tests compare both
+  const char* e = getenv("WGSR_DEPTH_SORT");  // read per call: tests compare the modes
   return e && strcmp(e, "full") == 0;
+}
+// With sort bins the default orders each bin's entries by depth after the bin
+// sort (k_bin_depth_sort: the pairs are duplicated in index order, no
+// Gaussian depth order exists); WGSR_DEPTH_SORT=global|full keeps the
+// Gaussian-level depth sort ahead of the duplication (the previous schedule,
+// and the one whose depth order wgsr_depth_order_offset exposes).
+// Default for small frames (<= kSmallFrameTiles tiles, e.g. TUM's 512 x 384:
+// bins of ~1k entries, one LDS-resident sort each); larger frames keep the
+// Gaussian-level sort (their 4 x 4-tile bins hold several thousand entries
+// each, where the per-bin passes cost more than the global ones).
+// WGSR_DEPTH_SORT=bins forces it on whenever sort bins are on.
+// ... unless the bins average more than this many entries (the host sees the
+// bin-pair count at its one wait and then falls back to the Gaussian-level
+// sort; WGSR_BIN_DEPTH_MAX_AVG overrides)
+size_t bin_depth_max_avg() {
+  const char* e = getenv("WGSR_BIN_DEPTH_MAX_AVG");  // (per call: tests force the fallback)
+  return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)6144;
+}
+bool depth_sort_bins(const wgsr_raster_args& a, int bshift) {
+  if (!bshift) return false;
+  const char* e = getenv("WGSR_DEPTH_SORT");
+  if (e && (strcmp(e, "full") == 0 || strcmp(e, "global") == 0)) return false;
+  if (e && strcmp(e, "bins") == 0) return true;
+  return Grid(a).nt <= kSmallFrameTiles;
 }
 constexpr int kDepthBits = 32;
 constexpr bool kFullDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;
 // byte offset of the last forward's depth order (rank -> Gaussian) in its
 // geometry buffer (wgsr_depth_order_offset)
-thread_local size_t g_depth_order_off = 0;
+thread_local int64_t g_depth_order_off = -1;  // -1: no depth order (bin_depth)
 
 int validate(const wgsr_raster_args* a) {
   if (!a) return set_error(WGSR_EINVAL, "null args");
@@ -272,7 +296,7 @@ int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset) {
 
 const char* wgsr_profile_stage_name(int i) { return (i >= 0 && i < WGSR_NUM_STAGES) ? kStageNames[i] : ""; }
 const char* wgsr_version(void) { return "wgsr 0.1 gfx950"; }
-int64_t wgsr_depth_order_offset(void) { return (int64_t)g_depth_order_off; }
+int64_t wgsr_depth_order_offset(void) { return g_depth_order_off; }
 
 size_t wgsr_geometry_bytes(int P) { return GeomLayout((size_t)(P > 0 ? P : 0)).total; }
 size_t wgsr_binning_bytes(int64_t N, int W, int H) {
@@ -319,10 +343,12 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   const Bins bins(grid.gx, grid.gy, bshift);
   // the depth sort's superblock sums are zeroed by k_preprocess's workgroups
   // (no memset launch), and so is the next forward's counter block
-  const bool full_depth = depth_sort_full();
+  bool bin_depth = depth_sort_bins(a, bshift);
+  const bool full_depth = !bin_depth && depth_sort_full();
   size_t sup_off = 0;
-  const size_t sup_words = full_depth ? sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off)
-                                      : depth_sort_sup_words((size_t)a.P);
+  const size_t sup_words = bin_depth    ? 0
+                           : full_depth ? sort_sup_words((size_t)a.P, 0, kDepthBits, &sup_off)
+                                        : depth_sort_sup_words((size_t)a.P);
   if (!full_depth) sup_off = depth_sort_sup_offset_words((size_t)a.P);
   ZeroJob zj{};
   if (dc) {
@@ -359,7 +385,9 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // waits for them, allocates the binning buffer and queues the rest.
   HostCounters& hc = host_counters();
   if (!hc.buf || !hc.ev) return set_error(WGSR_EHIP, "pinned counter buffer / event allocation failed");
-  if (hc.side) {
+  // (with the per-bin depth sort nothing would overlap the copy on the side
+  // stream, whose start waits out an event round trip: copy in stream order)
+  if (hc.side && !bin_depth) {
     HIPCHK(hipEventRecord(hc.pre, s));
     HIPCHK(hipStreamWaitEvent(hc.side, hc.pre, 0));
     HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, hc.side));
@@ -369,8 +397,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     HIPCHK(hipEventRecord(hc.ev, s));
   }
   // depth order of the Gaussians (culled ones carry key 0xFFFFFFFF -> last)
-  const uint32_t* depth_order = nullptr;
-  { StageTimer T(1, s);
+  const uint32_t* depth_order = nullptr;  // null: index order (bin_depth)
+  if (!bin_depth) { StageTimer T(1, s);
   if (full_depth) {
     bool in_alt = false;
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
@@ -406,7 +434,32 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   HIPCHK(hipEventSynchronize(hc.ev));
   sync_on_error.armed = false;
   const uint32_t* host_counter = hc.buf;
-  if (!full_depth) {
+  const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
+  // upstream num_rendered, exact (Gaussian, tile) pairs (<= N_rect), (Gaussian, bin) pairs
+  size_t N_rect = 0, N = 0, N_bin = 0;
+  for (int i = 0; i < kRectPairLanes; ++i) {
+    N_rect += partial[i];
+    N += partial[kRectPairLanes + i];
+    N_bin += partial[2 * kRectPairLanes + i];
+  }
+  if (bin_depth && N_bin > bin_depth_max_avg() * (size_t)bins.n) {
+    // bins too full for one LDS-resident sort each: the Gaussian-level depth
+    // sort after all (queued now, with its scratch zeroed and the scan redone
+    // in depth order)
+    bin_depth = false;
+    StageTimer T(1, s);
+    HIPCHK(hipMemsetAsync(at<uint32_t>(geom, GL.hist) + depth_sort_sup_offset_words((size_t)a.P), 0,
+                          4 * depth_sort_sup_words((size_t)a.P), s));
+    STAGE(a, s, launch_depth_sort(at<uint32_t>(geom, GL.dkey), at<uint32_t>(geom, GL.dkey_alt),
+                                  at<uint32_t>(geom, GL.dval), at<uint32_t>(geom, GL.dval_alt), (size_t)a.P,
+                                  counter + kDepthRangeOffset / 4, counter + 2, at<uint32_t>(geom, GL.hist), s));
+    depth_order = at<uint32_t>(geom, GL.dval_alt);
+    if (scan_sup)
+      HIPCHK(hipMemsetAsync(at<uint2>(geom, GL.bsup), 0,
+                            sizeof(uint2) * kScanSupStride * packed_scan_supers((size_t)a.P), s));
+    if (int e = queue_scan()) return e;
+  }
+  if (!full_depth && !bin_depth) {
     // depths spanning more than the three passes' bits: one more stable pass
     // over the bits above them, then the scan again in the final order
     const uint32_t* rw = host_counter + kDepthRangeOffset / 4;
@@ -430,17 +483,11 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       if (int e = queue_scan()) return e;
     }
   }
-  g_depth_order_off = (size_t)(reinterpret_cast<const uint8_t*>(depth_order) - static_cast<const uint8_t*>(geom));
+  g_depth_order_off = depth_order ? (int64_t)(reinterpret_cast<const uint8_t*>(depth_order) -
+                                              static_cast<const uint8_t*>(geom))
+                                  : (int64_t)-1;
   if (host_counter[1] && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
-  const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
-  // upstream num_rendered, exact (Gaussian, tile) pairs (<= N_rect), (Gaussian, bin) pairs
-  size_t N_rect = 0, N = 0, N_bin = 0;
-  for (int i = 0; i < kRectPairLanes; ++i) {
-    N_rect += partial[i];
-    N += partial[kRectPairLanes + i];
-    N_bin += partial[2 * kRectPairLanes + i];
-  }
   if (N > N_rect) return set_error(WGSR_EHIP, "internal: exact tile lists exceed the rectangles");
   if (N_bin > N_rect) return set_error(WGSR_EHIP, "internal: bin pairs exceed the rectangles");
 
@@ -449,9 +496,14 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // sort bins the per-tile lists follow it (2^2s entries per bin pair)
   const BinLayout BL(N_rect);
   const size_t lists_bytes = bshift ? align256(4 * ((size_t)N_bin << (2 * bshift))) : 0;
-  void* binning = call_alloc(binning_alloc, ctx, BL.total + lists_bytes);
-  if (!binning && BL.total + lists_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  // per-bin depth sort: the pairs' depth keys ride the bin sort as a second
+  // payload, in two arrays after the lists
+  const size_t pdep_words = bin_depth ? align256(4 * N_bin) / 4 : 0;
+  void* binning = call_alloc(binning_alloc, ctx, BL.total + lists_bytes + 8 * pdep_words);
+  if (!binning && BL.total + lists_bytes + pdep_words) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   uint32_t* lists = bshift ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
+  uint32_t* pdep = bin_depth ? at<uint32_t>(binning, BL.total + lists_bytes) : nullptr;
+  uint32_t* pdep_alt = bin_depth ? pdep + pdep_words : nullptr;
   uint2* ranges = at<uint2>(image, IL.ranges);
   // sorted pairs: (Gaussian, bin) pairs, or with bin shift 0 the exact
   // (Gaussian, tile) pairs themselves
@@ -476,7 +528,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bshift) {
       // (the backward's record flags live on the exact slots: zeroed here too)
       STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
-                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s));
+                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, odd ? pdep_alt : pdep));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
@@ -488,14 +540,28 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false,
                                  NL, 0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s,
-                                 &talt, bin_bounds, &bounds_done, bs_words != 0)); }
+                                 &talt, bin_bounds, &bounds_done, bs_words != 0, odd ? pdep_alt : pdep,
+                                 odd ? pdep : pdep_alt)); }
     // the Gaussian ids are the payload; the backward recomputes each pair's
     // record slot from (Gaussian, tile) instead of carrying it through the sort
     if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
     const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
+    const uint32_t* sorted_gid = at<uint32_t>(binning, BL.point_g);
+    if (bin_depth) {
+      // each bin by depth, into the spare key / payload buffers; scratch for
+      // bins beyond one LDS tile: the list region (>= 16 NL bytes)
+      StageTimer T(4, s);
+      uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
+      uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
+      STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift, at<uint2>(image, IL.tile_m),
+                                        bounds_done, pdep, okeys, ogid, lists, s));
+      bounds_done = true;
+      sorted_keys = okeys;
+      sorted_gid = ogid;
+    }
     StageTimer T(5, s);
     if (bshift) {
-      STAGE(a, s, launch_expand_bins(a, sorted_keys, at<uint32_t>(binning, BL.point_g), (uint32_t)NL, bshift,
+      STAGE(a, s, launch_expand_bins(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift,
                                      at<uint2>(image, IL.tile_m), bounds_done, lists, ranges,
                                      at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta), s));
     } else {

@@ -403,13 +403,14 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     uint32_t P, int bshift, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
-    uint32_t* __restrict__ vals, const ZeroJob zero) {
+    uint32_t* __restrict__ vals, const ZeroJob zero, const uint32_t* __restrict__ dkey,
+    uint32_t* __restrict__ pair_depth) {
   constexpr int NW = kDupScanThreads / 64;
   __shared__ uint2 s_w[NW], s_p[NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
-  const uint32_t g = in ? sorted_g[r] : 0u;
+  const uint32_t g = in ? (sorted_g ? sorted_g[r] : r) : 0u;  // (null: index order)
   // the whole 32-byte list record in one round trip (row table + rect, tb,
   // list length: one cache line)
   uint4 lw = make_uint4(0u, 0u, 0u, 0u), tab = lw;
@@ -419,6 +420,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   }
   const uint32_t v = lw.z;
   const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
+  const uint32_t dk = pair_depth && in && nb ? dkey[g] : 0u;  // (per-bin depth sort input)
   uint32_t rlo = 0, rhi = 0;
   bool tall = false;
   if (nb) {
@@ -507,9 +509,11 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     const int bx0 = x0 >> bshift, bw = ((x1 - 1) >> bshift) - bx0 + 1;
     const int row = (int)local / bw;
     const int bx = bx0 + ((int)local - row * bw), by = (y0 >> bshift) + row;
+    const uint32_t pd = pair_depth ? (uint32_t)__shfl((int)dk, lo, 64) : 0u;
     if (k < end) {
       keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, tl, rg) << 16);
       vals[k] = gg;
+      if (pair_depth) pair_depth[k] = pd;
     }
   }
 }
@@ -604,6 +608,286 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
       tile_len[tile] = c;
     }
   }
+}
+
+// ---- per-bin depth sort (the default with sort bins) ---------------------------
+// With the Gaussians duplicated in INDEX order (no global depth sort), the
+// stable bin sort leaves every bin's entries in index order, one entry per
+// Gaussian.  Sorting each bin stably by depth key then yields exactly the
+// order a stable global depth sort leaves inside the bin: depth bits, ties by
+// Gaussian index -- upstream's (tile | depth) key order with cub's stable tie
+// order.  One 512-thread workgroup per bin: the bin's depth
+// keys minus their minimum (R bits) are LSD-radix sorted in LDS, ceil(R / 9)
+// stable passes of <= 9-bit digits, each entry's position in the bin riding
+// along; the (key, Gaussian) pairs are then gathered in that order into the
+// spare key / payload buffers.  A bin of more than kBdsCap entries runs the
+// same passes chunk by chunk through global scratch (the sort-bin list
+// region, free until k_expand_bins writes it).
+constexpr int kBdsThreads = 512, kBdsWaves = kBdsThreads / 64, kBdsItems = 14;
+constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
+constexpr int kBdsMaxBits = 9, kBdsDigits = 1 << kBdsMaxBits;
+static_assert(kBdsDigits == kBdsThreads, "one digit per thread");
+
+struct BdsLds {
+  uint2 buf[kBdsCap];                     // (depth key, position in the bin)
+  uint32_t wcnt[kBdsWaves][kBdsDigits];   // per wave digit counts, then their prefix over waves
+  uint32_t base[kBdsDigits];              // per digit: first slot
+  uint32_t tmp[kBdsWaves];
+  uint32_t rng[2][kBdsWaves];
+};
+
+__device__ __forceinline__ uint32_t bds_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) s_tmp[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kBdsWaves; ++i) {
+    const uint32_t x = s_tmp[i];
+    base += i < w ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+// wave w owns the cn entries' slots [w pw, w pw + pw) (pw a multiple of 64,
+// so all eight waves share the work), walked 64 at a time: ranks follow slot
+// order (stable).  pk[j] packs the entry's position in the bin (bits 0-12),
+// its digit (13-21) and its rank among the wave's entries of that digit
+// (22-31, < 14 x 64); bds_rank fills bits 13-31.
+constexpr int kBdsPosBits = 13, kBdsRankShift = kBdsPosBits + kBdsMaxBits;
+static_assert(kBdsCap <= (1 << kBdsPosBits) && kBdsItems * 64 <= (1 << (32 - kBdsRankShift)), "pk packing");
+__device__ __forceinline__ uint32_t bds_digit(uint32_t pk) { return (pk >> kBdsPosBits) & (kBdsDigits - 1); }
+template <int JN>
+__device__ __forceinline__ void bds_rank(BdsLds& L, uint32_t cn, uint32_t mn, int shift, int bits,
+                                         const uint32_t (&k)[JN], uint32_t (&pk)[JN]) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+    const bool valid = le < cn;
+    const uint32_t d = ((k[j] - mn) >> shift) & mask;
+    const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    uint32_t old = 0;
+    if (valid && lane == leader) old = atomicAdd(&L.wcnt[w][d], (uint32_t)__popcll(peers));
+    old = (uint32_t)__shfl((int)old, leader & 63, 64);
+    const uint32_t rk = old + lanes_below(peers);
+    pk[j] = (pk[j] & ((1u << kBdsPosBits) - 1u)) | (d << kBdsPosBits) | (rk << kBdsRankShift);
+    __builtin_amdgcn_sched_barrier(0);  // one entry group at a time: few live registers
+  }
+}
+__device__ __forceinline__ uint32_t bds_slot(const BdsLds& L, uint32_t pk) {
+  const int w = threadIdx.x >> 6;
+  const uint32_t d = bds_digit(pk);
+  return L.base[d] + L.wcnt[w][d] + (pk >> kBdsRankShift);
+}
+
+// thread t (digit t): the waves' counts -> their exclusive prefix in place;
+// returns the digit's total
+__device__ __forceinline__ uint32_t bds_wave_prefix(BdsLds& L) {
+  const int t = threadIdx.x;
+  uint32_t run = 0;
+#pragma unroll
+  for (int q = 0; q < kBdsWaves; ++q) {
+    const uint32_t x = L.wcnt[q][t];
+    L.wcnt[q][t] = run;
+    run += x;
+  }
+  return run;
+}
+
+// Scratch written by other waves of this workgroup in the previous pass: the
+// workgroup barrier orders it (same CU, so the vector L1 is coherent for
+// them; an agent-scope fence would write back and invalidate the whole L2).
+__device__ __forceinline__ uint2 bds_load_scratch(const uint2* p) { return *p; }
+
+// a bin of n <= 64 JN x kBdsWaves entries: wave w owns slots [w JN 64,
+// (w + 1) JN 64), JN entries per lane in registers, every pass ranked in LDS
+template <int JN>
+__device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict__ skeys,
+                                          const uint32_t* __restrict__ sgid, const uint32_t* __restrict__ sdep,
+                                          uint32_t lo, uint32_t n, uint32_t mn, int R, int npass, int pbits,
+                                          uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  constexpr uint32_t kPosMask = (1u << kBdsPosBits) - 1u;
+  uint32_t k[JN], pk[JN];
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+    pk[j] = le;
+    k[j] = le < n ? sdep[lo + le] : 0u;
+  }
+  for (int p = 0; p < npass; ++p) {
+    const int shift = p * pbits, bits = min(pbits, R - shift);
+    bds_rank<JN>(L, n, mn, shift, bits, k, pk);
+    __syncthreads();
+    uint32_t all;
+    const uint32_t ex = bds_excl_scan(bds_wave_prefix(L), L.tmp, &all);
+    L.base[t] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+      if (le < n) L.buf[bds_slot(L, pk[j])] = make_uint2(k[j], pk[j] & kPosMask);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+      if (le < n) {
+        const uint2 kv = L.buf[le];
+        k[j] = kv.x;
+        pk[j] = kv.y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+    if (le < n) {
+      const uint32_t q = pk[j] & kPosMask;
+      okeys[lo + le] = skeys[lo + q];
+      ogid[lo + le] = sgid[lo + q];
+    }
+  }
+}
+
+// a bin beyond the LDS tile: each pass counts its digits over the whole bin,
+// then ranks kBdsCap-entry chunks in order with running digit bases, the
+// (key, position) pairs ping-ponging through global scratch
+__device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid,
+                                     const uint32_t* __restrict__ sdep, uint32_t lo, uint32_t n, uint32_t NL,
+                                     uint32_t mn, int R, int passes, int pbits, uint32_t* __restrict__ okeys,
+                                     uint32_t* __restrict__ ogid, uint2* scratch) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  constexpr int JN = 7;  // (chunks of half the LDS tile: fewer registers)
+  constexpr uint32_t kChunk = JN * kBdsThreads;
+  uint2* bufA = scratch + lo;
+  uint2* bufB = scratch + NL + lo;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = p * pbits, bits = min(pbits, R - shift);
+    const uint32_t mask = (1u << bits) - 1u;
+    const uint2* src = (p & 1) ? bufA : bufB;  // pass p - 1's output
+    uint2* dst = (p & 1) ? bufB : bufA;
+    auto load = [&](uint32_t e) -> uint2 {
+      return p == 0 ? make_uint2(sdep[lo + e], e) : bds_load_scratch(src + e);
+    };
+    L.base[t] = 0u;
+    __syncthreads();
+    for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) atomicAdd(&L.base[((load(e).x - mn) >> shift) & mask], 1u);
+    __syncthreads();
+    {
+      uint32_t all;
+      const uint32_t c = L.base[t];
+      const uint32_t ex = bds_excl_scan(c, L.tmp, &all);
+      L.base[t] = ex;
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+      const uint32_t cn = min(kChunk, n - c0);
+      uint32_t k[JN], pk[JN], pos[JN];  // (positions beyond the 13 bits of pk)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+        k[j] = 0u;
+        pos[j] = 0u;
+        pk[j] = 0u;
+        if (le < cn) {
+          const uint2 kv = load(c0 + le);
+          k[j] = kv.x;
+          pos[j] = kv.y;
+        }
+      }
+      bds_rank<JN>(L, cn, mn, shift, bits, k, pk);
+      __syncthreads();
+      const uint32_t tot = bds_wave_prefix(L);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+        if (le < cn) dst[bds_slot(L, pk[j])] = make_uint2(k[j], pos[j]);
+      }
+      __syncthreads();
+      L.base[t] += tot;
+#pragma unroll
+      for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  const uint2* fin = ((passes - 1) & 1) ? bufB : bufA;
+  for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
+    const uint32_t q = bds_load_scratch(fin + e).y;
+    okeys[lo + e] = skeys[lo + q];
+    ogid[lo + e] = sgid[lo + q];
+  }
+}
+
+__global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
+    const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid, const uint2* __restrict__ bounds,
+    const uint32_t* __restrict__ sdep, uint32_t NL, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid,
+    uint2* scratch) {
+  __shared__ BdsLds L;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint2 bb = bounds[blockIdx.x];
+  const uint32_t lo = bb.x, n = bb.y - bb.x;
+  if (n == 0) return;  // block-uniform
+#pragma unroll
+  for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
+  // the bin's key range -> pass plan
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
+    const uint32_t x = sdep[lo + e];
+    mn = min(mn, x);
+    mx = max(mx, x);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  }
+  if (lane == 0) {
+    L.rng[0][w] = mn;
+    L.rng[1][w] = mx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kBdsWaves; ++q) {
+    mn = min(mn, L.rng[0][q]);
+    mx = max(mx, L.rng[1][q]);
+  }
+  const uint32_t span = mx - mn;
+  const int R = span ? 32 - __clz((int)span) : 0;
+  const int passes = (R + kBdsMaxBits - 1) / kBdsMaxBits;
+  const int pbits = passes ? (R + passes - 1) / passes : 0;
+#ifdef WGSR_BDS_DIAG_PASSES  // timing diagnostics only (wrong order)
+  const int npass = min(passes, WGSR_BDS_DIAG_PASSES);
+#else
+  const int npass = passes;
+#endif
+  if (n <= 2u * kBdsThreads)
+    bds_small<2>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+  else if (n <= 4u * kBdsThreads)
+    bds_small<4>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+  else if (n <= 7u * kBdsThreads)
+    bds_small<7>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+  else if (n <= (uint32_t)kBdsCap)
+    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+  else if (passes == 0)
+    for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
+      okeys[lo + e] = skeys[lo + e];
+      ogid[lo + e] = sgid[lo + e];
+    }
+  else
+    bds_big(L, skeys, sgid, sdep, lo, n, NL, mn, R, passes, pbits, okeys, ogid, scratch);
 }
 
 // ---- tile ranges and the tiles' launch order ---------------------------------
@@ -1101,7 +1385,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s) {
+                                 hipStream_t s, uint32_t* pair_depth) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
@@ -1109,7 +1393,8 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
                      s, (uint32_t)a.P, bshift, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
-                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero);
+                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, at<uint32_t>(geom, L.dkey),
+                     pair_depth);
   return hipGetLastError();
 }
 
@@ -1125,6 +1410,21 @@ hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_
   }
   hipLaunchKernelGGL(k_expand_bins, dim3((uint32_t)B.n << bshift), dim3(kExpThreads), 0, s, sorted_keys, sorted_g, bounds, gx,
                      gy, bshift, B.bx, lists, ranges, tile_len, meta);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
+                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
+                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s) {
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  const Bins B(gx, gy, bshift);
+  if (!bounds_done) {  // (a one-pass sort already wrote them)
+    hipError_t e = hipMemsetAsync(bounds, 0, sizeof(uint2) * (size_t)B.n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
+  }
+  hipLaunchKernelGGL(k_bin_depth_sort, dim3((uint32_t)B.n), dim3(kBdsThreads), 0, s, sorted_keys, sorted_g, bounds,
+                     sdepth, NB, okeys, ogid, static_cast<uint2*>(scratch));
   return hipGetLastError();
 }
 

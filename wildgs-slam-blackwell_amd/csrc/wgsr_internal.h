@@ -20,7 +20,10 @@ int radix_passes(int begin_bit, int end_bit);
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt,
-                            uint2* digit_bounds = nullptr, bool* bounds_done = nullptr, bool sup_zeroed = false);
+                            uint2* digit_bounds = nullptr, bool* bounds_done = nullptr, bool sup_zeroed = false,
+                            uint32_t* xvals = nullptr, uint32_t* xvals_alt = nullptr);
+// (xvals / xvals_alt: an optional second payload, moved like vals and ending
+// in the same buffer parity; reduce-then-scan schedule)
 // words of `status` a reduce-then-scan sort accumulates superblock sums in
 // (zero before the sort; 0 = none), at *offset_words
 size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words);
@@ -73,9 +76,17 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 // Gaussian) pair expansion.
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s);
+                                 hipStream_t s, uint32_t* pair_depth = nullptr);
+// (pair_depth: each pair's depth key too -- the per-bin depth sort's input)
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
+// per-bin depth sort (pairs duplicated in index order): every bin's entries
+// stably by depth key (sdepth: the pairs' depth keys in bin-sorted order) ->
+// okeys / ogid (bounds written first unless bounds_done); scratch: >= 2 NB
+// uint2 (bins beyond one LDS tile)
+hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
+                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
+                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s);
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
 // tile, the lists in bin-sized regions of `lists` (2^2s x NB entries)
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
