@@ -40,6 +40,7 @@ STAGE_OF = {
     "k_duplicate_bins": "duplicate", "k_bin_bounds": "ranges", "k_expand_bins": "ranges",
     "k_render_bwd_split": "render_bwd", "k_sum_active": "gauss_bwd", "k_gauss_bwd_compact": "gauss_bwd",
     "k_depth_hist": "depth_sort", "k_depth_scatter": "depth_sort",
+    "k_bin_depth_sort": "tile_sort",  # (per-bin depth order: small frames)
 }
 
 
@@ -97,7 +98,8 @@ def main():
     # grid size of the depth-sort radix kernels: the smallest radix scatter grid
     # (the depth sort's own k_depth_* kernels: then every k_radix_* is the bin sort)
     rg = [g for (k, g) in keys if k == "k_radix_scatter"]
-    P_grid = 0 if any(k.startswith("k_depth_") for (k, g) in keys) else (min(rg) if rg else 0)
+    # (the per-bin schedule has no Gaussian-level sort: every k_radix_* is the bin sort)
+    P_grid = 0 if any(k.startswith("k_depth_") or k == "k_bin_depth_sort" for (k, g) in keys) else (min(rg) if rg else 0)
     rows, stages = [], defaultdict(lambda: {"hbm_bytes_per_step": 0.0, "valu_insts_per_step": 0.0,
                                             "launches_per_step": 0.0, "launch_kinds": []})
     hdr = (f"{'kernel':18s} {'grid':>9s} {'FETCH_KB':>10s} {'WRITE_KB':>10s} {'HBM_MB*':>9s} "

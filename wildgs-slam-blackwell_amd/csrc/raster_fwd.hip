@@ -623,7 +623,10 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 // spare key / payload buffers.  A bin of more than kBdsCap entries runs the
 // same passes chunk by chunk through global scratch (the sort-bin list
 // region, free until k_expand_bins writes it).
-constexpr int kBdsThreads = 512, kBdsWaves = kBdsThreads / 64, kBdsItems = 14;
+#ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort (7 or 14)
+#define WGSR_BDS_ITEMS 14
+#endif
+constexpr int kBdsThreads = 512, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
 constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
 constexpr int kBdsMaxBits = 9, kBdsDigits = 1 << kBdsMaxBits;
 static_assert(kBdsDigits == kBdsThreads, "one digit per thread");
@@ -706,22 +709,60 @@ __device__ __forceinline__ uint32_t bds_wave_prefix(BdsLds& L) {
 // them; an agent-scope fence would write back and invalidate the whole L2).
 __device__ __forceinline__ uint2 bds_load_scratch(const uint2* p) { return *p; }
 
+// the bin's key range over the workgroup -> (min key, R = bits of the span)
+__device__ __forceinline__ uint32_t bds_range(BdsLds& L, uint32_t mn, uint32_t mx, int& R) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  }
+  if (lane == 0) {
+    L.rng[0][w] = mn;
+    L.rng[1][w] = mx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kBdsWaves; ++q) {
+    mn = min(mn, L.rng[0][q]);
+    mx = max(mx, L.rng[1][q]);
+  }
+  const uint32_t span = mx - mn;
+  R = span ? 32 - __clz((int)span) : 0;
+  return mn;
+}
+__device__ __forceinline__ void bds_plan(int R, int& passes, int& pbits) {
+  passes = (R + kBdsMaxBits - 1) / kBdsMaxBits;
+  pbits = passes ? (R + passes - 1) / passes : 0;
+#ifdef WGSR_BDS_DIAG_PASSES  // timing diagnostics only (wrong order)
+  passes = min(passes, WGSR_BDS_DIAG_PASSES);
+#endif
+}
+
 // a bin of n <= 64 JN x kBdsWaves entries: wave w owns slots [w JN 64,
 // (w + 1) JN 64), JN entries per lane in registers, every pass ranked in LDS
 template <int JN>
 __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict__ skeys,
                                           const uint32_t* __restrict__ sgid, const uint32_t* __restrict__ sdep,
-                                          uint32_t lo, uint32_t n, uint32_t mn, int R, int npass, int pbits,
-                                          uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid) {
+                                          uint32_t lo, uint32_t n, uint32_t* __restrict__ okeys,
+                                          uint32_t* __restrict__ ogid) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   constexpr uint32_t kPosMask = (1u << kBdsPosBits) - 1u;
   uint32_t k[JN], pk[JN];
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     pk[j] = le;
     k[j] = le < n ? sdep[lo + le] : 0u;
+    if (le < n) {
+      mn = min(mn, k[j]);
+      mx = max(mx, k[j]);
+    }
   }
+  int R, npass, pbits;
+  mn = bds_range(L, mn, mx, R);
+  bds_plan(R, npass, pbits);
   for (int p = 0; p < npass; ++p) {
     const int shift = p * pbits, bits = min(pbits, R - shift);
     bds_rank<JN>(L, n, mn, shift, bits, k, pk);
@@ -765,9 +806,24 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
 // (key, position) pairs ping-ponging through global scratch
 __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid,
                                      const uint32_t* __restrict__ sdep, uint32_t lo, uint32_t n, uint32_t NL,
-                                     uint32_t mn, int R, int passes, int pbits, uint32_t* __restrict__ okeys,
-                                     uint32_t* __restrict__ ogid, uint2* scratch) {
+                                     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
+    const uint32_t x = sdep[lo + e];
+    mn = min(mn, x);
+    mx = max(mx, x);
+  }
+  int R, passes, pbits;
+  mn = bds_range(L, mn, mx, R);
+  bds_plan(R, passes, pbits);
+  if (passes == 0) {
+    for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
+      okeys[lo + e] = skeys[lo + e];
+      ogid[lo + e] = sgid[lo + e];
+    }
+    return;
+  }
   constexpr int JN = 7;  // (chunks of half the LDS tile: fewer registers)
   constexpr uint32_t kChunk = JN * kBdsThreads;
   uint2* bufA = scratch + lo;
@@ -836,58 +892,22 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     const uint32_t* __restrict__ sdep, uint32_t NL, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid,
     uint2* scratch) {
   __shared__ BdsLds L;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int t = threadIdx.x;
   const uint2 bb = bounds[blockIdx.x];
   const uint32_t lo = bb.x, n = bb.y - bb.x;
   if (n == 0) return;  // block-uniform
 #pragma unroll
-  for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
-  // the bin's key range -> pass plan
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
-    const uint32_t x = sdep[lo + e];
-    mn = min(mn, x);
-    mx = max(mx, x);
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-  }
-  if (lane == 0) {
-    L.rng[0][w] = mn;
-    L.rng[1][w] = mx;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kBdsWaves; ++q) {
-    mn = min(mn, L.rng[0][q]);
-    mx = max(mx, L.rng[1][q]);
-  }
-  const uint32_t span = mx - mn;
-  const int R = span ? 32 - __clz((int)span) : 0;
-  const int passes = (R + kBdsMaxBits - 1) / kBdsMaxBits;
-  const int pbits = passes ? (R + passes - 1) / passes : 0;
-#ifdef WGSR_BDS_DIAG_PASSES  // timing diagnostics only (wrong order)
-  const int npass = min(passes, WGSR_BDS_DIAG_PASSES);
-#else
-  const int npass = passes;
-#endif
+  for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
   if (n <= 2u * kBdsThreads)
-    bds_small<2>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+    bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
   else if (n <= 4u * kBdsThreads)
-    bds_small<4>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
+    bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
   else if (n <= 7u * kBdsThreads)
-    bds_small<7>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
-  else if (n <= (uint32_t)kBdsCap)
-    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, mn, R, npass, pbits, okeys, ogid);
-  else if (passes == 0)
-    for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
-      okeys[lo + e] = skeys[lo + e];
-      ogid[lo + e] = sgid[lo + e];
-    }
+    bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+  else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
+    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
   else
-    bds_big(L, skeys, sgid, sdep, lo, n, NL, mn, R, passes, pbits, okeys, ogid, scratch);
+    bds_big(L, skeys, sgid, sdep, lo, n, NL, okeys, ogid, scratch);
 }
 
 // ---- tile ranges and the tiles' launch order ---------------------------------
