@@ -626,10 +626,14 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 #ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort (7 or 14)
 #define WGSR_BDS_ITEMS 14
 #endif
-constexpr int kBdsThreads = 512, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
+#ifndef WGSR_BDS_THREADS  // workgroup size (512 or 1024)
+#define WGSR_BDS_THREADS 512
+#endif
+constexpr int kBdsThreads = WGSR_BDS_THREADS, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
 constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
 constexpr int kBdsMaxBits = 9, kBdsDigits = 1 << kBdsMaxBits;
-static_assert(kBdsDigits == kBdsThreads, "one digit per thread");
+static_assert(kBdsDigits <= kBdsThreads, "threads t < kBdsDigits own digit t");
+__device__ __forceinline__ bool bds_owns_digit() { return (int)threadIdx.x < kBdsDigits; }
 
 struct BdsLds {
   uint2 buf[kBdsCap];                     // (depth key, position in the bin)
@@ -695,6 +699,7 @@ __device__ __forceinline__ uint32_t bds_slot(const BdsLds& L, uint32_t pk) {
 __device__ __forceinline__ uint32_t bds_wave_prefix(BdsLds& L) {
   const int t = threadIdx.x;
   uint32_t run = 0;
+  if (!bds_owns_digit()) return 0u;
 #pragma unroll
   for (int q = 0; q < kBdsWaves; ++q) {
     const uint32_t x = L.wcnt[q][t];
@@ -769,7 +774,7 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
     __syncthreads();
     uint32_t all;
     const uint32_t ex = bds_excl_scan(bds_wave_prefix(L), L.tmp, &all);
-    L.base[t] = ex;
+    if (bds_owns_digit()) L.base[t] = ex;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
@@ -787,7 +792,8 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
       }
     }
 #pragma unroll
-    for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
+    for (int q = 0; q < kBdsWaves; ++q)
+      if (bds_owns_digit()) L.wcnt[q][t] = 0u;
     __syncthreads();
   }
 #pragma unroll
@@ -836,15 +842,15 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
     auto load = [&](uint32_t e) -> uint2 {
       return p == 0 ? make_uint2(sdep[lo + e], e) : bds_load_scratch(src + e);
     };
-    L.base[t] = 0u;
+    if (bds_owns_digit()) L.base[t] = 0u;
     __syncthreads();
     for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) atomicAdd(&L.base[((load(e).x - mn) >> shift) & mask], 1u);
     __syncthreads();
     {
       uint32_t all;
-      const uint32_t c = L.base[t];
+      const uint32_t c = bds_owns_digit() ? L.base[t] : 0u;
       const uint32_t ex = bds_excl_scan(c, L.tmp, &all);
-      L.base[t] = ex;
+      if (bds_owns_digit()) L.base[t] = ex;
     }
     __syncthreads();
     for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
@@ -872,9 +878,10 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
         if (le < cn) dst[bds_slot(L, pk[j])] = make_uint2(k[j], pos[j]);
       }
       __syncthreads();
-      L.base[t] += tot;
+      if (bds_owns_digit()) L.base[t] += tot;
 #pragma unroll
-      for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;
+      for (int q = 0; q < kBdsWaves; ++q)
+        if (bds_owns_digit()) L.wcnt[q][t] = 0u;
       __syncthreads();
     }
     __syncthreads();
@@ -897,8 +904,11 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
   const uint32_t lo = bb.x, n = bb.y - bb.x;
   if (n == 0) return;  // block-uniform
 #pragma unroll
-  for (int q = 0; q < kBdsWaves; ++q) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
-  if (n <= 2u * kBdsThreads)
+  for (int q = 0; q < kBdsWaves; ++q)
+    if (bds_owns_digit()) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
+  if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
+    bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+  else if (n <= 2u * kBdsThreads)
     bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
   else if (n <= 4u * kBdsThreads)
     bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
