@@ -204,11 +204,10 @@ bool depth_sort_full() {
 // Gaussian depth order exists); WGSR_DEPTH_SORT=global|full keeps the
 // Gaussian-level depth sort ahead of the duplication (the previous schedule,
 // and the one whose depth order wgsr_depth_order_offset exposes).
-// Default for small frames (<= kSmallFrameTiles tiles, e.g. TUM's 512 x 384:
-// bins of ~1k entries, one LDS-resident sort each); larger frames keep the
-// Gaussian-level sort (their 4 x 4-tile bins hold several thousand entries
-// each, where the per-bin passes cost more than the global ones).
-// WGSR_DEPTH_SORT=bins forces it on whenever sort bins are on.
+// The default whenever sort bins are on (A/B, ms/step: 100k 512x384 SH0
+// 0.218 -> 0.190; 200k / 500k / 1M at 1080p SH3 0.720 -> 0.674, 0.712 ->
+// 0.696, 0.807 -> 0.801).  WGSR_DEPTH_SORT=global|full keeps the
+// Gaussian-level sort.
 // ... unless the bins average more than this many entries (the host sees the
 // bin-pair count at its one wait and then falls back to the Gaussian-level
 // sort; WGSR_BIN_DEPTH_MAX_AVG overrides)
@@ -220,8 +219,8 @@ bool depth_sort_bins(const wgsr_raster_args& a, int bshift) {
   if (!bshift) return false;
   const char* e = getenv("WGSR_DEPTH_SORT");
   if (e && (strcmp(e, "full") == 0 || strcmp(e, "global") == 0)) return false;
-  if (e && strcmp(e, "bins") == 0) return true;
-  return Grid(a).nt <= kSmallFrameTiles;
+  (void)a;
+  return true;
 }
 constexpr int kDepthBits = 32;
 constexpr bool kFullDepthInAlt = ((kDepthBits + 7) / 8) % 2 == 1;

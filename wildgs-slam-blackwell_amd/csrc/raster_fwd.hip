@@ -624,10 +624,10 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 // same passes chunk by chunk through global scratch (the sort-bin list
 // region, free until k_expand_bins writes it).
 #ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort (7 or 14)
-#define WGSR_BDS_ITEMS 14
+#define WGSR_BDS_ITEMS 7
 #endif
 #ifndef WGSR_BDS_THREADS  // workgroup size (512 or 1024)
-#define WGSR_BDS_THREADS 512
+#define WGSR_BDS_THREADS 1024
 #endif
 constexpr int kBdsThreads = WGSR_BDS_THREADS, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
 constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
