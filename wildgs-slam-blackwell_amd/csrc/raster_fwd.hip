@@ -635,8 +635,19 @@ constexpr int kBdsMaxBits = 9, kBdsDigits = 1 << kBdsMaxBits;
 static_assert(kBdsDigits <= kBdsThreads, "threads t < kBdsDigits own digit t");
 __device__ __forceinline__ bool bds_owns_digit() { return (int)threadIdx.x < kBdsDigits; }
 
+// Peer groups (the wave's lanes holding the same digit) from per-(wave,
+// digit) 64-bit lane masks in LDS: one ds_or_b64 + one read per entry group
+// instead of one ballot and a 64-bit select per digit bit.  A wave's LDS
+// instructions complete in order, so every lane's OR lands before any lane's
+// read, and every read before the clear behind it.
+#ifndef WGSR_BDS_LDSMATCH
+#define WGSR_BDS_LDSMATCH 1
+#endif
 struct BdsLds {
   uint2 buf[kBdsCap];                     // (depth key, position in the bin)
+#if WGSR_BDS_LDSMATCH
+  unsigned long long match[kBdsWaves][kBdsDigits];  // lane masks per digit (zero between uses)
+#endif
   uint32_t wcnt[kBdsWaves][kBdsDigits];   // per wave digit counts, then their prefix over waves
   uint32_t base[kBdsDigits];              // per digit: first slot
   uint32_t tmp[kBdsWaves];
@@ -678,7 +689,14 @@ __device__ __forceinline__ void bds_rank(BdsLds& L, uint32_t cn, uint32_t mn, in
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     const bool valid = le < cn;
     const uint32_t d = ((k[j] - mn) >> shift) & mask;
+#if WGSR_BDS_LDSMATCH
+    (void)bits;
+    if (valid) atomicOr(&L.match[w][d], 1ull << lane);
+    const uint64_t peers = valid ? L.match[w][d] : 0ull;
+    if (valid) L.match[w][d] = 0ull;
+#else
     const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
+#endif
     const int leader = __ffsll((unsigned long long)peers) - 1;
     uint32_t old = 0;
     if (valid && lane == leader) old = atomicAdd(&L.wcnt[w][d], (uint32_t)__popcll(peers));
@@ -906,6 +924,9 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
 #pragma unroll
   for (int q = 0; q < kBdsWaves; ++q)
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
+#if WGSR_BDS_LDSMATCH
+  for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
+#endif
   if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
     bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
   else if (n <= 2u * kBdsThreads)
