@@ -54,20 +54,25 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4
 TILE = 16
 
 
-def byte_model(P, N, W, H, K, M):
-    """Algorithmic bytes per stage (SURVEY.md 8(d) per-unit figures).
+def grad_write_bytes(P, M):
+    """SURVEY.md 8(d)'s gradient-output write, P (12 + 12 + 12 M + 4 + 12 +
+    16 + 24): in this build the render backward streams it as the outputs'
+    zero fill and gauss_bwd writes only the ~8 % of rows that got gradient."""
+    return P * (12 + 12 + 12 * M + 4 + 12 + 16 + 24)
 
-    The gradient outputs' write, P (12 + 12 + 12 M + 4 + 12 + 16 + 24), is
-    booked to render_bwd: the render backward streams every output row's zero
-    fill, and gauss_bwd then writes only the ~8 % of rows that received
-    gradient (so gauss_bwd's figure is its read side only).  The total is
-    SURVEY's.  N is upstream's num_rendered (rectangle pairs), as SURVEY
-    defines it; the build lists fewer pairs (exact tile lists) and sorts
-    (Gaussian, bin) pairs -- the counter bytes (pass_roofline.counter_bytes)
-    are what it actually moves."""
+
+def byte_model(P, N, W, H, K, M):
+    """Algorithmic bytes per stage: SURVEY.md 8(d)'s per-unit figures, the
+    same table as DESIGN.md section 3.  The gradient-output write
+    (grad_write_bytes) is its own entry, "grad_write"; it is physically
+    streamed by the render backward (zero fill), so the roofline reports the
+    render backward's fraction both without it (``frac``) and with it
+    (``frac_incl_zero_fill``).  N is upstream's num_rendered (rectangle
+    pairs), as SURVEY defines it; the build lists fewer pairs (exact tile
+    lists) and sorts (Gaussian, bin) pairs -- the counter bytes
+    (pass_roofline.counter_bytes) are what it actually moves."""
     npix = W * H
     ntile = ((W + TILE - 1) // TILE) * ((H + TILE - 1) // TILE)
-    grad_write = P * (12 + 12 + 12 * M + 4 + 12 + 16 + 24)
     return {
         "preprocess": P * (44 + 12 * K) + 76 * P,
         "depth_sort": 16 * P,
@@ -76,8 +81,9 @@ def byte_model(P, N, W, H, K, M):
         "tile_sort": 24 * N,
         "ranges": 8 * N + 8 * ntile,
         "render_fwd": 44 * N + 28 * npix + 4 * P,
-        "render_bwd": 48 * N + 24 * npix + 40 * P + grad_write,
+        "render_bwd": 48 * N + 24 * npix + 40 * P,
         "gauss_bwd": P * (44 + 12 * K + 24 + 40),
+        "grad_write": grad_write_bytes(P, M),
     }
 
 
@@ -207,14 +213,10 @@ def main():
             allreduce_grads(gbuf)
         state.update(nr=nr, color=color, img=img)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
     exchange_check = None
     if vsb is not None:
         # the views exchange's summed gradients against the plain backward +
-        # RCCL all-reduce of the same views, once before timing.  Every rank
+        # RCCL all-reduce of the same views, once before warm-up and timing.  Every rank
         # falls back to the all-reduce exchange if any rank disagrees OR any
         # rank's exchange raised (decided over the gloo control group, which
         # does not depend on RCCL); if the all-reduce itself fails the run
@@ -255,6 +257,12 @@ def main():
                 print(json.dumps({"error": f"all-reduce fallback failed: {type(ex).__name__}: {ex}"[:600],
                                   "exchange_check": exchange_check}), file=sys.stderr)
                 sys.exit(1)
+
+    # warm-up AFTER the exchange check: an exchange that raises must reach the
+    # fallback, not end the run inside an untimed step
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
 
     # per-stage breakdown first, in untimed steps (HIP events around every
     # stage: each pair serialises the stream, ~2-3 us a stage); the timed
@@ -346,16 +354,19 @@ def main():
                            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                            "traffic": traffic, "algorithmic_bytes": model[dom],
                            "avg_launch_ms": ms_avg}
+        if dom == "render_bwd":
+            # the same launch also streams the gradient outputs' zero fill
+            zb = model[dom] + model["grad_write"]
+            out["roofline"]["algorithmic_bytes_incl_zero_fill"] = zb
+            out["roofline"]["frac_incl_zero_fill"] = zb / (ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS
         if traffic is not None:
             out["roofline"]["traffic_source"] = pmc.get("source")
-        # whole fwd+bwd pass against HBM (the north-star roofline) and the
-        # render kernels' pair arithmetic against the fp32 VALU peak
-        kernel_ms = sum(v[0] for k, v in timed.items()) / max(1, args.steps)
+        # whole fwd+bwd pass against HBM (the north-star roofline) over the
+        # timed step; the render kernels' pair arithmetic against the fp32 VALU peak
         total_bytes = sum(model.values())
         pairs = n_contrib_sum(state["img"], W, H)
         out["pass_roofline"] = {
-            "algorithmic_bytes": total_bytes, "kernel_ms": kernel_ms,
-            "achieved_GBps_kernels": total_bytes / (kernel_ms * 1e-3) / 1e9,
+            "algorithmic_bytes": total_bytes,
             "achieved_GBps_step": total_bytes / (ms_per_step * 1e-3) / 1e9,
             "frac_step": total_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS}
         if pmc:
@@ -406,12 +417,16 @@ def main():
                     out["roofline"]["valu_busy_frac"] = issue[dom]["valu_busy_frac_counters"]
                     out["roofline"]["clock_ghz"] = issue[dom]["clock_ghz_counters"]
                 vb = issue[dom].get("valu_busy_frac_counters")
+                if vb is not None and vb >= 0.85:
+                    out["roofline"]["bound"] = "valu"
                 what = ("VALU-issue bound" if (vb is not None and vb >= 0.85) else
                         "issue-latency bound at this size (too few waves per SIMD to keep the VALU busy)")
                 out["roofline"]["bound_note"] = (
                     f"{dom} is {what}: valu_busy_frac (the VALU pipe's busy share of the kernel's "
                     "SQ clocks, PMC) is its primary roofline; valu_issue_frac = wave-instructions per second "
-                    "against 1 per 4 cycles per SIMD at 2.4 GHz; frac is its HBM fraction")
+                    "against 1 per 4 cycles per SIMD at 2.4 GHz; frac is its HBM fraction over SURVEY 8(d)'s "
+                    "bytes for the kernel (48N + 24 Npix + 40P), frac_incl_zero_fill adds the gradient "
+                    "outputs' zero fill it also streams")
 
     if rank == 0 and world == 1 and not args.no_knn:
         # simple_knn.distCUDA2 over the scene's points

@@ -511,6 +511,37 @@ int wgsr_densify_emit(int64_t P, int M, const uint8_t* flags, const uint32_t* bl
 int wgsr_reset_opacity(int64_t P, float* opacity_raw, const uint8_t* visible, float value, float* exp_avg,
                        float* exp_avg_sq, void* stream);
 
+/* ---- map deformation (csrc/deform.hip, wgsr/store.py) ---------------------
+ * One keyframe's pose / depth update of Mapper._update_mapping_points
+ * (src/mapper.py:431-558; caller: _update_keyframes_from_frontend,
+ * mapper.py:365-429).  Host-computed, fp32, row-major:
+ *   T       = inv(inv(w2c_old) @ w2c_new)                (mapper.py:449 / 530)
+ *   q       = rotation_matrix_to_quaternion(T) (w,x,y,z)  (general_utils.py:138-162)
+ *   w2c_old, c2w_old = inv(w2c_old), K (the mapper's 3x3 intrinsics), depth /
+ *   depth_old ([H,W] device maps) -- the depth-rescale branch (method 1) only. */
+typedef struct wgsr_deform_frame {
+  int32_t kf_id;
+  int32_t method;       /* 0 = "rigid", 1 = depth rescale (method=None)      */
+  float T[16];
+  float q[4];
+  float w2c_old[16];
+  float c2w_old[16];
+  float K[9];
+  int32_t H, W;
+  const float* depth;
+  const float* depth_old;
+} wgsr_deform_frame;
+
+/* Applies every frame of `frames` (DEVICE array of nframes) to the rows of
+ * `bank` anchored to its keyframe (lut: DEVICE [lut_size] int32, kf_id ->
+ * frame index or -1): xyz, rotation (and scaling for method 1) as the
+ * reference does, and -- when any frame has rows -- every row's rotation
+ * normalised and the xyz / rotation (and, with a method-1 frame that has rows,
+ * scaling) Adam moments zeroed (replace_tensor_to_optimizer,
+ * gaussian_model.py:495-508).  flags: DEVICE scratch of 2 uint32. */
+int wgsr_deform_points(int64_t P, const wgsr_gaussian_bank* bank, const wgsr_deform_frame* frames, int nframes,
+                       const int32_t* lut, int lut_size, uint32_t* flags, void* stream);
+
 /* ---- SSIM for the mapping loss -------------------
  * Images are `planes` contiguous H x W fp32 planes (any leading dims
  * flattened; zero padding at the borders, as F.conv2d(padding=ws//2)).

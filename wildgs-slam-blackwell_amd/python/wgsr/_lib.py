@@ -79,6 +79,15 @@ class GaussianBank(ctypes.Structure):
                 ("exp_avg", _fp * 5), ("exp_avg_sq", _fp * 5), ("kf_id", _fp), ("n_obs", _fp)]
 
 
+class DeformFrame(ctypes.Structure):
+    """Mirror of ``wgsr_deform_frame`` (one keyframe of a map deformation)."""
+
+    _fields_ = [("kf_id", ctypes.c_int32), ("method", ctypes.c_int32), ("T", ctypes.c_float * 16),
+                ("q", ctypes.c_float * 4), ("w2c_old", ctypes.c_float * 16), ("c2w_old", ctypes.c_float * 16),
+                ("K", ctypes.c_float * 9), ("H", ctypes.c_int32), ("W", ctypes.c_int32), ("depth", _fp),
+                ("depth_old", _fp)]
+
+
 COMPACT_MAX_TENSORS = 32
 
 _lib = None
@@ -163,6 +172,8 @@ def load():
                                         ctypes.POINTER(GaussianBank), _fp]
         L.wgsr_reset_opacity.restype = c_int
         L.wgsr_reset_opacity.argtypes = [c_i64, _fp, _fp, ctypes.c_float, _fp, _fp, _fp]
+        L.wgsr_deform_points.restype = c_int
+        L.wgsr_deform_points.argtypes = [c_i64, ctypes.POINTER(GaussianBank), _fp, c_int, _fp, c_int, _fp, _fp]
         L.wgsr_sparse_grad_row_floats.restype = c_int
         L.wgsr_sparse_grad_row_floats.argtypes = [c_int]
         L.wgsr_sparse_mask_words.restype = c_i64
@@ -258,7 +269,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_uncer_loss_backward", "wgsr_uncer_loss_combine", "wgsr_track_blocks", "wgsr_tracking_loss", "wgsr_grad_mask",
     "wgsr_pose_state_floats", "wgsr_pose_step",
     "wgsr_mlp_scratch_bytes", "wgsr_mlp_grad_floats", "wgsr_mlp_forward", "wgsr_mlp_backward", "wgsr_dino_reg",
-    "wgsr_densify_blocks", "wgsr_densify_select", "wgsr_densify_emit", "wgsr_reset_opacity",
+    "wgsr_densify_blocks", "wgsr_densify_select", "wgsr_densify_emit", "wgsr_reset_opacity", "wgsr_deform_points",
     "wgsr_sparse_grad_row_floats", "wgsr_sparse_mask_words", "wgsr_sparse_pack_records",
     "wgsr_sparse_summary_block_words", "wgsr_sparse_exchange_summary", "wgsr_sparse_unpack_records",
     "wgsr_sparse_fill_radius", "wgsr_sparse_pack_grads", "wgsr_sparse_unpack_grads",

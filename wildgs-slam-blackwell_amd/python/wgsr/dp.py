@@ -26,6 +26,7 @@ on ROCm (over xGMI on one node); the CPU tests use "gloo".
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -59,6 +60,20 @@ class GradBuffer:
         return self.flat.numel() // max(P, 1)
 
 
+def _fault(var: str) -> str:
+    """Fault-injection hook for the first multi-GPU run's safety net (bench.py
+    exchange check; tests/test_gpu_bench_dp.py): ``$var`` = "raise" |
+    "perturb", applied on the ranks listed in WGSR_DP_FAULT_RANKS (comma
+    separated; default every rank).  Unset in normal runs."""
+    mode = os.environ.get(var, "")
+    if not mode:
+        return ""
+    ranks = os.environ.get("WGSR_DP_FAULT_RANKS", "")
+    if ranks and dist.is_initialized() and str(dist.get_rank()) not in ranks.split(","):
+        return ""
+    return mode
+
+
 def allreduce_grads(buf: GradBuffer, bucket_bytes: int = 256 << 20, async_op: bool = False,
                     average: bool = False):
     """SUM-all-reduce the flat gradient buffer in buckets of ``bucket_bytes``.
@@ -68,6 +83,8 @@ def allreduce_grads(buf: GradBuffer, bucket_bytes: int = 256 << 20, async_op: bo
     """
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return [] if async_op else None
+    if _fault("WGSR_DP_FAULT_ALLREDUCE") == "raise":
+        raise RuntimeError("WGSR_DP_FAULT_ALLREDUCE=raise: injected all-reduce failure (test hook)")
     flat = buf.flat
     per = max(1, bucket_bytes // flat.element_size())
     works = []
@@ -381,9 +398,23 @@ class ViewShardedBackward:
         geom, binning, image) of this rank's forward; cam is the dict of
         camera tensors/scalars (viewmatrix, projmatrix, projmatrix_raw,
         campos, tanfovx, tanfovy, bg).  -> (grads dict, tau [6] of this
-        rank's view, stats [P, 3] or None)."""
+        rank's view, stats [P, 3] or None).
+
+        Callers must not write into the gradient rows this rank does not own
+        between steps: the sparse exchange clears, at the next step, exactly
+        the rows its last gather scattered."""
+        fault = _fault("WGSR_DP_FAULT")
+        if fault == "raise":
+            raise RuntimeError("WGSR_DP_FAULT=raise: injected exchange failure (test hook)")
         if self.sparse:
-            return self._backward_sparse(fwd, dL_dcolor, dL_ddepth, scale_modifier)
+            out = self._backward_sparse(fwd, dL_dcolor, dL_ddepth, scale_modifier)
+        else:
+            out = self._backward_dense(fwd, dL_dcolor, dL_ddepth, scale_modifier)
+        if fault == "perturb":   # a 1 % error in one gradient tensor
+            out[0]["means3D"].mul_(1.01)
+        return out
+
+    def _backward_dense(self, fwd, dL_dcolor, dL_ddepth, scale_modifier):
         means3D, scales, rotations, shs, D, cam = fwd[:6]
         H, W = dL_dcolor.size(1), dL_dcolor.size(2)
         g = self.group

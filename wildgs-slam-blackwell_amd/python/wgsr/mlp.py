@@ -123,6 +123,7 @@ class UncertaintyMLP(nn.Module):
         nn.init.kaiming_uniform_(self.output_layer.weight, nonlinearity="relu")
         self.dropout_p = float(dropout_p)
         self.last_seed = None
+        self.seed_source = None  # optional callable -> the next forward's dropout seed (tests feed fixtures)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         H, W, C = x.shape[-3:]
@@ -130,7 +131,10 @@ class UncertaintyMLP(nn.Module):
         flat = x.reshape(-1, C)
         if flat.dtype != torch.float32 or not flat.is_cuda:
             raise RuntimeError("UncertaintyMLP: fp32 device features only (the HIP path has no CPU fallback)")
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # host generator: no device sync
+        if self.seed_source is not None:
+            seed = int(self.seed_source())
+        else:
+            seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # host generator: no device sync
         self.last_seed = seed
         l1, l2, lo = self.layers[0], self.layers[1], self.output_layer
         u = _MLPFn.apply(flat, l1.weight, l1.bias, l2.weight, l2.bias, lo.weight, lo.bias, self.dropout_p, seed)

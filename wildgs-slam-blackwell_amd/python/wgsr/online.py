@@ -36,11 +36,18 @@ densification on the device):
     DINO term, densify every ``init_gaussian_update`` and reset_opacity at
     ``init_gaussian_reset``.
 
+``update_keyframes``  (_update_keyframes_from_frontend + _update_mapping_points,
+mapper.py:365-558)
+    the tracker's new poses / depths of existing keyframes and the map
+    deformation of their anchored Gaussians, every keyframe in one device
+    pass (``GaussianStore.update_mapping_points``, csrc/deform.hip).
+``final_refine``  (mapper.py:1234-1372)
+    the end-of-sequence refinement iterations.
+
 Not restated (absent offline or outside the mapping path): the tracker and
 its keyframe decisions (the caller supplies keyframes with poses and
-depths), the frontend's depth / pose updates of existing keyframes
-(``_update_keyframes_from_frontend``), map deformation, DINO feature
-extraction (the caller supplies features), the GUI / printer, fast mode.
+depths, and the pose / depth updates), DINO feature extraction (the caller
+supplies features), the GUI / printer, fast mode.
 Random draws (view choice, point subsets, split noise, dropout) come from
 this object's generators, not the reference's global RNG streams.
 """
@@ -52,7 +59,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from .camera import PinholeCamera, focal2fov
+from .camera import PinholeCamera, focal2fov, get_world2view2
 from .mapping import MappingStep
 
 SH_C0 = 0.28209479177387814
@@ -118,6 +125,23 @@ class Keyframe:
         self.FoVx, self.FoVy = focal2fov(self.fx, self.W), focal2fov(self.fy, self.H)
         self.median_depth = self.depth.median()  # constant per keyframe (the loss's depth threshold)
 
+    def w2c(self) -> torch.Tensor:
+        """[4, 4] fp32 world->camera (mapper.py:387-389)."""
+        m = torch.eye(4)
+        m[:3, :3], m[:3, 3] = self.R.float().cpu(), self.T.float().cpu()
+        return m
+
+    def update_RT(self, R, T):
+        """Camera.update_RT (camera_utils.py:153-155) + the raster fields."""
+        self.R, self.T = torch.as_tensor(R).float().cpu(), torch.as_tensor(T).float().cpu()
+        dev = self.image.device
+        pc = PinholeCamera(R=self.R, T=self.T, fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy, W=self.W, H=self.H)
+        self.cam = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in pc.raster_fields().items()}
+
+    @property
+    def K(self) -> torch.Tensor:
+        return torch.tensor([[self.fx, 0.0, self.cx], [0.0, self.fy, self.cy], [0.0, 0.0, 1.0]])
+
 
 class OnlineMapper:
     def __init__(self, sh_degree: int = 0, feature_dim: int = 384, device="cuda", config: dict | None = None,
@@ -149,27 +173,57 @@ class OnlineMapper:
         self.events = []  # (iteration, "densify" | "reset", details)
 
     # ---- Gaussians from a keyframe (gaussian_model.py:108-226) ---------------
+    @staticmethod
+    def np_median(x: torch.Tensor) -> float:
+        """np.median of a float32 map (gaussian_model.py:150): the MEAN of the
+        two middle values for an even count (torch.median returns the lower
+        one), computed in fp32 as numpy does for a float32 array."""
+        v = x.reshape(-1).float()
+        n = v.numel()
+        lo = torch.kthvalue(v, (n - 1) // 2 + 1).values
+        hi = torch.kthvalue(v, n // 2 + 1).values if n % 2 == 0 else lo
+        return float(((lo + hi) / 2).item())
+
     @torch.no_grad()
-    def keyframe_points(self, kf: Keyframe, init: bool):
+    def keyframe_points(self, kf: Keyframe, init: bool, keep=None):
+        """create_pcd_from_image + create_pcd_from_image_and_depth
+        (gaussian_model.py:108-226) with Open3D's RGBD back-projection: the
+        exposure-corrected uint8 colours, every pixel with 0 < depth <
+        depth_trunc = 100 in row-major order, x = (u - cx) z / fx and
+        y = (v - cy) z / fy in double and moved to the world by
+        inverse(W2C) (Open3D computes in double; the reference then casts to
+        fp32), a random 1/downsample subset kept IN PIXEL ORDER (Open3D's
+        random_down_sample keeps int(ratio * n) points through
+        SelectByIndex), RGB2SH, the distCUDA2 scales with the adaptive point
+        size min(0.05, point_size * np.median(depth)), identity rotations,
+        opacity inverse_sigmoid(0.5).  ``keep``: the subset's indices into the
+        valid pixels (tests feed the reference's draw); default: drawn with
+        this mapper's generator."""
         from simple_knn._C import distCUDA2
         c = self.cfg
         ds = c["pcd_downsample_init"] if init else c["pcd_downsample"]
         image_ab = torch.clamp(torch.exp(kf.exposure_a) * kf.image + kf.exposure_b, 0.0, 1.0)
-        rgb = (image_ab * 255).byte().float() / 255.0                  # o3d colours of the uint8 image
+        u8 = (image_ab * 255).byte()
         depth = kf.depth[0]
         point_size = c["point_size"]
         if c["adaptive_pointsize"]:
-            point_size = min(0.05, point_size * float(depth.median()))
+            point_size = min(0.05, point_size * self.np_median(depth))
         valid = (depth > 0) & (depth < 100.0)                          # depth_trunc = 100
         v, u = torch.nonzero(valid, as_tuple=True)
-        z = depth[v, u]
-        pc = torch.stack([(u.float() - kf.cx) * z / kf.fx, (v.float() - kf.cy) * z / kf.fy, z], 1)
-        R, T = kf.R.to(self.dev).float(), kf.T.to(self.dev).float()
-        pw = (pc - T[None]) @ R                                         # extrinsic W2C -> world
-        n = pw.shape[0]
-        keep = torch.randperm(n, device=self.dev, generator=self.gen)[: int(n / ds)]
-        xyz = pw[keep].contiguous()
-        col = rgb[:, v[keep], u[keep]].T
+        n = v.numel()
+        if keep is None:
+            keep = torch.randperm(n, device=self.dev, generator=self.gen)[: int((1.0 / ds) * n)]
+            keep = torch.sort(keep).values
+        else:
+            keep = torch.as_tensor(keep, device=self.dev, dtype=torch.long)
+        v, u = v[keep], u[keep]
+        z = depth[v, u].double()
+        pc = torch.stack([(u.double() - kf.cx) * z / kf.fx, (v.double() - kf.cy) * z / kf.fy, z,
+                          torch.ones_like(z)], 0)
+        w2c = get_world2view2(kf.R.float().cpu(), kf.T.float().cpu()).double()   # getWorld2View2 (fp32)
+        pose = torch.linalg.inv(w2c).to(self.dev)
+        xyz = (pose @ pc)[:3].T.float().contiguous()
+        col = (u8[:, v, u].T.double() / 255.0).float()
         feats = torch.zeros(xyz.shape[0], self.M, 3, device=self.dev)
         feats[:, 0] = (col - 0.5) / SH_C0                               # RGB2SH
         dist2 = torch.clamp_min(distCUDA2(xyz), 0.0000001) * point_size
@@ -243,6 +297,23 @@ class OnlineMapper:
             window.remove(window[N_dont_touch + int(np.argmax(inv_dist))])
         return window
 
+    def _perm(self, n: int) -> torch.Tensor:
+        """The DINO term's feature sampling draw (the reference's
+        torch.randperm(n), mapper.py:1155-1157 / 1334-1336)."""
+        return torch.randperm(n, device=self.dev, generator=self.gen)
+
+    def _dino_term(self, neighbours, kf):
+        """reg_mult * compute_dino_regularization_loss on features sampled from
+        the neighbouring keyframes' (stack positions ci-2 .. ci+2) feature maps
+        (mapper.py:1141-1164, 1320-1340), and its backward into the MLP."""
+        from .uncertainty import dino_regularization_loss
+        c = self.cfg
+        st = c["reg_stride"]
+        buf = torch.stack([self.keyframes[k].features for k in neighbours]).view(-1, kf.features.shape[-1])
+        ns = buf.shape[0] // (st ** 4)
+        sf = buf[self._perm(buf.shape[0])[:ns]].unsqueeze(0)
+        (c["reg_mult"] * dino_regularization_loss(self.net(sf), sf)).backward()
+
     # ---- one optimisation iteration ------------------------------------------
     def _iteration(self, kf: Keyframe, neighbours, initialization: bool, update: bool, reset: str | None,
                    occ_window=None):
@@ -269,12 +340,7 @@ class OnlineMapper:
                                                   c["train_frac_fix"], c["train_frac_fix"],
                                                   freeze_uncertainty_loss=freeze, median_depth=kf.median_depth)
             if self.iterations_after_densify_or_reset >= 20:
-                from .uncertainty import dino_regularization_loss
-                st = c["reg_stride"]
-                buf = torch.stack([self.keyframes[k].features for k in neighbours]).view(-1, kf.features.shape[-1])
-                ns = buf.shape[0] // (st ** 4)
-                sf = buf[torch.randperm(buf.shape[0], device=self.dev, generator=self.gen)[:ns]].unsqueeze(0)
-                (c["reg_mult"] * dino_regularization_loss(self.net(sf), sf)).backward()
+                self._dino_term(neighbours, kf)
         vis = out["radii"] > 0
         if occ_window is not None:  # last iteration of a map_opt_online call (mapper.py:1174-1175)
             self._update_occ_aware_visibility(occ_window)
@@ -298,13 +364,19 @@ class OnlineMapper:
         ms.optimizer_step()
         ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
                                  lr_delay_mult=c["position_lr_delay_mult"], max_steps=c["position_lr_max_steps"])
-        if self.kopt is not None and kf.uid in self.kopt_uids:
-            ea.grad, eb.grad = out["dexposure_a"].reshape(1), out["dexposure_b"].reshape(1)
-            self.kopt.step()
-            ea.grad = eb.grad = None
+        self._exposure_step(kf, out)
         self.uopt.step()
         self.uopt.zero_grad()
         return out
+
+    def _exposure_step(self, kf, out):
+        """keyframe_optimizers.step() + zero_grad(set_to_none=True): only the
+        rendered keyframe's exposures carry a gradient; others are skipped."""
+        if self.kopt is not None and kf.uid in self.kopt_uids:
+            kf.exposure_a.grad = out["dexposure_a"].reshape(1)
+            kf.exposure_b.grad = out["dexposure_b"].reshape(1)
+            self.kopt.step()
+            kf.exposure_a.grad = kf.exposure_b.grad = None
 
     def _new_exposure_optimizer(self):
         """mapper.py:219-241: a fresh Adam over the window's exposures (not kf 0)."""
@@ -349,6 +421,70 @@ class OnlineMapper:
         if split:
             self.map_opt_online(self.window, 1)
         return added
+
+    def update_keyframes(self, updates: dict, deform: bool = True):
+        """Mapper._update_keyframes_from_frontend (mapper.py:365-429): the
+        tracker's new poses (and, in the reference's ablation without metric
+        depth, new depths) of existing keyframes.  ``updates``: {kf uid:
+        (w2c [4, 4], depth [1, H, W] or None)}.  A keyframe whose pose is
+        unchanged (allclose, atol 1e-6) and that has no new depth is skipped;
+        the others get the new pose (and depth) and, with ``deform``
+        (mapping.deform_gaussians, default True), their anchored Gaussians
+        are moved by ``GaussianStore.update_mapping_points`` -- every
+        keyframe in one pass.  As in the reference, the depth-rescale branch
+        is handed the keyframe's depth AFTER it was replaced by the new one
+        (mapper.py:399-401 then 423-429), so its rescale factor is 1.
+        Returns the number of keyframes moved."""
+        frames = []
+        for k, (w2c, depth) in updates.items():
+            kf = self.keyframes[k]
+            w2c = torch.as_tensor(w2c, dtype=torch.float32).cpu()
+            w2c_old = kf.w2c()
+            if torch.allclose(w2c_old, w2c, atol=1e-6) and depth is None:
+                continue
+            kf.update_RT(w2c[:3, :3], w2c[:3, 3])
+            if depth is not None:
+                kf.depth = depth.to(kf.image.device, torch.float32).reshape(1, kf.H, kf.W).contiguous()
+                kf.median_depth = kf.depth.median()
+            fr = {"kf_id": k, "w2c": w2c, "w2c_old": w2c_old}
+            if depth is not None:
+                fr.update(method="depth", depth=kf.depth[0], depth_old=kf.depth[0])
+            frames.append(fr)
+        if deform and frames and self.ms is not None:
+            K = self.keyframes[frames[0]["kf_id"]].K
+            self.ms.store.update_mapping_points(frames, K)
+        return len(frames)
+
+    def final_refine(self, iters: int = 26000):
+        """Mapper.final_refine (mapper.py:1234-1372): uniform random
+        keyframes, the uncertainty-aware loss on the RAW render (the exposure
+        applied once), the uncertainty loss frozen for 200 iterations after
+        the last densify / reset and the DINO term after them, the isotropic
+        term; Adam for the Gaussians (no densification), the last window's
+        exposure optimizer and the MLP.  (The reference's preceding
+        _update_keyframes_from_frontend is ``update_keyframes``.)"""
+        c = self.cfg
+        ms = self.ms
+        stack = [k for k in self.keyframes]
+        for _ in range(iters):
+            self.iteration_count += 1
+            self.iterations_after_densify_or_reset += 1
+            ci = int(self.rng.choice(len(stack)))
+            kf = self.keyframes[stack[ci]]
+            unc = self.net(kf.features)
+            freeze = self.iterations_after_densify_or_reset < 200
+            out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg,
+                                                  unc, c["train_frac_fix"], c["train_frac_fix"],
+                                                  freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
+                                                  pre_exposed=False)
+            if self.iterations_after_densify_or_reset >= 200:
+                self._dino_term([stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))], kf)
+            ms.optimizer_step()
+            ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
+                                     lr_delay_mult=c["position_lr_delay_mult"], max_steps=c["position_lr_max_steps"])
+            self._exposure_step(kf, out)
+            self.uopt.step()
+            self.uopt.zero_grad()
 
     def map_opt_online(self, window, iters: int = 1):
         """mapper.py:1049-1219."""

@@ -37,6 +37,29 @@ def inverse_sigmoid(x: torch.Tensor) -> torch.Tensor:
     return torch.log(x / (1 - x))
 
 
+def rotation_matrix_to_quaternion(R: torch.Tensor) -> torch.Tensor:
+    """general_utils.rotation_matrix_to_quaternion (general_utils.py:138-162),
+    op for op in fp32: [B, >=3, >=3] -> [B, 4] (w, x, y, z), including its sign
+    rule q_i *= sign(q_i (R_kj - R_jk)) (a zero difference zeroes q_i)."""
+    z = torch.tensor(0.0, dtype=R.dtype)
+    q = torch.zeros((R.size(0), 4), dtype=R.dtype)
+    q[:, 0] = torch.sqrt(torch.max(z, 1 + R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2])) / 2
+    q[:, 1] = torch.sqrt(torch.max(z, 1 + R[:, 0, 0] - R[:, 1, 1] - R[:, 2, 2])) / 2
+    q[:, 2] = torch.sqrt(torch.max(z, 1 - R[:, 0, 0] + R[:, 1, 1] - R[:, 2, 2])) / 2
+    q[:, 3] = torch.sqrt(torch.max(z, 1 - R[:, 0, 0] - R[:, 1, 1] + R[:, 2, 2])) / 2
+    q[:, 1] *= torch.sign(q[:, 1] * (R[:, 2, 1] - R[:, 1, 2]))
+    q[:, 2] *= torch.sign(q[:, 2] * (R[:, 0, 2] - R[:, 2, 0]))
+    q[:, 3] *= torch.sign(q[:, 3] * (R[:, 1, 0] - R[:, 0, 1]))
+    return q
+
+
+def deform_transform(w2c: torch.Tensor, w2c_old: torch.Tensor):
+    """(T, q) of mapper.py:449-460 / 530-545: T = inv(inv(w2c_old) @ w2c),
+    q = rotation_matrix_to_quaternion(T), fp32 on the host."""
+    T = torch.linalg.inv(torch.linalg.inv(w2c_old) @ w2c)
+    return T, rotation_matrix_to_quaternion(T.unsqueeze(0))[0]
+
+
 class GaussianStore:
     def __init__(self, xyz, features, opacity, scaling, rotation, capacity: int | None = None,
                  kf_id=None, n_obs=None, growth: float = 1.5):
@@ -234,6 +257,71 @@ class GaussianStore:
         """inverse_sigmoid(torch.ones_like(opacity) * c), evaluated on the
         device as the reference does (one element: the value is per row)."""
         return float(inverse_sigmoid(torch.ones(1, device=self.device) * c).item())
+
+    def update_mapping_points(self, frames, K=None):
+        """Mapper._update_mapping_points (src/mapper.py:431-558) for several
+        keyframes in ONE pass over the rows (csrc/deform.hip).
+
+        frames: iterable of dicts with ``kf_id``, ``w2c`` (new world->camera,
+        [4, 4]), ``w2c_old`` ([4, 4]) and, for the depth-rescale branch
+        (the reference's ``method=None``), ``depth`` / ``depth_old`` ([H, W]
+        maps); ``method`` "rigid" (default when no depth is given) or
+        "depth".  K: the mapper's 3x3 intrinsics (depth branch).  The 4x4
+        transformation and its quaternion are formed on the host in fp32
+        exactly as the reference forms them (torch.linalg.inv,
+        rotation_matrix_to_quaternion); the per-row work, the normalisation of
+        every rotation and the moment resets of replace_tensor_to_optimizer
+        run on the device.  Returns the number of frames passed on."""
+        L = _lib.load()
+        frames = list(frames)
+        if self.P == 0 or not frames:
+            return 0
+        arr = (_lib.DeformFrame * len(frames))()
+        seen = set()
+        keep = []
+        Kc = None if K is None else torch.as_tensor(K, dtype=torch.float32).cpu().reshape(3, 3)
+        for j, fr in enumerate(frames):
+            k = int(fr["kf_id"])
+            if k in seen:
+                raise ValueError(f"update_mapping_points: keyframe {k} given twice")
+            seen.add(k)
+            method = fr.get("method") or ("rigid" if fr.get("depth") is None else "depth")
+            w2c = torch.as_tensor(fr["w2c"], dtype=torch.float32).cpu().reshape(4, 4)
+            w2c_old = torch.as_tensor(fr["w2c_old"], dtype=torch.float32).cpu().reshape(4, 4)
+            T, q = deform_transform(w2c, w2c_old)
+            f = arr[j]
+            f.kf_id, f.method = k, (0 if method == "rigid" else 1)
+            f.T[:] = T.flatten().tolist()
+            f.q[:] = q.tolist()
+            if method != "rigid":
+                if Kc is None:
+                    raise ValueError("update_mapping_points: the depth branch needs the intrinsics K")
+                d = fr["depth"].to(device=self.device, dtype=torch.float32).contiguous()
+                d_old = fr["depth_old"].to(device=self.device, dtype=torch.float32).contiguous()
+                if d.dim() != 2 or d.shape != d_old.shape:
+                    raise ValueError("update_mapping_points: depth / depth_old must be [H, W] maps of one shape")
+                keep += [d, d_old]
+                f.w2c_old[:] = w2c_old.flatten().tolist()
+                f.c2w_old[:] = torch.linalg.inv(w2c_old).flatten().tolist()
+                f.K[:] = Kc.flatten().tolist()
+                f.H, f.W = int(d.shape[0]), int(d.shape[1])
+                f.depth, f.depth_old = d.data_ptr(), d_old.data_ptr()
+        lut_h = torch.full((max(seen) + 1 if max(seen) >= 0 else 1,), -1, dtype=torch.int32)
+        for j, fr in enumerate(frames):
+            if int(fr["kf_id"]) >= 0:
+                lut_h[int(fr["kf_id"])] = j
+        dev = self.device
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        frames_d = raw.to(dev)
+        lut = lut_h.to(dev)
+        flags = torch.empty(2, dtype=torch.int32, device=dev)
+        bank = self._bank_struct(self.cur)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_deform_points(self.P, ctypes.byref(bank), frames_d.data_ptr(), len(frames),
+                                            lut.data_ptr(), int(lut.numel()), flags.data_ptr(),
+                                            _lib.stream_handle(dev)))
+        self._deform_keep = (keep, frames_d, lut, flags)  # alive until the next call (stream order)
+        return len(frames)
 
     def _reset_opacity(self, vis, value):
         L = _lib.load()
