@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--iters", type=int, default=450)
     ap.add_argument("--gt-gaussians", type=int, default=400_000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--refine-iters", type=int, default=300, help="final_refine iterations after the last keyframe")
+    ap.add_argument("--no-deform", action="store_true", help="skip the per-keyframe pose updates / map deformation")
     a = ap.parse_args()
     from diff_gaussian_rasterization import _C
     from wgsr.camera import PinholeCamera
@@ -119,8 +121,30 @@ def main():
     torch.cuda.synchronize()
     t_init = time.perf_counter() - t0
     ins_ms, it_ms, its = [], 0.0, 0
-    for kf in kfs[a.init_keyframes:]:
+    deform_ms, deform_kfs = [], 0
+
+    def nudge(k, scale):
+        """a small pose correction of keyframe k (the tracker's BA / loop
+        closure moving existing keyframes): rotation about y, translation"""
+        kfk = m.keyframes[k]
+        ang = math.radians(0.05 * scale)
+        c, s_ = math.cos(ang), math.sin(ang)
+        dR = torch.tensor([[c, 0.0, s_], [0.0, 1.0, 0.0], [-s_, 0.0, c]])
+        w2c = kfk.w2c().clone()
+        w2c[:3, :3] = dR @ w2c[:3, :3]
+        w2c[:3, 3] += torch.tensor([0.002 * scale, -0.001 * scale, 0.0])
+        return w2c
+
+    for n_kf, kf in enumerate(kfs[a.init_keyframes:]):
         torch.cuda.synchronize()
+        if not a.no_deform:
+            # _update_keyframes_from_frontend before the insertion (mapper.py:194):
+            # every existing keyframe's pose moved a little, its Gaussians deformed
+            t0 = time.perf_counter()
+            moved = m.update_keyframes({k: (nudge(k, 1.0 + 0.1 * n_kf), None) for k in list(m.keyframes)})
+            torch.cuda.synchronize()
+            deform_ms.append(1e3 * (time.perf_counter() - t0))
+            deform_kfs += moved
         t0 = time.perf_counter()
         vis = m.visibility(kf)
         m.keyframes[kf.uid] = kf
@@ -139,6 +163,16 @@ def main():
         ins_ms.append(1e3 * (t1 - t0))
         it_ms += 1e3 * (t2 - t1)
         its += n
+    # final_refine (mapper.py:1234-1372) after the final pose update of every keyframe
+    refine_ms = None
+    if a.refine_iters > 0:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if not a.no_deform:
+            m.update_keyframes({k: (nudge(k, 2.0), None) for k in list(m.keyframes)})
+        m.final_refine(a.refine_iters)
+        torch.cuda.synchronize()
+        refine_ms = 1e3 * (time.perf_counter() - t0) / a.refine_iters
     # PSNR of the final map against every keyframe's ground truth
     ps = []
     for kf in kfs:
@@ -150,11 +184,16 @@ def main():
                     f"({a.init_keyframes} init x {a.init_iters} its, then {a.iters} its per keyframe)",
         "ms_per_mapping_iteration": it_ms / max(its, 1), "mapping_iterations": its,
         "ms_per_keyframe_insertion": sum(ins_ms) / max(len(ins_ms), 1),
+        "ms_per_deformation_call": (sum(deform_ms) / len(deform_ms)) if deform_ms else None,
+        "keyframes_deformed_per_call": (deform_kfs / len(deform_ms)) if deform_ms else None,
+        "final_refine_iterations": a.refine_iters, "ms_per_final_refine_iteration": refine_ms,
         "init_seconds": t_init, "gaussians_final": m.ms.P,
         "events": [(i, k, v) for i, k, v in m.events][:40],
         "psnr_db_mean": sum(ps) / len(ps), "psnr_db_per_keyframe": ps,
         "note": "uncertainty-aware loss + DINO regulariser + isotropic term, densify/prune, opacity reset, "
-                "Adam (Gaussians, exposures, MLP); wall clock with a device sync per keyframe"}))
+                "Adam (Gaussians, exposures, MLP); before every insertion each existing keyframe's pose is "
+                "nudged and its Gaussians deformed (update_keyframes, one device pass); final_refine at the "
+                "end; wall clock with a device sync per keyframe"}))
 
 
 if __name__ == "__main__":

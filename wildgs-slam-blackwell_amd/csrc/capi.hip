@@ -498,11 +498,16 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // per-bin depth sort: the pairs' depth keys ride the bin sort as a second
   // payload, in two arrays after the lists
   const size_t pdep_words = bin_depth ? align256(4 * N_bin) / 4 : 0;
-  void* binning = call_alloc(binning_alloc, ctx, BL.total + lists_bytes + 8 * pdep_words);
-  if (!binning && BL.total + lists_bytes + pdep_words) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  // per-bin depth sort: scratch of the bins beyond one LDS tile (two uint2
+  // ping-pong arrays; not the list region, which the same kernel now writes)
+  const size_t bds_bytes = bin_depth ? align256(16 * (size_t)N_bin) : 0;
+  const size_t binning_bytes = BL.total + lists_bytes + 8 * pdep_words + bds_bytes;
+  void* binning = call_alloc(binning_alloc, ctx, binning_bytes);
+  if (!binning && binning_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   uint32_t* lists = bshift ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
   uint32_t* pdep = bin_depth ? at<uint32_t>(binning, BL.total + lists_bytes) : nullptr;
   uint32_t* pdep_alt = bin_depth ? pdep + pdep_words : nullptr;
+  void* bds_scratch = bin_depth ? static_cast<void*>(at<char>(binning, BL.total + lists_bytes + 8 * pdep_words)) : nullptr;
   uint2* ranges = at<uint2>(image, IL.ranges);
   // sorted pairs: (Gaussian, bin) pairs, or with bin shift 0 the exact
   // (Gaussian, tile) pairs themselves
@@ -549,17 +554,32 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bin_depth) {
       // each bin by depth, into the spare key / payload buffers; scratch for
       // bins beyond one LDS tile: the list region (>= 16 NL bytes)
+      // ... and emits the per-tile lists and ranges itself (no k_expand_bins)
       StageTimer T(4, s);
       uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
       uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
+      // (WGSR_BDS_EMIT=0: the sorted bins to okeys / ogid and k_expand_bins)
+      static const bool emit = [] {
+        const char* e = getenv("WGSR_BDS_EMIT");
+        return !(e && atoi(e) == 0);
+      }();
       STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift, at<uint2>(image, IL.tile_m),
-                                        bounds_done, pdep, okeys, ogid, lists, s));
+                                        bounds_done, pdep, okeys, ogid, bds_scratch, s, emit ? lists : nullptr,
+                                        ranges, at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta)));
       bounds_done = true;
-      sorted_keys = okeys;
-      sorted_gid = ogid;
+      if (!emit) {
+        sorted_keys = okeys;
+        sorted_gid = ogid;
+      }
     }
     StageTimer T(5, s);
-    if (bshift) {
+    static const bool emitted = [] {
+      const char* e = getenv("WGSR_BDS_EMIT");
+      return !(e && atoi(e) == 0);
+    }();
+    if (bin_depth && emitted) {
+      // (lists and ranges written by the per-bin depth sort)
+    } else if (bshift) {
       STAGE(a, s, launch_expand_bins(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift,
                                      at<uint2>(image, IL.tile_m), bounds_done, lists, ranges,
                                      at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta), s));

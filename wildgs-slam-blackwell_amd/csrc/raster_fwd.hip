@@ -83,7 +83,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
     int i, const Cam& c, const f3 p, const f3 sc, const float4 q, const float o, const f3 sh_rgb,
-    uint32_t sh_cbits, uint4& w, uint2& rcw) {
+    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
   rcw = make_uint2(0u, 0u);
@@ -143,7 +143,7 @@ __device__ __forceinline__ uint3 preprocess_one(
   const float4 B = make_float4(kConicXY * (-b * det_inv), o, lim, 0.f);
   splat[3 * (size_t)i + 0] = A;
   splat[3 * (size_t)i + 1] = B;
-  splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
+  if (write_color) splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rcw = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
   // exact tile list length (row_span); upstream's num_rendered counts the rect
   const Reach rr = reach_of(A, B);
@@ -163,7 +163,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     cnt += len;
   }
   lrec[i].tab = tab;
-  clamped[i] = cbits;
+  if (write_color) clamped[i] = cbits;
   // bins of the rect (exact lists are per tile; a bin list holds every
   // Gaussian whose rect meets the bin, and the render waves cull the rest)
   const uint32_t nb = cnt == 0 ? 0u
@@ -272,6 +272,140 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     if (knlo) atomicMax(&drange[kRectPairLanes + blockIdx.x % kRectPairLanes], knlo);
   }
   // scratch the next kernels need zeroed (the depth sort's superblock sums)
+  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
+}
+
+// ---- k_preprocess2: the SH slab streams into LDS while the geometry runs ----
+// The same per-Gaussian work as k_preprocess, reordered so that the SH
+// fetch no longer sits in front of the geometry: the wave first queues its
+// 64 rows' evaluated coefficients as LDS-DMA loads (global_load_lds: no VGPR
+// holds them in flight), in a chunk-major layout [chunk][lane] (chunk = 4
+// floats when rows are 16-byte aligned, else 1) so that each lane later
+// reads its own row conflict-free; then it loads the parameters and runs the
+// projection / covariance / rectangle / row-table work and writes the
+// geometry records; only then does it wait for the slab and evaluate the
+// colour -- for visible Gaussians only (k_preprocess evaluates every lane).
+// Outputs are bit-identical to k_preprocess (same operation sequences).
+template <int kD, int kCh>
+__device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lane, f3 dir, uint32_t& cbits) {
+  constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, NCH = (NF + kCh - 1) / kCh;
+  float sh[NCH * kCh];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    if constexpr (kCh == 4) {
+      const float4 v = reinterpret_cast<const float4*>(s_sh)[k * 64 + lane];
+      sh[4 * k] = v.x;
+      sh[4 * k + 1] = v.y;
+      sh[4 * k + 2] = v.z;
+      sh[4 * k + 3] = v.w;
+    } else {
+      sh[k] = s_sh[k * 64 + lane];
+    }
+  }
+  return sh_to_rgb(kD, sh, dir, cbits);
+}
+
+template <int kCh>
+__device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_sh, int lane, f3 dir,
+                                             uint32_t& cbits) {
+  switch (D) {
+    case 0: return sh_rgb_lds<0, kCh>(s_sh, lane, dir, cbits);
+    case 1: return sh_rgb_lds<1, kCh>(s_sh, lane, dir, cbits);
+    case 2: return sh_rgb_lds<2, kCh>(s_sh, lane, dir, cbits);
+    default: return sh_rgb_lds<3, kCh>(s_sh, lane, dir, cbits);
+  }
+}
+
+template <int kCh>
+__global__ __launch_bounds__(kPreWave) void k_preprocess2(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
+    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero) {
+  extern __shared__ float s_sh[];  // nch x 64 x kCh floats (chunk-major)
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  const bool sh_on = shs != nullptr && colors == nullptr;
+  if (sh_on) {  // uniform: queue the slab first
+    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + kCh - 1) / kCh;
+    const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
+    for (int k = 0; k < nch; ++k) {
+      if constexpr (kCh == 4)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
+                                         (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src + k),
+                                         (__attribute__((address_space(3))) void*)(s_sh + 64 * k), 4, 0, 0);
+    }
+  }
+  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  f3 sc = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  float o = 0.f;
+  if (i < P) {
+    if (!cov_pre) {
+      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+      q = reinterpret_cast<const float4*>(rots)[i];
+    }
+    o = opac[i];
+  }
+  uint3 ac = make_uint3(0u, 0u, 0u);
+  uint32_t khi = 0u, knlo = 0u;
+  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+  if (i < P) {
+    uint2 rcw;
+    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
+                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, !sh_on);
+    radii[i] = (int32_t)w.x;
+    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    if (bshift) tb[i] = w.z;
+    dkey[i] = w.w;
+    if (w.w != 0xFFFFFFFFu) {
+      khi = w.w;
+      knlo = ~w.w;
+    }
+    n_touched[i] = 0;
+    gflag[i] = 0;
+  }
+  if (sh_on) {
+    __builtin_amdgcn_s_waitcnt(0);  // the slab has landed (one wave per workgroup)
+    __syncthreads();
+    if (i < P && w.x != 0u) {  // visible: the colour record
+#pragma clang fp contract(off)
+      f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+      const float len = sqrtf(dot3(dir, dir));
+      dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+      uint32_t cbits = 0;
+      const f3 rgb = sh_rgb_lds_deg<kCh>(D, s_sh, lane, dir, cbits);
+      splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
+      clamped[i] = cbits;
+    }
+  }
+  unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    area += __shfl_xor(area, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+    nbin += __shfl_xor(nbin, off, 64);
+    khi = max(khi, (uint32_t)__shfl_xor((int)khi, off, 64));
+    knlo = max(knlo, (uint32_t)__shfl_xor((int)knlo, off, 64));
+  }
+  if (lane == 0) {
+    atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
+    atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
+    atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
+    if (khi) atomicMax(&drange[blockIdx.x % kRectPairLanes], khi);
+    if (knlo) atomicMax(&drange[kRectPairLanes + blockIdx.x % kRectPairLanes], knlo);
+  }
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
 }
 
@@ -652,7 +786,97 @@ struct BdsLds {
   uint32_t base[kBdsDigits];              // per digit: first slot
   uint32_t tmp[kBdsWaves];
   uint32_t rng[2][kBdsWaves];
+  uint32_t etot[kBdsWaves][16];           // emit: per-wave entries per tile of the bin
+  uint32_t erun[16];                      // emit: entries per tile emitted so far
 };
+
+// The bin's exact per-tile lists, emitted straight from the depth-sorted bin
+// (what k_expand_bins does from a global copy of it): tile k = r 2^s + c of
+// the bin gets, in depth order, every entry whose key has bit 16 + k set, at
+// lists[2^2s lo + k n + ...] (n = the bin's length: no count pass, no
+// overlap).  One chunk: wave w's lanes hold sorted positions (w JN + j) 64 +
+// lane of it in m[j] (the tile mask, 0 if none) and g[j] (the Gaussian);
+// per-wave counts per tile first, their prefix over the waves, then a
+// stable per-tile compaction (one ballot per (entry group, tile)).
+struct BdsEmit {
+  uint32_t* __restrict__ lists;
+  uint2* __restrict__ ranges;
+  uint32_t* __restrict__ tile_len;
+  uint32_t* __restrict__ meta;
+  int gx, gy, bshift, gbx;
+};
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I0, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>{});
+    static_for<I0 + 1, N>(f);
+  }
+}
+
+template <int JN>
+__device__ __forceinline__ void bds_emit_chunk(BdsLds& L, const uint32_t (&m)[JN], const uint32_t (&g)[JN],
+                                               uint32_t cnt, int NT, uint32_t* __restrict__ out, uint32_t n) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t mine = 0;  // lane k < NT: this wave's entries of tile k
+  static_for<0, JN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if ((uint32_t)(w * JN + j) * 64u < cnt) {  // wave-uniform
+      const uint32_t mj = m[j];
+#pragma unroll 1
+      for (int k = 0; k < NT; ++k) {  // (k: an SGPR)
+        const uint64_t b = wave_ballot((mj >> k) & 1u);
+        mine += lane == k ? (uint32_t)__popcll(b) : 0u;
+      }
+    }
+  });
+  if (lane < 16) L.etot[w][lane] = mine;
+  __syncthreads();
+  uint32_t pre = 0;  // lane k: first slot of this wave's entries of tile k
+  if (lane < NT) {
+    pre = L.erun[lane];
+    for (int q = 0; q < w; ++q) pre += L.etot[q][lane];
+  }
+  static_for<0, JN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if ((uint32_t)(w * JN + j) * 64u < cnt) {
+      const uint32_t mj = m[j], gj = g[j];
+#pragma unroll 1
+      for (int k = 0; k < NT; ++k) {
+        const bool bit = (mj >> k) & 1u;
+        const uint64_t b = wave_ballot(bit);
+        if (b != 0) {  // wave-uniform
+          const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)pre, k);
+          if (bit) out[(size_t)k * n + base + lanes_below(b)] = gj;
+          pre += lane == k ? (uint32_t)__popcll(b) : 0u;
+        }
+      }
+    }
+  });
+  __syncthreads();  // every wave has read erun
+  if (w == kBdsWaves - 1 && lane < NT) L.erun[lane] = pre;  // the last wave's end = the running totals
+  __syncthreads();
+}
+
+// the bin's ranges / list lengths (and the lists' location flag), after its last chunk
+__device__ __forceinline__ void bds_emit_ranges(const BdsLds& L, const BdsEmit& E, uint32_t bin, uint32_t lo,
+                                                uint32_t n) {
+  const int t = threadIdx.x;
+  const int B = 1 << E.bshift;
+  if (bin == 0 && t == 0) E.meta[0] = 1u;  // the lists are the sort-bin region
+  if (t < B * B) {
+    const int r = t >> E.bshift, c = t & (B - 1);
+    const int bx = (int)(bin % (uint32_t)E.gbx), by = (int)(bin / (uint32_t)E.gbx);
+    const int tx = (bx << E.bshift) + c, ty = (by << E.bshift) + r;
+    if (tx < E.gx && ty < E.gy) {
+      const uint32_t tile = (uint32_t)ty * (uint32_t)E.gx + (uint32_t)tx;
+      const uint32_t b0 = (lo << (2 * E.bshift)) + (uint32_t)t * n;
+      const uint32_t c_t = n ? L.erun[t] : 0u;
+      E.ranges[tile] = make_uint2(b0, b0 + c_t);
+      E.tile_len[tile] = c_t;
+    }
+  }
+}
 
 __device__ __forceinline__ uint32_t bds_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -768,7 +992,7 @@ template <int JN>
 __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict__ skeys,
                                           const uint32_t* __restrict__ sgid, const uint32_t* __restrict__ sdep,
                                           uint32_t lo, uint32_t n, uint32_t* __restrict__ okeys,
-                                          uint32_t* __restrict__ ogid) {
+                                          uint32_t* __restrict__ ogid, bool E, const BdsEmit& EM) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   constexpr uint32_t kPosMask = (1u << kBdsPosBits) - 1u;
   uint32_t k[JN], pk[JN];
@@ -814,6 +1038,25 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
       if (bds_owns_digit()) L.wcnt[q][t] = 0u;
     __syncthreads();
   }
+  if (E) {  // the per-tile lists straight from the sorted bin
+    uint32_t m[JN], g[JN];
+    const uint32_t tmask = (1u << (1 << (2 * EM.bshift))) - 1u;
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+      m[j] = 0u;
+      g[j] = 0u;
+      if (le < n) {
+        const uint32_t q = pk[j] & kPosMask;
+        m[j] = (skeys[lo + q] >> 16) & tmask;
+        g[j] = sgid[lo + q];
+      }
+    }
+    if (t < 16) L.erun[t] = 0u;
+    __syncthreads();
+    bds_emit_chunk<JN>(L, m, g, n, 1 << (2 * EM.bshift), EM.lists + ((size_t)lo << (2 * EM.bshift)), n);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
@@ -825,12 +1068,44 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
   }
 }
 
+// the emit of a bin beyond the LDS tile: chunks of JN x kBdsThreads sorted
+// positions, their bin positions from the final pass's scratch (fin; null:
+// already in order), running per-tile counts across the chunks
+template <int JN>
+__device__ __forceinline__ void bds_emit_big(BdsLds& L, const uint32_t* __restrict__ skeys,
+                                             const uint32_t* __restrict__ sgid, const uint2* fin, uint32_t lo,
+                                             uint32_t n, const BdsEmit& E) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t tmask = (1u << (1 << (2 * E.bshift))) - 1u;
+  constexpr uint32_t kChunk = JN * kBdsThreads;
+  if (t < 16) L.erun[t] = 0u;
+  __syncthreads();
+  uint32_t* out = E.lists + ((size_t)lo << (2 * E.bshift));
+  for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+    const uint32_t cn = min(kChunk, n - c0);
+    uint32_t m[JN], g[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+      m[j] = 0u;
+      g[j] = 0u;
+      if (le < cn) {
+        const uint32_t q = fin ? bds_load_scratch(fin + c0 + le).y : c0 + le;
+        m[j] = (skeys[lo + q] >> 16) & tmask;
+        g[j] = sgid[lo + q];
+      }
+    }
+    bds_emit_chunk<JN>(L, m, g, cn, 1 << (2 * E.bshift), out, n);
+  }
+}
+
 // a bin beyond the LDS tile: each pass counts its digits over the whole bin,
 // then ranks kBdsCap-entry chunks in order with running digit bases, the
 // (key, position) pairs ping-ponging through global scratch
 __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid,
                                      const uint32_t* __restrict__ sdep, uint32_t lo, uint32_t n, uint32_t NL,
-                                     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch) {
+                                     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch,
+                                     bool E, const BdsEmit& EM) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
   for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
@@ -841,14 +1116,18 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
   int R, passes, pbits;
   mn = bds_range(L, mn, mx, R);
   bds_plan(R, passes, pbits);
+  constexpr int JN = 7;  // (chunks of half the LDS tile: fewer registers)
   if (passes == 0) {
+    if (E) {
+      bds_emit_big<JN>(L, skeys, sgid, nullptr, lo, n, EM);
+      return;
+    }
     for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
       okeys[lo + e] = skeys[lo + e];
       ogid[lo + e] = sgid[lo + e];
     }
     return;
   }
-  constexpr int JN = 7;  // (chunks of half the LDS tile: fewer registers)
   constexpr uint32_t kChunk = JN * kBdsThreads;
   uint2* bufA = scratch + lo;
   uint2* bufB = scratch + NL + lo;
@@ -905,6 +1184,10 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
     __syncthreads();
   }
   const uint2* fin = ((passes - 1) & 1) ? bufB : bufA;
+  if (E) {
+    bds_emit_big<JN>(L, skeys, sgid, fin, lo, n, EM);
+    return;
+  }
   for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
     const uint32_t q = bds_load_scratch(fin + e).y;
     okeys[lo + e] = skeys[lo + q];
@@ -915,12 +1198,17 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
 __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid, const uint2* __restrict__ bounds,
     const uint32_t* __restrict__ sdep, uint32_t NL, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid,
-    uint2* scratch) {
+    uint2* scratch, BdsEmit emit) {
   __shared__ BdsLds L;
   const int t = threadIdx.x;
   const uint2 bb = bounds[blockIdx.x];
   const uint32_t lo = bb.x, n = bb.y - bb.x;
-  if (n == 0) return;  // block-uniform
+  // (a flag, not a pointer to the by-value argument: that would put it in scratch)
+  const bool E = emit.lists != nullptr;
+  if (n == 0) {  // block-uniform
+    if (E) bds_emit_ranges(L, emit, blockIdx.x, lo, 0u);
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < kBdsWaves; ++q)
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
@@ -928,17 +1216,18 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
 #endif
   if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
-    bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+    bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 2u * kBdsThreads)
-    bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+    bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 4u * kBdsThreads)
-    bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+    bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 7u * kBdsThreads)
-    bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+    bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
-    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid);
+    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else
-    bds_big(L, skeys, sgid, sdep, lo, n, NL, okeys, ogid, scratch);
+    bds_big(L, skeys, sgid, sdep, lo, n, NL, okeys, ogid, scratch, E, emit);
+  if (E) bds_emit_ranges(L, emit, blockIdx.x, lo, n);
 }
 
 // ---- tile ranges and the tiles' launch order ---------------------------------
@@ -1424,6 +1713,26 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  // k_preprocess2 (LDS-DMA slab behind the geometry) unless WGSR_PRE=1
+  static const bool pre_v1 = [] {
+    const char* e = getenv("WGSR_PRE");
+    return e && atoi(e) == 1;
+  }();
+  if (!pre_v1) {
+    const bool sh_on = a.shs && !a.colors;
+    const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
+    const int nf = 3 * (a.D + 1) * (a.D + 1);
+    const int kch = ch4 ? 4 : 1;
+    const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
+    auto kern = ch4 ? k_preprocess2<4> : k_preprocess2<1>;
+    hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds2, s, a.P, a.D, a.M, a.means3D,
+                       a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
+                       a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
+                       at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
+                       at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs,
+                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero);
+    return hipGetLastError();
+  }
   const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreRows * (3 * (size_t)a.M + 1) : 0;
   hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
                      a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
@@ -1466,7 +1775,8 @@ hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_
 
 hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
                                  uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
-                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s) {
+                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s, uint32_t* lists,
+                                 uint2* ranges, uint32_t* tile_len, uint32_t* meta) {
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const Bins B(gx, gy, bshift);
   if (!bounds_done) {  // (a one-pass sort already wrote them)
@@ -1474,8 +1784,11 @@ hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sort
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bin_bounds, dim3((NB + 255) / 256), dim3(256), 0, s, sorted_keys, NB, bounds);
   }
+  // lists != null: the per-tile lists and ranges are emitted here (no
+  // k_expand_bins); else the sorted bins go to okeys / ogid
+  const BdsEmit emit{lists, ranges, tile_len, meta, gx, gy, bshift, B.bx};
   hipLaunchKernelGGL(k_bin_depth_sort, dim3((uint32_t)B.n), dim3(kBdsThreads), 0, s, sorted_keys, sorted_g, bounds,
-                     sdepth, NB, okeys, ogid, static_cast<uint2*>(scratch));
+                     sdepth, NB, okeys, ogid, static_cast<uint2*>(scratch), emit);
   return hipGetLastError();
 }
 

@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup, uint2* __restrict__ bounds,
     const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout) {
   constexpr int kTile = 256 * I;
-  __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16)
-  __shared__ uint32_t s_x[kTile];  // the second payload (xin: the bin sort's depth keys)
+  __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16); then the
+                                  // second payload (xin: the bin sort's depth keys) -- no extra LDS
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
@@ -316,10 +316,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const size_t e = base + (size_t)j * 64 + lane;
     const uint32_t d = (key[j] >> shift) & mask;
     const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];  // block-local slot in digit order
-    if (e < n) {
-      s_buf[slot] = make_uint2(key[j], val[j]);
-      if (xin) s_x[slot] = xv[j];
-    }
+    if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
   }
   __syncthreads();
   const uint32_t cnt = (uint32_t)min((size_t)kTile, (size_t)n - blk0);
@@ -332,7 +329,25 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
       const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
       kout[dst] = kv.x;
       vout[dst] = kv.y;
-      if (xin) xout[dst] = s_x[i];
+    }
+  }
+  if (xin) {  // the second payload replaces the values in the staging buffer (keys kept)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < I; ++j) {
+      const size_t e = base + (size_t)j * 64 + lane;
+      const uint32_t d = (key[j] >> shift) & mask;
+      if (e < n) s_buf[s_lbase[d] + s_wcnt[w][d] + rank[j]].y = xv[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < I; ++r) {
+      const uint32_t i = (uint32_t)t + 256u * r;
+      if (i < cnt) {
+        const uint2 kx = s_buf[i];
+        const uint32_t d = (kx.x >> shift) & mask;
+        xout[s_gbase[d] + (i - s_lbase[d])] = kx.y;
+      }
     }
   }
 }

@@ -81,12 +81,16 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 // per-bin depth sort (pairs duplicated in index order): every bin's entries
-// stably by depth key (sdepth: the pairs' depth keys in bin-sorted order) ->
-// okeys / ogid (bounds written first unless bounds_done); scratch: >= 2 NB
-// uint2 (bins beyond one LDS tile)
+// stably by depth key (sdepth: the pairs' depth keys in bin-sorted order)
+// (bounds written first unless bounds_done); scratch: >= 2 NB uint2 (bins
+// beyond one LDS tile).  With lists: the per-tile exact lists, ranges,
+// tile_len and meta emitted straight from each sorted bin (what
+// launch_expand_bins would make of it); else the sorted bins -> okeys / ogid.
 hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
                                  uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
-                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s);
+                                 uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s,
+                                 uint32_t* lists = nullptr, uint2* ranges = nullptr, uint32_t* tile_len = nullptr,
+                                 uint32_t* meta = nullptr);
 // per-tile exact lists out of the bin-sorted pairs: ranges / tile_len per
 // tile, the lists in bin-sized regions of `lists` (2^2s x NB entries)
 hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,

@@ -18,6 +18,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
+#include <exception>
 #include <sstream>
 #include <string>
 
@@ -52,7 +53,8 @@ void need_lib() {
     throw std::runtime_error("diff_gaussian_rasterization._native: libwgsr entry points not bound");
 }
 
-void check(int code) {
+void check(int code, const std::exception_ptr& alloc_failure = nullptr) {
+  if (code == 3 /* WGSR_EALLOC */ && alloc_failure) std::rethrow_exception(alloc_failure);
   if (code != 0) {
     std::ostringstream s;
     s << "wgsr error " << code << ": " << g_lib.last_error();
@@ -98,14 +100,24 @@ const float* fp(const at::Tensor& t) { return t.defined() ? t.data_ptr<float>() 
 
 // allocation callbacks: torch uint8 tensors kept in the context; a buffer of
 // n bytes is the first n bytes of a max(n, 1)-byte tensor (as _lib._make_alloc)
+// No exception may unwind through libwgsr's extern "C" frames: a failed
+// allocation (e.g. torch's OutOfMemoryError) is kept and NULL returned, the
+// library reports WGSR_EALLOC through its own error path, and check() then
+// rethrows the original exception.
 struct Alloc {
   at::Device dev;
   at::Tensor geom, binning, image, scratch;
+  std::exception_ptr failure;
   explicit Alloc(const at::Device& d) : dev(d) {}
-  void* take(at::Tensor& slot, size_t n) {
-    at::Tensor base = at::empty({(int64_t)(n > 0 ? n : 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
-    slot = base.narrow(0, 0, (int64_t)n);
-    return base.data_ptr();
+  void* take(at::Tensor& slot, size_t n) noexcept {
+    try {
+      at::Tensor base = at::empty({(int64_t)(n > 0 ? n : 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+      slot = base.narrow(0, 0, (int64_t)n);
+      return base.data_ptr();
+    } catch (...) {
+      if (!failure) failure = std::current_exception();
+      return nullptr;
+    }
   }
 };
 void* alloc_geom(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->geom, n); }
@@ -186,7 +198,7 @@ rasterize_gaussians(const OptT& background, const at::Tensor& means3D, const Opt
                                  out_depth.data_ptr<float>(), out_opacity.data_ptr<float>(),
                                  P ? radii.data_ptr<int32_t>() : nullptr, P ? n_touched.data_ptr<int32_t>() : nullptr,
                                  &nr, stream_of(dev));
-  check(code);
+  check(code, al.failure);
   const at::Tensor empty = at::empty({0}, at::TensorOptions().dtype(at::kByte).device(dev));
   return {nr,
           out_color,
@@ -276,7 +288,7 @@ rasterize_gaussians_backward(const OptT& background, const at::Tensor& means3D, 
       dL_dopacity.data_ptr<float>(), dL_dmeans3D.data_ptr<float>(), dL_dcov3D.data_ptr<float>(),
       dL_dsh.numel() ? dL_dsh.data_ptr<float>() : nullptr, dL_dscales.data_ptr<float>(),
       dL_drotations.data_ptr<float>(), dL_dtau.data_ptr<float>(), stream_of(dev));
-  check(code);
+  check(code, al.failure);
   return {dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau};
 }
 
