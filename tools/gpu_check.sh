@@ -15,7 +15,12 @@ for s in $STEPS; do
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$? ;;
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1; rc=$?
+      # PYTEST_K: a -k expression (may contain spaces); PYTEST_ARGS: extra words
+      if [ -n "${PYTEST_K:-}" ]; then
+        timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider -k "$PYTEST_K" ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1; rc=$?
+      else
+        timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 400 -p no:cacheprovider ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1; rc=$?
+      fi
       if [ $rc -ge 2 ] && [ $rc -le 5 ]; then rc=0; fi ;;  # pytest usage/collection codes are not GPU faults
     bench)
       timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench${SFX:-}.json 2> $OUT/bench${SFX:-}.err; rc=$? ;;

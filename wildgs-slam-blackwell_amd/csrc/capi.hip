@@ -70,6 +70,16 @@ struct DevCounters {
   int parity = 0;
   bool failed = false;
 };
+// WGSR_BDS_EMIT: 1 / 0 forces the per-tile list emit of the per-bin depth
+// sort on / off (-1: by bin size)
+int bds_emit_mode() {
+  static const int m = [] {
+    const char* e = getenv("WGSR_BDS_EMIT");
+    return e ? (atoi(e) ? 1 : 0) : -1;
+  }();
+  return m;
+}
+
 DevCounters* dev_counters(hipStream_t s) {
   static const bool off = [] {
     const char* e = getenv("WGSR_COUNTER_MEMSET");
@@ -558,11 +568,12 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       StageTimer T(4, s);
       uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
       uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
-      // (WGSR_BDS_EMIT=0: the sorted bins to okeys / ogid and k_expand_bins)
-      static const bool emit = [] {
-        const char* e = getenv("WGSR_BDS_EMIT");
-        return !(e && atoi(e) == 0);
-      }();
+      // Emitting the lists from the sort kernel pays for small bins (2 x 2
+      // tiles: TUM 512 x 384, 35.4 -> 33.8 us for sort + lists); with 4 x 4-tile
+      // bins (1080p) the 16-tile compaction inside the one-workgroup-per-CU
+      // sort costs more than k_expand_bins' 4x wider grid (140.8 vs 131.3 us).
+      // WGSR_BDS_EMIT=0 / 1 forces either.
+      const bool emit = bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1);
       STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift, at<uint2>(image, IL.tile_m),
                                         bounds_done, pdep, okeys, ogid, bds_scratch, s, emit ? lists : nullptr,
                                         ranges, at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta)));
@@ -573,11 +584,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       }
     }
     StageTimer T(5, s);
-    static const bool emitted = [] {
-      const char* e = getenv("WGSR_BDS_EMIT");
-      return !(e && atoi(e) == 0);
-    }();
-    if (bin_depth && emitted) {
+    if (bin_depth && (bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1))) {
       // (lists and ranges written by the per-bin depth sort)
     } else if (bshift) {
       STAGE(a, s, launch_expand_bins(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift,
