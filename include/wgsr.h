@@ -83,6 +83,26 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args,
                            int32_t* radii, int32_t* n_touched, int64_t* num_rendered,
                            void* stream);
 
+/* Capacity mode of wgsr_rasterize_forward (no upstream counterpart): the
+ * same outputs with NO host synchronisation, so that a whole mapping
+ * iteration can be captured in a HIP graph (wgsr/online.py).  The state
+ * buffers are sized for `cap` (Gaussian, tile) rectangle pairs (upstream's
+ * num_rendered bounds the exact and bin pairs); pass cap as num_rendered to
+ * wgsr_rasterize_backward.  counts (device, 5 uint32): N_rect, N_exact,
+ * N_bin (saturating), overflow (N_rect > cap), min(N_bin, cap).  After an
+ * overflow the images are undefined and the backward writes zero gradients;
+ * callers skip their optimizer step on counts[3] (wgsr_adam_step_dev).
+ * Needs the default sort-bin configuration (WGSR_EINVAL otherwise) and
+ * prefiltered = 0. */
+int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap,
+                               wgsr_alloc_fn geom_alloc, wgsr_alloc_fn binning_alloc,
+                               wgsr_alloc_fn image_alloc, void* alloc_ctx,
+                               float* out_color, float* out_depth, float* out_opacity,
+                               int32_t* radii, int32_t* n_touched, uint32_t* counts,
+                               void* stream);
+/* Bytes of the binning buffer wgsr_rasterize_forward_cap requests for `cap`. */
+size_t wgsr_binning_bytes_cap(const wgsr_raster_args* args, int64_t cap);
+
 /* Replaces _C.rasterize_gaussians_backward.
  * Inputs: the forward's radii, state buffers and num_rendered; upstream
  * gradients dL_dcolor [3,H,W] and dL_ddepth [1,H,W].
@@ -375,6 +395,14 @@ int wgsr_mlp_grad_floats(int C);
 int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
                      const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed,
                      float* h1d, float* h2d, float* o_pre, float* u, void* stream);
+/* wgsr_mlp_forward with the dropout seed read from device memory (a
+ * graph-replayed mapping iteration draws a new seed per step). */
+int wgsr_mlp_forward_dev_seed(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                              const float* b2, const float* W3, const float* b3, float dropout_p,
+                              const uint32_t* seed, float* h1d, float* h2d, float* o_pre, float* u, void* stream);
+/* keys[i] = 31-bit hash of (seed, i), i < n (seed_dev, when not NULL, holds
+ * the seed): sorting the keys gives the DINO term's random sample order. */
+int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t* keys, void* stream);
 int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
                       const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
                       float* scratch, float* grad, void* stream);
@@ -440,6 +468,15 @@ typedef struct wgsr_adam_tensor {
  * 1-beta is formed in double and rounded once, as torch does. */
 int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
                    void* stream);
+
+/* wgsr_adam_step with the per-step scalars in DEVICE memory, for a step
+ * replayed from a HIP graph: tensor i uses scalars[3 i + 0..2] = step_size,
+ * bias_correction2_sqrt, step_size_tail (its own fields are ignored);
+ * skip (or NULL): no update at all when *skip != 0 (a capacity-mode forward
+ * that overflowed); weight_decay: torch.optim.Adam's L2 term, the gradient
+ * used is grad + weight_decay * param (0: none). */
+int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
+                       double weight_decay, const float* scalars, const uint32_t* skip, void* stream);
 
 /* One row-major tensor for row compaction: rows of `row_bytes` (a multiple
  * of 4) from `src` [P rows]; `dst` receives the kept rows in order. */

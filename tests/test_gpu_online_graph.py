@@ -1,0 +1,202 @@
+"""The graph-replayed mapping iteration (wgsr.online_graph) and the pieces it
+is built from, against their eager counterparts:
+
+* wgsr_rasterize_forward_cap (capacity mode, no host wait) renders exactly
+  what wgsr_rasterize_forward renders, reports upstream's num_rendered in
+  counts[0], and its backward (num_rendered = cap) matches; an overflow
+  (cap < N_rect) is flagged and leaves all-zero gradients;
+* wgsr_adam_step_dev (device scalars, skip word, L2 weight decay) equals
+  wgsr_adam_step / torch.optim.Adam;
+* wgsr_mlp_forward_dev_seed equals wgsr_mlp_forward with the same seed, and
+  wgsr_random_keys equals its numpy restatement;
+* OnlineMapper.map_opt_online / final_refine with graphs: the same map, MLP
+  and exposures as the eager loop from the same seeds, iterations replayed,
+  and a forced capacity overflow recovers (recapture, event recorded).
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_online import _keyframes
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _scene(P=20000, W=160, H=120, seed=0):
+    from wgsr.camera import synthetic_camera
+    g = torch.Generator().manual_seed(seed)
+    xyz = (torch.rand(P, 3, generator=g) - 0.5) * torch.tensor([4.0, 3.0, 2.0]) + torch.tensor([0.0, 0.0, 5.0])
+    scales = torch.full((P, 3), 0.03) * (0.5 + torch.rand(P, 3, generator=g))
+    rots = torch.nn.functional.normalize(torch.randn(P, 4, generator=g), dim=1)
+    opac = 0.2 + 0.7 * torch.rand(P, 1, generator=g)
+    shs = torch.randn(P, 1, 3, generator=g) * 0.5
+    cam = synthetic_camera(W, H).raster_fields()
+    cam = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in cam.items()}
+    return [t.to(DEV).contiguous() for t in (xyz, opac, scales, rots, shs)], cam, W, H
+
+
+def _backward(args, cam, fwd, W, H, dcol, ddep):
+    from diff_gaussian_rasterization import _C
+    xyz, opac, scales, rots, shs = args
+    e = torch.empty(0, device=DEV)
+    return _C.rasterize_gaussians_backward(torch.zeros(3, device=DEV), xyz, fwd[2], e, scales, rots, 1.0, e,
+                                           cam["viewmatrix"], cam["projmatrix"], cam["projmatrix_raw"],
+                                           cam["tanfovx"], cam["tanfovy"], dcol, ddep, shs, 0, cam["campos"],
+                                           fwd[3], fwd[0], fwd[4], fwd[5], False)
+
+
+def test_capacity_forward_matches_and_overflow_zeroes_gradients():
+    from diff_gaussian_rasterization import _C
+    from wgsr.mapping import rasterize_forward_cap
+    args, cam, W, H = _scene()
+    xyz, opac, scales, rots, shs = args
+    bg = torch.zeros(3, device=DEV)
+    e = torch.empty(0, device=DEV)
+    ref = _C.rasterize_gaussians(bg, xyz, e, opac, scales, rots, 1.0, e, cam["viewmatrix"], cam["projmatrix"],
+                                 cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, shs, 0, cam["campos"],
+                                 False, False)
+    N = ref[0]
+    assert N > 1000
+    counts = torch.zeros(5, dtype=torch.int32, device=DEV)
+    out = rasterize_forward_cap(bg, xyz, opac, scales, rots, shs, 0, cam, H, W, N + 12345, counts)
+    c = counts.cpu().tolist()
+    assert c[0] == N and c[3] == 0 and 0 < c[2] <= c[1] <= N and c[4] == c[2]
+    for i in (1, 2, 6, 7, 8):
+        assert torch.equal(out[i], ref[i]), i
+    g = torch.Generator(device=DEV).manual_seed(1)
+    dcol = torch.randn(3, H, W, device=DEV, generator=g)
+    ddep = torch.randn(1, H, W, device=DEV, generator=g)
+    gr = _backward(args, cam, ref, W, H, dcol, ddep)
+    gc = _backward(args, cam, out, W, H, dcol, ddep)
+    for a, b in zip(gr, gc):
+        assert torch.equal(a, b)
+    # overflow: flagged, no host error, every gradient zero
+    counts.zero_()
+    small = rasterize_forward_cap(bg, xyz, opac, scales, rots, shs, 0, cam, H, W, N // 3, counts)
+    c = counts.cpu().tolist()
+    assert c[0] == N and c[3] == 1 and c[4] == min(c[2], N // 3)
+    go = _backward(args, cam, small, W, H, dcol, ddep)
+    for t in go:
+        assert not t.any()
+
+
+def test_adam_step_dev_matches_host_scalars_and_torch_weight_decay():
+    from wgsr import _lib
+    L = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    n = 1037
+    mk = lambda: torch.randn(n, device=DEV, generator=g)  # noqa: E731
+    p, gr, m, v = mk(), mk(), mk().abs() * 0.1, mk().abs() * 0.01
+    st = _lib.stream_handle(DEV)
+    outs = []
+    for dev_mode in (False, True):
+        pp, mm, vv = p.clone(), m.clone(), v.clone()
+        t = _lib.AdamTensor(pp.data_ptr(), gr.data_ptr(), mm.data_ptr(), vv.data_ptr(), n, 1e-3 / 0.1, 0.03)
+        arr = (_lib.AdamTensor * 1)(t)
+        if dev_mode:
+            sc = torch.tensor([1e-3 / 0.1, 0.03, 0.0], device=DEV)
+            skip = torch.zeros(1, dtype=torch.int32, device=DEV)
+            _lib.check(L.wgsr_adam_step_dev(arr, 1, 0.9, 0.999, 1e-15, 0.0, sc.data_ptr(), skip.data_ptr(), st))
+        else:
+            _lib.check(L.wgsr_adam_step(arr, 1, 0.9, 0.999, 1e-15, st))
+        outs.append((pp, mm, vv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # skip word set: nothing moves
+    pp, mm, vv = p.clone(), m.clone(), v.clone()
+    t = _lib.AdamTensor(pp.data_ptr(), gr.data_ptr(), mm.data_ptr(), vv.data_ptr(), n, 1.0, 1.0)
+    sc = torch.tensor([1.0, 1.0, 0.0], device=DEV)
+    skip = torch.ones(1, dtype=torch.int32, device=DEV)
+    _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, 0.0, sc.data_ptr(),
+                                    skip.data_ptr(), st))
+    assert torch.equal(pp, p) and torch.equal(mm, m) and torch.equal(vv, v)
+    # weight decay: torch.optim.Adam(weight_decay=wd), three steps
+    wd, lr = 1e-2, 4e-3
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=lr, weight_decay=wd)
+    pp = p.clone()
+    mm, vv = torch.zeros_like(p), torch.zeros_like(p)
+    for k in range(1, 4):
+        gk = mk()
+        ref.grad = gk.clone()
+        opt.step()
+        t = _lib.AdamTensor(pp.data_ptr(), gk.data_ptr(), mm.data_ptr(), vv.data_ptr(), n, 0.0, 1.0)
+        sc = torch.tensor([lr / (1 - 0.9 ** k), (1 - 0.999 ** k) ** 0.5, 0.0], device=DEV)
+        _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, wd, sc.data_ptr(), None, st))
+    torch.testing.assert_close(pp, ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_mlp_device_seed_and_random_keys():
+    from wgsr import _lib
+    from wgsr.mlp import UncertaintyMLP, _mix32, forward_raw
+    torch.manual_seed(0)
+    net = UncertaintyMLP(128).to(DEV)
+    x = torch.randn(300, 128, device=DEV)
+    seed = 123456789
+    net.seed_source = lambda: seed
+    u_ref = net(x.view(1, 300, 128))[0]
+    u, _ = forward_raw(net, x, torch.tensor([seed], dtype=torch.int32, device=DEV))
+    assert torch.equal(u, u_ref)
+    L = _lib.load()
+    n = 5000
+    keys = torch.empty(n, dtype=torch.int32, device=DEV)
+    sd = torch.tensor([seed], dtype=torch.int32, device=DEV)
+    _lib.check(L.wgsr_random_keys(n, 0, sd.data_ptr(), keys.data_ptr(), _lib.stream_handle(DEV)))
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint32)
+        want = (_mix32(np.uint32(seed) ^ _mix32(i * np.uint32(0x9E3779B9) + np.uint32(0x632BE5AB))) >> 1)
+    assert np.array_equal(keys.cpu().numpy(), want.astype(np.int32))
+
+
+CFG = {"init_itr_num": 30, "init_gaussian_update": 100, "init_gaussian_reset": 10_000, "mapping_itr_num": 60,
+       "gaussian_update_every": 100_000, "gaussian_update_offset": 99_999, "gaussian_reset": 100_001,
+       "window_size": 4}
+
+
+def _run(graphs: bool, cap=None, refine=0):
+    from wgsr.online import OnlineMapper
+    kfs = _keyframes(4)
+    m = OnlineMapper(sh_degree=0, device=DEV, config=CFG, seed=3)
+    if not graphs:
+        m.graphs = None
+    m.initialize(kfs[:2])
+    if graphs and cap is not None:
+        m.graphs.cap = cap
+    for kf in kfs[2:]:
+        m.insert_keyframe(kf, iters=60)
+    if refine:
+        m.iterations_after_densify_or_reset = 1000
+        m.final_refine(refine)
+    torch.cuda.synchronize()
+    return m
+
+
+def _state(m):
+    out = {n: m.ms.store.param(n).clone() for n in m.ms.GROUPS}
+    out.update({f"mlp{i}": p.detach().clone() for i, p in enumerate(m.net.parameters())})
+    out["exposure"] = torch.stack([torch.cat([k.exposure_a, k.exposure_b]) for k in m.keyframes.values()])
+    return out
+
+
+def test_graph_replayed_loop_matches_eager():
+    a = _state(_run(False, refine=40))
+    mg = _run(True, refine=40)
+    b = _state(mg)
+    st = mg.graphs.stats
+    assert st["replays"] > 100 and st["captures"] >= 2 and st["overflows"] == 0, st
+    assert mg.graphs.disabled is None
+    for k in a:
+        assert a[k].shape == b[k].shape, k
+        rel = float((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-12))
+        assert rel <= 2e-3, (k, rel)
+
+
+def test_graph_capacity_overflow_recovers():
+    m = _run(True, cap=512)
+    st = m.graphs.stats
+    assert st["overflows"] >= 1 and st["skipped_iterations"] >= 1, st
+    assert any(k == "capacity_overflow" for _, k, _ in m.events)
+    assert m.graphs.cap > 512 and int(m.graphs.sticky_np[0]) == 0
+    for n in m.ms.GROUPS:
+        assert torch.isfinite(m.ms.store.param(n)).all()

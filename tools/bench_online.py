@@ -190,6 +190,8 @@ def main():
         "init_seconds": t_init, "gaussians_final": m.ms.P,
         "events": [(i, k, v) for i, k, v in m.events][:40],
         "psnr_db_mean": sum(ps) / len(ps), "psnr_db_per_keyframe": ps,
+        "graph": (dict(m.graphs.stats, cap=m.graphs.cap, disabled=m.graphs.disabled) if m.graphs is not None
+                  and os.environ.get("WGSR_ONLINE_GRAPH", "1") != "0" else None),
         "note": "uncertainty-aware loss + DINO regulariser + isotropic term, densify/prune, opacity reset, "
                 "Adam (Gaussians, exposures, MLP); before every insertion each existing keyframe's pose is "
                 "nudged and its Gaussians deformed (update_keyframes, one device pass); final_refine at the "

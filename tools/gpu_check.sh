@@ -26,6 +26,14 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench${SFX:-}.json 2> $OUT/bench${SFX:-}.err; rc=$? ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/prof_bench${SFX:-}.json 2> $GRAFT_REPO_ROOT/$OUT/prof${SFX:-}.err); rc=$? ;;
+    online)
+      # the configs[4]-shaped mapper loop (graph-replayed steady state by default)
+      timeout -k 10 600 python tools/bench_online.py ${ONLINE_ARGS:-} > $OUT/online${SFX:-}.json 2> $OUT/online${SFX:-}.err; rc=$? ;;
+    online0)
+      # ... the same run with every iteration eager (A/B)
+      WGSR_ONLINE_GRAPH=0 timeout -k 10 600 python tools/bench_online.py ${ONLINE_ARGS:-} > $OUT/online0${SFX:-}.json 2> $OUT/online0${SFX:-}.err; rc=$? ;;
+    onlineprof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/onlineprof${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/tools/bench_online.py --keyframes 4 --init-iters 100 --iters 150 --refine-iters 100 ${ONLINE_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/onlineprof${SFX:-}.json 2> $GRAFT_REPO_ROOT/$OUT/onlineprof${SFX:-}.err); rc=$? ;;
     f1)
       timeout -k 10 300 python tools/bench_f1.py > $OUT/bench_f1.json 2> $OUT/bench_f1.err; rc=$? ;;
     f2)

@@ -384,7 +384,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   } sync_on_error{s};
   { StageTimer T(0, s);
   const hipError_t pe = launch_preprocess(a, geom, radii, n_touched, counter + 1,
-                                          reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s);
+                                          reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s,
+                                          at<uint32_t>(image, IL.meta));
   if (pe == hipSuccess && dc) dc->parity ^= 1;  // k_preprocess, which zeroes the other block, is queued
   sync_on_error.armed = true;
   STAGE(a, s, pe); }
@@ -605,6 +606,134 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, at<uint32_t>(image, IL.tile_m), s)); }
   *num_rendered = (int64_t)N_rect;
+  return WGSR_OK;
+}
+
+size_t wgsr_binning_bytes_cap(const wgsr_raster_args* args, int64_t cap) {
+  if (!args || cap < 0) return 0;
+  const int bshift = bin_shift(*args);
+  const size_t C = (size_t)cap;
+  return BinLayout(C).total + align256(4 * (C << (2 * bshift))) + 8 * (align256(4 * C) / 4) + align256(16 * C);
+}
+
+// Capacity mode (wgsr.h): the forward above without its one host wait.  The
+// buffers are sized for `cap` (Gaussian, tile) rectangle pairs -- upstream's
+// num_rendered, which bounds the exact pairs and the bin pairs too -- and the
+// device-side counts take the place of the host's: k_cap_counts turns the
+// counter partials into counts[] and the overflow flag, the bin sort reads
+// its key count from counts[4], and an overflow (N_rect > cap) leaves the
+// render backward a zero fill (ImageLayout::meta[1]).  Only the default
+// configuration: sort bins with the per-bin depth sort and the one-pass bin
+// sort that hands back the bin bounds.  Every launch is stream-ordered
+// device work with host-known sizes, so the call can be captured in a HIP
+// graph (the next forward's counter block is zeroed by a memset here, not by
+// the parity scheme of the host-synchronised forward).
+int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_alloc_fn geom_alloc,
+                               wgsr_alloc_fn binning_alloc, wgsr_alloc_fn image_alloc, void* ctx, float* out_color,
+                               float* out_depth, float* out_opacity, int32_t* radii, int32_t* n_touched,
+                               uint32_t* counts, void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  const wgsr_raster_args& a = *args;
+  hipStream_t s = (hipStream_t)stream;
+  if (cap <= 0 || cap >= ((int64_t)1 << 30)) return set_error(WGSR_EINVAL, "capacity %lld out of range", (long long)cap);
+  if (!counts) return set_error(WGSR_EINVAL, "missing counts buffer");
+  if (a.prefiltered) return set_error(WGSR_EINVAL, "capacity mode: prefiltered is not supported");
+  const size_t HW = (size_t)a.W * a.H;
+  if (a.P == 0) {
+    call_alloc(geom_alloc, ctx, 0);
+    call_alloc(binning_alloc, ctx, 0);
+    call_alloc(image_alloc, ctx, 0);
+    HIPCHK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(out_opacity, 0, HW * sizeof(float), s));
+    HIPCHK(hipMemsetAsync(counts, 0, 5 * sizeof(uint32_t), s));
+    return WGSR_OK;
+  }
+  const Grid grid(a);
+  const int bshift = bin_shift(a);
+  if (!bshift || !depth_sort_bins(a, bshift))
+    return set_error(WGSR_EINVAL, "capacity mode needs sort bins with the per-bin depth sort");
+  const Bins bins(grid.gx, grid.gy, bshift);
+  const int bits = num_bits((uint32_t)bins.n) > 0 ? num_bits((uint32_t)bins.n) : 1;
+  if (!((size_t)8 << bits <= (size_t)16 * grid.nt))
+    return set_error(WGSR_EINVAL, "capacity mode: the bin bounds do not fit the tile_m region");
+  const GeomLayout GL((size_t)a.P);
+  const ImageLayout IL(a.W, a.H);
+  void* geom = call_alloc(geom_alloc, ctx, GL.total);
+  if (!geom) return set_error(WGSR_EALLOC, "geometry buffer allocation failed");
+  void* image = call_alloc(image_alloc, ctx, IL.total);
+  if (!image) return set_error(WGSR_EALLOC, "image buffer allocation failed");
+  const size_t C = (size_t)cap;
+  const BinLayout BL(C);
+  const size_t lists_bytes = align256(4 * (C << (2 * bshift)));
+  const size_t pdep_words = align256(4 * C) / 4;
+  const size_t binning_bytes = BL.total + lists_bytes + 8 * pdep_words + align256(16 * C);
+  void* binning = call_alloc(binning_alloc, ctx, binning_bytes);
+  if (!binning) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  uint32_t* lists = at<uint32_t>(binning, BL.total);
+  uint32_t* pdep = at<uint32_t>(binning, BL.total + lists_bytes);
+  uint32_t* pdep_alt = pdep + pdep_words;
+  void* bds_scratch = at<char>(binning, BL.total + lists_bytes + 8 * pdep_words);
+  uint32_t* counter = at<uint32_t>(geom, GL.counter);
+  uint32_t* meta = at<uint32_t>(image, IL.meta);
+  HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
+  ZeroJob zj{};
+  const bool scan_sup = scan_sup_mode();
+  if (scan_sup) {
+    zj.p[zj.count] = at<float>(geom, GL.bsup);
+    zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
+  }
+  { StageTimer T(0, s);
+  STAGE(a, s, launch_preprocess(a, geom, radii, n_touched, counter + 1,
+                                reinterpret_cast<unsigned long long*>(counter + 4), bshift, zj, s, meta)); }
+  STAGE(a, s, launch_cap_counts(reinterpret_cast<const unsigned long long*>(counter + 4), (uint64_t)C, (uint64_t)C,
+                                counts, meta, s));
+  { StageTimer T(2, s);  // block sums of (list length, bins) in index order
+  STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, nullptr, (size_t)a.P, at<uint32_t>(geom, GL.bsum), s,
+                                 scan_sup ? at<uint2>(geom, GL.bsup) : nullptr)); }
+  const bool odd = radix_passes(0, bits) % 2 == 1;
+  uint32_t* vin = at<uint32_t>(binning, odd ? BL.slot_g : BL.point_g);
+  uint32_t* valt = at<uint32_t>(binning, odd ? BL.point_g : BL.slot_g);
+  size_t bs_off = 0;
+  const size_t bs_words = sort_sup_words(C, 0, bits, &bs_off);
+  ZeroJob zb{};
+  if (bs_words) {
+    zb.p[0] = reinterpret_cast<float*>(at<uint32_t>(binning, BL.hist) + bs_off);
+    zb.n[0] = bs_words;
+    zb.count = 1;
+  }
+  { StageTimer T(3, s);  // (pairs past the capacity are not written; exact-slot flags likewise)
+  STAGE(a, s, launch_duplicate_bins(a, geom, nullptr, bshift, at<uint8_t>(binning, BL.flag),
+                                    at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, odd ? pdep_alt : pdep,
+                                    (uint32_t)C, (uint32_t)C)); }
+  bool talt = false, bounds_done = false;
+  uint2* bin_bounds = at<uint2>(image, IL.tile_m);
+  { StageTimer T(4, s);
+  STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false, C,
+                               0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s, &talt,
+                               bin_bounds, &bounds_done, bs_words != 0, odd ? pdep_alt : pdep, odd ? pdep : pdep_alt,
+                               counts + 4)); }
+  if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
+  if (!bounds_done) return set_error(WGSR_EHIP, "internal: capacity mode without the sort's bin bounds");
+  const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
+  const uint32_t* sorted_gid = at<uint32_t>(binning, BL.point_g);
+  uint2* ranges = at<uint2>(image, IL.ranges);
+  const bool emit = bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1);
+  uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
+  uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
+  { StageTimer T(4, s);
+  STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)C, bshift, bin_bounds, true, pdep, okeys,
+                                    ogid, bds_scratch, s, emit ? lists : nullptr, ranges,
+                                    at<uint32_t>(image, IL.tile_len), meta)); }
+  if (!emit) { StageTimer T(5, s);
+    STAGE(a, s, launch_expand_bins(a, okeys, ogid, (uint32_t)C, bshift, bin_bounds, true, lists, ranges,
+                                   at<uint32_t>(image, IL.tile_len), meta, s));
+  }
+  g_depth_order_off = -1;
+  { StageTimer T(6, s);
+  STAGE(a, s, launch_render_fwd(a, ranges, lists, geom, out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
+                                at<uint32_t>(image, IL.n_contrib), n_touched, at<uint32_t>(image, IL.tile_m), s)); }
   return WGSR_OK;
 }
 

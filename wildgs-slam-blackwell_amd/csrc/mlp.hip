@@ -80,9 +80,11 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __re
                                                  const float* __restrict__ W1, const float* __restrict__ b1,
                                                  const float* __restrict__ W2, const float* __restrict__ b2,
                                                  const float* __restrict__ W3, const float* __restrict__ b3, float p,
-                                                 uint32_t seed, float* __restrict__ h1d, float* __restrict__ h2d,
+                                                 uint32_t seed, const uint32_t* __restrict__ seed_dev,
+                                                 float* __restrict__ h1d, float* __restrict__ h2d,
                                                  float* __restrict__ o_pre, float* __restrict__ u) {
   constexpr int CW = R / 16, TXN = 64 / CW;
+  if (seed_dev) seed = *seed_dev;  // (a graph-replayed forward: this step's seed from device memory)
   __shared__ float sA[R][kLd], sB[64][kLd];
   const int t = threadIdx.x, ty = t / TXN, tx = t % TXN;
   const int r0 = blockIdx.x * R;
@@ -286,6 +288,17 @@ using namespace wgsr;
     if (_e != hipSuccess) return set_error(WGSR_EHIP, "%s: %s", name, hipGetErrorString(_e)); \
   } while (0)
 
+// Sampling keys of the DINO term's feature draw (wgsr.h wgsr_random_keys):
+// 31-bit hashes of (seed, index); the ascending order of the keys is the
+// random permutation.
+__global__ __launch_bounds__(256) void k_random_keys(int64_t n, uint32_t seed, const uint32_t* __restrict__ seed_dev,
+                                                     int32_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t sd = seed_dev ? *seed_dev : seed;
+  keys[i] = (int32_t)(mix32(sd ^ mix32((uint32_t)i * 0x9E3779B9U + 0x632BE5ABU)) >> 1);
+}
+
 extern "C" {
 
 size_t wgsr_mlp_scratch_bytes(int N, int C) {
@@ -296,9 +309,9 @@ size_t wgsr_mlp_scratch_bytes(int N, int C) {
 
 int wgsr_mlp_grad_floats(int C) { return C > 0 ? mlp_partial_floats(C) : 0; }
 
-int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
-                     const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed, float* h1d,
-                     float* h2d, float* o_pre, float* u, void* stream) {
+static int mlp_forward_impl(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                            const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed,
+                            const uint32_t* seed_dev, float* h1d, float* h2d, float* o_pre, float* u, void* stream) {
   if (N < 0 || C <= 0 || C % 64 != 0) return set_error(WGSR_EINVAL, "wgsr_mlp_forward: C must be a positive multiple of 64");
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return set_error(WGSR_EINVAL, "wgsr_mlp_forward: dropout_p in [0, 1)");
   if (N == 0) return WGSR_OK;
@@ -306,11 +319,33 @@ int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float*
     return set_error(WGSR_EINVAL, "wgsr_mlp_forward: null pointer");
   if ((N + 63) / 64 >= 1024)  // enough 64-row workgroups to fill the chip
     hipLaunchKernelGGL(k_mlp_fwd<64>, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
-                       b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
+                       b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
   else
     hipLaunchKernelGGL(k_mlp_fwd<16>, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
-                       b2, W3, b3, dropout_p, seed, h1d, h2d, o_pre, u);
+                       b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
   MLPCHK("wgsr_mlp_forward");
+  return WGSR_OK;
+}
+
+int wgsr_mlp_forward(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                     const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed, float* h1d,
+                     float* h2d, float* o_pre, float* u, void* stream) {
+  return mlp_forward_impl(N, C, X, W1, b1, W2, b2, W3, b3, dropout_p, seed, nullptr, h1d, h2d, o_pre, u, stream);
+}
+
+int wgsr_mlp_forward_dev_seed(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                              const float* b2, const float* W3, const float* b3, float dropout_p,
+                              const uint32_t* seed, float* h1d, float* h2d, float* o_pre, float* u, void* stream) {
+  if (!seed) return set_error(WGSR_EINVAL, "wgsr_mlp_forward_dev_seed: null seed");
+  return mlp_forward_impl(N, C, X, W1, b1, W2, b2, W3, b3, dropout_p, 0u, seed, h1d, h2d, o_pre, u, stream);
+}
+
+int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t* keys, void* stream) {
+  if (n < 0 || (n > 0 && !keys)) return set_error(WGSR_EINVAL, "wgsr_random_keys: bad arguments");
+  if (n == 0) return WGSR_OK;
+  hipLaunchKernelGGL(k_random_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, seed,
+                     seed_dev, keys);
+  MLPCHK("wgsr_random_keys");
   return WGSR_OK;
 }
 

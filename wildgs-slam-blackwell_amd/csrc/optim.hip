@@ -27,7 +27,22 @@ struct AdamBatch {
   int64_t ustart[kAdamMax + 1];  // first 4-element unit of each tensor (each starts on a unit)
   int n;
   float beta2, w1, w2, eps;  // w1 = 1 - beta1, w2 = 1 - beta2, rounded from double like torch's scalars
+  // wgsr_adam_step_dev: per-tensor (step_size, bias_correction2_sqrt,
+  // step_size_tail) from device memory, the skip word, the L2 weight decay
+  const float* sc;
+  const uint32_t* skip;
+  float wd;
 };
+
+// tensor k's step scalars: its own fields, or the device triple
+struct AdamScal {
+  float neg_step, neg_tail, bc2s;
+};
+__device__ __forceinline__ AdamScal adam_scal(const AdamBatch& b, int k) {
+  const wgsr_adam_tensor& T = b.t[k];
+  if (b.sc) return {-b.sc[3 * k], -b.sc[3 * k + 2], b.sc[3 * k + 1]};
+  return {-T.step_size, -T.step_size_tail, T.bias_correction2_sqrt};
+}
 
 // Same arithmetic, in the same order, as torch's _multi_tensor_adam (fp32
 // opmath): exp_avg.lerp_(grad, 1 - beta1); exp_avg_sq.mul_(beta2)
@@ -43,17 +58,18 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 }
 
 // -step size of element e (the optional two-rate split, wgsr.h)
-__device__ __forceinline__ float neg_step_of(const wgsr_adam_tensor& T, int64_t e) {
-  if (T.split_period <= 0) return -T.step_size;
+__device__ __forceinline__ float neg_step_of(const wgsr_adam_tensor& T, const AdamScal& S, int64_t e) {
+  if (T.split_period <= 0) return S.neg_step;
   const int64_t c = (T.numel < (int64_t)1 << 32) ? (int64_t)((uint32_t)e % (uint32_t)T.split_period) : e % T.split_period;
-  return c >= T.split_len ? -T.step_size_tail : -T.step_size;
+  return c >= T.split_len ? S.neg_tail : S.neg_step;
 }
 
-__device__ __forceinline__ void adam_scalar(const wgsr_adam_tensor& T, int64_t e0, float w1, float beta2, float w2,
-                                            float eps) {
+__device__ __forceinline__ void adam_scalar(const wgsr_adam_tensor& T, const AdamScal& S, int64_t e0, float w1,
+                                            float beta2, float w2, float eps, float wd) {
   for (int64_t e = e0; e < min(e0 + 4, T.numel); ++e) {
     float p = T.param[e], m = T.exp_avg[e], v = T.exp_avg_sq[e];
-    adam_elem(p, T.grad[e], m, v, w1, beta2, w2, eps, neg_step_of(T, e), T.bias_correction2_sqrt);
+    const float g = wd != 0.f ? fmaf(wd, p, T.grad[e]) : T.grad[e];
+    adam_elem(p, g, m, v, w1, beta2, w2, eps, neg_step_of(T, S, e), S.bc2s);
     T.param[e] = p;
     T.exp_avg[e] = m;
     T.exp_avg_sq[e] = v;
@@ -67,8 +83,9 @@ __device__ __forceinline__ void adam_scalar(const wgsr_adam_tensor& T, int64_t e
 // starts on a unit); ragged tails and unaligned tensors take the scalar path.
 constexpr int kAdamU = 2;
 __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
+  if (b.skip && *b.skip) return;  // (uniform: the whole grid leaves)
   const int64_t units = b.ustart[b.n];
-  const float w1 = b.w1, w2 = b.w2, beta2 = b.beta2, eps = b.eps;
+  const float w1 = b.w1, w2 = b.w2, beta2 = b.beta2, eps = b.eps, wd = b.wd;
   for (int64_t tile = (int64_t)blockIdx.x * (256 * kAdamU); tile < units; tile += (int64_t)gridDim.x * (256 * kAdamU)) {
     float4 p[kAdamU], g[kAdamU], m[kAdamU], v[kAdamU];
     int ti[kAdamU];
@@ -99,15 +116,22 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
       const int64_t u = tile + j * 256 + threadIdx.x;
       if (u >= units) continue;
       const wgsr_adam_tensor& T = b.t[ti[j]];
+      const AdamScal S = adam_scal(b, ti[j]);
       if (!vec[j]) {
-        adam_scalar(T, e0[j], w1, beta2, w2, eps);
+        adam_scalar(T, S, e0[j], w1, beta2, w2, eps, wd);
         continue;
       }
-      const float bc2s = T.bias_correction2_sqrt;
-      float ns[4] = {-T.step_size, -T.step_size, -T.step_size, -T.step_size};
+      const float bc2s = S.bc2s;
+      float ns[4] = {S.neg_step, S.neg_step, S.neg_step, S.neg_step};
       if (T.split_period > 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ns[k] = neg_step_of(T, e0[j] + k);
+        for (int k = 0; k < 4; ++k) ns[k] = neg_step_of(T, S, e0[j] + k);
+      }
+      if (wd != 0.f) {
+        g[j].x = fmaf(wd, p[j].x, g[j].x);
+        g[j].y = fmaf(wd, p[j].y, g[j].y);
+        g[j].z = fmaf(wd, p[j].z, g[j].z);
+        g[j].w = fmaf(wd, p[j].w, g[j].w);
       }
       adam_elem(p[j].x, g[j].x, m[j].x, v[j].x, w1, beta2, w2, eps, ns[0], bc2s);
       adam_elem(p[j].y, g[j].y, m[j].y, v[j].y, w1, beta2, w2, eps, ns[1], bc2s);
@@ -217,9 +241,13 @@ using namespace wgsr;
 
 extern "C" {
 
-int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps, void* stream) {
+static int adam_step_impl(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps, double wd,
+                          const float* scalars, const uint32_t* skip, void* stream) {
   if (n < 0 || n > kAdamMax || (n > 0 && !tensors)) return set_error(WGSR_EINVAL, "wgsr_adam_step: 0..%d tensors", kAdamMax);
   AdamBatch b{};
+  b.sc = scalars;
+  b.skip = skip;
+  b.wd = (float)wd;
   b.n = n;
   b.beta2 = (float)beta2;
   b.w1 = (float)(1.0 - beta1);
@@ -239,6 +267,16 @@ int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double 
   hipLaunchKernelGGL(k_adam_multi, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_adam_step: %s", hipGetErrorString(e));
+}
+
+int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps, void* stream) {
+  return adam_step_impl(tensors, n, beta1, beta2, eps, 0.0, nullptr, nullptr, stream);
+}
+
+int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
+                       double weight_decay, const float* scalars, const uint32_t* skip, void* stream) {
+  if (!scalars) return set_error(WGSR_EINVAL, "wgsr_adam_step_dev: missing device scalars");
+  return adam_step_impl(tensors, n, beta1, beta2, eps, weight_decay, scalars, skip, stream);
 }
 
 int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,

@@ -596,6 +596,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __shared__ uint32_t sG[kBatch];
   __shared__ float sP[kBatch][11];
   __shared__ uint32_t sHit[kBatch];
+  // a capacity-mode forward that overflowed its buffers (ImageLayout::meta[1])
+  // leaves no gradient: the zero fill only, no record, no flag (the
+  // per-Gaussian backward then finds nothing to sum); the caller's optimizer
+  // steps skip on the same flag
+  if (meta[1]) {
+    zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
+    return;
+  }
   // where the forward left the tile lists (ImageLayout::meta)
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
@@ -761,6 +769,10 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
 #if WGSR_BWD_SPLIT_EPAIR
   __shared__ BwdPairRec sPairs[4][kBatch / 2];
 #endif
+  if (meta[1]) {  // overflowed capacity-mode forward (see k_render_bwd_quad)
+    zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
+    return;
+  }
   // where the forward left the tile lists (ImageLayout::meta)
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];

@@ -69,6 +69,15 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I0, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>{});
+    static_for<I0 + 1, N>(f);
+  }
+}
+
 // One Gaussian of k_preprocess; returns (rect area, exact list length, bins
 // touched), 0 if culled.  The per-Gaussian words every Gaussian gets (radius,
 // list length, tb, depth key) are returned in `w` (radius, cnt, tb, key) and
@@ -182,6 +191,45 @@ __device__ __forceinline__ uint3 preprocess_one(
 // its own 3M-float run.  (A smaller table lets more waves share a CU but
 // measured no faster at 1M/1080p: 8 rows 97 us, 16 rows 95, 32 rows 95, 64
 // rows 90.)
+// A preprocess wave's pair counts (upstream's num_rendered, exact pairs, bin
+// pairs) and visible depth-key range into the counter block: one atomic per
+// wave each, spread over kRectPairLanes words.  The wave sums / maxima are
+// DPP row reductions + four readlanes (SGPR results, no LDS round trips);
+// per-lane rect areas of 2^26 or more (images beyond ~17 Gpixel) take the
+// 64-bit shuffle path.
+__device__ __forceinline__ void wave_pair_counts(const uint3 ac, uint32_t khi, uint32_t knlo,
+                                                 unsigned long long* __restrict__ rect_pairs,
+                                                 unsigned long long* __restrict__ list_pairs,
+                                                 unsigned long long* __restrict__ bin_pairs,
+                                                 uint32_t* __restrict__ drange) {
+  const uint32_t slot = blockIdx.x % kRectPairLanes;
+  unsigned long long area, cnt, nbin;
+  if (wave_any(ac.x >= (1u << 26))) {
+    area = ac.x;
+    cnt = ac.y;
+    nbin = ac.z;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      area += __shfl_xor(area, off, 64);
+      cnt += __shfl_xor(cnt, off, 64);
+      nbin += __shfl_xor(nbin, off, 64);
+    }
+  } else {  // (list and bin counts never exceed the rect area)
+    area = wave_total_u32(ac.x);
+    cnt = wave_total_u32(ac.y);
+    nbin = wave_total_u32(ac.z);
+  }
+  const uint32_t kh = wave_maximum_u32(khi), kn = wave_maximum_u32(knlo);
+  if (threadIdx.x % 64 == 0) {
+    atomicAdd(&rect_pairs[slot], area);
+    atomicAdd(&list_pairs[slot], cnt);
+    atomicAdd(&bin_pairs[slot], nbin);
+    // the depth sort's key range (DepthKeyPlan): max key, max complement
+    if (kh) atomicMax(&drange[slot], kh);
+    if (kn) atomicMax(&drange[kRectPairLanes + slot], kn);
+  }
+}
+
 constexpr int kPreWave = 64;
 #ifndef WGSR_PRE_ROWS
 #define WGSR_PRE_ROWS 64
@@ -197,11 +245,13 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero) {
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
+    uint32_t* __restrict__ meta) {
 
   extern __shared__ float s_sh[];  // kPreRows x (3M + 1) floats when SH colours are used
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
   const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
   // every input (camera, per-Gaussian parameters) is loaded up front, so its
   // latency overlaps the SH slab's instead of following the colour evaluation
@@ -254,23 +304,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
   }
   // upstream num_rendered, the exact pair count and the bin pair count: one
   // atomic per wave each, spread over kRectPairLanes words
-  unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    area += __shfl_xor(area, off, 64);
-    cnt += __shfl_xor(cnt, off, 64);
-    nbin += __shfl_xor(nbin, off, 64);
-    khi = max(khi, (uint32_t)__shfl_xor((int)khi, off, 64));
-    knlo = max(knlo, (uint32_t)__shfl_xor((int)knlo, off, 64));
-  }
-  if (lane == 0) {
-    atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
-    atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
-    atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
-    // the depth sort's key range (DepthKeyPlan): max key, max complement
-    if (khi) atomicMax(&drange[blockIdx.x % kRectPairLanes], khi);
-    if (knlo) atomicMax(&drange[kRectPairLanes + blockIdx.x % kRectPairLanes], knlo);
-  }
+  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
   // scratch the next kernels need zeroed (the depth sort's superblock sums)
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
 }
@@ -327,10 +361,12 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
     unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero) {
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
+    uint32_t* __restrict__ meta) {
   extern __shared__ float s_sh[];  // nch x 64 x kCh floats (chunk-major)
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
   const bool sh_on = shs != nullptr && colors == nullptr;
   if (sh_on) {  // uniform: queue the slab first
     const int nf = 3 * (D + 1) * (D + 1), nch = (nf + kCh - 1) / kCh;
@@ -390,22 +426,95 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       clamped[i] = cbits;
     }
   }
-  unsigned long long area = ac.x, cnt = ac.y, nbin = ac.z;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    area += __shfl_xor(area, off, 64);
-    cnt += __shfl_xor(cnt, off, 64);
-    nbin += __shfl_xor(nbin, off, 64);
-    khi = max(khi, (uint32_t)__shfl_xor((int)khi, off, 64));
-    knlo = max(knlo, (uint32_t)__shfl_xor((int)knlo, off, 64));
+  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
+  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
+}
+
+// ---- k_preprocess3: the SH coefficients in VGPRs (WGSR_PRE=3, A/B) ----------
+// k_preprocess2 without LDS: each lane's evaluated coefficients (16-byte
+// loads of its own row, issued first) stay in registers across the geometry,
+// so the workgroup's occupancy is set by VGPRs instead of the 12 KB slab.
+// Needs 16-byte aligned rows (3M % 4 == 0); outputs bit-identical.
+template <int kD>
+__global__ __launch_bounds__(kPreWave) void k_preprocess3(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
+    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
+    uint32_t* __restrict__ meta) {
+  constexpr int NF = 3 * (kD + 1) * (kD + 1), NC = (NF + 3) / 4;
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
+  // the parameters first, unconditionally (clamped row): the in-order load
+  // counter lets the geometry start while the 12 coefficient loads behind
+  // them are still in flight
+  const int ic = min(i, P - 1);
+  f3 p = mk3(means[3 * ic], means[3 * ic + 1], means[3 * ic + 2]);
+  f3 sc = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  if (!cov_pre) {  // (uniform)
+    sc = mk3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
+    q = reinterpret_cast<const float4*>(rots)[ic];
   }
-  if (lane == 0) {
-    atomicAdd(&rect_pairs[blockIdx.x % kRectPairLanes], area);
-    atomicAdd(&list_pairs[blockIdx.x % kRectPairLanes], cnt);
-    atomicAdd(&bin_pairs[blockIdx.x % kRectPairLanes], nbin);
-    if (khi) atomicMax(&drange[blockIdx.x % kRectPairLanes], khi);
-    if (knlo) atomicMax(&drange[kRectPairLanes + blockIdx.x % kRectPairLanes], knlo);
+  // (a volatile read keeps this load ahead of the coefficient loads: sunk to
+  // its use, its wait would also wait for the coefficients -- the load
+  // counter is in order)
+  float o = *reinterpret_cast<const volatile float*>(opac + ic);
+  float sh[4 * NC];
+  {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v* src = reinterpret_cast<const f4v*>(shs + (size_t)ic * (3 * M));
+    static_for<0, NC>([&](auto k) {
+      const f4v v = __builtin_nontemporal_load(src + k.value);
+      sh[4 * k.value] = v.x;
+      sh[4 * k.value + 1] = v.y;
+      sh[4 * k.value + 2] = v.z;
+      sh[4 * k.value + 3] = v.w;
+    });
   }
+  if (i >= P) {
+    p = mk3(0.f, 0.f, 1.f);
+    o = 0.f;
+  }
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  uint3 ac = make_uint3(0u, 0u, 0u);
+  uint32_t khi = 0u, knlo = 0u;
+  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+  if (i < P) {
+    uint2 rcw;
+    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
+                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, false);
+    radii[i] = (int32_t)w.x;
+    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    if (bshift) tb[i] = w.z;
+    dkey[i] = w.w;
+    if (w.w != 0xFFFFFFFFu) {
+      khi = w.w;
+      knlo = ~w.w;
+    }
+    n_touched[i] = 0;
+    gflag[i] = 0;
+    if (w.x != 0u) {  // visible: the colour record
+#pragma clang fp contract(off)
+      f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+      const float len = sqrtf(dot3(dir, dir));
+      dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+      uint32_t cbits = 0;
+      const f3 rgb = sh_to_rgb(kD, sh, dir, cbits);
+      splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
+      clamped[i] = cbits;
+    }
+  }
+  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
 }
 
@@ -538,7 +647,9 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
     uint32_t* __restrict__ vals, const ZeroJob zero, const uint32_t* __restrict__ dkey,
-    uint32_t* __restrict__ pair_depth) {
+    uint32_t* __restrict__ pair_depth, uint32_t cap_slots, uint32_t cap_pairs) {
+  // (cap_slots / cap_pairs: the capacity-mode forward's buffer sizes -- writes
+  // past them are dropped and the forward flags the overflow; ~0 otherwise)
   constexpr int NW = kDupScanThreads / 64;
   __shared__ uint2 s_w[NW], s_p[NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -605,7 +716,8 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const uint2 wt = s_w[w];  // the wave's totals
   if (in) slot_start[g] = wb.x + ic - cnt;
   // the wave's slots are contiguous: one byte store per lane per 64 slots
-  for (uint32_t k = lane; k < wt.x; k += 64) pflag[wb.x + k] = 0;
+  for (uint32_t k = lane; k < wt.x; k += 64)
+    if (wb.x + k < cap_slots) pflag[wb.x + k] = 0;
   // scratch the bin sort needs zeroed (its superblock sums)
   zero_share(zero, blockIdx.x, gridDim.x, t, kDupScanThreads);
   if (wt.y == 0) return;  // wave-uniform; no barrier below
@@ -644,7 +756,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     const int row = (int)local / bw;
     const int bx = bx0 + ((int)local - row * bw), by = (y0 >> bshift) + row;
     const uint32_t pd = pair_depth ? (uint32_t)__shfl((int)dk, lo, 64) : 0u;
-    if (k < end) {
+    if (k < end && k < cap_pairs) {
       keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, tl, rg) << 16);
       vals[k] = gg;
       if (pair_depth) pair_depth[k] = pd;
@@ -805,14 +917,6 @@ struct BdsEmit {
   uint32_t* __restrict__ meta;
   int gx, gy, bshift, gbx;
 };
-// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
-template <int I0, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I0 < N) {
-    f(std::integral_constant<int, I0>{});
-    static_for<I0 + 1, N>(f);
-  }
-}
 
 template <int JN>
 __device__ __forceinline__ void bds_emit_chunk(BdsLds& L, const uint32_t (&m)[JN], const uint32_t (&g)[JN],
@@ -1704,9 +1808,43 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 
 }  // namespace
 
+// Capacity-mode forward: the counter block's partial pair counts (upstream's
+// rect pairs, exact pairs, bin pairs: kRectPairLanes u64 each) -> counts[0..2]
+// (saturating u32), the bin-pair count clamped to the buffers (counts[4], what
+// the sort reads as its key count) and the overflow flag (counts[3] and the
+// image buffer's meta[1], which makes the render backward a no-op).
+__global__ __launch_bounds__(64) void k_cap_counts(const unsigned long long* __restrict__ partial,
+                                                   uint64_t cap_rect, uint64_t cap_bin, uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ meta) {
+  const int t = threadIdx.x;
+  unsigned long long r = partial[t], e = partial[kRectPairLanes + t], b = partial[2 * kRectPairLanes + t];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    r += __shfl_xor(r, off, 64);
+    e += __shfl_xor(e, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  if (t == 0) {
+    const uint32_t ovf = (r > cap_rect || b > cap_bin) ? 1u : 0u;
+    counts[0] = (uint32_t)min(r, 0xFFFFFFFFull);
+    counts[1] = (uint32_t)min(e, 0xFFFFFFFFull);
+    counts[2] = (uint32_t)min(b, 0xFFFFFFFFull);
+    counts[3] = ovf;
+    counts[4] = (uint32_t)min(b, (unsigned long long)cap_bin);
+    meta[1] = ovf;
+  }
+}
+static_assert(kRectPairLanes == 64, "k_cap_counts: one lane per partial");
+
+hipError_t launch_cap_counts(const unsigned long long* partial, uint64_t cap_rect, uint64_t cap_bin, uint32_t* counts,
+                             uint32_t* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_cap_counts, dim3(1), dim3(64), 0, s, partial, cap_rect, cap_bin, counts, meta);
+  return hipGetLastError();
+}
+
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
                              uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, const ZeroJob& zero,
-                             hipStream_t s) {
+                             hipStream_t s, uint32_t* meta) {
   unsigned long long* list_pairs = rect_pairs + kRectPairLanes;
   unsigned long long* bin_pairs = rect_pairs + 2 * kRectPairLanes;
   uint32_t* drange = reinterpret_cast<uint32_t*>(rect_pairs + 3 * kRectPairLanes);  // kDepthRangeOffset
@@ -1714,11 +1852,23 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   // k_preprocess2 (LDS-DMA slab behind the geometry) unless WGSR_PRE=1
-  static const bool pre_v1 = [] {
+  static const int pre_mode = [] {
     const char* e = getenv("WGSR_PRE");
-    return e && atoi(e) == 1;
+    return e ? atoi(e) : 2;
   }();
-  if (!pre_v1) {
+  if (pre_mode == 3 && a.shs && !a.colors && (a.M * 3) % 4 == 0 &&
+      (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) {
+    auto kern = a.D == 0 ? k_preprocess3<0> : a.D == 1 ? k_preprocess3<1> : a.D == 2 ? k_preprocess3<2>
+                                                                                    : k_preprocess3<3>;
+    hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), 0, s, a.P, a.D, a.M, a.means3D,
+                       a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
+                       a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
+                       at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
+                       at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs,
+                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
+    return hipGetLastError();
+  }
+  if (pre_mode != 1) {
     const bool sh_on = a.shs && !a.colors;
     const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
     const int nf = 3 * (a.D + 1) * (a.D + 1);
@@ -1730,7 +1880,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                        a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                        at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                        at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs,
-                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero);
+                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
     return hipGetLastError();
   }
   const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreRows * (3 * (size_t)a.M + 1) : 0;
@@ -1739,13 +1889,13 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
                      a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
                      at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
                      at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs, bshift,
-                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero);
+                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
   return hipGetLastError();
 }
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t* pair_depth) {
+                                 hipStream_t s, uint32_t* pair_depth, uint32_t cap_slots, uint32_t cap_pairs) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
@@ -1754,7 +1904,7 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
                      at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, at<uint32_t>(geom, L.dkey),
-                     pair_depth);
+                     pair_depth, cap_slots, cap_pairs);
   return hipGetLastError();
 }
 

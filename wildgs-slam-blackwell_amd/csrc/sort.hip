@@ -96,9 +96,11 @@ constexpr uint32_t kSupBlocks = kSortSupBlocks;
 template <int I>
 __global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, int shift,
                                                     int bits, uint32_t nb, uint32_t* __restrict__ hist,
-                                                    uint32_t* __restrict__ sup, uint32_t nsup) {
+                                                    uint32_t* __restrict__ sup, uint32_t nsup,
+                                                    const uint32_t* __restrict__ ndev) {
   __shared__ uint32_t s_h[256];
   const int t = threadIdx.x;
+  if (ndev) n = min(n, *ndev);  // capacity mode: the live key count from the device
   s_h[t] = 0;
   uint32_t k[I];
   const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, k);
@@ -219,8 +221,12 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
     uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup, uint2* __restrict__ bounds,
-    const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout) {
+    const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout, const uint32_t* __restrict__ ndev) {
   constexpr int kTile = 256 * I;
+  if (ndev) {  // capacity mode (reduce-then-scan only): blocks past the live keys have nothing to move
+    n = min(n, *ndev);
+    if (!kOnesweep && (size_t)blockIdx.x * kTile >= n && !(blockIdx.x == 0 && bounds)) return;
+  }
   __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16); then the
                                   // second payload (xin: the bin sort's depth keys) -- no extra LDS
   __shared__ uint32_t s_wcnt[4][256];
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
   }
   __syncthreads();
-  const uint32_t cnt = (uint32_t)min((size_t)kTile, (size_t)n - blk0);
+  const uint32_t cnt = (size_t)n > blk0 ? (uint32_t)min((size_t)kTile, (size_t)n - blk0) : 0u;
 #pragma unroll
   for (int r = 0; r < I; ++r) {
     const uint32_t i = (uint32_t)t + 256u * r;
@@ -359,9 +365,11 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
 // in the per-digit steps.
 template <int DIG, int I>
 __global__ __launch_bounds__(256) void k_radix_hist_wide(const uint32_t* __restrict__ keys, uint32_t n, int shift,
-                                                         int bits, uint32_t nb, uint32_t* __restrict__ hist) {
+                                                         int bits, uint32_t nb, uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ ndev) {
   __shared__ uint32_t s_h[DIG];
   const int t = threadIdx.x;
+  if (ndev) n = min(n, *ndev);
 #pragma unroll
   for (int k = 0; k < DIG / 256; ++k) s_h[t + 256 * k] = 0;
   uint32_t key[I];
@@ -378,8 +386,12 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, uint2* __restrict__ digit_bounds, const uint32_t* __restrict__ xin,
-    uint32_t* __restrict__ xout) {
+    uint32_t* __restrict__ xout, const uint32_t* __restrict__ ndev) {
   constexpr int kT = 256 * I, DPT = DIG / 256;
+  if (ndev) {
+    n = min(n, *ndev);
+    if ((size_t)blockIdx.x * kT >= n && !(blockIdx.x == 0 && digit_bounds)) return;
+  }
   __shared__ uint2 s_buf[kT];  // (key, value) in digit order, then the second payload (xin)
   __shared__ uint32_t s_wcnt[4][DIG];
   __shared__ uint32_t s_lbase[DIG];
@@ -459,7 +471,7 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     rank[j] = slot;  // (kept for the second payload)
   }
   __syncthreads();
-  const uint32_t cnt = (uint32_t)min((size_t)kT, (size_t)n - blk0);
+  const uint32_t cnt = (size_t)n > blk0 ? (uint32_t)min((size_t)kT, (size_t)n - blk0) : 0u;
   uint32_t dsts[I];
 #pragma unroll
   for (int r = 0; r < I; ++r) {
@@ -713,7 +725,7 @@ __global__ __launch_bounds__(256) void k_depth_scatter(const uint32_t* __restric
   __syncthreads();
   // the last pass writes keys only when a fix-up pass over extra_bits follows
   const bool wkeys = PASS < kDepthPasses - 1 || pl.extra_bits > 0;
-  const uint32_t cnt = (uint32_t)min((size_t)kTile, (size_t)n - blk0);
+  const uint32_t cnt = (size_t)n > blk0 ? (uint32_t)min((size_t)kTile, (size_t)n - blk0) : 0u;
 #pragma unroll
   for (int r = 0; r < I; ++r) {
     const uint32_t i = (uint32_t)t + 256u * r;
@@ -920,25 +932,26 @@ template <int I>
 static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt,
                                    bool vals_iota, size_t n, int begin_bit, int end_bit, uint32_t* status,
                                    uint32_t* totals, hipStream_t stream, bool* result_in_alt, uint2* digit_bounds,
-                                   bool* bounds_done, bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt) {
+                                   bool* bounds_done, bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt,
+                                   const uint32_t* ndev) {
   const uint32_t nb = sort_blocks(n);
   if (wide_pass(end_bit - begin_bit) && n <= (size_t)kStCount) {
     const int bits = end_bit - begin_bit;
     // status doubles as the [DIG][nb] per-block histogram (DIG <= 1024 <= 256 x kMaxSortPasses rows)
     if (bits <= 9) {
       hipLaunchKernelGGL((k_radix_hist_wide<512, I>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
-                         bits, nb, status);
+                         bits, nb, status, ndev);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(512), dim3(256), 0, stream, status, nb, totals);
       hipLaunchKernelGGL((k_radix_scatter_wide<512, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
                          vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt);
+                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt, ndev);
     } else {
       hipLaunchKernelGGL((k_radix_hist_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
-                         bits, nb, status);
+                         bits, nb, status, ndev);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(1024), dim3(256), 0, stream, status, nb, totals);
       hipLaunchKernelGGL((k_radix_scatter_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
                          vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt);
+                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt, ndev);
     }
     *result_in_alt = true;
     if (bounds_done) *bounds_done = digit_bounds && begin_bit == 0;
@@ -947,7 +960,7 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
   const int passes = (end_bit - begin_bit + 7) / 8;
   if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;
   // (the second payload rides the reduce-then-scan schedule only)
-  const bool onesweep = !xvals && (sort_mode() == 1 || (sort_mode() == 2 && n <= kSmallSortN));
+  const bool onesweep = !xvals && !ndev && (sort_mode() == 1 || (sort_mode() == 2 && n <= kSmallSortN));
   uint32_t* ghist = totals;                          // onesweep: [passes][256]; rts: digit totals
   uint32_t* vcount = totals + kMaxSortPasses * 256;  // onesweep: virtual block counters [passes]
   if (onesweep) {
@@ -980,18 +993,18 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
     if (onesweep) {
       hipLaunchKernelGGL((k_radix_scatter<true, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
                          (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u, nullptr, nullptr, nullptr);
+                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u, nullptr, nullptr, nullptr, nullptr);
     } else {
       // status doubles as the [256][nb] per-block histogram (and, in
       // superblock mode, holds the passes' [256][nsup] superblock sums after it)
       uint32_t* sp = sup ? sup + (size_t)p * 256 * nsup : nullptr;
       hipLaunchKernelGGL(k_radix_hist<I>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status,
-                         sp, nsup);
+                         sp, nsup, ndev);
       if (!sp) hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
       // a single superblock pass over bits [0, end_bit) also writes the digit bounds
       uint2* db = (sp && passes == 1 && begin_bit == 0) ? digit_bounds : nullptr;
       hipLaunchKernelGGL((k_radix_scatter<false, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup, db, xi, xo);
+                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup, db, xi, xo, ndev);
       if (db && bounds_done) *bounds_done = true;
     }
     iota = false;
@@ -1006,7 +1019,7 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done,
-                            bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt) {
+                            bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt, const uint32_t* ndev) {
   *result_in_alt = false;
   if (!xvals != !xvals_alt) return hipErrorInvalidValue;
   if (bounds_done) *bounds_done = false;
@@ -1021,15 +1034,15 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     case kTinySortItems:
       return radix_sort_tiled<kTinySortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
                                               totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed,
-                                              xvals, xvals_alt);
+                                              xvals, xvals_alt, ndev);
     case kSmallSortItems:
       return radix_sort_tiled<kSmallSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit,
                                                status, totals, stream, result_in_alt, digit_bounds, bounds_done,
-                                               sup_zeroed, xvals, xvals_alt);
+                                               sup_zeroed, xvals, xvals_alt, ndev);
     default:
       return radix_sort_tiled<kSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
                                           totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed,
-                                              xvals, xvals_alt);
+                                              xvals, xvals_alt, ndev);
   }
 }
 

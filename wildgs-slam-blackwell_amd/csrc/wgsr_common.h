@@ -61,6 +61,34 @@ __device__ __forceinline__ float dpp_row_sum16(float x) {
   return x;
 }
 
+// The same for unsigned sums / maxima (bound_ctrl zeros: the identity of both)
+__device__ __forceinline__ uint32_t dpp_row_sum16_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  return x;
+}
+__device__ __forceinline__ uint32_t dpp_row_max16_u32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+  return x;
+}
+// wave-uniform (SGPR) total / maximum: DPP row reductions, then the four row
+// results read from lanes 15, 31, 47, 63 (no LDS round trips; all lanes active)
+__device__ __forceinline__ uint32_t wave_total_u32(uint32_t x) {
+  x = dpp_row_sum16_u32(x);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+         (uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_maximum_u32(uint32_t x) {
+  x = dpp_row_max16_u32(x);
+  return max(max((uint32_t)__builtin_amdgcn_readlane((int)x, 15), (uint32_t)__builtin_amdgcn_readlane((int)x, 31)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)x, 47), (uint32_t)__builtin_amdgcn_readlane((int)x, 63)));
+}
+
 __device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
   return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -929,7 +957,8 @@ struct ImageLayout {
     tile_m = take(16 * nt);    // deepest contributor per tile quadrant (backward work)
     order_bwd = take(4 * nt);  // the backward's launch order (heaviest first per XCD chunk)
     meta = take(16);           // [0]: where the forward left the tile lists (1: sort-bin region
-                               // after the binning layout, 0: point_g) -- read by the backward
+                               // after the binning layout, 0: point_g) -- read by the backward;
+                               // [1]: capacity-mode overflow (the backward leaves no gradient)
     final_T = take(4 * (size_t)W * H);
     n_contrib = take(4 * (size_t)W * H);
     total = o;

@@ -21,7 +21,10 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt,
                             uint2* digit_bounds = nullptr, bool* bounds_done = nullptr, bool sup_zeroed = false,
-                            uint32_t* xvals = nullptr, uint32_t* xvals_alt = nullptr);
+                            uint32_t* xvals = nullptr, uint32_t* xvals_alt = nullptr,
+                            const uint32_t* ndev = nullptr);
+// (ndev: capacity mode -- n is the capacity the grid is sized for, *ndev the
+// live key count, read on the device; reduce-then-scan / wide schedules only)
 // (xvals / xvals_alt: an optional second payload, moved like vals and ending
 // in the same buffer parity; reduce-then-scan schedule)
 // words of `status` a reduce-then-scan sort accumulates superblock sums in
@@ -70,13 +73,18 @@ struct RasterGrid {
 // rect_pairs[2 kRectPairLanes..3 kRectPairLanes) += bins touched (bshift > 0;
 // geometry tb[g] = exact list length | bins touched << 16)
 hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* radii, int32_t* n_touched,
-                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, const ZeroJob& zero, hipStream_t s);
+                             uint32_t* err_flag, unsigned long long* rect_pairs, int bshift, const ZeroJob& zero, hipStream_t s, uint32_t* meta);
+// capacity-mode forward: counter partials -> counts [N_rect, N_exact, N_bin,
+// overflow, clamped N_bin] and the overflow flag into meta[1]
+hipError_t launch_cap_counts(const unsigned long long* partial, uint64_t cap_rect, uint64_t cap_bin, uint32_t* counts,
+                             uint32_t* meta, hipStream_t s);
 // Sort bins: after packed_scan_blocks, the scan's down-sweep (slot_start[g],
 // the slot flags zeroed) fused with the (bin | exact tile mask << 16,
 // Gaussian) pair expansion.
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t* pair_depth = nullptr);
+                                 hipStream_t s, uint32_t* pair_depth = nullptr,
+                                 uint32_t cap_slots = 0xFFFFFFFFu, uint32_t cap_pairs = 0xFFFFFFFFu);
 // (pair_depth: each pair's depth key too -- the per-bin depth sort's input)
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);

@@ -201,6 +201,10 @@ def load():
         L.wgsr_mlp_grad_floats.argtypes = [c_int]
         L.wgsr_mlp_forward.restype = c_int
         L.wgsr_mlp_forward.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float, ctypes.c_uint32] + [_fp] * 4 + [_fp]
+        L.wgsr_mlp_forward_dev_seed.restype = c_int
+        L.wgsr_mlp_forward_dev_seed.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float, _fp] + [_fp] * 4 + [_fp]
+        L.wgsr_random_keys.restype = c_int
+        L.wgsr_random_keys.argtypes = [c_i64, ctypes.c_uint32, _fp, _fp, _fp]
         L.wgsr_mlp_backward.restype = c_int
         L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
         L.wgsr_dino_reg.restype = c_int
@@ -222,6 +226,14 @@ def load():
         L.wgsr_adam_step.restype = c_int
         L.wgsr_adam_step.argtypes = [ctypes.POINTER(AdamTensor), c_int, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, _fp]
+        L.wgsr_adam_step_dev.restype = c_int
+        L.wgsr_adam_step_dev.argtypes = [ctypes.POINTER(AdamTensor), c_int, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_double, _fp, _fp, _fp]
+        L.wgsr_rasterize_forward_cap.restype = c_int
+        L.wgsr_rasterize_forward_cap.argtypes = [P_ARGS, c_i64, ALLOC_FN, ALLOC_FN, ALLOC_FN, ctypes.c_void_p,
+                                                 _fp, _fp, _fp, _fp, _fp, _fp, _fp]
+        L.wgsr_binning_bytes_cap.restype = c_sz
+        L.wgsr_binning_bytes_cap.argtypes = [P_ARGS, c_i64]
         L.wgsr_compact_rows.restype = c_int
         L.wgsr_compact_rows.argtypes = [_fp, c_i64, ctypes.POINTER(RowTensor), c_int, ALLOC_FN,
                                         ctypes.c_void_p, _fp]
@@ -258,7 +270,8 @@ EXPORTED_SYMBOLS = (
     "wgsr_rasterize_forward", "wgsr_rasterize_backward", "wgsr_mark_visible", "wgsr_dist_cuda2",
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
     "wgsr_version", "wgsr_depth_order_offset", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
-    "wgsr_adam_step", "wgsr_compact_rows",
+    "wgsr_adam_step", "wgsr_adam_step_dev", "wgsr_compact_rows",
+    "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",

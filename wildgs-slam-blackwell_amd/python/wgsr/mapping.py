@@ -24,6 +24,7 @@ composition (tests/test_gpu_mapping.py).  No fallback: libwgsr.so must load.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -37,6 +38,41 @@ DEFAULT_LR = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 2.5e-3 / 20.0, "opacity":
 
 def _blocks(n):
     return int(_lib.load().wgsr_map_blocks(int(n)))
+
+
+def rasterize_forward_cap(bg, means3D, opacity, scales, rotations, sh, degree: int, cam: dict, H: int, W: int,
+                          cap: int, counts):
+    """The rasteriser forward in capacity mode (wgsr_rasterize_forward_cap):
+    ``_C.rasterize_gaussians``' outputs with no host wait, its buffers sized
+    for ``cap`` (Gaussian, tile) pairs and num_rendered = ``cap``; counts
+    (int32 [5] device tensor): N_rect, N_exact, N_bin, overflow, min(N_bin,
+    cap).  For graph capture (wgsr.online); not an upstream entry point."""
+    L = _lib.load()
+    dev = means3D.device
+    P = int(means3D.shape[0])
+    f = dict(dtype=torch.float32, device=dev)
+    color = torch.empty(3, H, W, **f)
+    depth = torch.empty(1, H, W, **f)
+    opac = torch.empty(1, H, W, **f)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    n_touched = torch.empty(P, dtype=torch.int32, device=dev)
+    p = _lib.ptr
+    a = _lib.RasterArgs(P=P, D=int(degree), M=int(sh.shape[1]), W=int(W), H=int(H), bg=p(bg), means3D=p(means3D),
+                        colors=None, opacities=p(opacity), scales=p(scales), rotations=p(rotations),
+                        cov3D_precomp=None, shs=p(sh), viewmatrix=p(cam["viewmatrix"]),
+                        projmatrix=p(cam["projmatrix"]), projmatrix_raw=p(cam["projmatrix_raw"]),
+                        campos=p(cam["campos"]), scale_modifier=1.0, tan_fovx=float(cam["tanfovx"]),
+                        tan_fovy=float(cam["tanfovy"]), prefiltered=0, debug=0)
+    with torch.cuda.device(dev), _lib.AllocRequest(dev) as req:
+        code = L.wgsr_rasterize_forward_cap(ctypes.byref(a), int(cap), _lib.ALLOC_GEOM, _lib.ALLOC_BINNING,
+                                            _lib.ALLOC_IMAGE, None, p(color), p(depth), p(opac),
+                                            p(radii) if P else None, p(n_touched) if P else None, p(counts),
+                                            _lib.stream_handle(dev))
+    _lib.check(code)
+    empty = torch.empty(0, dtype=torch.uint8, device=dev)
+    b = req.buffers
+    return (int(cap), color, radii, b.get("geom", empty), b.get("binning", empty), b.get("image", empty), depth,
+            opac, n_touched)
 
 
 class MappingStep:
@@ -183,8 +219,9 @@ class MappingStep:
         self._skip = getattr(self, "_skip", set()) | {"opacity"}
 
     # -----------------------------------------------------------------------
-    def _render(self, cam: dict, H: int, W: int, bg):
-        """Activations (+ isotropic partial sums) and the rasteriser forward."""
+    def _render(self, cam: dict, H: int, W: int, bg, cap: int | None = None, counts=None):
+        """Activations (+ isotropic partial sums) and the rasteriser forward
+        (``cap``: the capacity-mode forward, its counts into ``counts``)."""
         from diff_gaussian_rasterization import _C
         L = _lib.load()
         dev = self.xyz.device
@@ -195,6 +232,9 @@ class MappingStep:
             _lib.check(L.wgsr_gaussian_activate(self.P, p(self.opacity), p(self.scaling), p(self.rotation),
                                                 p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
                                                 p(self.iso_part), _lib.stream_handle(dev)))
+        if cap is not None:
+            return rasterize_forward_cap(bg, self.xyz, a["opacity"], a["scales"], a["rotations"], self.features,
+                                         self.D, cam, H, W, cap, counts)
         return _C.rasterize_gaussians(
             bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
             cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
@@ -287,7 +327,8 @@ class MappingStep:
     def forward_backward_uncertainty(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg, uncertainty,
                                      train_frac: float, ssim_frac: float, config: dict | None = None,
                                      initialization: bool = False, freeze_uncertainty_loss: bool = False,
-                                     median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True):
+                                     median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True,
+                                     cap: int | None = None, counts=None):
         """The reference's DEFAULT mapping iteration (uncertainty_params.activate):
         get_loss_mapping_uncertainty (slam_utils.py:146-258) + 10 * isotropic
         loss, and their backward.
@@ -313,13 +354,15 @@ class MappingStep:
         opt_params.lambda_dssim, uncertainty_params.*); defaults are
         configs/wildgs_slam.yaml's.  ``median_depth``: optional cached
         ``gt_depth.median()`` (constant per keyframe).  ``full_resolution``
-        (depth rendered at another size) is not supported.  Returns the dict of
+        (depth rendered at another size) is not supported.  ``cap`` /
+        ``counts``: the capacity-mode forward (no host wait; graph capture,
+        wgsr.online).  Returns the dict of
         ``forward_backward`` plus ``uncertainty_grad`` and ``uncertainty_loss``."""
         from . import uncertainty as U
         cfg = U.flatten_config(config)
         P = self.P
         H, W = gt_image.shape[-2], gt_image.shape[-1]
-        fwd = self._render(cam, H, W, bg)
+        fwd = self._render(cam, H, W, bg, cap, counts)
         nr, image, radii, depth, opac_img = fwd[0], fwd[1], fwd[2], fwd[6], fwd[7]
         w_iso = iso_weight / (3 * P) if P else 0.0
         loss, state = U.loss_forward(image, depth, opac_img, gt_image, gt_depth, exposure_a, exposure_b, uncertainty,
@@ -368,6 +411,52 @@ class MappingStep:
         dev = self.store.device
         with torch.cuda.device(dev):
             _lib.check(L.wgsr_adam_step(arr, len(ts), b1, b2, self.eps, _lib.stream_handle(dev)))
+
+    def adam_tensors(self):
+        """The Gaussian groups as wgsr_adam_tensor rows for wgsr_adam_step_dev
+        (3 scalars per group in GROUPS order, from ``adam_scalars``)."""
+        ts = []
+        for name in self.GROUPS:
+            prm = self.store.param(name)
+            t = _lib.AdamTensor(prm.data_ptr(), self.store.grad(name).data_ptr(),
+                                self.store.exp_avg(name).data_ptr(), self.store.exp_avg_sq(name).data_ptr(),
+                                prm.numel(), 0.0, 1.0)
+            if name == "features":
+                t.split_period, t.split_len = 3 * self.M, 3
+            ts.append(t)
+        return ts
+
+    def adam_scalars(self, out):
+        """optimizer_step's per-group scalars of one step that skips no group,
+        into ``out`` (float32 [15]: step_size, sqrt(1 - beta2^n), tail step
+        size per group); advances the step counts as optimizer_step does."""
+        b1, b2 = self.betas
+        lr = self.lr
+        for i, (name, step, tail) in enumerate((("xyz", lr["xyz"], lr["xyz"]),
+                                                ("features", lr["f_dc"], lr["f_rest"]),
+                                                ("opacity", lr["opacity"], lr["opacity"]),
+                                                ("scaling", lr["scaling"], lr["scaling"]),
+                                                ("rotation", lr["rotation"], lr["rotation"]))):
+            self.steps[name] += 1
+            n = self.steps[name]
+            bc1 = 1.0 - b1 ** n
+            out[3 * i] = step / bc1
+            out[3 * i + 1] = math.sqrt(1.0 - b2 ** n)
+            out[3 * i + 2] = tail / bc1
+
+    @torch.no_grad()
+    def optimizer_step_dev(self, tensors, scalars, skip):
+        """optimizer_step with the scalars in device memory (``scalars``:
+        float32 [15] device tensor, see adam_scalars) and a device skip word
+        (a capacity-mode forward's overflow flag): ONE launch whose arguments
+        do not change between steps, so it can be captured in a graph."""
+        L = _lib.load()
+        b1, b2 = self.betas
+        arr = (_lib.AdamTensor * len(tensors))(*tensors)
+        dev = self.store.device
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_adam_step_dev(arr, len(tensors), b1, b2, self.eps, 0.0, _lib.ptr(scalars),
+                                            _lib.ptr(skip), _lib.stream_handle(dev)))
 
     def step(self, *args, **kwargs):
         """forward_backward + optimizer_step (one reference mapping iteration

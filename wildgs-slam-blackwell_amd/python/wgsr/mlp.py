@@ -98,6 +98,44 @@ class _MLPFn(torch.autograd.Function):
         return None, gW1, gb1, gW2, gb2, gW3, gb3, None, None
 
 
+def forward_raw(net, x, seed_dev):
+    """The forward of ``net`` on x [N, C] without autograd, the dropout seed
+    read from device memory (``seed_dev``: int32 [1] holding the uint32 bits):
+    -> (u [N], saved) for ``backward_raw``.  What a graph-replayed mapping
+    iteration runs (wgsr.online); the launches and arithmetic are
+    ``_MLPFn``'s."""
+    N, C = x.shape
+    dev = x.device
+    L = _lib.load()
+    l1, l2, lo = net.layers[0], net.layers[1], net.output_layer
+    ws = [t.detach() for t in (l1.weight, l1.bias, l2.weight, l2.bias, lo.weight, lo.bias)]
+    h1d = torch.empty(N, HIDDEN, device=dev)
+    h2d = torch.empty(N, HIDDEN, device=dev)
+    o = torch.empty(N, device=dev)
+    u = torch.empty(N, device=dev)
+    pt = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_mlp_forward_dev_seed(N, C, pt(x), *[pt(t) for t in ws], float(net.dropout_p), pt(seed_dev),
+                                               pt(h1d), pt(h2d), pt(o), pt(u), _lib.stream_handle(dev)))
+    return u, (x, ws[2], ws[4], h1d, h2d, o, float(net.dropout_p))
+
+
+def backward_raw(saved, du):
+    """-> the flat parameter gradient (wgsr_mlp_grad_floats(C) floats, the
+    parameters' order) of a ``forward_raw`` for dL/du = du [N]."""
+    x, W2, W3, h1d, h2d, o, p = saved
+    N, C = x.shape
+    dev = x.device
+    L = _lib.load()
+    grad = torch.empty(int(L.wgsr_mlp_grad_floats(C)), device=dev)
+    scratch = torch.empty(max(1, int(L.wgsr_mlp_scratch_bytes(N, C)) // 4), device=dev)
+    pt = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_mlp_backward(N, C, pt(x), pt(W2), pt(W3), p, pt(h1d), pt(h2d), pt(o), pt(du), pt(scratch),
+                                       pt(grad), _lib.stream_handle(dev)))
+    return grad
+
+
 class UncertaintyMLP(nn.Module):
     """MLPNetwork(input_dim=C) with the reference defaults, on libwgsr."""
 

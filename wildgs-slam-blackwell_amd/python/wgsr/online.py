@@ -166,7 +166,14 @@ class OnlineMapper:
         self.keyframes: dict[int, Keyframe] = {}
         self.window: list[int] = []
         self.occ_vis: dict[int, torch.Tensor] = {}
-        self.kopt = None
+        from .online_graph import IterationGraphs, KeyframeBank
+        # every keyframe's per-view data (and its exposure + Adam moments) in
+        # slot-indexed device banks; the Keyframe tensors become views
+        self.bank = KeyframeBank(self.dev)
+        self.kopt_uids: set[int] = set()   # the window's exposure optimiser (mapper.py:219-241)
+        self.kopt_steps: dict[int, int] = {}
+        self._max_nr = 0                   # largest num_rendered seen (the graphs' first capacity)
+        self.graphs = IterationGraphs(self) if self.dev.type == "cuda" else None
         self.iteration_count = 0
         self.iterations_after_densify_or_reset = 0
         self.bg = torch.zeros(3, device=self.dev)
@@ -299,8 +306,17 @@ class OnlineMapper:
 
     def _perm(self, n: int) -> torch.Tensor:
         """The DINO term's feature sampling draw (the reference's
-        torch.randperm(n), mapper.py:1155-1157 / 1334-1336)."""
-        return torch.randperm(n, device=self.dev, generator=self.gen)
+        torch.randperm(n), mapper.py:1155-1157 / 1334-1336): the stable
+        ascending order of 31-bit hash keys of a seed drawn from torch's
+        host generator (wgsr_random_keys) -- the draw the graph-replayed
+        iteration makes on the device from the same seed."""
+        from . import _lib
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        keys = torch.empty(n, dtype=torch.int32, device=self.dev)
+        L = _lib.load()
+        with torch.cuda.device(self.dev):
+            _lib.check(L.wgsr_random_keys(n, seed, None, _lib.ptr(keys), _lib.stream_handle(self.dev)))
+        return torch.argsort(keys, stable=True)
 
     def _dino_term(self, neighbours, kf):
         """reg_mult * compute_dino_regularization_loss on features sampled from
@@ -341,6 +357,7 @@ class OnlineMapper:
                                                   freeze_uncertainty_loss=freeze, median_depth=kf.median_depth)
             if self.iterations_after_densify_or_reset >= 20:
                 self._dino_term(neighbours, kf)
+        self._max_nr = max(self._max_nr, int(out["num_rendered"]))
         vis = out["radii"] > 0
         if occ_window is not None:  # last iteration of a map_opt_online call (mapper.py:1174-1175)
             self._update_occ_aware_visibility(occ_window)
@@ -371,24 +388,34 @@ class OnlineMapper:
 
     def _exposure_step(self, kf, out):
         """keyframe_optimizers.step() + zero_grad(set_to_none=True): only the
-        rendered keyframe's exposures carry a gradient; others are skipped."""
-        if self.kopt is not None and kf.uid in self.kopt_uids:
-            kf.exposure_a.grad = out["dexposure_a"].reshape(1)
-            kf.exposure_b.grad = out["dexposure_b"].reshape(1)
-            self.kopt.step()
-            kf.exposure_a.grad = kf.exposure_b.grad = None
+        rendered keyframe's exposures carry a gradient; others are skipped.
+        torch.optim.Adam(lr=exposure_lr) arithmetic (wgsr_adam_step) on the
+        keyframe's row of the exposure bank (a, b share one step count: they
+        always step together)."""
+        if kf.uid not in self.kopt_uids:
+            return
+        from . import _lib
+        self.kopt_steps[kf.uid] += 1
+        n = self.kopt_steps[kf.uid]
+        da, db = out["dexposure_a"], out["dexposure_b"]
+        g = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
+        prm, m, v = self.bank.ex_ptrs(kf.uid)
+        lr = self.cfg["exposure_lr"]
+        t = _lib.AdamTensor(prm, g.data_ptr(), m, v, 2, lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n))
+        L = _lib.load()
+        with torch.cuda.device(self.dev):
+            _lib.check(L.wgsr_adam_step((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, _lib.stream_handle(self.dev)))
 
     def _new_exposure_optimizer(self):
-        """mapper.py:219-241: a fresh Adam over the window's exposures (not kf 0)."""
-        from .optim import FusedAdam
-        params, uids = [], set()
-        for k in self.window:
-            if k == 0:
-                continue
-            kf = self.keyframes[k]
-            params += [kf.exposure_a, kf.exposure_b]
-            uids.add(k)
-        self.kopt = FusedAdam(params, lr=self.cfg["exposure_lr"]) if params else None
+        """mapper.py:219-241: a fresh Adam over the window's exposures (not kf
+        0): zero moments and step counts on their exposure-bank rows."""
+        self.bank.sync(self.keyframes)
+        uids = {k for k in self.window if k != 0 and k in self.keyframes}
+        if uids:
+            rows = torch.tensor([self.bank.slots[k] for k in sorted(uids)], device=self.dev)
+            with torch.no_grad():
+                self.bank.ex[rows, 1:] = 0.0
+        self.kopt_steps = {k: 0 for k in uids}
         self.kopt_uids = uids
 
     # ---- the reference's entry points ----------------------------------------
@@ -403,6 +430,7 @@ class OnlineMapper:
             self.window = [kf.uid] + self.window
         self._new_exposure_optimizer()
         stack = list(self.window)
+        self.bank.sync(self.keyframes)
         for it in range(c["init_itr_num"] if iters is None else iters):
             kf = self.keyframes[stack[int(self.rng.integers(len(stack)))]]
             update = it % c["init_gaussian_update"] == 0
@@ -414,6 +442,7 @@ class OnlineMapper:
         """The Mapper's per-keyframe work (mapper.py:153-266)."""
         vis = self.visibility(kf)
         self.keyframes[kf.uid] = kf
+        self.bank.sync(self.keyframes)
         self.window = self._add_to_window(kf.uid, vis, self.window)
         added = self._add_points(kf, init=False)
         self._new_exposure_optimizer()
@@ -453,6 +482,7 @@ class OnlineMapper:
         if deform and frames and self.ms is not None:
             K = self.keyframes[frames[0]["kf_id"]].K
             self.ms.store.update_mapping_points(frames, K)
+        self.bank.sync(self.keyframes)  # (the new cameras / depths into the banks)
         return len(frames)
 
     def final_refine(self, iters: int = 26000):
@@ -466,17 +496,28 @@ class OnlineMapper:
         c = self.cfg
         ms = self.ms
         stack = [k for k in self.keyframes]
+        self.bank.sync(self.keyframes)
         for _ in range(iters):
-            self.iteration_count += 1
-            self.iterations_after_densify_or_reset += 1
             ci = int(self.rng.choice(len(stack)))
             kf = self.keyframes[stack[ci]]
+            if (self.graphs is not None and self.iterations_after_densify_or_reset + 1 >= 200
+                    and self.graphs.step(kf, [stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))],
+                                         refine=True)):
+                self.iteration_count += 1
+                self.iterations_after_densify_or_reset += 1
+                ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
+                                         lr_delay_mult=c["position_lr_delay_mult"],
+                                         max_steps=c["position_lr_max_steps"])
+                continue
+            self.iteration_count += 1
+            self.iterations_after_densify_or_reset += 1
             unc = self.net(kf.features)
             freeze = self.iterations_after_densify_or_reset < 200
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg,
                                                   unc, c["train_frac_fix"], c["train_frac_fix"],
                                                   freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
                                                   pre_exposed=False)
+            self._max_nr = max(self._max_nr, int(out["num_rendered"]))
             if self.iterations_after_densify_or_reset >= 200:
                 self._dino_term([stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))], kf)
             ms.optimizer_step()
@@ -501,6 +542,8 @@ class OnlineMapper:
             prob[:] = 1.0
         prob /= prob.sum()
         split = False
+        self.bank.sync(self.keyframes)
+        ms = self.ms
         for it in range(iters):
             ci = int(self.rng.choice(len(stack), p=prob))
             kf = self.keyframes[stack[ci]]
@@ -508,6 +551,17 @@ class OnlineMapper:
             nxt = self.iteration_count + 1
             update = nxt % c["gaussian_update_every"] == c["gaussian_update_offset"]
             reset = "nonvisible" if (nxt % c["gaussian_reset"] == 0 and not update) else None
-            self._iteration(kf, nb, False, update, reset, occ_window=window if it == iters - 1 else None)
+            last = it == iters - 1
+            # the steady state (no densify / reset / visibility update, the
+            # DINO term on) as a graph replay (wgsr.online_graph)
+            if (self.graphs is not None and not update and reset is None and not last
+                    and self.iterations_after_densify_or_reset + 1 >= 20 and self.graphs.step(kf, nb)):
+                self.iteration_count += 1
+                self.iterations_after_densify_or_reset += 1
+                ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
+                                         lr_delay_mult=c["position_lr_delay_mult"],
+                                         max_steps=c["position_lr_max_steps"])
+                continue
+            self._iteration(kf, nb, False, update, reset, occ_window=window if last else None)
             split = split or update or reset is not None
         return split

@@ -1,0 +1,451 @@
+"""Graph-replayed mapping iterations for ``wgsr.online``.
+
+The reference's mapper (src/mapper.py:1083-1219, 1234-1372) runs each
+mapping iteration as ~100 eager kernels with several host synchronisations;
+the eager restatement in ``OnlineMapper._iteration`` fuses them to ~35
+launches, but one mapping iteration at TUM scale is still bounded by the
+host: ~1.8 ms of wall clock for ~0.7 ms of kernels, with the rasteriser's one
+host wait (num_rendered) draining the queue every iteration.
+
+Here the steady-state iteration -- no densify / reset, no visibility update,
+the DINO term on, the uncertainty loss not frozen -- is captured ONCE per
+(map state, neighbour count) as a HIP graph and replayed:
+
+* the keyframe is chosen on the host as before and handed over as a slot
+  index: every keyframe's image, depth, features, camera, median depth and
+  exposure (+ its Adam moments) live in slot-indexed device banks
+  (``KeyframeBank``; the Keyframe objects' tensors are views into them), and
+  the graph gathers the chosen slot's rows (index_select) and scatters the
+  exposure back;
+* the rasteriser runs in capacity mode (wgsr_rasterize_forward_cap): buffers
+  sized for ``cap`` pairs, counts on the device, no host wait.  An overflow
+  (more pairs than ``cap``) makes the iteration a no-op for every optimiser
+  (device skip word) and is seen by the host a few iterations later through a
+  pinned flag, which recaptures with a larger capacity;
+* everything that changes per step -- the three dropout / sampling seeds,
+  every Adam step size and bias correction (Gaussians, MLP, exposure), the
+  exposure skip flag, the slot indices -- arrives in one 256-byte block
+  copied host->device ahead of the replay (a ring of pinned blocks);
+* the uncertainty MLP, the DINO sampling (hash keys + stable argsort) and
+  regulariser, and all three Adams run without autograd (wgsr.mlp.forward_raw
+  / backward_raw, wgsr.uncertainty.dino_reg_raw, wgsr_adam_step_dev).
+
+The eager path draws the same seeds in the same order and uses the same
+kernels, so a replayed iteration computes what ``_iteration`` computes
+(tests/test_gpu_online_graph.py compares them).  Any change of the map's
+shape (P, the store's banks, the keyframe banks) invalidates the graphs;
+they are recaptured lazily.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from .mlp import backward_raw, forward_raw
+from .uncertainty import dino_reg_raw
+
+CAM_FLOATS = 52  # viewmatrix 16 | projmatrix 16 | projmatrix_raw 16 | campos 3 | pad
+
+
+class KeyframeBank:
+    """Slot-indexed device banks of the keyframes' per-view data.
+
+    ``sync(keyframes)`` adopts new keyframes (copies their tensors into a
+    slot and rebinds the Keyframe's fields to views of it) and refreshes
+    fields a caller replaced (a pose update's new camera tensors, a new
+    depth).  The exposure bank ``ex`` [K, 3, 2] = (a, b), Adam exp_avg,
+    Adam exp_avg_sq per slot is always kept (the exposure optimiser steps
+    through it); the image banks only while every keyframe has the same
+    image / feature shape and field of view (``uniform``)."""
+
+    def __init__(self, dev):
+        self.dev = torch.device(dev)
+        self.cap = 0
+        self.slots: dict[int, int] = {}
+        self.kfs: dict[int, object] = {}
+        self.ex = torch.zeros(0, 3, 2, device=self.dev)
+        self.shape = None   # (H, W, h, w, C)
+        self.tan = None     # (tanfovx, tanfovy)
+        self.uniform = True
+        self.image = self.depth = self.feat = self.cam = self.med = None
+        self.version = 0
+
+    # -- layout ------------------------------------------------------------
+    def _alloc(self, cap):
+        old = (self.ex, self.image, self.depth, self.feat, self.cam, self.med)
+        n = self.cap
+        self.ex = torch.zeros(cap, 3, 2, device=self.dev)
+        self.ex[:n].copy_(old[0][:n])
+        if self.uniform and self.shape is not None:
+            H, W, h, w, C = self.shape
+            shapes = ((3, H, W), (1, H, W), (h, w, C), (CAM_FLOATS,), ())
+            new = [torch.zeros((cap,) + s, device=self.dev) for s in shapes]
+            for t, o in zip(new, old[1:]):
+                if o is not None and n:
+                    t[:n].copy_(o[:n])
+            self.image, self.depth, self.feat, self.cam, self.med = new
+        self.cap = cap
+        self.version += 1
+        for uid, kf in self.kfs.items():
+            self._bind(uid, kf)
+
+    def _addr(self, t, slot):
+        return t.data_ptr() + slot * t[0].numel() * t.element_size()
+
+    def _stale(self, uid, kf):
+        s = self.slots[uid]
+        out = []
+        base = self._addr(self.ex, s)
+        if kf.exposure_a.data_ptr() != base or kf.exposure_b.data_ptr() != base + 4:
+            out.append("ex")
+        if self.uniform and self.image is not None:
+            for name, bank, t in (("image", self.image, kf.image), ("depth", self.depth, kf.depth),
+                                  ("feat", self.feat, kf.features), ("med", self.med, kf.median_depth)):
+                if not torch.is_tensor(t) or t.data_ptr() != self._addr(bank, s):
+                    out.append(name)
+            cb = self._addr(self.cam, s)
+            if any(kf.cam[k].data_ptr() != cb + 4 * o for k, o in
+                   (("viewmatrix", 0), ("projmatrix", 16), ("projmatrix_raw", 32), ("campos", 48))):
+                out.append("cam")
+        return out
+
+    def _store(self, uid, kf, fields):
+        s = self.slots[uid]
+        with torch.no_grad():
+            if "ex" in fields:
+                self.ex[s, 0, 0:1].copy_(kf.exposure_a.detach().reshape(1))
+                self.ex[s, 0, 1:2].copy_(kf.exposure_b.detach().reshape(1))
+            if not (self.uniform and self.image is not None):
+                return
+            if "image" in fields:
+                self.image[s].copy_(kf.image.reshape(self.image.shape[1:]))
+            if "depth" in fields:
+                self.depth[s].copy_(kf.depth.reshape(self.depth.shape[1:]))
+            if "feat" in fields:
+                self.feat[s].copy_(kf.features.reshape(self.feat.shape[1:]))
+            if "med" in fields:
+                self.med[s].copy_(torch.as_tensor(kf.median_depth, device=self.dev).reshape(()))
+            if "cam" in fields:
+                c = self.cam[s]
+                for k, o, n in (("viewmatrix", 0, 16), ("projmatrix", 16, 16), ("projmatrix_raw", 32, 16),
+                                ("campos", 48, 3)):
+                    c[o:o + n].copy_(kf.cam[k].reshape(-1))
+
+    def _bind(self, uid, kf):
+        s = self.slots[uid]
+        kf.exposure_a = self.ex[s, 0, 0:1]
+        kf.exposure_b = self.ex[s, 0, 1:2]
+        if self.uniform and self.image is not None:
+            kf.image = self.image[s]
+            kf.depth = self.depth[s]
+            kf.features = self.feat[s]
+            kf.median_depth = self.med[s]
+            c = self.cam[s]
+            kf.cam = dict(kf.cam, viewmatrix=c[0:16].view(4, 4), projmatrix=c[16:32].view(4, 4),
+                          projmatrix_raw=c[32:48].view(4, 4), campos=c[48:51])
+
+    def _check_shape(self, kf):
+        H, W = kf.image.shape[-2:]
+        h, w, C = kf.features.shape[-3:]
+        shp = (int(H), int(W), int(h), int(w), int(C))
+        tan = (float(kf.cam["tanfovx"]), float(kf.cam["tanfovy"]))
+        ok = (kf.image.dtype == torch.float32 and kf.features.dtype == torch.float32
+              and kf.depth.numel() == H * W and kf.image.device == self.dev)
+        if self.shape is None and ok:
+            self.shape, self.tan = shp, tan
+            return
+        if not ok or shp != self.shape or tan != self.tan:
+            self.uniform = False  # (graphs off; the exposure bank stays)
+
+    # -- public ------------------------------------------------------------
+    def sync(self, keyframes: dict):
+        """Adopt new keyframes, refresh replaced fields of adopted ones."""
+        for uid, kf in keyframes.items():
+            if uid in self.slots and self.kfs.get(uid) is kf:
+                st = self._stale(uid, kf)
+                if st:
+                    self._store(uid, kf, st)
+                    self._bind(uid, kf)
+        for uid, kf in keyframes.items():
+            if self.kfs.get(uid) is kf:
+                continue
+            if uid not in self.slots:
+                was_uniform = self.uniform
+                self._check_shape(kf)
+                if was_uniform and not self.uniform:
+                    self.version += 1  # (graphs off from here on)
+                need_images = self.uniform and self.image is None and self.shape is not None
+                if len(self.slots) >= self.cap or need_images:
+                    # (re)allocates and rebinds the keyframes adopted so far;
+                    # this one is bound below, after its data is stored
+                    self._alloc(max(16, 2 * self.cap, len(self.slots) + 1))
+                self.slots[uid] = len(self.slots)
+            with torch.no_grad():
+                self.ex[self.slots[uid], 1:].zero_()
+            self._store(uid, kf, ("ex", "image", "depth", "feat", "med", "cam"))
+            self.kfs[uid] = kf
+            self._bind(uid, kf)
+
+    def ex_ptrs(self, uid):
+        """(param, exp_avg, exp_avg_sq) device addresses of uid's exposure row."""
+        b = self._addr(self.ex, self.slots[uid])
+        return b, b + 8, b + 16
+
+
+class IterationGraphs:
+    """The steady-state mapping iteration as replayed HIP graphs (module doc)."""
+
+    NF = 40                       # float words of the per-step block
+    F_GAUSS, F_MLP, F_EXPO, F_EXSKIP = 3, 18, 36, 39
+    RING = 16
+
+    def __init__(self, mapper):
+        self.m = mapper
+        dev = mapper.dev
+        self.dev = dev
+        self.block = torch.zeros(256, dtype=torch.uint8, device=dev)
+        self.f32 = self.block[:160].view(torch.float32)
+        self.i32 = self.block[:160].view(torch.int32)
+        self.i64 = self.block[160:208].view(torch.int64)
+        self.ring = torch.zeros(self.RING, 256, dtype=torch.uint8).pin_memory()
+        rn = self.ring.numpy()
+        self.ring_f = rn[:, :160].view(np.float32)
+        self.ring_u = rn[:, :160].view(np.uint32)
+        self.ring_i = rn[:, 160:208].view(np.int64)
+        self.ring_ev = [None] * self.RING
+        self.slot = 0
+        self.counts = torch.zeros(5, dtype=torch.int32, device=dev)
+        self.sticky = torch.zeros(2, dtype=torch.int64, device=dev)   # overflowed replays, max N_rect
+        self.sticky_host = torch.zeros(2, dtype=torch.int64).pin_memory()
+        self.sticky_np = self.sticky_host.numpy()
+        self.graphs = {}
+        self.key = None
+        self.pool = None
+        self.cap = None
+        self.S = None
+        self.disabled = None  # reason string once disabled
+        self.stats = {"captures": 0, "replays": 0, "overflows": 0, "skipped_iterations": 0}
+
+    # -- eligibility -----------------------------------------------------------
+    def usable(self) -> bool:
+        m = self.m
+        if self.disabled is not None or os.environ.get("WGSR_ONLINE_GRAPH", "1") == "0":
+            return False
+        if m.dev.type != "cuda" or m.ms is None or m.ms.P == 0 or getattr(m.ms, "_skip", None):
+            return False
+        if m.net.seed_source is not None or "_perm" in m.__dict__:
+            return False  # a test feeds the random draws: eager only
+        return m.bank.uniform and m.bank.image is not None
+
+    def _map_key(self):
+        st = self.m.ms.store
+        return (st.P, st.cur, id(st.banks), self.m.bank.version)
+
+    def invalidate(self):
+        self.graphs = {}
+        self.pool = None
+        self.S = None
+
+    # -- static state ----------------------------------------------------------
+    def _build_static(self):
+        m = self.m
+        B = m.bank
+        H, W, h, w, C = B.shape
+        dev = self.dev
+        S = type("Static", (), {})()
+        S.image4 = torch.zeros(1, 3, H, W, device=dev)
+        S.depth4 = torch.zeros(1, 1, H, W, device=dev)
+        S.feat4 = torch.zeros(1, h, w, C, device=dev)
+        S.cam2 = torch.zeros(1, CAM_FLOATS, device=dev)
+        S.med = torch.zeros(1, device=dev)
+        S.ex = torch.zeros(1, 3, 2, device=dev)
+        S.nbf = torch.zeros(5, h, w, C, device=dev)
+        c = S.cam2[0]
+        S.cam = dict(viewmatrix=c[0:16].view(4, 4), projmatrix=c[16:32].view(4, 4), projmatrix_raw=c[32:48].view(4, 4),
+                     campos=c[48:51], tanfovx=B.tan[0], tanfovy=B.tan[1], image_height=H, image_width=W)
+        S.skip_ex = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the MLP optimiser's state must exist before a capture bakes its addresses in
+        opt = m.uopt
+        S.mlp_params = list(m.net.parameters())
+        S.mlp_steps = []
+        for p in S.mlp_params:
+            st = opt.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            S.mlp_steps.append(st["step"])
+        g = opt.param_groups[0]
+        S.mlp_lr, S.mlp_betas, S.mlp_eps, S.mlp_wd = g["lr"], g["betas"], g["eps"], g.get("weight_decay", 0.0)
+        m.ms.iso_part  # noqa: B018  (allocated outside the capture)
+        self.S = S
+
+    def _body(self, nbc: int, refine: bool):
+        """One mapping iteration's device work (captured; see the module doc)."""
+        m, S = self.m, self.S
+        ms, B, c = m.ms, m.bank, m.cfg
+        L = _lib.load()
+        dev = self.dev
+        st = _lib.stream_handle(dev)
+        p = _lib.ptr
+        H, W, h, w, C = B.shape
+        idx = self.i64[0:1]
+        torch.index_select(B.image, 0, idx, out=S.image4)
+        torch.index_select(B.depth, 0, idx, out=S.depth4)
+        torch.index_select(B.feat, 0, idx, out=S.feat4)
+        torch.index_select(B.cam, 0, idx, out=S.cam2)
+        torch.index_select(B.med, 0, idx, out=S.med)
+        torch.index_select(B.ex, 0, idx, out=S.ex)
+        torch.index_select(B.feat, 0, self.i64[1:1 + nbc], out=S.nbf[:nbc])
+        # the uncertainty MLP on the keyframe's features, the loss + rasteriser
+        # forward/backward (capacity mode), the MLP backward of the loss
+        u, sv = forward_raw(m.net, S.feat4.view(h * w, C), self.i32[0:1])
+        out = ms.forward_backward_uncertainty(S.cam, S.image4[0], S.depth4[0], S.ex[0, 0, 0:1], S.ex[0, 0, 1:2], m.bg,
+                                              u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
+                                              freeze_uncertainty_loss=False, median_depth=S.med,
+                                              pre_exposed=not refine, cap=self.cap, counts=self.counts)
+        G = backward_raw(sv, out["uncertainty_grad"].reshape(-1).contiguous())
+        # the DINO term on features sampled from the neighbouring keyframes
+        n = nbc * h * w
+        ns = n // (c["reg_stride"] ** 4)
+        keys = torch.empty(n, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_random_keys(n, 0, p(self.i32[1:2]), p(keys), st))
+        perm = torch.argsort(keys, stable=True)[:ns]
+        sf = S.nbf[:nbc].view(n, C).index_select(0, perm)
+        u2, sv2 = forward_raw(m.net, sf, self.i32[2:3])
+        _, gu = dino_reg_raw(u2, sf)
+        G = G + backward_raw(sv2, gu * float(c["reg_mult"]))
+        skip = self.counts[3:4]
+        # Adam: the Gaussians, the keyframe's exposure (skipped unless the
+        # window optimiser holds it), the MLP (L2 weight decay)
+        ms.optimizer_step_dev(ms.adam_tensors(), self.f32[self.F_GAUSS:self.F_GAUSS + 15], skip)
+        torch.maximum(skip, self.i32[self.F_EXSKIP:self.F_EXSKIP + 1], out=S.skip_ex)
+        da, db = out["dexposure_a"], out["dexposure_b"]
+        gex = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
+        exb = S.ex.data_ptr()
+        t = _lib.AdamTensor(exb, gex.data_ptr(), exb + 8, exb + 16, 2, 0.0, 1.0)
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, 0.0,
+                                            p(self.f32[self.F_EXPO:self.F_EXPO + 3]), p(S.skip_ex), st))
+        B.ex.index_copy_(0, idx, S.ex)
+        ts, off = [], 0
+        opt = m.uopt
+        for prm in S.mlp_params:
+            k = prm.numel()
+            sto = opt.state[prm]
+            ts.append(_lib.AdamTensor(prm.data_ptr(), G.data_ptr() + 4 * off, sto["exp_avg"].data_ptr(),
+                                      sto["exp_avg_sq"].data_ptr(), k, 0.0, 1.0))
+            off += k
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * len(ts))(*ts), len(ts), S.mlp_betas[0], S.mlp_betas[1],
+                                            S.mlp_eps, S.mlp_wd, p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip),
+                                            st))
+        # overflow bookkeeping, seen by the host through pinned memory
+        self.sticky[0:1] += skip.to(torch.int64)
+        torch.maximum(self.sticky[1:2], self.counts[0:1].to(torch.int64) & 0xFFFFFFFF, out=self.sticky[1:2])
+        self.sticky_host.copy_(self.sticky, non_blocking=True)
+
+    def _capture(self, nbc: int, refine: bool):
+        if self.S is None:
+            self._build_static()
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g, pool=self.pool):
+                self._body(nbc, refine)
+        except Exception as e:  # e.g. a configuration the capacity-mode forward does not cover
+            self.disabled = f"{type(e).__name__}: {e}"
+            self.invalidate()
+            return None
+        if self.pool is None:
+            self.pool = g.pool()
+        self.graphs[(nbc, refine)] = g
+        self.stats["captures"] += 1
+        return g
+
+    # -- the step ----------------------------------------------------------------
+    def _check_capacity(self):
+        """Grow the capacity (and recapture) after an overflow, or when the
+        largest pair count seen comes within 3/4 of it."""
+        ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
+        if self.cap is not None and not ovf and mx <= 0.75 * self.cap:
+            return
+        if self.cap is None:
+            self.cap = max(1 << 16, 2 * int(self.m._max_nr) + 4096)
+            return
+        torch.cuda.synchronize(self.dev)
+        ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
+        if ovf:
+            self.stats["overflows"] += 1
+            self.stats["skipped_iterations"] += ovf
+            # the skipped steps advanced no moments on the device: undo their counts
+            for name in self.m.ms.GROUPS:
+                self.m.ms.steps[name] -= ovf
+            if self.S is not None:
+                for t in self.S.mlp_steps:
+                    t -= ovf
+            self.m.events.append((self.m.iteration_count, "capacity_overflow", {"cap": self.cap, "skipped": ovf}))
+        self.cap = max(2 * self.cap if ovf else self.cap, 2 * mx + 4096)
+        self.sticky.zero_()
+        self.sticky_np[:] = 0
+        self.invalidate()
+
+    def step(self, kf, neighbours, refine: bool = False) -> bool:
+        """Run one steady-state iteration on keyframe ``kf`` as a graph replay;
+        False when the graph path does not apply (the caller runs it eagerly)."""
+        if not self.usable():
+            return False
+        m = self.m
+        nbc = len(neighbours)
+        if not 1 <= nbc <= 5:
+            return False
+        key = self._map_key()
+        if key != self.key:
+            self.invalidate()
+            self.key = key
+        self._check_capacity()
+        g = self.graphs.get((nbc, refine))
+        if g is None:
+            g = self._capture(nbc, refine)
+            if g is None:
+                return False
+        S = self.S
+        i = self.slot
+        self.slot = (i + 1) % self.RING
+        ev = self.ring_ev[i]
+        if ev is not None:
+            ev.synchronize()
+        f, u, ix = self.ring_f[i], self.ring_u[i], self.ring_i[i]
+        # the seeds in the eager path's order: MLP forward, DINO draw, DINO MLP forward
+        for j in range(3):
+            u[j] = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        m.ms.adam_scalars(f[self.F_GAUSS:self.F_GAUSS + 15])
+        b1, b2 = S.mlp_betas
+        n = float(S.mlp_steps[0]) + 1.0
+        bc1 = 1.0 - b1 ** n
+        bc2s = math.sqrt(1.0 - b2 ** n)
+        f[self.F_MLP:self.F_MLP + 18] = np.tile(np.array([S.mlp_lr / bc1, bc2s, S.mlp_lr / bc1], np.float32), 6)
+        if kf.uid in m.kopt_uids:
+            m.kopt_steps[kf.uid] += 1
+            ne = m.kopt_steps[kf.uid]
+            lr = m.cfg["exposure_lr"]
+            f[self.F_EXPO:self.F_EXPO + 3] = (lr / (1.0 - 0.9 ** ne), math.sqrt(1.0 - 0.999 ** ne), 0.0)
+            u[self.F_EXSKIP] = 0
+        else:
+            u[self.F_EXSKIP] = 1
+        ix[0] = m.bank.slots[kf.uid]
+        for j, k in enumerate(neighbours):
+            ix[1 + j] = m.bank.slots[k]
+        self.block.copy_(self.ring[i], non_blocking=True)
+        if ev is None:
+            ev = self.ring_ev[i] = torch.cuda.Event()
+        ev.record()
+        g.replay()
+        torch._foreach_add_(S.mlp_steps, 1.0)
+        self.stats["replays"] += 1
+        return True

@@ -277,26 +277,31 @@ DINO_SIMILARITY_THRESHOLD = 0.75
 DINO_EPS = float(torch.finfo(torch.float32).eps)
 
 
+def dino_reg_raw(u, feat):
+    """wgsr_dino_reg (csrc/dino.hip) on u [N], feat [N, C] (device, fp32,
+    contiguous): -> (loss 0-d, d loss / d u [N]), no autograd."""
+    L = _lib.load()
+    N, C = feat.shape
+    dev = feat.device
+    fn = torch.empty(N, C, device=dev)
+    sim = torch.empty(N, N, device=dev)
+    row_var = torch.empty(N, device=dev)
+    grad_u = torch.empty(N, device=dev)
+    loss = torch.empty((), device=dev)
+    pt = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_dino_reg(pt(u), pt(feat), N, C, DINO_TOP_K, DINO_SIMILARITY_THRESHOLD, DINO_EPS,
+                                   pt(fn), pt(sim), pt(row_var), pt(grad_u), pt(loss), _lib.stream_handle(dev)))
+    return loss, grad_u
+
+
 class _DinoReg(torch.autograd.Function):
     """wgsr_dino_reg (csrc/dino.hip): the whole regulariser in four launches;
     d loss / d u is produced by the forward and scaled in the backward."""
 
     @staticmethod
     def forward(ctx, u, feat):
-        from . import _lib
-        L = _lib.load()
-        N, C = feat.shape
-        dev = feat.device
-        fn = torch.empty(N, C, device=dev)
-        sim = torch.empty(N, N, device=dev)
-        row_var = torch.empty(N, device=dev)
-        grad_u = torch.empty(N, device=dev)
-        loss = torch.empty((), device=dev)
-        pt = _lib.ptr
-        with torch.cuda.device(dev):
-            _lib.check(L.wgsr_dino_reg(pt(u), pt(feat), N, C, DINO_TOP_K, DINO_SIMILARITY_THRESHOLD, DINO_EPS,
-                                       pt(fn), pt(sim), pt(row_var), pt(grad_u), pt(loss),
-                                       _lib.stream_handle(dev)))
+        loss, grad_u = dino_reg_raw(u, feat)
         ctx.save_for_backward(grad_u)
         return loss
 
