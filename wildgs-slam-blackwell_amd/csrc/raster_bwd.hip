@@ -1305,6 +1305,12 @@ __device__ __forceinline__ void cov_to_scale_rot(float4 q, f3 sv, float scale_mo
 
 // Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
 // holds its 3M SH coefficients on entry and its dL/dsh row on exit.
+// a listed Gaussian's parameters, loaded ahead of its record sums
+// (k_gauss_bwd_compact with WGSR_GBC_PREFETCH)
+struct GbPre {
+  f3 mean, sv;
+  float4 q;
+};
 __device__ __forceinline__ void gauss_bwd_one(
     int i, int D, int M, bool live, const uint32_t* __restrict__ clamped, const float g[10],
     const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
@@ -1312,9 +1318,11 @@ __device__ __forceinline__ void gauss_bwd_one(
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
     const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
     float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau, bool have_pre = false,
+    GbPre pre = GbPre{}) {
   // dm_sh: the SH term of dL/dmean when the caller ran sh_backward itself
-  // (shrow null); zero otherwise.
+  // (shrow null); zero otherwise.  pre: the parameters, already loaded
+  // (no cov3D_precomp then).
   const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
   if (!live) {  // culled, or (sparse) no partial record: every output is zero
     for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
@@ -1325,11 +1333,14 @@ __device__ __forceinline__ void gauss_bwd_one(
     return;
   }
   // parameters first: their loads overlap the partial-record walk below
-  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+  const f3 mean = have_pre ? pre.mean : mk3(means[i3], means[i3 + 1], means[i3 + 2]);
   float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
   f3 sv = mk3(0.f, 0.f, 0.f);
   float cv[6];
-  if (cov_pre) {
+  if (have_pre) {
+    sv = pre.sv;
+    q = pre.q;
+  } else if (cov_pre) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
   } else {
@@ -1510,6 +1521,11 @@ constexpr int kGbcThreads = 256;
 #define WGSR_GBC_ROUNDS 2
 #endif
 constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
+// WGSR_GBC_PREFETCH=1 (A/B): the listed Gaussians' parameters load before the
+// record sums instead of after them
+#ifndef WGSR_GBC_PREFETCH
+#define WGSR_GBC_PREFETCH 0
+#endif
 constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
 // WGSR_GBC_FLAT=0: one 16-lane group per listed Gaussian sums its records
 // (a dependent slot-range load per group pass)
@@ -1517,7 +1533,10 @@ constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
 #define WGSR_GBC_FLAT 1
 #endif
 #if WGSR_GBC_FLAT
-constexpr int kRecChunk = 512;  // flattened record slots staged in LDS at a time
+#ifndef WGSR_GBC_RECCHUNK
+#define WGSR_GBC_RECCHUNK 512
+#endif
+constexpr int kRecChunk = WGSR_GBC_RECCHUNK;  // flattened record slots staged in LDS at a time
 #endif
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
@@ -1567,6 +1586,27 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   if (nlive == 0) return;  // block-uniform
   __syncthreads();
+#if WGSR_GBC_PREFETCH
+  // every listed Gaussian's parameters (and a touch of its SH row's lines)
+  // loaded now, while the record sums below wait on their own round trips
+  GbPre pre[kGbcRounds];
+  uint32_t pcl[kGbcRounds];
+  float touch = 0.f;
+#pragma unroll
+  for (int r = 0; r < kGbcRounds; ++r) {
+    const uint32_t c = r * kGbcThreads + t;
+    const int i = c < nlive ? (int)s_list[c] : 0;
+    const size_t i3 = 3 * (size_t)i;
+    pre[r].mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+    pre[r].sv = cov_pre ? mk3(0.f, 0.f, 0.f) : mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
+    pre[r].q = cov_pre ? make_float4(1.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4*>(rots)[i];
+    pcl[r] = clamped[i];
+    if (o_sh) {
+      const float* row = shs + (size_t)i * (3 * M);
+      for (int k = 0; k < 3 * M; k += 32) touch += row[k];
+    }
+  }
+#endif
 #if WGSR_GBC_FLAT
   // record sums over the listed Gaussians' slots flattened into one list:
   // their slot ranges in one round trip, then kRecChunk slots at a time every
@@ -1695,15 +1735,28 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     // SH backward first: its dL/dmean term goes into gauss_bwd_one's single
     // store of the row (no read-modify-write of o_m3d behind its stores)
     f3 dm_sh = mk3(0.f, 0.f, 0.f);
+#if WGSR_GBC_PREFETCH && WGSR_GBC_FLAT
+    const bool hp = cov_pre == nullptr;
+    const GbPre pp = pre[r];
+    const f3 pmean = pre[r].mean;
+    const uint32_t pcb = pcl[r];
+#else
+    const bool hp = false;
+    const GbPre pp{};
+    const f3 pmean = mk3(means[3 * (size_t)i], means[3 * (size_t)i + 1], means[3 * (size_t)i + 2]);
+    const uint32_t pcb = clamped[i];
+#endif
     if (o_sh) {
-      const size_t i3 = 3 * (size_t)i, S = 3 * (size_t)M;
-      dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
-                          mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
-                          o_sh + (size_t)i * S);
+      const size_t S = 3 * (size_t)M;
+      dm_sh = sh_backward(D, M, shs + (size_t)i * S, pmean, mk3(campos_p[0], campos_p[1], campos_p[2]), pcb,
+                          mk3(g[6], g[7], g[8]), o_sh + (size_t)i * S);
     }
     gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, dm_sh, scale_mod, viewm, projm,
-                  praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
+                  praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau, hp, pp);
   }
+#if WGSR_GBC_PREFETCH
+  asm volatile("" ::"v"(touch));  // (the touch loads' only use: waited for here, at the end)
+#endif
 }
 
 // ---- view-sharded backward (wgsr/dp.py) ---------------------
