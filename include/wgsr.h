@@ -403,6 +403,18 @@ int wgsr_mlp_forward_dev_seed(int N, int C, const float* X, const float* W1, con
 /* keys[i] = 31-bit hash of (seed, i), i < n (seed_dev, when not NULL, holds
  * the seed): sorting the keys gives the DINO term's random sample order. */
 int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t* keys, void* stream);
+/* perm[0..n) = the stable ascending order of wgsr_random_keys(n, seed) (the
+ * DINO term's sample draw) in two launches; keys: n words of scratch.
+ * n <= wgsr_random_perm_max(). */
+int64_t wgsr_random_perm_max(void);
+int wgsr_random_perm(int64_t n, uint32_t seed, const uint32_t* seed_dev, uint32_t* keys, int32_t* perm,
+                     void* stream);
+/* wgsr_mlp_backward with dL_du scaled by du_scale, and with accumulate != 0
+ * the gradient ADDED to grad (a second backward into the same parameters,
+ * as autograd accumulates). */
+int wgsr_mlp_backward_acc(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                          const float* h1d, const float* h2d, const float* o_pre, const float* dL_du, float du_scale,
+                          int accumulate, float* scratch, float* grad, void* stream);
 int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
                       const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
                       float* scratch, float* grad, void* stream);
@@ -477,6 +489,31 @@ int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double 
  * used is grad + weight_decay * param (0: none). */
 int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
                        double weight_decay, const float* scalars, const uint32_t* skip, void* stream);
+
+/* ---- The graph-replayed mapping iteration (wgsr/online_graph.py) -------
+ * No reference counterpart: device-side steps that let one captured graph
+ * serve every keyframe (mapper.py:1083-1219 per iteration). */
+typedef struct wgsr_gather_job {
+  const void* src;            /* rows of src_stride_words 32-bit words       */
+  void* dst;                  /* nrows contiguous rows of row_words words    */
+  int64_t row_words;
+  int64_t src_stride_words;   /* >= row_words                                */
+  int32_t idx_offset;         /* row r of dst = src row idx[idx_offset + r]  */
+  int32_t nrows;
+} wgsr_gather_job;
+#define WGSR_GATHER_MAX_JOBS 8
+/* Every job's rows in one launch (the chosen keyframe's image, depth,
+ * features, camera, median depth and exposure, its neighbours' features). */
+int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, void* stream);
+/* The keyframe exposure optimiser's step (torch.optim.Adam arithmetic, as
+ * wgsr_adam_step) on row idx[0] of bank [K][3][2] = (a, b), exp_avg,
+ * exp_avg_sq, with grad [2] and scalars = (step_size, sqrt(1 - beta2^n));
+ * skipped when *skip_a or *skip_b is non-zero.  With sticky and counts (the
+ * capacity-mode forward's, or NULL): sticky[0] += counts[3], sticky[1] =
+ * max(sticky[1], counts[0]). */
+int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, const float* scalars,
+                       const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
+                       int64_t* sticky, const uint32_t* counts, void* stream);
 
 /* One row-major tensor for row compaction: rows of `row_bytes` (a multiple
  * of 4) from `src` [P rows]; `dst` receives the kept rows in order. */

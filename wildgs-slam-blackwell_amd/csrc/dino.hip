@@ -32,9 +32,10 @@ constexpr int kSimK = 32;     // feature-dimension chunk staged in LDS
 
 // one wave per row: fn[i] = x[i] / max(||x[i]||, 1e-12)
 __global__ __launch_bounds__(256) void k_dino_normalize(const float* __restrict__ x, int N, int C,
-                                                        float* __restrict__ fn) {
+                                                        float* __restrict__ fn, float* __restrict__ grad_u) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= N) return;
+  if (lane == 0) grad_u[i] = 0.f;  // (k_dino_select adds into it: no memset launch)
   const float* xi = x + (size_t)i * C;
   float ss = 0.f;
   for (int c = lane; c < C; c += 64) ss = fmaf(xi[c], xi[c], ss);
@@ -69,6 +70,59 @@ __global__ __launch_bounds__(256) void k_dino_similarity(const float* __restrict
       acc[1][1] = fmaf(a1, b1, acc[1][1]);
     }
     __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int i = i0 + 2 * ty + a, j = j0 + 2 * tx + b;
+      if (i < N && j < N) S[(size_t)i * N + j] = acc[a][b];
+    }
+}
+
+// The same tiles with both 32-row operand blocks streamed into LDS ONCE, over
+// the whole feature dimension (LDS-DMA, 16 B per lane, every load in flight
+// at once) instead of 12 dependent chunk rounds; float4 chunk k4 of row r
+// sits at k4 ^ ((r >> 1) & 15) so that the 16 column rows 2 tx a wave reads
+// at one k land on distinct banks.  Same products in the same k order:
+// bit-identical to k_dino_similarity.  C % 64 == 0, C <= 384 (96 KB of LDS).
+constexpr int kSim2MaxC = 384;
+__global__ __launch_bounds__(256) void k_dino_similarity2(const float* __restrict__ fn, int N, int C,
+                                                          float* __restrict__ S) {
+  extern __shared__ float4 s_sim[];  // [2][32][C / 4]
+  const int t = threadIdx.x, tx = t & 15, ty = t >> 4, w = t >> 6, lane = t & 63;
+  const int i0 = blockIdx.y * kSimTile, j0 = blockIdx.x * kSimTile, C4 = C >> 2;
+  float4* const sa = s_sim;
+  float4* const sb = s_sim + kSimTile * C4;
+  {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const float4* src = reinterpret_cast<const float4*>(fn);
+    const int per_op = kSimTile * C4;  // float4 slots per operand (a multiple of 64 when C % 8 == 0)
+    for (int b = 64 * w; b < 2 * per_op; b += 256) {  // (uniform) 64 slots per DMA instruction
+      const int sl = b + lane;
+      const int op = sl >= per_op, s2 = sl - op * per_op, r = s2 / C4, k4 = s2 - r * C4;
+      const int row = min((op ? j0 : i0) + r, N - 1);  // rows past N: a valid row, never stored
+      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)row * C4 + (k4 ^ ((r >> 1) & 15))),
+                                       (lds_ptr)(s_sim + b), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  __syncthreads();
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  const int ra = 2 * ty, rb = 2 * tx;
+  const int za = ty & 15, zb = tx & 15;  // (r >> 1) & 15 of rows 2 ty (+1) and 2 tx (+1)
+  for (int k4 = 0; k4 < C4; ++k4) {
+    const float4 a0 = sa[ra * C4 + (k4 ^ za)], a1 = sa[(ra + 1) * C4 + (k4 ^ za)];
+    const float4 b0 = sb[rb * C4 + (k4 ^ zb)], b1 = sb[(rb + 1) * C4 + (k4 ^ zb)];
+    const float av0[4] = {a0.x, a0.y, a0.z, a0.w}, av1[4] = {a1.x, a1.y, a1.z, a1.w};
+    const float bv0[4] = {b0.x, b0.y, b0.z, b0.w}, bv1[4] = {b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[0][0] = fmaf(av0[q], bv0[q], acc[0][0]);
+      acc[0][1] = fmaf(av0[q], bv1[q], acc[0][1]);
+      acc[1][0] = fmaf(av1[q], bv0[q], acc[1][0]);
+      acc[1][1] = fmaf(av1[q], bv1[q], acc[1][1]);
+    }
   }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -202,15 +256,17 @@ int wgsr_dino_reg(const float* u, const float* feat, int N, int C, int top_k, fl
     return set_error(WGSR_EINVAL, "wgsr_dino_reg: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int K = top_k < N ? top_k : N;
-  hipError_t e = hipMemsetAsync(grad_u, 0, sizeof(float) * (size_t)N, s);
-  if (e != hipSuccess) return set_error(WGSR_EHIP, "wgsr_dino_reg: %s", hipGetErrorString(e));
   const unsigned rows4 = (unsigned)((N + 3) / 4), tiles = (unsigned)((N + kSimTile - 1) / kSimTile);
-  hipLaunchKernelGGL(k_dino_normalize, dim3(rows4), dim3(256), 0, s, feat, N, C, fn_scratch);
-  hipLaunchKernelGGL(k_dino_similarity, dim3(tiles, tiles), dim3(256), 0, s, fn_scratch, N, C, sim_scratch);
+  hipLaunchKernelGGL(k_dino_normalize, dim3(rows4), dim3(256), 0, s, feat, N, C, fn_scratch, grad_u);
+  if (C % 64 == 0 && C <= kSim2MaxC)  // (fn_scratch: a 16-byte aligned caller buffer)
+    hipLaunchKernelGGL(k_dino_similarity2, dim3(tiles, tiles), dim3(256), sizeof(float) * 2 * kSimTile * (size_t)C, s,
+                       fn_scratch, N, C, sim_scratch);
+  else
+    hipLaunchKernelGGL(k_dino_similarity, dim3(tiles, tiles), dim3(256), 0, s, fn_scratch, N, C, sim_scratch);
   hipLaunchKernelGGL(k_dino_select, dim3(rows4), dim3(256), 0, s, sim_scratch, u, N, K, thresh, eps,
                      1.f / (float)N, row_var, grad_u);
   hipLaunchKernelGGL(k_dino_mean, dim3(1), dim3(256), 0, s, row_var, N, loss);
-  e = hipGetLastError();
+  const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_dino_reg: %s", hipGetErrorString(e));
 }
 

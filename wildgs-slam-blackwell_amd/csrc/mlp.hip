@@ -19,6 +19,8 @@
 // Dropout masks come from a counter hash of (seed, layer, row, column) -- the
 // same draw in forward and backward, and reproducible from the seed
 // (wgsr/mlp.py restates it for the tests).  Everything is fp32.
+#include <stdlib.h>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -134,6 +136,121 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __re
   }
 }
 
+// Few rows (the mapper's 27 x 36 feature map, the DINO term's ~300
+// samples): 16 rows per workgroup with the whole of W1, the rows' C
+// features and W2 streamed into LDS in ONE round of LDS-DMA loads
+// (global_load_lds, 16 B per lane: no staging registers, every load in
+// flight at once -- instead of a K-slab loop of dependent load -> barrier ->
+// multiply-add steps), then layer 1 as C/4 steps of four k with b128 LDS
+// reads (each wave's four rows broadcast; lane c reads row c of W1, whose
+// float4 chunks are XOR-swizzled by c mod 16 so the 16 lanes of every b128
+// pass hit distinct banks), layers 2 and 3 from LDS.  Same sums in the same
+// k order as k_mlp_fwd: bit-identical outputs.
+constexpr int kSmallRows = 16;
+__host__ __device__ inline size_t mlp_small_lds(int C) {
+  return sizeof(float) * ((size_t)(kHid + kSmallRows) * C + (size_t)kHid * kHid + (size_t)kSmallRows * 68);
+}
+template <int kC>
+__global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __restrict__ X,
+                                                       const float* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ W2, const float* __restrict__ b2,
+                                                       const float* __restrict__ W3, const float* __restrict__ b3,
+                                                       float p, uint32_t seed, const uint32_t* __restrict__ seed_dev,
+                                                       float* __restrict__ h1d, float* __restrict__ h2d,
+                                                       float* __restrict__ o_pre, float* __restrict__ u) {
+  constexpr int C4 = kC / 4;  // float4s per row
+  extern __shared__ float4 s_mlp4[];
+  float4* const sW = s_mlp4;                       // [64][C4], chunk k4 of row c at k4 ^ (c & 15)
+  float4* const sX = sW + kHid * C4;               // [16][C4]
+  float4* const sW2 = sX + kSmallRows * C4;        // [64][16], swizzled as sW
+  float* const sH = reinterpret_cast<float*>(sW2 + kHid * 16);  // [16][68] layer inputs
+  if (seed_dev) seed = *seed_dev;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, col = t & 63, rq = t >> 6;
+  const int r0 = blockIdx.x * kSmallRows;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const float4* W1v = reinterpret_cast<const float4*>(W1);
+    const float4* W2v = reinterpret_cast<const float4*>(W2);
+    const float4* Xv = reinterpret_cast<const float4*>(X);
+    constexpr int NW1 = kHid * C4 / 256, NX = kSmallRows * C4 / 256, NW2 = kHid * 16 / 256;
+    static_assert(NW1 * 256 == kHid * C4 && NX * 256 == kSmallRows * C4, "C: a multiple of 64");
+#pragma unroll
+    for (int q = 0; q < NW1; ++q) {  // wave w fills slots [(w NW1 + q) 64, +64)
+      const int sl = (w * NW1 + q) * 64 + lane, c = sl / C4, k4 = sl - c * C4;
+      __builtin_amdgcn_global_load_lds((const void*)(W1v + c * C4 + (k4 ^ (c & 15))),
+                                       (lds_ptr)(sW + (w * NW1 + q) * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NX; ++q) {  // rows past N re-read row N - 1 (their outputs are not stored)
+      const int sl = (w * NX + q) * 64 + lane, r = sl / C4, k4 = sl - r * C4;
+      __builtin_amdgcn_global_load_lds((const void*)(Xv + (size_t)min(r0 + r, N - 1) * C4 + k4),
+                                       (lds_ptr)(sX + (w * NX + q) * 64), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NW2; ++q) {
+      const int sl = (w * NW2 + q) * 64 + lane, c = sl >> 4, k4 = sl & 15;
+      __builtin_amdgcn_global_load_lds((const void*)(W2v + c * 16 + (k4 ^ (c & 15))),
+                                       (lds_ptr)(sW2 + (w * NW2 + q) * 64), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // (this wave's DMA has landed; the barrier covers the others)
+  }
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int sw = col & 15;
+#pragma unroll 4
+  for (int k4 = 0; k4 < C4; ++k4) {
+    const float4 b = sW[col * C4 + (k4 ^ sw)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 a = sX[(4 * rq + i) * C4 + k4];
+      acc[i] = fmaf(a.x, b.x, acc[i]);
+      acc[i] = fmaf(a.y, b.y, acc[i]);
+      acc[i] = fmaf(a.z, b.z, acc[i]);
+      acc[i] = fmaf(a.w, b.w, acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * rq + i;
+    float v = fmaxf(acc[i] + b1[col], 0.f);
+    v = keep_elem(seed, 0, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
+    sH[r * 68 + col] = v;
+    if (r0 + r < N) h1d[(size_t)(r0 + r) * kHid + col] = v;
+    acc[i] = 0.f;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int k4 = 0; k4 < 16; ++k4) {
+    const float4 b = sW2[col * 16 + (k4 ^ sw)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 a = *reinterpret_cast<const float4*>(&sH[(4 * rq + i) * 68 + 4 * k4]);
+      acc[i] = fmaf(a.x, b.x, acc[i]);
+      acc[i] = fmaf(a.y, b.y, acc[i]);
+      acc[i] = fmaf(a.z, b.z, acc[i]);
+      acc[i] = fmaf(a.w, b.w, acc[i]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * rq + i;
+    float v = fmaxf(acc[i] + b2[col], 0.f);
+    v = keep_elem(seed, 1, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
+    sH[r * 68 + col] = v;  // layer-3 input
+    if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + col] = v;
+  }
+  __syncthreads();
+  if (t < kSmallRows && r0 + t < N) {
+    float o = 0.f;
+    for (int k = 0; k < kHid; ++k) o = fmaf(sH[t * 68 + k], W3[k], o);
+    o += b3[0];
+    o_pre[r0 + t] = o;
+    u[r0 + t] = o > 20.f ? o : log1pf(expf(o));  // nn.Softplus(beta 1, threshold 20)
+  }
+}
+
 // partial layout per workgroup: dW1 [64][C] | db1 [64] | dW2 [64][64] | db2 [64] | dW3 [64] | db3
 __host__ __device__ inline int mlp_partial_floats(int C) { return kHid * C + kHid + kHid * kHid + kHid + kHid + 1; }
 
@@ -141,7 +258,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
                                                  const float* __restrict__ W2, const float* __restrict__ W3, float p,
                                                  const float* __restrict__ h1d, const float* __restrict__ h2d,
                                                  const float* __restrict__ o_pre, const float* __restrict__ du,
-                                                 float* __restrict__ part) {
+                                                 float* __restrict__ part, float du_scale) {
   __shared__ float sH1[64][kLd], sDA2[64][kLd], sDA1[64][kLd], sT[64][kLd];
   __shared__ float sDo[kRows];
   const int t = threadIdx.x, ty = t >> 4, tx = t & 15;
@@ -157,7 +274,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   if (t < kRows) {
     float d = 0.f;
     if (r0 + t < N) {
-      const float o = o_pre[r0 + t], g = du[r0 + t];
+      const float o = o_pre[r0 + t], g = du[r0 + t] * du_scale;
       const float z = expf(o);
       d = o > 20.f ? g : g * z / (z + 1.f);  // softplus backward
     }
@@ -254,27 +371,164 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
   }
 }
 
+// k_mlp_bwd with every global load issued up front: the kept activations,
+// W2 and the X slab stream into LDS in their natural row-major layouts by
+// LDS-DMA (no staging registers, one round trip instead of three), and the
+// products read those operands as [k][column] (one b128 read per k, lanes
+// on consecutive columns).  Rows past N re-read row N - 1 (finite) and get a
+// zero upstream gradient, so they add nothing.  Same products summed in the
+// same order as k_mlp_bwd: bit-identical partials.
+__device__ __forceinline__ void tile_mac_kc(const float (*A)[kLd], const float* __restrict__ Bt, int ty, int tx,
+                                            float (&acc)[4][4]) {
+#pragma unroll 8
+  for (int k = 0; k < 64; ++k) {
+    float a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][k];
+    const float4 b4 = *reinterpret_cast<const float4*>(&Bt[k * 64 + tx * 4]);
+    const float b[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __restrict__ X,
+                                                  const float* __restrict__ W2, const float* __restrict__ W3, float p,
+                                                  const float* __restrict__ h1d, const float* __restrict__ h2d,
+                                                  const float* __restrict__ o_pre, const float* __restrict__ du,
+                                                  float* __restrict__ part, float du_scale) {
+  __shared__ float4 sH1v[1024], sH2v[1024], sW2v[1024], sXv[1024];  // [64][64] each, natural layouts
+  __shared__ float sA[64][kLd], sB[64][kLd];
+  __shared__ float sDo[kRows];
+  const float* const sH1 = reinterpret_cast<const float*>(sH1v);
+  const float* const sH2 = reinterpret_cast<const float*>(sH2v);
+  const float* const sW2 = reinterpret_cast<const float*>(sW2v);
+  const float* const sX = reinterpret_cast<const float*>(sXv);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, ty = t >> 4, tx = t & 15;
+  const int r0 = blockIdx.x * kRows, c0 = 64 * (int)blockIdx.y;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  float o = 0.f, g = 0.f;
+  if (t < kRows && r0 + t < N) {
+    o = o_pre[r0 + t];
+    g = du[r0 + t] * du_scale;
+  }
+  {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const int C4 = C >> 2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // wave w fills float4 slots [(4 w + q) 64, +64): row sl / 16, chunk sl % 16
+      const int sl = (4 * w + q) * 64 + lane, row = min(r0 + (sl >> 4), N - 1), c4 = sl & 15;
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(h1d) + (size_t)row * 16 + c4),
+                                       (lds_ptr)(sH1v + (4 * w + q) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(h2d) + (size_t)row * 16 + c4),
+                                       (lds_ptr)(sH2v + (4 * w + q) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(W2) + sl),
+                                       (lds_ptr)(sW2v + (4 * w + q) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(reinterpret_cast<const float4*>(X) + (size_t)row * C4 + (c0 >> 2) + c4),
+          (lds_ptr)(sXv + (4 * w + q) * 64), 16, 0, 0);
+    }
+  }
+  float* out = part + (size_t)blockIdx.x * mlp_partial_floats(C);
+  float* gW1 = out;
+  float* gb1 = gW1 + kHid * C;
+  float* gW2 = gb1 + kHid;
+  float* gb2 = gW2 + kHid * kHid;
+  float* gW3 = gb2 + kHid;
+  float* gb3 = gW3 + kHid;
+  if (t < kRows) {
+    float d = 0.f;
+    if (r0 + t < N) {
+      const float z = expf(o);
+      d = o > 20.f ? g : g * z / (z + 1.f);  // softplus backward
+    }
+    sDo[t] = d;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (the barrier covers the others)
+  __syncthreads();
+  const bool head = blockIdx.y == 0;  // writes the non-dW1 gradients
+  if (head && t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s = fmaf(sDo[r], sH2[r * 64 + t], s);
+    gW3[t] = s;
+  } else if (head && t == kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sDo[r];
+    gb3[0] = s;
+  }
+  // dA2 = do W3 through ReLU / dropout: sA[r][o], and transposed sB[o][r]
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    const float v = sH2[r * 64 + c] > 0.f ? sDo[r] * W3[c] * scale : 0.f;
+    sA[r][c] = v;
+    sB[c][r] = v;
+  }
+  __syncthreads();
+  if (head) {  // dW2[o][i] = sum_r dA2[r][o] h1[r][i]
+    float acc[4][4] = {};
+    tile_mac_kc(sB, sH1, ty, tx, acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
+  }
+  if (head && t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sA[r][t];
+    gb2[t] = s;
+  }
+  // dA1[r][i] = sum_o dA2[r][o] W2[o][i] through ReLU / dropout, into sB as [i][r]
+  float acc1[4][4] = {};
+  tile_mac_kc(sA, sW2, ty, tx, acc1);
+  __syncthreads();  // (every wave is done reading sB as dA2 transposed)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = ty * 4 + i, c = tx * 4 + j;
+      sB[c][r] = sH1[r * 64 + c] > 0.f ? acc1[i][j] * scale : 0.f;
+    }
+  __syncthreads();
+  if (head && t < kHid) {
+    float s = 0.f;
+    for (int r = 0; r < kRows; ++r) s += sB[t][r];
+    gb1[t] = s;
+  }
+  // this workgroup's 64-column chunk of dW1[o][c] = sum_r dA1[r][o] X[r][c]
+  float acc[4][4] = {};
+  tile_mac_kc(sB, sX, ty, tx, acc);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gW1[(size_t)(ty * 4 + i) * C + c0 + tx * 4 + j] = acc[i][j];
+}
+
 // two-stage fixed-order sum over the row blocks' partials: grid.y segments of
 // kSeg blocks each write a segment sum (stage 1), then stage 2 adds the
 // segments in order
 constexpr int kSeg = 16;
+// (acc: the final sums are added to what `seg` / `grad` holds -- a second
+// backward accumulating into the first one's gradient, as autograd does)
 __global__ __launch_bounds__(256) void k_mlp_reduce_seg(int nblocks, int total, const float* __restrict__ part,
-                                                        float* __restrict__ seg) {
+                                                        float* __restrict__ seg, int acc) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   const int b0 = blockIdx.y * kSeg, b1 = min(nblocks, b0 + kSeg);
   float s = 0.f;
   for (int b = b0; b < b1; ++b) s += part[(size_t)b * total + e];
-  seg[(size_t)blockIdx.y * total + e] = s;
+  float* d = &seg[(size_t)blockIdx.y * total + e];
+  *d = acc ? *d + s : s;
 }
 
 __global__ __launch_bounds__(256) void k_mlp_reduce(int nseg, int total, const float* __restrict__ seg,
-                                                    float* __restrict__ grad) {
+                                                    float* __restrict__ grad, int acc) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
   float s = 0.f;
   for (int b = 0; b < nseg; ++b) s += seg[(size_t)b * total + e];
-  grad[e] = s;
+  grad[e] = acc ? grad[e] + s : s;
 }
 
 }  // namespace
@@ -317,7 +571,17 @@ static int mlp_forward_impl(int N, int C, const float* X, const float* W1, const
   if (N == 0) return WGSR_OK;
   if (!X || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !h1d || !h2d || !o_pre || !u)
     return set_error(WGSR_EINVAL, "wgsr_mlp_forward: null pointer");
-  if ((N + 63) / 64 >= 1024)  // enough 64-row workgroups to fill the chip
+  static const bool small_off = [] {
+    const char* e = getenv("WGSR_MLP_SMALL");
+    return e && atoi(e) == 0;
+  }();
+  if (!small_off && (N + 63) / 64 < 1024 && (C == 64 || C == 128 || C == 256 || C == 384) &&
+      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W1) | reinterpret_cast<uintptr_t>(W2)) & 15) == 0) {
+    auto kern = C == 384 ? k_mlp_fwd_small<384> : C == 256 ? k_mlp_fwd_small<256>
+              : C == 128 ? k_mlp_fwd_small<128> : k_mlp_fwd_small<64>;
+    hipLaunchKernelGGL(kern, dim3((N + kSmallRows - 1) / kSmallRows), dim3(256), mlp_small_lds(C), (hipStream_t)stream,
+                       N, X, W1, b1, W2, b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
+  } else if ((N + 63) / 64 >= 1024)  // enough 64-row workgroups to fill the chip
     hipLaunchKernelGGL(k_mlp_fwd<64>, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
                        b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
   else
@@ -340,6 +604,21 @@ int wgsr_mlp_forward_dev_seed(int N, int C, const float* X, const float* W1, con
   return mlp_forward_impl(N, C, X, W1, b1, W2, b2, W3, b3, dropout_p, 0u, seed, h1d, h2d, o_pre, u, stream);
 }
 
+int64_t wgsr_random_perm_max(void) { return (int64_t)argsort_small_max(); }
+
+int wgsr_random_perm(int64_t n, uint32_t seed, const uint32_t* seed_dev, uint32_t* keys, int32_t* perm,
+                     void* stream) {
+  if (n < 0 || n > (int64_t)argsort_small_max() || (n > 0 && (!keys || !perm)))
+    return set_error(WGSR_EINVAL, "wgsr_random_perm: 0 <= n <= %u and buffers required", argsort_small_max());
+  if (n == 0) return WGSR_OK;
+  hipLaunchKernelGGL(k_random_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, seed,
+                     seed_dev, reinterpret_cast<int32_t*>(keys));
+  const hipError_t e = launch_argsort_small(keys, (uint32_t)n, reinterpret_cast<uint32_t*>(perm), (hipStream_t)stream);
+  if (e != hipSuccess) return set_error(WGSR_EHIP, "wgsr_random_perm: %s", hipGetErrorString(e));
+  MLPCHK("wgsr_random_perm");
+  return WGSR_OK;
+}
+
 int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t* keys, void* stream) {
   if (n < 0 || (n > 0 && !keys)) return set_error(WGSR_EINVAL, "wgsr_random_keys: bad arguments");
   if (n == 0) return WGSR_OK;
@@ -349,26 +628,56 @@ int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t
   return WGSR_OK;
 }
 
-int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
-                      const float* h1d, const float* h2d, const float* o_pre, const float* dL_du, float* scratch,
-                      float* grad, void* stream) {
+static int mlp_backward_impl(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                             const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
+                             float du_scale, int accumulate, float* scratch, float* grad, void* stream) {
   if (N < 0 || C <= 0 || C % 64 != 0) return set_error(WGSR_EINVAL, "wgsr_mlp_backward: C must be a positive multiple of 64");
   const int total = mlp_partial_floats(C);
-  if (N == 0) return hipMemsetAsync(grad, 0, sizeof(float) * total, (hipStream_t)stream) == hipSuccess
-                         ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_mlp_backward: memset");
+  if (N == 0) {
+    if (accumulate) return WGSR_OK;
+    return hipMemsetAsync(grad, 0, sizeof(float) * total, (hipStream_t)stream) == hipSuccess
+               ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_mlp_backward: memset");
+  }
   if (!X || !W2 || !W3 || !h1d || !h2d || !o_pre || !dL_du || !scratch || !grad)
     return set_error(WGSR_EINVAL, "wgsr_mlp_backward: null pointer");
   const int nb = (N + kRows - 1) / kRows;
-  hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p, h1d,
-                     h2d, o_pre, dL_du, scratch);
+  static const bool bwd1 = [] {
+    const char* e = getenv("WGSR_MLP_BWD");
+    return e && atoi(e) == 1;
+  }();
+  const bool aligned = ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W2) |
+                         reinterpret_cast<uintptr_t>(h1d) | reinterpret_cast<uintptr_t>(h2d)) & 15) == 0;
+  // (one workgroup per CU: the few-row grids of the mapper only)
+  if (!bwd1 && aligned && (size_t)nb * (C / 64) <= 1024)
+    hipLaunchKernelGGL(k_mlp_bwd2, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p,
+                       h1d, h2d, o_pre, dL_du, scratch, du_scale);
+  else
+    hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p,
+                       h1d, h2d, o_pre, dL_du, scratch, du_scale);
   const int nseg = (nb + kSeg - 1) / kSeg;
-  float* seg = scratch + (size_t)nb * total;
+  // one segment (<= 16 row blocks: the mapper's feature maps): its sum is
+  // the gradient -- the second stage would be a copy
+  float* seg = nseg == 1 ? grad : scratch + (size_t)nb * total;
   hipLaunchKernelGGL(k_mlp_reduce_seg, dim3((total + 255) / 256, nseg), dim3(256), 0, (hipStream_t)stream, nb, total,
-                     scratch, seg);
-  hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nseg, total, seg,
-                     grad);
+                     scratch, seg, nseg == 1 ? accumulate : 0);
+  if (nseg > 1)
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nseg, total, seg,
+                       grad, accumulate);
   MLPCHK("wgsr_mlp_backward");
   return WGSR_OK;
+}
+
+int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                      const float* h1d, const float* h2d, const float* o_pre, const float* dL_du, float* scratch,
+                      float* grad, void* stream) {
+  return mlp_backward_impl(N, C, X, W2, W3, dropout_p, h1d, h2d, o_pre, dL_du, 1.f, 0, scratch, grad, stream);
+}
+
+int wgsr_mlp_backward_acc(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
+                          const float* h1d, const float* h2d, const float* o_pre, const float* dL_du, float du_scale,
+                          int accumulate, float* scratch, float* grad, void* stream) {
+  return mlp_backward_impl(N, C, X, W2, W3, dropout_p, h1d, h2d, o_pre, dL_du, du_scale, accumulate, scratch, grad,
+                           stream);
 }
 
 }  // extern "C"

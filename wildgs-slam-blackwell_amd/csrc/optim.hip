@@ -233,6 +233,62 @@ __global__ __launch_bounds__(256) void k_compact_gather(const uint8_t* __restric
   }
 }
 
+// ---- the graph-replayed mapping iteration's small steps (wgsr/online_graph.py) --
+constexpr int kGatherMax = WGSR_GATHER_MAX_JOBS;
+struct GatherBatch {
+  wgsr_gather_job j[kGatherMax];
+  int64_t ustart[kGatherMax + 1];  // first unit of each job (units: 4 words when vec, else 1)
+  bool vec[kGatherMax];
+  int n;
+  const int64_t* idx;
+};
+// dst rows r of job k = src row idx[idx_offset + r] (every job in one launch)
+__global__ __launch_bounds__(256) void k_gather_rows(GatherBatch b) {
+  const int64_t units = b.ustart[b.n];
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < units; u += (int64_t)gridDim.x * 256) {
+    int k = 0;
+    while (k + 1 < b.n && u >= b.ustart[k + 1]) ++k;
+    const wgsr_gather_job& J = b.j[k];
+    const int64_t v = u - b.ustart[k];
+    if (b.vec[k]) {
+      const int64_t per = J.row_words / 4, r = v / per, c = v - r * per;
+      const int64_t sr = b.idx[J.idx_offset + r];
+      reinterpret_cast<uint4*>(J.dst)[r * per + c] =
+          reinterpret_cast<const uint4*>(J.src)[sr * (J.src_stride_words / 4) + c];
+    } else {
+      const int64_t r = v / J.row_words, c = v - r * J.row_words;
+      const int64_t sr = b.idx[J.idx_offset + r];
+      static_cast<uint32_t*>(J.dst)[r * J.row_words + c] =
+          static_cast<const uint32_t*>(J.src)[sr * J.src_stride_words + c];
+    }
+  }
+}
+
+// One keyframe exposure step on its bank row (Adam, torch arithmetic as
+// k_adam_multi) unless either skip word is set, plus the overflow
+// bookkeeping of the capacity-mode forward: sticky[0] += counts[3],
+// sticky[1] = max(sticky[1], counts[0]).
+__global__ __launch_bounds__(64) void k_exposure_step(float* __restrict__ bank, const int64_t* __restrict__ idx,
+                                                      const float* __restrict__ grad, const float* __restrict__ sc,
+                                                      const uint32_t* __restrict__ skip_a,
+                                                      const uint32_t* __restrict__ skip_b, float w1, float beta2,
+                                                      float w2, float eps, long long* __restrict__ sticky,
+                                                      const uint32_t* __restrict__ counts) {
+  const int l = threadIdx.x;
+  if (l < 2 && !(*skip_a | *skip_b)) {
+    float* row = bank + 6 * idx[0];  // (a, b), exp_avg (a, b), exp_avg_sq (a, b)
+    float p = row[l], m = row[2 + l], v = row[4 + l];
+    adam_elem(p, grad[l], m, v, w1, beta2, w2, eps, -sc[0], sc[1]);
+    row[l] = p;
+    row[2 + l] = m;
+    row[4 + l] = v;
+  }
+  if (l == 0 && sticky && counts) {
+    sticky[0] += (long long)counts[3];
+    sticky[1] = max(sticky[1], (long long)counts[0]);
+  }
+}
+
 }  // namespace
 
 }  // namespace wgsr
@@ -277,6 +333,43 @@ int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, dou
                        double weight_decay, const float* scalars, const uint32_t* skip, void* stream) {
   if (!scalars) return set_error(WGSR_EINVAL, "wgsr_adam_step_dev: missing device scalars");
   return adam_step_impl(tensors, n, beta1, beta2, eps, weight_decay, scalars, skip, stream);
+}
+
+int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, void* stream) {
+  if (n < 0 || n > kGatherMax || (n > 0 && (!jobs || !idx)))
+    return set_error(WGSR_EINVAL, "wgsr_gather_rows: 0..%d jobs and an index array", kGatherMax);
+  GatherBatch b{};
+  b.n = n;
+  b.idx = idx;
+  b.ustart[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    const wgsr_gather_job& J = jobs[k];
+    if (J.nrows < 0 || J.row_words < 0 || J.src_stride_words < J.row_words || J.idx_offset < 0 ||
+        (J.nrows > 0 && J.row_words > 0 && (!J.src || !J.dst)))
+      return set_error(WGSR_EINVAL, "wgsr_gather_rows: job %d is malformed", k);
+    b.j[k] = J;
+    b.vec[k] = J.row_words % 4 == 0 && J.src_stride_words % 4 == 0 &&
+               ((reinterpret_cast<uintptr_t>(J.src) | reinterpret_cast<uintptr_t>(J.dst)) & 15) == 0;
+    b.ustart[k + 1] = b.ustart[k] + (int64_t)J.nrows * (b.vec[k] ? J.row_words / 4 : J.row_words);
+  }
+  const int64_t units = b.ustart[n];
+  if (units == 0) return WGSR_OK;
+  const int64_t blocks = std::min<int64_t>((units + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, b);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_gather_rows: %s", hipGetErrorString(e));
+}
+
+int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, const float* scalars,
+                       const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
+                       int64_t* sticky, const uint32_t* counts, void* stream) {
+  if (!bank || !idx || !grad || !scalars || !skip_a || !skip_b)
+    return set_error(WGSR_EINVAL, "wgsr_exposure_step: null pointer");
+  hipLaunchKernelGGL(k_exposure_step, dim3(1), dim3(64), 0, (hipStream_t)stream, bank, idx, grad, scalars, skip_a,
+                     skip_b, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     reinterpret_cast<long long*>(sticky), counts);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_exposure_step: %s", hipGetErrorString(e));
 }
 
 int wgsr_compact_rows(const uint8_t* keep, int64_t P, const wgsr_row_tensor* tensors, int n,

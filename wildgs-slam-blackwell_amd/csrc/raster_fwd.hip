@@ -1166,8 +1166,8 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     if (le < n) {
       const uint32_t q = pk[j] & kPosMask;
-      okeys[lo + le] = skeys[lo + q];
-      ogid[lo + le] = sgid[lo + q];
+      if (okeys) okeys[lo + le] = skeys[lo + q];  // (uniform; null: the stable argsort of k_argsort_small)
+      ogid[lo + le] = sgid ? sgid[lo + q] : q;
     }
   }
 }
@@ -1920,6 +1920,40 @@ hipError_t launch_expand_bins(const wgsr_raster_args& a, const uint32_t* sorted_
   }
   hipLaunchKernelGGL(k_expand_bins, dim3((uint32_t)B.n << bshift), dim3(kExpThreads), 0, s, sorted_keys, sorted_g, bounds, gx,
                      gy, bshift, B.bx, lists, ranges, tile_len, meta);
+  return hipGetLastError();
+}
+
+namespace {
+// Stable argsort of n <= kBdsCap 32-bit keys in one workgroup: the per-bin
+// depth sort's LDS passes on a single "bin" whose payload is the position
+// (ties keep index order).  perm[i] = the index of the i-th smallest key.
+__global__ __launch_bounds__(kBdsThreads) void k_argsort_small(const uint32_t* __restrict__ keys, uint32_t n,
+                                                              uint32_t* __restrict__ perm) {
+  __shared__ BdsLds L;
+  const int t = threadIdx.x;
+  const BdsEmit none{};
+#pragma unroll
+  for (int q = 0; q < kBdsWaves; ++q)
+    if (bds_owns_digit()) L.wcnt[q][t] = 0u;
+#if WGSR_BDS_LDSMATCH
+  for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
+#endif
+  if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
+    bds_small<1>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+  else if (n <= 2u * kBdsThreads)
+    bds_small<2>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+  else if (n <= 4u * kBdsThreads)
+    bds_small<4>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+  else
+    bds_small<kBdsItems>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+}
+}  // namespace
+
+uint32_t argsort_small_max() { return (uint32_t)kBdsCap; }
+hipError_t launch_argsort_small(const uint32_t* keys, uint32_t n, uint32_t* perm, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > (uint32_t)kBdsCap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_argsort_small, dim3(1), dim3(kBdsThreads), 0, s, keys, n, perm);
   return hipGetLastError();
 }
 

@@ -94,6 +94,9 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
 // beyond one LDS tile).  With lists: the per-tile exact lists, ranges,
 // tile_len and meta emitted straight from each sorted bin (what
 // launch_expand_bins would make of it); else the sorted bins -> okeys / ogid.
+// stable argsort of n <= argsort_small_max() keys in one workgroup (perm: positions)
+uint32_t argsort_small_max();
+hipError_t launch_argsort_small(const uint32_t* keys, uint32_t n, uint32_t* perm, hipStream_t s);
 hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
                                  uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
                                  uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s,

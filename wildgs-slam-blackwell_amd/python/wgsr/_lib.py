@@ -47,6 +47,16 @@ class AdamTensor(ctypes.Structure):
                 ("split_len", ctypes.c_int64), ("step_size_tail", ctypes.c_float)]
 
 
+class GatherJob(ctypes.Structure):
+    """Mirror of ``wgsr_gather_job``."""
+
+    _fields_ = [("src", _fp), ("dst", _fp), ("row_words", ctypes.c_int64), ("src_stride_words", ctypes.c_int64),
+                ("idx_offset", ctypes.c_int32), ("nrows", ctypes.c_int32)]
+
+
+GATHER_MAX_JOBS = 8
+
+
 class RowTensor(ctypes.Structure):
     """Mirror of ``wgsr_row_tensor``."""
 
@@ -205,6 +215,17 @@ def load():
         L.wgsr_mlp_forward_dev_seed.argtypes = [c_int, c_int] + [_fp] * 7 + [ctypes.c_float, _fp] + [_fp] * 4 + [_fp]
         L.wgsr_random_keys.restype = c_int
         L.wgsr_random_keys.argtypes = [c_i64, ctypes.c_uint32, _fp, _fp, _fp]
+        L.wgsr_random_perm_max.restype = c_i64
+        L.wgsr_random_perm_max.argtypes = []
+        L.wgsr_random_perm.restype = c_int
+        L.wgsr_random_perm.argtypes = [c_i64, ctypes.c_uint32, _fp, _fp, _fp, _fp]
+        L.wgsr_mlp_backward_acc.restype = c_int
+        L.wgsr_mlp_backward_acc.argtypes = ([c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 4
+                                            + [ctypes.c_float, c_int, _fp, _fp, _fp])
+        L.wgsr_gather_rows.restype = c_int
+        L.wgsr_gather_rows.argtypes = [ctypes.POINTER(GatherJob), c_int, _fp, _fp]
+        L.wgsr_exposure_step.restype = c_int
+        L.wgsr_exposure_step.argtypes = [_fp] * 6 + [ctypes.c_double] * 3 + [_fp, _fp, _fp]
         L.wgsr_mlp_backward.restype = c_int
         L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
         L.wgsr_dino_reg.restype = c_int
@@ -272,6 +293,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_version", "wgsr_depth_order_offset", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_adam_step_dev", "wgsr_compact_rows",
     "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
+    "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",

@@ -240,10 +240,10 @@ class MappingStep:
             cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
             self.D, cam["campos"], False, False)
 
-    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float):
+    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True):
         """Rasteriser backward straight into the gradient storage, activation
         backward (isotropic term folded in), densification statistics.
-        -> (dL/dmeans2D, dL/dtau summed over P)."""
+        -> (dL/dmeans2D, dL/dtau summed over P, or None without need_tau)."""
         from diff_gaussian_rasterization import _C
         L = _lib.load()
         dev = self.xyz.device
@@ -266,7 +266,7 @@ class MappingStep:
                 p(self.grad["scaling"]), p(self.grad["rotation"]), st))
             _lib.check(L.wgsr_densification_stats(self.P, p(radii), p(dL_dmeans2D), p(self.max_radii2D),
                                                   p(self.xyz_gradient_accum), p(self.denom), st))
-        return dL_dmeans2D, dL_dtau.sum(0)
+        return dL_dmeans2D, (dL_dtau.sum(0) if need_tau else None)
 
     def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
                          alpha: float = 0.95, lambda_dssim: float = 0.2, rgb_threshold: float = 0.01,
@@ -328,7 +328,7 @@ class MappingStep:
                                      train_frac: float, ssim_frac: float, config: dict | None = None,
                                      initialization: bool = False, freeze_uncertainty_loss: bool = False,
                                      median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True,
-                                     cap: int | None = None, counts=None):
+                                     cap: int | None = None, counts=None, need_tau: bool = True):
         """The reference's DEFAULT mapping iteration (uncertainty_params.activate):
         get_loss_mapping_uncertainty (slam_utils.py:146-258) + 10 * isotropic
         loss, and their backward.
@@ -369,10 +369,11 @@ class MappingStep:
                                      train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
                                      median_depth, extra=(self.iso_part, w_iso), pre_exposed=pre_exposed)
         d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state)
-        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso)
+        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso, need_tau)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:
             uncertainty.backward(d_unc.to(uncertainty.dtype))
-        return {"loss": loss, "dexposure_a": d_a, "dexposure_b": d_b, "drho": tau[:3], "dtheta": tau[3:],
+        return {"loss": loss, "dexposure_a": d_a, "dexposure_b": d_b,
+                "drho": tau[:3] if tau is not None else None, "dtheta": tau[3:] if tau is not None else None,
                 "radii": radii, "image": image, "depth": depth, "num_rendered": nr, "uncertainty_grad": d_unc,
                 "uncertainty_loss": state.uncertainty_loss}
 

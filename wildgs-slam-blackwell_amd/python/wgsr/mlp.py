@@ -120,19 +120,22 @@ def forward_raw(net, x, seed_dev):
     return u, (x, ws[2], ws[4], h1d, h2d, o, float(net.dropout_p))
 
 
-def backward_raw(saved, du):
+def backward_raw(saved, du, scale: float = 1.0, accumulate_into=None):
     """-> the flat parameter gradient (wgsr_mlp_grad_floats(C) floats, the
-    parameters' order) of a ``forward_raw`` for dL/du = du [N]."""
+    parameters' order) of a ``forward_raw`` for dL/du = scale * du [N]; with
+    ``accumulate_into`` (an earlier result) the gradient is added to it in
+    place (autograd's accumulation of a second backward) and it is returned."""
     x, W2, W3, h1d, h2d, o, p = saved
     N, C = x.shape
     dev = x.device
     L = _lib.load()
-    grad = torch.empty(int(L.wgsr_mlp_grad_floats(C)), device=dev)
+    grad = accumulate_into if accumulate_into is not None else torch.empty(int(L.wgsr_mlp_grad_floats(C)), device=dev)
     scratch = torch.empty(max(1, int(L.wgsr_mlp_scratch_bytes(N, C)) // 4), device=dev)
     pt = _lib.ptr
     with torch.cuda.device(dev):
-        _lib.check(L.wgsr_mlp_backward(N, C, pt(x), pt(W2), pt(W3), p, pt(h1d), pt(h2d), pt(o), pt(du), pt(scratch),
-                                       pt(grad), _lib.stream_handle(dev)))
+        _lib.check(L.wgsr_mlp_backward_acc(N, C, pt(x), pt(W2), pt(W3), p, pt(h1d), pt(h2d), pt(o), pt(du),
+                                           float(scale), int(accumulate_into is not None), pt(scratch), pt(grad),
+                                           _lib.stream_handle(dev)))
     return grad
 
 

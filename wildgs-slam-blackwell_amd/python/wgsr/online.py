@@ -315,6 +315,11 @@ class OnlineMapper:
         keys = torch.empty(n, dtype=torch.int32, device=self.dev)
         L = _lib.load()
         with torch.cuda.device(self.dev):
+            if n <= int(L.wgsr_random_perm_max()):  # one-workgroup stable sort (wgsr_random_perm)
+                perm = torch.empty(n, dtype=torch.int32, device=self.dev)
+                _lib.check(L.wgsr_random_perm(n, seed, None, _lib.ptr(keys), _lib.ptr(perm),
+                                              _lib.stream_handle(self.dev)))
+                return perm
             _lib.check(L.wgsr_random_keys(n, seed, None, _lib.ptr(keys), _lib.stream_handle(self.dev)))
         return torch.argsort(keys, stable=True)
 
@@ -348,13 +353,14 @@ class OnlineMapper:
                                                       [kf.features[::st, ::st]])).backward(retain_graph=True)
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, ea, eb, self.bg, unc,
                                                   c["train_frac_fix"], c["train_frac_fix"], initialization=True,
-                                                  median_depth=kf.median_depth)
+                                                  median_depth=kf.median_depth, need_tau=False)
         else:
             unc = self.net(kf.features)
             freeze = self.iterations_after_densify_or_reset < 20
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, ea, eb, self.bg, unc,
                                                   c["train_frac_fix"], c["train_frac_fix"],
-                                                  freeze_uncertainty_loss=freeze, median_depth=kf.median_depth)
+                                                  freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
+                                                  need_tau=False)
             if self.iterations_after_densify_or_reset >= 20:
                 self._dino_term(neighbours, kf)
         self._max_nr = max(self._max_nr, int(out["num_rendered"]))
@@ -516,7 +522,7 @@ class OnlineMapper:
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg,
                                                   unc, c["train_frac_fix"], c["train_frac_fix"],
                                                   freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
-                                                  pre_exposed=False)
+                                                  pre_exposed=False, need_tau=False)
             self._max_nr = max(self._max_nr, int(out["num_rendered"]))
             if self.iterations_after_densify_or_reset >= 200:
                 self._dino_term([stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))], kf)

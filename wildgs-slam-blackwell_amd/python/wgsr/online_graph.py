@@ -15,8 +15,8 @@ the DINO term on, the uncertainty loss not frozen -- is captured ONCE per
   index: every keyframe's image, depth, features, camera, median depth and
   exposure (+ its Adam moments) live in slot-indexed device banks
   (``KeyframeBank``; the Keyframe objects' tensors are views into them), and
-  the graph gathers the chosen slot's rows (index_select) and scatters the
-  exposure back;
+  the graph gathers the chosen slot's rows (one wgsr_gather_rows launch) and
+  steps the exposure on its bank row (wgsr_exposure_step);
 * the rasteriser runs in capacity mode (wgsr_rasterize_forward_cap): buffers
   sized for ``cap`` pairs, counts on the device, no host wait.  An overflow
   (more pairs than ``cap``) makes the iteration a no-op for every optimiser
@@ -40,6 +40,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 
 import numpy as np
 import torch
@@ -225,10 +226,14 @@ class IterationGraphs:
         self.graphs = {}
         self.key = None
         self.pool = None
+        self.stream = None
         self.cap = None
         self.S = None
         self.disabled = None  # reason string once disabled
-        self.stats = {"captures": 0, "replays": 0, "overflows": 0, "skipped_iterations": 0}
+        self.stats = {"captures": 0, "replays": 0, "overflows": 0, "skipped_iterations": 0, "capture_s": 0.0,
+                      "replay_call_s": 0.0, "step_host_s": 0.0}
+        # capacity = max(min_cap, cap_scale x the largest recent pair count + cap_margin)
+        self.min_cap, self.cap_scale, self.cap_margin = 1 << 16, 2.0, 4096
 
     # -- eligibility -----------------------------------------------------------
     def usable(self) -> bool:
@@ -262,12 +267,13 @@ class IterationGraphs:
         S.feat4 = torch.zeros(1, h, w, C, device=dev)
         S.cam2 = torch.zeros(1, CAM_FLOATS, device=dev)
         S.med = torch.zeros(1, device=dev)
-        S.ex = torch.zeros(1, 3, 2, device=dev)
+        S.ex = torch.zeros(2, device=dev)          # the keyframe's exposure (a, b)
         S.nbf = torch.zeros(5, h, w, C, device=dev)
+        S.keys = torch.zeros(5 * h * w, dtype=torch.int32, device=dev)
+        S.perm = torch.zeros(5 * h * w, dtype=torch.int32, device=dev)
         c = S.cam2[0]
         S.cam = dict(viewmatrix=c[0:16].view(4, 4), projmatrix=c[16:32].view(4, 4), projmatrix_raw=c[32:48].view(4, 4),
                      campos=c[48:51], tanfovx=B.tan[0], tanfovy=B.tan[1], image_height=H, image_width=W)
-        S.skip_ex = torch.zeros(1, dtype=torch.int32, device=dev)
         # the MLP optimiser's state must exist before a capture bakes its addresses in
         opt = m.uopt
         S.mlp_params = list(m.net.parameters())
@@ -284,6 +290,20 @@ class IterationGraphs:
         m.ms.iso_part  # noqa: B018  (allocated outside the capture)
         self.S = S
 
+    def _gather_jobs(self, nbc: int):
+        """wgsr_gather_rows jobs: the chosen slot's rows into the static
+        buffers, the neighbours' features (one launch)."""
+        B, S = self.m.bank, self.S
+        p = _lib.ptr
+
+        def job(bank, dst, off, n, words=None, stride=None):
+            rw = bank[0].numel() if words is None else words
+            return _lib.GatherJob(p(bank), p(dst), rw, rw if stride is None else stride, off, n)
+        jobs = [job(B.image, S.image4, 0, 1), job(B.depth, S.depth4, 0, 1), job(B.feat, S.feat4, 0, 1),
+                job(B.cam, S.cam2, 0, 1), job(B.med, S.med, 0, 1), job(B.ex, S.ex, 0, 1, words=2, stride=6),
+                job(B.feat, S.nbf, 1, nbc)]
+        return (_lib.GatherJob * len(jobs))(*jobs)
+
     def _body(self, nbc: int, refine: bool):
         """One mapping iteration's device work (captured; see the module doc)."""
         m, S = self.m, self.S
@@ -293,46 +313,44 @@ class IterationGraphs:
         st = _lib.stream_handle(dev)
         p = _lib.ptr
         H, W, h, w, C = B.shape
-        idx = self.i64[0:1]
-        torch.index_select(B.image, 0, idx, out=S.image4)
-        torch.index_select(B.depth, 0, idx, out=S.depth4)
-        torch.index_select(B.feat, 0, idx, out=S.feat4)
-        torch.index_select(B.cam, 0, idx, out=S.cam2)
-        torch.index_select(B.med, 0, idx, out=S.med)
-        torch.index_select(B.ex, 0, idx, out=S.ex)
-        torch.index_select(B.feat, 0, self.i64[1:1 + nbc], out=S.nbf[:nbc])
+        with torch.cuda.device(dev):
+            jobs = self._gather_jobs(nbc)
+            _lib.check(L.wgsr_gather_rows(jobs, len(jobs), p(self.i64), st))
         # the uncertainty MLP on the keyframe's features, the loss + rasteriser
         # forward/backward (capacity mode), the MLP backward of the loss
         u, sv = forward_raw(m.net, S.feat4.view(h * w, C), self.i32[0:1])
-        out = ms.forward_backward_uncertainty(S.cam, S.image4[0], S.depth4[0], S.ex[0, 0, 0:1], S.ex[0, 0, 1:2], m.bg,
+        out = ms.forward_backward_uncertainty(S.cam, S.image4[0], S.depth4[0], S.ex[0:1], S.ex[1:2], m.bg,
                                               u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
                                               freeze_uncertainty_loss=False, median_depth=S.med,
-                                              pre_exposed=not refine, cap=self.cap, counts=self.counts)
+                                              pre_exposed=not refine, cap=self.cap, counts=self.counts,
+                                              need_tau=False)
         G = backward_raw(sv, out["uncertainty_grad"].reshape(-1).contiguous())
         # the DINO term on features sampled from the neighbouring keyframes
+        # (reg_mult x its gradient accumulated into the MLP's)
         n = nbc * h * w
         ns = n // (c["reg_stride"] ** 4)
-        keys = torch.empty(n, dtype=torch.int32, device=dev)
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_random_keys(n, 0, p(self.i32[1:2]), p(keys), st))
-        perm = torch.argsort(keys, stable=True)[:ns]
+            if n <= int(L.wgsr_random_perm_max()):
+                _lib.check(L.wgsr_random_perm(n, 0, p(self.i32[1:2]), p(S.keys), p(S.perm), st))
+                perm = S.perm[:ns]
+            else:  # (large feature maps: the same keys, torch's stable sort)
+                _lib.check(L.wgsr_random_keys(n, 0, p(self.i32[1:2]), p(S.keys), st))
+                perm = torch.argsort(S.keys[:n], stable=True)[:ns]
         sf = S.nbf[:nbc].view(n, C).index_select(0, perm)
         u2, sv2 = forward_raw(m.net, sf, self.i32[2:3])
         _, gu = dino_reg_raw(u2, sf)
-        G = G + backward_raw(sv2, gu * float(c["reg_mult"]))
+        backward_raw(sv2, gu, scale=float(c["reg_mult"]), accumulate_into=G)
         skip = self.counts[3:4]
-        # Adam: the Gaussians, the keyframe's exposure (skipped unless the
-        # window optimiser holds it), the MLP (L2 weight decay)
+        # Adam: the Gaussians, the keyframe's exposure on its bank row (skipped
+        # unless the window optimiser holds it; also the overflow bookkeeping),
+        # the MLP (L2 weight decay)
         ms.optimizer_step_dev(ms.adam_tensors(), self.f32[self.F_GAUSS:self.F_GAUSS + 15], skip)
-        torch.maximum(skip, self.i32[self.F_EXSKIP:self.F_EXSKIP + 1], out=S.skip_ex)
         da, db = out["dexposure_a"], out["dexposure_b"]
         gex = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
-        exb = S.ex.data_ptr()
-        t = _lib.AdamTensor(exb, gex.data_ptr(), exb + 8, exb + 16, 2, 0.0, 1.0)
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, 0.0,
-                                            p(self.f32[self.F_EXPO:self.F_EXPO + 3]), p(S.skip_ex), st))
-        B.ex.index_copy_(0, idx, S.ex)
+            _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), p(self.f32[self.F_EXPO:self.F_EXPO + 2]),
+                                            p(skip), p(self.i32[self.F_EXSKIP:self.F_EXSKIP + 1]), 0.9, 0.999, 1e-8,
+                                            p(self.sticky), p(self.counts), st))
         ts, off = [], 0
         opt = m.uopt
         for prm in S.mlp_params:
@@ -345,42 +363,58 @@ class IterationGraphs:
             _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * len(ts))(*ts), len(ts), S.mlp_betas[0], S.mlp_betas[1],
                                             S.mlp_eps, S.mlp_wd, p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip),
                                             st))
-        # overflow bookkeeping, seen by the host through pinned memory
-        self.sticky[0:1] += skip.to(torch.int64)
-        torch.maximum(self.sticky[1:2], self.counts[0:1].to(torch.int64) & 0xFFFFFFFF, out=self.sticky[1:2])
+        # the overflow bookkeeping, seen by the host through pinned memory
         self.sticky_host.copy_(self.sticky, non_blocking=True)
 
     def _capture(self, nbc: int, refine: bool):
+        t0 = time.perf_counter()
+        try:
+            return self._capture_timed(nbc, refine)
+        finally:
+            self.stats["capture_s"] += time.perf_counter() - t0
+
+    def _capture_timed(self, nbc: int, refine: bool):
         if self.S is None:
             self._build_static()
-        torch.cuda.synchronize(self.dev)
+        # (capture_begin / capture_end directly: torch.cuda.graph's context
+        # also runs gc.collect() and empty_cache() per capture, tens of ms)
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(self.dev)
+        cur = torch.cuda.current_stream(self.dev)
+        self.stream.wait_stream(cur)
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g, pool=self.pool):
-                self._body(nbc, refine)
+            with torch.cuda.stream(self.stream):
+                g.capture_begin(pool=self.pool)
+                try:
+                    self._body(nbc, refine)
+                finally:
+                    g.capture_end()
         except Exception as e:  # e.g. a configuration the capacity-mode forward does not cover
             self.disabled = f"{type(e).__name__}: {e}"
             self.invalidate()
             return None
-        if self.pool is None:
-            self.pool = g.pool()
+        cur.wait_stream(self.stream)
         self.graphs[(nbc, refine)] = g
         self.stats["captures"] += 1
         return g
 
     # -- the step ----------------------------------------------------------------
-    def _check_capacity(self):
-        """Grow the capacity (and recapture) after an overflow, or when the
-        largest pair count seen comes within 3/4 of it."""
+    def _check_capacity(self, new_generation: bool):
+        """The pair capacity: twice the largest upstream num_rendered seen since
+        the last check (replays through the pinned copy of the device maximum,
+        eager iterations through the mapper's own record) + 4096.  Changed --
+        and the graphs recaptured -- after an overflow, when the maximum comes
+        within 3/4 of the capacity, or, for a new map state, when it is more
+        than twice what is needed (the map shrank after a prune)."""
         ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
-        if self.cap is not None and not ovf and mx <= 0.75 * self.cap:
+        if not new_generation and self.cap is not None and not ovf and mx <= 0.75 * self.cap:
             return
-        if self.cap is None:
-            self.cap = max(1 << 16, 2 * int(self.m._max_nr) + 4096)
-            return
-        torch.cuda.synchronize(self.dev)
-        ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
         if ovf:
+            torch.cuda.synchronize(self.dev)
+            ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
             self.stats["overflows"] += 1
             self.stats["skipped_iterations"] += ovf
             # the skipped steps advanced no moments on the device: undo their counts
@@ -390,25 +424,33 @@ class IterationGraphs:
                 for t in self.S.mlp_steps:
                     t -= ovf
             self.m.events.append((self.m.iteration_count, "capacity_overflow", {"cap": self.cap, "skipped": ovf}))
-        self.cap = max(2 * self.cap if ovf else self.cap, 2 * mx + 4096)
+        want = max(self.min_cap, int(self.cap_scale * max(mx, int(self.m._max_nr))) + self.cap_margin)
+        if ovf and self.cap is not None:
+            want = max(want, 2 * self.cap)
+        if self.cap is None or ovf or mx > 0.75 * self.cap or want > self.cap or 2 * want < self.cap:
+            if self.cap is not None and want != self.cap:
+                self.invalidate()
+            self.cap = want
+        self.m._max_nr = 0
         self.sticky.zero_()
         self.sticky_np[:] = 0
-        self.invalidate()
 
     def step(self, kf, neighbours, refine: bool = False) -> bool:
         """Run one steady-state iteration on keyframe ``kf`` as a graph replay;
         False when the graph path does not apply (the caller runs it eagerly)."""
         if not self.usable():
             return False
+        t_step = time.perf_counter()
         m = self.m
         nbc = len(neighbours)
         if not 1 <= nbc <= 5:
             return False
         key = self._map_key()
-        if key != self.key:
+        fresh = key != self.key
+        if fresh:
             self.invalidate()
             self.key = key
-        self._check_capacity()
+        self._check_capacity(fresh)
         g = self.graphs.get((nbc, refine))
         if g is None:
             g = self._capture(nbc, refine)
@@ -445,7 +487,11 @@ class IterationGraphs:
         if ev is None:
             ev = self.ring_ev[i] = torch.cuda.Event()
         ev.record()
+        t_rep = time.perf_counter()
         g.replay()
+        t_end = time.perf_counter()
         torch._foreach_add_(S.mlp_steps, 1.0)
         self.stats["replays"] += 1
+        self.stats["replay_call_s"] += t_end - t_rep
+        self.stats["step_host_s"] += time.perf_counter() - t_step
         return True
