@@ -1538,6 +1538,7 @@ constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
 #endif
 constexpr int kRecChunk = WGSR_GBC_RECCHUNK;  // flattened record slots staged in LDS at a time
 #endif
+template <int kR>
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
     const ListRec* __restrict__ lrec, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
@@ -1548,34 +1549,34 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
     float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
   constexpr int NW = kGbcThreads / 64;
-  __shared__ uint32_t s_list[kGbcSpan];
+  __shared__ uint32_t s_list[(kGbcThreads * kR)];
 #if WGSR_GBC_FLAT
-  __shared__ uint32_t s_s0[kGbcSpan], s_n[kGbcSpan], s_off[kGbcSpan + 1];
+  __shared__ uint32_t s_s0[(kGbcThreads * kR)], s_n[(kGbcThreads * kR)], s_off[(kGbcThreads * kR) + 1];
   __shared__ uint2 s_tmp4[4];
   __shared__ float s_rec[kRecChunk][10];
 #else
-  __shared__ float s_g[kGbcSpan][11];
+  __shared__ float s_g[(kGbcThreads * kR)][11];
 #endif
-  __shared__ uint32_t s_wc[kGbcRounds][NW];
+  __shared__ uint32_t s_wc[kR][NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int i0 = blockIdx.x * kGbcSpan;
+  const int i0 = blockIdx.x * (kGbcThreads * kR);
   // compaction of the live Gaussians (list order = index order)
-  bool live[kGbcRounds];
-  uint64_t bal[kGbcRounds];
+  bool live[kR];
+  uint64_t bal[kR];
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r) {
+  for (int r = 0; r < kR; ++r) {
     const int i = i0 + r * kGbcThreads + t;
     live[r] = i < P && gflag[i] != 0;
   }
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r) {
+  for (int r = 0; r < kR; ++r) {
     bal[r] = wave_ballot(live[r]);
     if (lane == 0) s_wc[r][w] = (uint32_t)__popcll(bal[r]);
   }
   __syncthreads();
   uint32_t nlive = 0;
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r) {
+  for (int r = 0; r < kR; ++r) {
     uint32_t base = nlive;
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
@@ -1589,11 +1590,11 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
 #if WGSR_GBC_PREFETCH
   // every listed Gaussian's parameters (and a touch of its SH row's lines)
   // loaded now, while the record sums below wait on their own round trips
-  GbPre pre[kGbcRounds];
-  uint32_t pcl[kGbcRounds];
+  GbPre pre[kR];
+  uint32_t pcl[kR];
   float touch = 0.f;
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r) {
+  for (int r = 0; r < kR; ++r) {
     const uint32_t c = r * kGbcThreads + t;
     const int i = c < nlive ? (int)s_list[c] : 0;
     const size_t i3 = 3 * (size_t)i;
@@ -1620,10 +1621,10 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   __syncthreads();
   {
-    uint32_t v[kGbcRounds], loc = 0;
+    uint32_t v[kR], loc = 0;
 #pragma unroll
-    for (int r = 0; r < kGbcRounds; ++r) {
-      const uint32_t c = kGbcRounds * t + r;
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t c = kR * t + r;
       v[r] = c < nlive ? s_n[c] : 0u;
       loc += v[r];
     }
@@ -1631,8 +1632,8 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     uint32_t ex = block_excl_scan256_2(make_uint2(loc, 0u), s_tmp4, &tot2).x;
     const uint32_t tot = tot2.x;
 #pragma unroll
-    for (int r = 0; r < kGbcRounds; ++r) {
-      const uint32_t c = kGbcRounds * t + r;
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t c = kR * t + r;
       if (c < nlive) s_off[c] = ex;
       ex += v[r];
     }
@@ -1640,9 +1641,9 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   __syncthreads();
   const uint32_t total = s_off[nlive];
-  float acc[kGbcRounds][10];
+  float acc[kR][10];
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r)
+  for (int r = 0; r < kR; ++r)
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[r][k] = 0.f;
   for (uint32_t base = 0; base < total; base += kRecChunk) {
@@ -1666,7 +1667,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kGbcRounds; ++r) {
+    for (int r = 0; r < kR; ++r) {
       const uint32_t c = r * kGbcThreads + t;
       if (c < nlive) {
         const uint32_t qa = max(s_off[c], base), qb = min(s_off[c + 1], base + kRecChunk);
@@ -1678,7 +1679,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     __syncthreads();
   }
 #pragma unroll
-  for (int r = 0; r < kGbcRounds; ++r) {
+  for (int r = 0; r < kR; ++r) {
     const uint32_t c = r * kGbcThreads + t;
     if (c >= nlive) break;
     const int i = (int)s_list[c];
@@ -1971,7 +1972,13 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
   const char* ce = getenv("WGSR_GB_COMPACT");  // read per call: tests compare the sparse kernels
   if (sparse && zeroed && !(ce && strcmp(ce, "0") == 0)) {
     // (no pair listed: gflag is all zero and nothing is written)
-    hipLaunchKernelGGL(k_gauss_bwd_compact, dim3((a.P + kGbcSpan - 1) / kGbcSpan), dim3(kGbcThreads), 0, s, a.P,
+    // one round (256 Gaussians per workgroup) when two rounds would leave
+    // fewer than two workgroups per CU (the mapper's ~100k-Gaussian maps):
+    // the per-workgroup chain of dependent loads is the kernel's time there
+    const bool one = a.P < 256 * 1024 && kGbcRounds >= 2;
+    const int span = one ? kGbcThreads : kGbcSpan;
+    hipLaunchKernelGGL(one ? k_gauss_bwd_compact<1> : k_gauss_bwd_compact<kGbcRounds>,
+                       dim3((a.P + span - 1) / span), dim3(kGbcThreads), 0, s, a.P,
                        a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
                        at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
                        a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,

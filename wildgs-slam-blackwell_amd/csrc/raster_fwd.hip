@@ -787,6 +787,9 @@ __global__ __launch_bounds__(256) void k_bin_bounds(const uint32_t* __restrict__
 // threads 44 us; one wave per row 73 us -- a bin's ~2000 entries then take
 // ~35 dependent steps; 512 threads 55 us -- fewer workgroups in flight.)
 constexpr int kExpThreads = 256;
+#ifndef WGSR_EXP_ITEMS  // entries per thread per compaction step (1 or 2; A/B)
+#define WGSR_EXP_ITEMS 1
+#endif
 __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __restrict__ skeys,
                                                              const uint32_t* __restrict__ sgid,
                                                              const uint2* __restrict__ bounds, int gx, int gy,
@@ -809,6 +812,51 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
   const size_t base0 = ((size_t)lo << (2 * bshift)) + (size_t)(r << bshift) * len;
   const uint32_t shift = 16u + ((uint32_t)r << bshift), rmask = (1u << B) - 1u;
   uint32_t count[4] = {0u, 0u, 0u, 0u};
+#if WGSR_EXP_ITEMS == 2
+  // two entries per thread per step (half the steps and barriers)
+  __shared__ uint32_t s_wc2[NW][4];
+  uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
+  uint32_t key2 = lo + 256 + t < hi ? skeys[lo + 256 + t] : 0u, gid2 = lo + 256 + t < hi ? sgid[lo + 256 + t] : 0u;
+  asm volatile("" ::"v"(key), "v"(gid), "v"(key2), "v"(gid2));
+  for (uint32_t e0 = lo; e0 < hi; e0 += 2 * kExpThreads) {
+    const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
+    const uint32_t bits2 = (key2 >> shift) & rmask, my_gid2 = gid2;
+    const uint32_t e1 = e0 + 2 * kExpThreads + t, e2 = e1 + kExpThreads;
+    key = e1 < hi ? skeys[e1] : 0u;
+    gid = e1 < hi ? sgid[e1] : 0u;
+    key2 = e2 < hi ? skeys[e2] : 0u;
+    gid2 = e2 < hi ? sgid[e2] : 0u;
+    uint64_t m[4], m2[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m[c] = wave_ballot(c < B && ((bits >> c) & 1u));
+      m2[c] = wave_ballot(c < B && ((bits2 >> c) & 1u));
+      if (lane == 0 && c < B) {
+        s_wc[w][c] = (uint32_t)__popcll(m[c]);
+        s_wc2[w][c] = (uint32_t)__popcll(m2[c]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= B) break;
+      uint32_t off = count[c], tot = 0, off2 = 0, tot2 = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        const uint32_t v = s_wc[k][c], v2 = s_wc2[k][c];
+        off += k < w ? v : 0u;
+        off2 += k < w ? v2 : 0u;
+        tot += v;
+        tot2 += v2;
+      }
+      if ((bits >> c) & 1u) lists[base0 + (size_t)c * len + off + lanes_below(m[c])] = my_gid;
+      if ((bits2 >> c) & 1u) lists[base0 + (size_t)c * len + count[c] + tot + off2 + lanes_below(m2[c])] = my_gid2;
+      count[c] += tot + tot2;
+    }
+    __syncthreads();
+    asm volatile("" ::"v"(key), "v"(gid), "v"(key2), "v"(gid2));
+  }
+#else
   uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
   // the next step's entries load while this step runs: the empty asm uses
   // below make the compiler wait for them at the END of a step (without
@@ -842,6 +890,7 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
     __syncthreads();
     asm volatile("" ::"v"(key), "v"(gid));
   }
+#endif
   if (t < B) {
     const int tx = (bx << bshift) + t;
     if (tx < gx) {

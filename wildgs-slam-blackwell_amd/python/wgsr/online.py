@@ -88,7 +88,7 @@ def lr_helper(step, lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_
         delay_rate = lr_delay_mult + (1 - lr_delay_mult) * np.sin(0.5 * np.pi * np.clip(step / lr_delay_steps, 0, 1))
     else:
         delay_rate = 1.0
-    t = np.clip(step / max_steps, 0, 1)
+    t = min(max(step / max_steps, 0.0), 1.0)  # (np.clip's value, without its per-call overhead)
     return float(delay_rate * np.exp(np.log(lr_init) * (1 - t) + np.log(lr_final) * t))
 
 
@@ -187,8 +187,11 @@ class OnlineMapper:
         one), computed in fp32 as numpy does for a float32 array."""
         v = x.reshape(-1).float()
         n = v.numel()
-        lo = torch.kthvalue(v, (n - 1) // 2 + 1).values
-        hi = torch.kthvalue(v, n // 2 + 1).values if n % 2 == 0 else lo
+        # one sort for both order statistics (two kthvalue calls took ~0.75 ms
+        # each on a 512 x 384 map on the device)
+        sv = torch.sort(v).values
+        lo = sv[(n - 1) // 2]
+        hi = sv[n // 2] if n % 2 == 0 else lo
         return float(((lo + hi) / 2).item())
 
     @torch.no_grad()

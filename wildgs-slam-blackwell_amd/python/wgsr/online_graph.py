@@ -463,9 +463,9 @@ class IterationGraphs:
         if ev is not None:
             ev.synchronize()
         f, u, ix = self.ring_f[i], self.ring_u[i], self.ring_i[i]
-        # the seeds in the eager path's order: MLP forward, DINO draw, DINO MLP forward
-        for j in range(3):
-            u[j] = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        # the seeds in the eager path's order: MLP forward, DINO draw, DINO MLP
+        # forward (one batched draw: the same three values as three single ones)
+        u[0:3] = torch.randint(0, 2 ** 31 - 1, (3,)).tolist()
         m.ms.adam_scalars(f[self.F_GAUSS:self.F_GAUSS + 15])
         b1, b2 = S.mlp_betas
         n = float(S.mlp_steps[0]) + 1.0
