@@ -409,6 +409,30 @@ int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t
 int64_t wgsr_random_perm_max(void);
 int wgsr_random_perm(int64_t n, uint32_t seed, const uint32_t* seed_dev, uint32_t* keys, int32_t* perm,
                      void* stream);
+/* perm[0..k) = the first k entries of wgsr_random_perm's permutation (the
+ * DINO term keeps only n / reg_stride^4 of the draw), in one launch and
+ * without a sort of all n; n <= wgsr_random_perm_prefix_max_n(),
+ * k <= min(n, wgsr_random_perm_prefix_max_k()). */
+int64_t wgsr_random_perm_prefix_max_n(void);
+int64_t wgsr_random_perm_prefix_max_k(void);
+int wgsr_random_perm_prefix(int64_t n, int64_t k, uint32_t seed, const uint32_t* seed_dev, int32_t* perm,
+                            void* stream);
+/* Two uncertainty-MLP forwards in one launch (the mapping iteration's
+ * keyframe features and the DINO term's sample): rows [0, N1) are X1's with
+ * the dropout seed *seed1, rows [N1, N1 + N2) X2's with *seed2 -- each
+ * segment's dropout draw is the one its own wgsr_mlp_forward_dev_seed would
+ * make; h1d / h2d / o_pre / u hold N1 + N2 rows.  The backward sums both
+ * segments' parameter gradients (upstream du1 x du_scale1 and du2 x
+ * du_scale2) into grad (added to it with accumulate != 0); scratch:
+ * wgsr_mlp_scratch_bytes(N1 + N2, C). */
+int wgsr_mlp_forward_seg2(int N1, int N2, int C, const float* X1, const float* X2, const float* W1, const float* b1,
+                          const float* W2, const float* b2, const float* W3, const float* b3, float dropout_p,
+                          const uint32_t* seed1, const uint32_t* seed2, float* h1d, float* h2d, float* o_pre,
+                          float* u, void* stream);
+int wgsr_mlp_backward_seg2(int N1, int N2, int C, const float* X1, const float* X2, const float* W2, const float* W3,
+                           float dropout_p, const float* h1d, const float* h2d, const float* o_pre, const float* du1,
+                           const float* du2, float du_scale1, float du_scale2, int accumulate, float* scratch,
+                           float* grad, void* stream);
 /* wgsr_mlp_backward with dL_du scaled by du_scale, and with accumulate != 0
  * the gradient ADDED to grad (a second backward into the same parameters,
  * as autograd accumulates). */

@@ -222,6 +222,7 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     g = torch.Generator(device=DEV).manual_seed(0)
     bank = torch.randn(10, 3, 8, 12, device=DEV, generator=g)
     ex = torch.randn(10, 3, 2, device=DEV, generator=g)
+    ex[:, 2].abs_()  # exp_avg_sq >= 0 (a negative one makes both steps NaN, and NaN != NaN)
     idx = torch.tensor([7, 2, 4, 9], dtype=torch.int64, device=DEV)
     d1 = torch.empty(1, 3, 8, 12, device=DEV)
     d3 = torch.empty(3, 3, 8, 12, device=DEV)
@@ -245,7 +246,10 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     got = ex.clone()
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, p(sticky),
                                     p(counts), st))
-    assert torch.equal(got, ref) and sticky.tolist() == [0, 1234]
+    # (the same arithmetic as the Adam kernel; the compiler may contract its
+    # multiply-adds differently in the two kernels: a few ulp)
+    assert torch.allclose(got, ref, rtol=1e-6, atol=1e-7) and sticky.tolist() == [0, 1234]
+    assert torch.equal(got[:7], ex[:7]) and torch.equal(got[8:], ex[8:])  # only the indexed row moves
     before = got.clone()
     counts[3] = 1
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), p(sc), p(one), p(zero), 0.9, 0.999, 1e-8, p(sticky),
@@ -263,4 +267,47 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     G1 = backward_raw(sv, du1)
     want = G1 + backward_raw(sv, du2 * 0.5)
     got = backward_raw(sv, du2, scale=0.5, accumulate_into=G1.clone())
-    assert torch.equal(got, want)
+    assert torch.allclose(got, want, rtol=1e-6, atol=1e-6 * float(want.abs().max()))
+
+
+@pytest.mark.gpu
+def test_random_perm_prefix_and_mlp_two_segments():
+    from wgsr import _lib
+    from wgsr.mlp import UncertaintyMLP, _mix32, backward_raw, backward_raw2, forward_raw, forward_raw2
+    L = _lib.load()
+    st = _lib.stream_handle(DEV)
+    p = _lib.ptr
+    assert int(L.wgsr_random_perm_prefix_max_n()) >= 8192 and int(L.wgsr_random_perm_prefix_max_k()) >= 1024
+    # the first k entries of the stable ascending key order, host and device seeds
+    for seed, n, k in ((987654321, 4860, 303), (5, 1, 1), (77, 1000, 1000), (123, 8192, 1024), (9, 3000, 1)):
+        perm = torch.full((k,), -1, dtype=torch.int32, device=DEV)
+        _lib.check(L.wgsr_random_perm_prefix(n, k, seed, None, p(perm), st))
+        with np.errstate(over="ignore"):
+            i = np.arange(n, dtype=np.uint32)
+            want = (_mix32(np.uint32(seed) ^ _mix32(i * np.uint32(0x9E3779B9) + np.uint32(0x632BE5AB))) >> 1)
+        ref = np.argsort(want.astype(np.int64), kind="stable")[:k]
+        assert np.array_equal(perm.cpu().numpy(), ref), (n, k)
+        sd = torch.tensor([seed], dtype=torch.int64, device=DEV).to(torch.int32)
+        perm2 = torch.full((k,), -1, dtype=torch.int32, device=DEV)
+        _lib.check(L.wgsr_random_perm_prefix(n, k, 0, p(sd), p(perm2), st))
+        assert torch.equal(perm, perm2)
+    with pytest.raises(RuntimeError):
+        _lib.check(L.wgsr_random_perm_prefix(100, 101, 1, None, p(perm), st))
+    # two MLP segments in one launch == one launch per segment (outputs bitwise;
+    # the summed gradient up to the order of the sums)
+    torch.manual_seed(3)
+    net = UncertaintyMLP(384).to(DEV)
+    x1, x2 = torch.randn(972, 384, device=DEV), torch.randn(303, 384, device=DEV)
+    s1 = torch.tensor([11], dtype=torch.int32, device=DEV)
+    s2 = torch.tensor([-7], dtype=torch.int32, device=DEV)
+    ua, sv = forward_raw2(net, x1, x2, s1, s2)
+    u1, sv1 = forward_raw(net, x1, s1)
+    u2, sv2 = forward_raw(net, x2, s2)
+    assert torch.equal(ua, torch.cat([u1, u2]))
+    assert torch.equal(sv[4], torch.cat([sv1[3], sv2[3]])) and torch.equal(sv[5], torch.cat([sv1[4], sv2[4]]))
+    du1, du2 = torch.randn(972, device=DEV), torch.randn(303, device=DEV)
+    G = backward_raw2(sv, du1, du2, 1.0, 0.5)
+    want = backward_raw(sv1, du1) + backward_raw(sv2, du2 * 0.5)
+    assert torch.allclose(G, want, rtol=1e-5, atol=1e-5 * float(want.abs().max()))
+    Gacc = backward_raw2(sv, du1, du2, 1.0, 0.5, accumulate_into=want.clone())
+    assert torch.allclose(Gacc, 2 * want, rtol=1e-5, atol=2e-5 * float(want.abs().max()))

@@ -94,6 +94,9 @@ for s in $STEPS; do
         (cd /tmp && WGSR_LIB=$GRAFT_REPO_ROOT/$lib timeout -k 10 300 rocprofv3 --pmc ${PMC_COUNTERS} --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_ab_$v -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_ab_$v.err); rc=$?
         if [ $rc -ne 0 ]; then break; fi
       done ;;
+    profenv)
+      # ENV_AB="base NAME=VALUE ...": rocprofv3 kernel stats of bench.py per setting (tools/prof_env.sh)
+      bash tools/prof_env.sh; rc=$? ;;
     dp2)
       # N = 2 rehearsal of the multi-GPU bench path on the box's one GPU: two
       # ranks share cuda:0 over gloo (device tensors staged through host memory)

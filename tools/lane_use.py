@@ -9,7 +9,7 @@ sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__im
 from wgsr.scene import make_scene
 W,H=1920,1080
 P=int(sys.argv[1]) if len(sys.argv)>1 else 1_000_000
-S=40000
+S=int(__import__("os").environ.get("S","40000"))
 sc=make_scene(P,W,H,3,seed=0)
 idx=torch.randperm(P,generator=torch.Generator().manual_seed(1))[:S]
 m=sc.means3D[idx].double().numpy(); s=sc.scales[idx].double().numpy(); q=sc.rotations[idx].double().numpy(); o=sc.opacities[idx,0].double().numpy()

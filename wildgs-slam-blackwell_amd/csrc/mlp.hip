@@ -150,6 +150,22 @@ constexpr int kSmallRows = 16;
 __host__ __device__ inline size_t mlp_small_lds(int C) {
   return sizeof(float) * ((size_t)(kHid + kSmallRows) * C + (size_t)kHid * kHid + (size_t)kSmallRows * 68);
 }
+// Two row segments in one launch (wgsr_mlp_forward_seg2): rows [0, N1) are
+// X's with the seed `seed`, rows [N1, N) X2's rows 0, 1, ... with `seed2` --
+// the dropout draw of each segment is the one its own launch would make
+// (row numbers restart at the segment), outputs stay contiguous.
+struct MlpSeg2 {
+  int N1;                                  // rows of the first segment (N: none after it)
+  const float* X2;                         // the second segment's rows
+  uint32_t seed2;
+  const uint32_t* seed2_dev;
+};
+__device__ __forceinline__ bool seg2_keep(uint32_t seed, const MlpSeg2& sg, uint32_t seed2, int layer, uint32_t row,
+                                          int col, float p) {
+  const bool second = (int)row >= sg.N1;
+  return keep_elem(second ? seed2 : seed, layer, second ? row - (uint32_t)sg.N1 : row, col, p);
+}
+
 template <int kC>
 __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __restrict__ X,
                                                        const float* __restrict__ W1, const float* __restrict__ b1,
@@ -157,7 +173,8 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
                                                        const float* __restrict__ W3, const float* __restrict__ b3,
                                                        float p, uint32_t seed, const uint32_t* __restrict__ seed_dev,
                                                        float* __restrict__ h1d, float* __restrict__ h2d,
-                                                       float* __restrict__ o_pre, float* __restrict__ u) {
+                                                       float* __restrict__ o_pre, float* __restrict__ u,
+                                                       const MlpSeg2 sg) {
   constexpr int C4 = kC / 4;  // float4s per row
   extern __shared__ float4 s_mlp4[];
   float4* const sW = s_mlp4;                       // [64][C4], chunk k4 of row c at k4 ^ (c & 15)
@@ -165,6 +182,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
   float4* const sW2 = sX + kSmallRows * C4;        // [64][16], swizzled as sW
   float* const sH = reinterpret_cast<float*>(sW2 + kHid * 16);  // [16][68] layer inputs
   if (seed_dev) seed = *seed_dev;
+  const uint32_t seed2 = sg.seed2_dev ? *sg.seed2_dev : sg.seed2;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, col = t & 63, rq = t >> 6;
   const int r0 = blockIdx.x * kSmallRows;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
@@ -184,8 +202,9 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
 #pragma unroll
     for (int q = 0; q < NX; ++q) {  // rows past N re-read row N - 1 (their outputs are not stored)
       const int sl = (w * NX + q) * 64 + lane, r = sl / C4, k4 = sl - r * C4;
-      __builtin_amdgcn_global_load_lds((const void*)(Xv + (size_t)min(r0 + r, N - 1) * C4 + k4),
-                                       (lds_ptr)(sX + (w * NX + q) * 64), 16, 0, 0);
+      const int rr = min(r0 + r, N - 1);
+      const float4* src = rr < sg.N1 ? Xv + (size_t)rr * C4 : reinterpret_cast<const float4*>(sg.X2) + (size_t)(rr - sg.N1) * C4;
+      __builtin_amdgcn_global_load_lds((const void*)(src + k4), (lds_ptr)(sX + (w * NX + q) * 64), 16, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < NW2; ++q) {
@@ -214,7 +233,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * rq + i;
     float v = fmaxf(acc[i] + b1[col], 0.f);
-    v = keep_elem(seed, 0, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
+    v = seg2_keep(seed, sg, seed2, 0, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
     sH[r * 68 + col] = v;
     if (r0 + r < N) h1d[(size_t)(r0 + r) * kHid + col] = v;
     acc[i] = 0.f;
@@ -237,7 +256,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * rq + i;
     float v = fmaxf(acc[i] + b2[col], 0.f);
-    v = keep_elem(seed, 1, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
+    v = seg2_keep(seed, sg, seed2, 1, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
     sH[r * 68 + col] = v;  // layer-3 input
     if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + col] = v;
   }
@@ -394,11 +413,19 @@ __device__ __forceinline__ void tile_mac_kc(const float (*A)[kLd], const float* 
   }
 }
 
+// (two row segments as k_mlp_fwd_small's: rows >= N1 take X2's rows and the
+// upstream gradient du2 x du_scale2)
+struct MlpBwdSeg2 {
+  int N1;
+  const float* X2;
+  const float* du2;
+  float du_scale2;
+};
 __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __restrict__ X,
                                                   const float* __restrict__ W2, const float* __restrict__ W3, float p,
                                                   const float* __restrict__ h1d, const float* __restrict__ h2d,
                                                   const float* __restrict__ o_pre, const float* __restrict__ du,
-                                                  float* __restrict__ part, float du_scale) {
+                                                  float* __restrict__ part, float du_scale, const MlpBwdSeg2 sg) {
   __shared__ float4 sH1v[1024], sH2v[1024], sW2v[1024], sXv[1024];  // [64][64] each, natural layouts
   __shared__ float sA[64][kLd], sB[64][kLd];
   __shared__ float sDo[kRows];
@@ -412,7 +439,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
   float o = 0.f, g = 0.f;
   if (t < kRows && r0 + t < N) {
     o = o_pre[r0 + t];
-    g = du[r0 + t] * du_scale;
+    g = r0 + t < sg.N1 ? du[r0 + t] * du_scale : sg.du2[r0 + t - sg.N1] * sg.du_scale2;
   }
   {
     typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -426,9 +453,10 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
                                        (lds_ptr)(sH2v + (4 * w + q) * 64), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(W2) + sl),
                                        (lds_ptr)(sW2v + (4 * w + q) * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(reinterpret_cast<const float4*>(X) + (size_t)row * C4 + (c0 >> 2) + c4),
-          (lds_ptr)(sXv + (4 * w + q) * 64), 16, 0, 0);
+      const float4* xr = row < sg.N1 ? reinterpret_cast<const float4*>(X) + (size_t)row * C4
+                                     : reinterpret_cast<const float4*>(sg.X2) + (size_t)(row - sg.N1) * C4;
+      __builtin_amdgcn_global_load_lds((const void*)(xr + (c0 >> 2) + c4), (lds_ptr)(sXv + (4 * w + q) * 64), 16, 0,
+                                       0);
     }
   }
   float* out = part + (size_t)blockIdx.x * mlp_partial_floats(C);
@@ -553,7 +581,94 @@ __global__ __launch_bounds__(256) void k_random_keys(int64_t n, uint32_t seed, c
   keys[i] = (int32_t)(mix32(sd ^ mix32((uint32_t)i * 0x9E3779B9U + 0x632BE5ABU)) >> 1);
 }
 
+// The first k entries of wgsr_random_perm's permutation -- the stable
+// ascending order of k_random_keys' keys -- in one workgroup, without sorting
+// all n: each index's 44-bit composite (key << 13 | index; unique, and
+// ascending composites are the stable key order) stays in registers, four
+// 11-bit radix-select passes (LDS histogram, block scan) find the k-th
+// smallest composite, the k composites at or below it are appended to LDS,
+// and each is placed by counting the smaller ones.
+constexpr int kPpThreads = 1024, kPpItems = 8, kPpMaxN = kPpThreads * kPpItems, kPpMaxK = kPpThreads;
+static_assert(kPpMaxN <= 8192, "13 index bits");
+__global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32_t seed,
+                                                            const uint32_t* __restrict__ seed_dev,
+                                                            int32_t* __restrict__ perm) {
+  __shared__ uint32_t hist[2048];
+  __shared__ uint32_t wsum[kPpThreads / 64];
+  __shared__ uint32_t sel[2];
+  __shared__ unsigned long long list[kPpMaxK];
+  __shared__ uint32_t cnt;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t sd = seed_dev ? *seed_dev : seed;
+  unsigned long long c[kPpItems];
+#pragma unroll
+  for (int j = 0; j < kPpItems; ++j) {
+    const int i = t + kPpThreads * j;
+    const uint32_t key = mix32(sd ^ mix32((uint32_t)i * 0x9E3779B9U + 0x632BE5ABU)) >> 1;  // k_random_keys
+    c[j] = i < n ? ((unsigned long long)key << 13) | (unsigned long long)i : ~0ull;
+  }
+  unsigned long long prefix = 0ull, pmask = 0ull;
+  uint32_t want = (uint32_t)k;  // rank (1-based) of the wanted composite among those matching the prefix
+#pragma unroll 1
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 33 - 11 * pass;  // bits 43-33, 32-22, 21-11, 10-0
+    hist[t] = 0u;
+    hist[t + kPpThreads] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPpItems; ++j)
+      if (c[j] != ~0ull && (c[j] & pmask) == prefix) atomicAdd(&hist[(uint32_t)(c[j] >> shift) & 2047u], 1u);
+    __syncthreads();
+    const uint32_t h0 = hist[2 * t], h1 = hist[2 * t + 1], sm = h0 + h1;
+    const uint32_t inc = wave_incl_scan(sm);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < kPpThreads / 64; ++q) base += q < w ? wsum[q] : 0u;
+    const uint32_t e0 = base + inc - sm, e1 = e0 + h0;
+    if (e0 < want && want <= e0 + h0) {
+      sel[0] = 2u * t;
+      sel[1] = want - e0;
+    } else if (e1 < want && want <= e1 + h1) {
+      sel[0] = 2u * t + 1u;
+      sel[1] = want - e1;
+    }
+    __syncthreads();
+    prefix |= (unsigned long long)sel[0] << shift;
+    pmask |= 2047ull << shift;
+    want = sel[1];
+    __syncthreads();  // (sel and hist are rewritten by the next pass)
+  }
+  if (t == 0) cnt = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPpItems; ++j)
+    if (c[j] <= prefix) list[atomicAdd(&cnt, 1u)] = c[j];  // exactly k of them (prefix: the k-th smallest)
+  __syncthreads();
+  if (t < k) {
+    const unsigned long long v = list[t];
+    uint32_t r = 0;
+    for (int q = 0; q < k; ++q) r += list[q] < v ? 1u : 0u;
+    perm[r] = (int32_t)(v & 8191ull);
+  }
+}
+
 extern "C" {
+
+int64_t wgsr_random_perm_prefix_max_n(void) { return kPpMaxN; }
+int64_t wgsr_random_perm_prefix_max_k(void) { return kPpMaxK; }
+
+int wgsr_random_perm_prefix(int64_t n, int64_t k, uint32_t seed, const uint32_t* seed_dev, int32_t* perm,
+                            void* stream) {
+  if (n < 0 || n > kPpMaxN || k < 0 || k > n || k > kPpMaxK || (k > 0 && !perm))
+    return set_error(WGSR_EINVAL, "wgsr_random_perm_prefix: 0 <= k <= min(n, %d), n <= %d", kPpMaxK, kPpMaxN);
+  if (k == 0) return WGSR_OK;
+  hipLaunchKernelGGL(k_perm_prefix, dim3(1), dim3(kPpThreads), 0, (hipStream_t)stream, (int)n, (int)k, seed, seed_dev,
+                     perm);
+  MLPCHK("wgsr_random_perm_prefix");
+  return WGSR_OK;
+}
 
 size_t wgsr_mlp_scratch_bytes(int N, int C) {
   if (N <= 0 || C <= 0) return 0;
@@ -563,6 +678,25 @@ size_t wgsr_mlp_scratch_bytes(int N, int C) {
 
 int wgsr_mlp_grad_floats(int C) { return C > 0 ? mlp_partial_floats(C) : 0; }
 
+static bool mlp_small_ok(int N, int C, const float* X, const float* W1, const float* W2) {
+  static const bool small_off = [] {
+    const char* e = getenv("WGSR_MLP_SMALL");
+    return e && atoi(e) == 0;
+  }();
+  return !small_off && (N + 63) / 64 < 1024 && (C == 64 || C == 128 || C == 256 || C == 384) &&
+         ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W1) | reinterpret_cast<uintptr_t>(W2)) & 15) == 0;
+}
+
+static void launch_mlp_fwd_small(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
+                                 const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed,
+                                 const uint32_t* seed_dev, float* h1d, float* h2d, float* o_pre, float* u,
+                                 const MlpSeg2& sg, void* stream) {
+  auto kern = C == 384 ? k_mlp_fwd_small<384> : C == 256 ? k_mlp_fwd_small<256>
+            : C == 128 ? k_mlp_fwd_small<128> : k_mlp_fwd_small<64>;
+  hipLaunchKernelGGL(kern, dim3((N + kSmallRows - 1) / kSmallRows), dim3(256), mlp_small_lds(C), (hipStream_t)stream,
+                     N, X, W1, b1, W2, b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u, sg);
+}
+
 static int mlp_forward_impl(int N, int C, const float* X, const float* W1, const float* b1, const float* W2,
                             const float* b2, const float* W3, const float* b3, float dropout_p, uint32_t seed,
                             const uint32_t* seed_dev, float* h1d, float* h2d, float* o_pre, float* u, void* stream) {
@@ -571,16 +705,9 @@ static int mlp_forward_impl(int N, int C, const float* X, const float* W1, const
   if (N == 0) return WGSR_OK;
   if (!X || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !h1d || !h2d || !o_pre || !u)
     return set_error(WGSR_EINVAL, "wgsr_mlp_forward: null pointer");
-  static const bool small_off = [] {
-    const char* e = getenv("WGSR_MLP_SMALL");
-    return e && atoi(e) == 0;
-  }();
-  if (!small_off && (N + 63) / 64 < 1024 && (C == 64 || C == 128 || C == 256 || C == 384) &&
-      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W1) | reinterpret_cast<uintptr_t>(W2)) & 15) == 0) {
-    auto kern = C == 384 ? k_mlp_fwd_small<384> : C == 256 ? k_mlp_fwd_small<256>
-              : C == 128 ? k_mlp_fwd_small<128> : k_mlp_fwd_small<64>;
-    hipLaunchKernelGGL(kern, dim3((N + kSmallRows - 1) / kSmallRows), dim3(256), mlp_small_lds(C), (hipStream_t)stream,
-                       N, X, W1, b1, W2, b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
+  if (mlp_small_ok(N, C, X, W1, W2)) {
+    launch_mlp_fwd_small(N, C, X, W1, b1, W2, b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u,
+                         MlpSeg2{N, nullptr, 0u, nullptr}, stream);
   } else if ((N + 63) / 64 >= 1024)  // enough 64-row workgroups to fill the chip
     hipLaunchKernelGGL(k_mlp_fwd<64>, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W1, b1, W2,
                        b2, W3, b3, dropout_p, seed, seed_dev, h1d, h2d, o_pre, u);
@@ -630,7 +757,8 @@ int wgsr_random_keys(int64_t n, uint32_t seed, const uint32_t* seed_dev, int32_t
 
 static int mlp_backward_impl(int N, int C, const float* X, const float* W2, const float* W3, float dropout_p,
                              const float* h1d, const float* h2d, const float* o_pre, const float* dL_du,
-                             float du_scale, int accumulate, float* scratch, float* grad, void* stream) {
+                             float du_scale, int accumulate, float* scratch, float* grad, void* stream,
+                             const MlpBwdSeg2* seg2 = nullptr) {
   if (N < 0 || C <= 0 || C % 64 != 0) return set_error(WGSR_EINVAL, "wgsr_mlp_backward: C must be a positive multiple of 64");
   const int total = mlp_partial_floats(C);
   if (N == 0) {
@@ -648,9 +776,10 @@ static int mlp_backward_impl(int N, int C, const float* X, const float* W2, cons
   const bool aligned = ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W2) |
                          reinterpret_cast<uintptr_t>(h1d) | reinterpret_cast<uintptr_t>(h2d)) & 15) == 0;
   // (one workgroup per CU: the few-row grids of the mapper only)
-  if (!bwd1 && aligned && (size_t)nb * (C / 64) <= 1024)
+  if (seg2 || (!bwd1 && aligned && (size_t)nb * (C / 64) <= 1024))  // (seg2: checked by the caller)
     hipLaunchKernelGGL(k_mlp_bwd2, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p,
-                       h1d, h2d, o_pre, dL_du, scratch, du_scale);
+                       h1d, h2d, o_pre, dL_du, scratch, du_scale,
+                       seg2 ? *seg2 : MlpBwdSeg2{N, nullptr, nullptr, 0.f});
   else
     hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p,
                        h1d, h2d, o_pre, dL_du, scratch, du_scale);
@@ -678,6 +807,53 @@ int wgsr_mlp_backward_acc(int N, int C, const float* X, const float* W2, const f
                           int accumulate, float* scratch, float* grad, void* stream) {
   return mlp_backward_impl(N, C, X, W2, W3, dropout_p, h1d, h2d, o_pre, dL_du, du_scale, accumulate, scratch, grad,
                            stream);
+}
+
+int wgsr_mlp_forward_seg2(int N1, int N2, int C, const float* X1, const float* X2, const float* W1, const float* b1,
+                          const float* W2, const float* b2, const float* W3, const float* b3, float dropout_p,
+                          const uint32_t* seed1, const uint32_t* seed2, float* h1d, float* h2d, float* o_pre,
+                          float* u, void* stream) {
+  if (N1 < 0 || N2 < 0 || C <= 0 || C % 64 != 0 || !seed1 || !seed2 || (N2 > 0 && !X2))
+    return set_error(WGSR_EINVAL, "wgsr_mlp_forward_seg2: bad arguments");
+  const int N = N1 + N2;
+  if (N1 > 0 && N2 > 0 && mlp_small_ok(N, C, X1, W1, W2) && (reinterpret_cast<uintptr_t>(X2) & 15) == 0 &&
+      (dropout_p >= 0.f && dropout_p < 1.f) && X1 && b1 && b2 && W3 && b3 && h1d && h2d && o_pre && u) {
+    launch_mlp_fwd_small(N, C, X1, W1, b1, W2, b2, W3, b3, dropout_p, 0u, seed1, h1d, h2d, o_pre, u,
+                         MlpSeg2{N1, X2, 0u, seed2}, stream);
+    MLPCHK("wgsr_mlp_forward_seg2");
+    return WGSR_OK;
+  }
+  // (otherwise one launch per segment, outputs at the second one's offset)
+  int rc = mlp_forward_impl(N1, C, X1, W1, b1, W2, b2, W3, b3, dropout_p, 0u, seed1, h1d, h2d, o_pre, u, stream);
+  if (rc != WGSR_OK || N2 == 0) return rc;
+  return mlp_forward_impl(N2, C, X2, W1, b1, W2, b2, W3, b3, dropout_p, 0u, seed2, h1d + (size_t)N1 * kHid,
+                          h2d + (size_t)N1 * kHid, o_pre + N1, u + N1, stream);
+}
+
+int wgsr_mlp_backward_seg2(int N1, int N2, int C, const float* X1, const float* X2, const float* W2, const float* W3,
+                           float dropout_p, const float* h1d, const float* h2d, const float* o_pre, const float* du1,
+                           const float* du2, float du_scale1, float du_scale2, int accumulate, float* scratch,
+                           float* grad, void* stream) {
+  if (N1 < 0 || N2 < 0 || C <= 0 || C % 64 != 0 || (N2 > 0 && (!X2 || !du2)))
+    return set_error(WGSR_EINVAL, "wgsr_mlp_backward_seg2: bad arguments");
+  const int N = N1 + N2, nb = (N + kRows - 1) / kRows;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(X1) | reinterpret_cast<uintptr_t>(X2) |
+                         reinterpret_cast<uintptr_t>(W2) | reinterpret_cast<uintptr_t>(h1d) |
+                         reinterpret_cast<uintptr_t>(h2d)) & 15) == 0;
+  static const bool bwd1 = [] {
+    const char* e = getenv("WGSR_MLP_BWD");
+    return e && atoi(e) == 1;
+  }();
+  if (N1 > 0 && N2 > 0 && aligned && !bwd1 && (size_t)nb * (C / 64) <= 1024) {
+    const MlpBwdSeg2 sg{N1, X2, du2, du_scale2};
+    return mlp_backward_impl(N, C, X1, W2, W3, dropout_p, h1d, h2d, o_pre, du1, du_scale1, accumulate, scratch, grad,
+                             stream, &sg);
+  }
+  int rc = mlp_backward_impl(N1, C, X1, W2, W3, dropout_p, h1d, h2d, o_pre, du1, du_scale1, accumulate, scratch, grad,
+                             stream);
+  if (rc != WGSR_OK || N2 == 0) return rc;
+  return mlp_backward_impl(N2, C, X2, W2, W3, dropout_p, h1d + (size_t)N1 * kHid, h2d + (size_t)N1 * kHid,
+                           o_pre + N1, du2, du_scale2, 1, scratch, grad, stream);
 }
 
 }  // extern "C"

@@ -1526,7 +1526,6 @@ constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
 #ifndef WGSR_GBC_PREFETCH
 #define WGSR_GBC_PREFETCH 0
 #endif
-constexpr int kGbcSpan = kGbcThreads * kGbcRounds;
 // WGSR_GBC_FLAT=0: one 16-lane group per listed Gaussian sums its records
 // (a dependent slot-range load per group pass)
 #ifndef WGSR_GBC_FLAT
@@ -1975,9 +1974,16 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
     // one round (256 Gaussians per workgroup) when two rounds would leave
     // fewer than two workgroups per CU (the mapper's ~100k-Gaussian maps):
     // the per-workgroup chain of dependent loads is the kernel's time there
-    const bool one = a.P < 256 * 1024 && kGbcRounds >= 2;
-    const int span = one ? kGbcThreads : kGbcSpan;
-    hipLaunchKernelGGL(one ? k_gauss_bwd_compact<1> : k_gauss_bwd_compact<kGbcRounds>,
+    // (WGSR_GBC_R = 1..4 forces the rounds per workgroup: A/B)
+    static const int force_r = [] {
+      const char* e = getenv("WGSR_GBC_R");
+      const int v = e ? atoi(e) : 0;
+      return v >= 1 && v <= 4 ? v : 0;
+    }();
+    const int nr = force_r ? force_r : (a.P < 256 * 1024 && kGbcRounds >= 2) ? 1 : kGbcRounds;
+    const int span = kGbcThreads * nr;
+    hipLaunchKernelGGL(nr == 1 ? k_gauss_bwd_compact<1> : nr == 2 ? k_gauss_bwd_compact<2>
+                       : nr == 3 ? k_gauss_bwd_compact<3> : k_gauss_bwd_compact<4>,
                        dim3((a.P + span - 1) / span), dim3(kGbcThreads), 0, s, a.P,
                        a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
                        at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,

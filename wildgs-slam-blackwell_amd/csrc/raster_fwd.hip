@@ -320,14 +320,17 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess(
 // geometry records; only then does it wait for the slab and evaluate the
 // colour -- for visible Gaussians only (k_preprocess evaluates every lane).
 // Outputs are bit-identical to k_preprocess (same operation sequences).
+// kCh == 8: the row-major slab of k_preprocess2<8> (whole rows, 16-byte
+// chunks, row stride NCH chunks: only launched when every coefficient of the
+// row is evaluated, 3 (D + 1)^2 == 3 M)
 template <int kD, int kCh>
 __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lane, f3 dir, uint32_t& cbits) {
-  constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, NCH = (NF + kCh - 1) / kCh;
-  float sh[NCH * kCh];
+  constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, kC = kCh == 8 ? 4 : kCh, NCH = (NF + kC - 1) / kC;
+  float sh[NCH * kC];
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
-    if constexpr (kCh == 4) {
-      const float4 v = reinterpret_cast<const float4*>(s_sh)[k * 64 + lane];
+    if constexpr (kCh >= 4) {
+      const float4 v = reinterpret_cast<const float4*>(s_sh)[kCh == 8 ? lane * NCH + k : k * 64 + lane];
       sh[4 * k] = v.x;
       sh[4 * k + 1] = v.y;
       sh[4 * k + 2] = v.z;
@@ -369,10 +372,19 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
   const bool sh_on = shs != nullptr && colors == nullptr;
   if (sh_on) {  // uniform: queue the slab first
-    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + kCh - 1) / kCh;
+    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + (kCh == 8 ? 4 : kCh) - 1) / (kCh == 8 ? 4 : kCh);
     const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
+    // kCh == 8: the wave's 64 rows as one contiguous run of 16-byte chunks,
+    // lane l of load k taking chunk 64 k + l (coalesced: each load covers
+    // 1 KB of HBM instead of 64 rows' 16 bytes each); the LDS copy is then
+    // row-major (a lane's reads stride 3M floats: 4-way bank conflicts, cheap)
+    const size_t c_end = (size_t)P * (3 * M) / 4;  // chunks in the whole table
     for (int k = 0; k < nch; ++k) {
-      if constexpr (kCh == 4)
+      if constexpr (kCh == 8) {
+        const size_t c = min((size_t)i0 * (3 * M) / 4 + (size_t)(64 * k + lane), c_end - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(shs + 4 * c),
+                                         (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+      } else if constexpr (kCh == 4)
         __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
                                          (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
       else
@@ -921,6 +933,9 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 #ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort (7 or 14)
 #define WGSR_BDS_ITEMS 7
 #endif
+#ifndef WGSR_BDS_FINE  // entries per lane in steps of one (0: 1, 2, 4, 7 only)
+#define WGSR_BDS_FINE 1
+#endif
 #ifndef WGSR_BDS_THREADS  // workgroup size (512 or 1024)
 #define WGSR_BDS_THREADS 1024
 #endif
@@ -1372,8 +1387,21 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 2u * kBdsThreads)
     bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#if WGSR_BDS_FINE
+  // (every step of JN: a bin's time is its busiest wave's chain of JN entry
+  // groups per pass, and a coarser JN leaves the last waves idle -- 4.7k
+  // entries at JN = 7 keep 11 of 16 waves busy, at JN = 5 all 15 it needs)
+  else if (n <= 3u * kBdsThreads)
+    bds_small<3>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#endif
   else if (n <= 4u * kBdsThreads)
     bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#if WGSR_BDS_FINE
+  else if (n <= 5u * kBdsThreads)
+    bds_small<5>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+  else if (n <= 6u * kBdsThreads)
+    bds_small<6>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#endif
   else if (n <= 7u * kBdsThreads)
     bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
@@ -1923,7 +1951,10 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
     const int nf = 3 * (a.D + 1) * (a.D + 1);
     const int kch = ch4 ? 4 : 1;
     const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
-    auto kern = ch4 ? k_preprocess2<4> : k_preprocess2<1>;
+    // (WGSR_PRE=4, A/B, whole rows evaluated only: the coalesced row-major
+    // slab k_preprocess2<8> -- 112 vs 102 us at 1M / SH3: the strided
+    // chunk-major gather is not the limit)
+    auto kern = ch4 ? ((nf == 3 * a.M && pre_mode == 4) ? k_preprocess2<8> : k_preprocess2<4>) : k_preprocess2<1>;
     hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds2, s, a.P, a.D, a.M, a.means3D,
                        a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
                        a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,

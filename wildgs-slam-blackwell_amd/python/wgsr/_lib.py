@@ -219,6 +219,17 @@ def load():
         L.wgsr_random_perm_max.argtypes = []
         L.wgsr_random_perm.restype = c_int
         L.wgsr_random_perm.argtypes = [c_i64, ctypes.c_uint32, _fp, _fp, _fp, _fp]
+        L.wgsr_random_perm_prefix_max_n.restype = c_i64
+        L.wgsr_random_perm_prefix_max_n.argtypes = []
+        L.wgsr_random_perm_prefix_max_k.restype = c_i64
+        L.wgsr_random_perm_prefix_max_k.argtypes = []
+        L.wgsr_random_perm_prefix.restype = c_int
+        L.wgsr_random_perm_prefix.argtypes = [c_i64, c_i64, ctypes.c_uint32, _fp, _fp, _fp]
+        L.wgsr_mlp_forward_seg2.restype = c_int
+        L.wgsr_mlp_forward_seg2.argtypes = [c_int, c_int, c_int] + [_fp] * 8 + [ctypes.c_float] + [_fp] * 7
+        L.wgsr_mlp_backward_seg2.restype = c_int
+        L.wgsr_mlp_backward_seg2.argtypes = ([c_int, c_int, c_int] + [_fp] * 4 + [ctypes.c_float] + [_fp] * 5
+                                             + [ctypes.c_float, ctypes.c_float, c_int, _fp, _fp, _fp])
         L.wgsr_mlp_backward_acc.restype = c_int
         L.wgsr_mlp_backward_acc.argtypes = ([c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 4
                                             + [ctypes.c_float, c_int, _fp, _fp, _fp])
@@ -293,7 +304,8 @@ EXPORTED_SYMBOLS = (
     "wgsr_version", "wgsr_depth_order_offset", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_adam_step_dev", "wgsr_compact_rows",
     "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
-    "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
+    "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_random_perm_prefix_max_n", "wgsr_random_perm_prefix_max_k",
+    "wgsr_random_perm_prefix", "wgsr_mlp_forward_seg2", "wgsr_mlp_backward_seg2", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",

@@ -139,6 +139,50 @@ def backward_raw(saved, du, scale: float = 1.0, accumulate_into=None):
     return grad
 
 
+def forward_raw2(net, x1, x2, seed1_dev, seed2_dev):
+    """``forward_raw`` of x1 [N1, C] (dropout seed ``seed1_dev``) and of x2
+    [N2, C] (``seed2_dev``) in one launch (wgsr_mlp_forward_seg2): -> (u
+    [N1 + N2], saved) for ``backward_raw2``; each segment's dropout draw and
+    output are those of its own ``forward_raw``."""
+    N1, C = x1.shape
+    N2 = x2.shape[0]
+    dev = x1.device
+    L = _lib.load()
+    l1, l2, lo = net.layers[0], net.layers[1], net.output_layer
+    ws = [t.detach() for t in (l1.weight, l1.bias, l2.weight, l2.bias, lo.weight, lo.bias)]
+    N = N1 + N2
+    h1d = torch.empty(N, HIDDEN, device=dev)
+    h2d = torch.empty(N, HIDDEN, device=dev)
+    o = torch.empty(N, device=dev)
+    u = torch.empty(N, device=dev)
+    pt = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_mlp_forward_seg2(N1, N2, C, pt(x1), pt(x2), *[pt(t) for t in ws], float(net.dropout_p),
+                                           pt(seed1_dev), pt(seed2_dev), pt(h1d), pt(h2d), pt(o), pt(u),
+                                           _lib.stream_handle(dev)))
+    return u, (x1, x2, ws[2], ws[4], h1d, h2d, o, float(net.dropout_p))
+
+
+def backward_raw2(saved, du1, du2, scale1: float = 1.0, scale2: float = 1.0, accumulate_into=None):
+    """-> the flat parameter gradient of a ``forward_raw2`` for upstream
+    gradients scale1 x du1 [N1] and scale2 x du2 [N2] (one backward launch
+    over both segments; ``accumulate_into`` as in ``backward_raw``)."""
+    x1, x2, W2, W3, h1d, h2d, o, p = saved
+    N1, C = x1.shape
+    N2 = x2.shape[0]
+    dev = x1.device
+    L = _lib.load()
+    grad = accumulate_into if accumulate_into is not None else torch.empty(int(L.wgsr_mlp_grad_floats(C)), device=dev)
+    scratch = torch.empty(max(1, int(L.wgsr_mlp_scratch_bytes(N1 + N2, C)) // 4), device=dev)
+    pt = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_mlp_backward_seg2(N1, N2, C, pt(x1), pt(x2), pt(W2), pt(W3), p, pt(h1d), pt(h2d), pt(o),
+                                            pt(du1), pt(du2), float(scale1), float(scale2),
+                                            int(accumulate_into is not None), pt(scratch), pt(grad),
+                                            _lib.stream_handle(dev)))
+    return grad
+
+
 class UncertaintyMLP(nn.Module):
     """MLPNetwork(input_dim=C) with the reference defaults, on libwgsr."""
 

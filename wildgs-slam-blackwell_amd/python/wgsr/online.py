@@ -307,24 +307,31 @@ class OnlineMapper:
             window.remove(window[N_dont_touch + int(np.argmax(inv_dist))])
         return window
 
-    def _perm(self, n: int) -> torch.Tensor:
+    def _perm(self, n: int, k: int | None = None) -> torch.Tensor:
         """The DINO term's feature sampling draw (the reference's
         torch.randperm(n), mapper.py:1155-1157 / 1334-1336): the stable
         ascending order of 31-bit hash keys of a seed drawn from torch's
         host generator (wgsr_random_keys) -- the draw the graph-replayed
-        iteration makes on the device from the same seed."""
+        iteration makes on the device from the same seed.  With k: only its
+        first k entries (wgsr_random_perm_prefix where it applies)."""
         from . import _lib
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
-        keys = torch.empty(n, dtype=torch.int32, device=self.dev)
         L = _lib.load()
+        if k is not None and n <= int(L.wgsr_random_perm_prefix_max_n()) and k <= int(L.wgsr_random_perm_prefix_max_k()):
+            perm = torch.empty(max(k, 1), dtype=torch.int32, device=self.dev)
+            with torch.cuda.device(self.dev):
+                _lib.check(L.wgsr_random_perm_prefix(n, k, seed, None, _lib.ptr(perm), _lib.stream_handle(self.dev)))
+            return perm[:k]
+        keys = torch.empty(n, dtype=torch.int32, device=self.dev)
         with torch.cuda.device(self.dev):
             if n <= int(L.wgsr_random_perm_max()):  # one-workgroup stable sort (wgsr_random_perm)
                 perm = torch.empty(n, dtype=torch.int32, device=self.dev)
                 _lib.check(L.wgsr_random_perm(n, seed, None, _lib.ptr(keys), _lib.ptr(perm),
                                               _lib.stream_handle(self.dev)))
-                return perm
+                return perm if k is None else perm[:k]
             _lib.check(L.wgsr_random_keys(n, seed, None, _lib.ptr(keys), _lib.stream_handle(self.dev)))
-        return torch.argsort(keys, stable=True)
+        perm = torch.argsort(keys, stable=True)
+        return perm if k is None else perm[:k]
 
     def _dino_term(self, neighbours, kf):
         """reg_mult * compute_dino_regularization_loss on features sampled from
@@ -335,7 +342,9 @@ class OnlineMapper:
         st = c["reg_stride"]
         buf = torch.stack([self.keyframes[k].features for k in neighbours]).view(-1, kf.features.shape[-1])
         ns = buf.shape[0] // (st ** 4)
-        sf = buf[self._perm(buf.shape[0])[:ns]].unsqueeze(0)
+        # (a test's fixture draw replaces _perm(n) on the instance: full length)
+        perm = self._perm(buf.shape[0])[:ns] if "_perm" in self.__dict__ else self._perm(buf.shape[0], ns)
+        sf = buf[perm].unsqueeze(0)
         (c["reg_mult"] * dino_regularization_loss(self.net(sf), sf)).backward()
 
     # ---- one optimisation iteration ------------------------------------------

@@ -26,12 +26,16 @@ the DINO term on, the uncertainty loss not frozen -- is captured ONCE per
   every Adam step size and bias correction (Gaussians, MLP, exposure), the
   exposure skip flag, the slot indices -- arrives in one 256-byte block
   copied host->device ahead of the replay (a ring of pinned blocks);
-* the uncertainty MLP, the DINO sampling (hash keys + stable argsort) and
-  regulariser, and all three Adams run without autograd (wgsr.mlp.forward_raw
-  / backward_raw, wgsr.uncertainty.dino_reg_raw, wgsr_adam_step_dev).
+* the uncertainty MLP, the DINO sampling (the first n / reg_stride^4 entries
+  of the hash-key permutation, wgsr_random_perm_prefix) and regulariser, and
+  all three Adams run without autograd; the MLP's two forwards (keyframe
+  features, DINO sample) are one launch and its two backwards one more
+  (wgsr.mlp.forward_raw2 / backward_raw2, wgsr.uncertainty.dino_reg_raw,
+  wgsr_adam_step_dev).
 
 The eager path draws the same seeds in the same order and uses the same
-kernels, so a replayed iteration computes what ``_iteration`` computes
+kernels (the MLP per segment), so a replayed iteration computes what
+``_iteration`` computes up to the order of the MLP gradient's sum
 (tests/test_gpu_online_graph.py compares them).  Any change of the map's
 shape (P, the store's banks, the keyframe banks) invalidates the graphs;
 they are recaptured lazily.
@@ -46,7 +50,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .mlp import backward_raw, forward_raw
+from .mlp import backward_raw, backward_raw2, forward_raw, forward_raw2
 from .uncertainty import dino_reg_raw
 
 CAM_FLOATS = 52  # viewmatrix 16 | projmatrix 16 | projmatrix_raw 16 | campos 3 | pad
@@ -316,30 +320,41 @@ class IterationGraphs:
         with torch.cuda.device(dev):
             jobs = self._gather_jobs(nbc)
             _lib.check(L.wgsr_gather_rows(jobs, len(jobs), p(self.i64), st))
-        # the uncertainty MLP on the keyframe's features, the loss + rasteriser
-        # forward/backward (capacity mode), the MLP backward of the loss
-        u, sv = forward_raw(m.net, S.feat4.view(h * w, C), self.i32[0:1])
-        out = ms.forward_backward_uncertainty(S.cam, S.image4[0], S.depth4[0], S.ex[0:1], S.ex[1:2], m.bg,
-                                              u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
-                                              freeze_uncertainty_loss=False, median_depth=S.med,
-                                              pre_exposed=not refine, cap=self.cap, counts=self.counts,
-                                              need_tau=False)
-        G = backward_raw(sv, out["uncertainty_grad"].reshape(-1).contiguous())
-        # the DINO term on features sampled from the neighbouring keyframes
-        # (reg_mult x its gradient accumulated into the MLP's)
+        # the DINO term's draw: features sampled from the neighbouring
+        # keyframes (the first ns entries of the random permutation)
         n = nbc * h * w
         ns = n // (c["reg_stride"] ** 4)
         with torch.cuda.device(dev):
-            if n <= int(L.wgsr_random_perm_max()):
+            if n <= int(L.wgsr_random_perm_prefix_max_n()) and ns <= int(L.wgsr_random_perm_prefix_max_k()):
+                _lib.check(L.wgsr_random_perm_prefix(n, ns, 0, p(self.i32[1:2]), p(S.perm), st))
+                perm = S.perm[:ns]
+            elif n <= int(L.wgsr_random_perm_max()):
                 _lib.check(L.wgsr_random_perm(n, 0, p(self.i32[1:2]), p(S.keys), p(S.perm), st))
                 perm = S.perm[:ns]
             else:  # (large feature maps: the same keys, torch's stable sort)
                 _lib.check(L.wgsr_random_keys(n, 0, p(self.i32[1:2]), p(S.keys), st))
                 perm = torch.argsort(S.keys[:n], stable=True)[:ns]
         sf = S.nbf[:nbc].view(n, C).index_select(0, perm)
-        u2, sv2 = forward_raw(m.net, sf, self.i32[2:3])
-        _, gu = dino_reg_raw(u2, sf)
-        backward_raw(sv2, gu, scale=float(c["reg_mult"]), accumulate_into=G)
+        # the uncertainty MLP on the keyframe's features and on the sample (one
+        # launch, each with its own dropout draw), the loss + rasteriser
+        # forward/backward (capacity mode), the DINO term, and one MLP backward
+        # of both (the DINO gradient scaled by reg_mult: autograd's sum)
+        if ns > 0:
+            u_all, sv = forward_raw2(m.net, S.feat4.view(h * w, C), sf, self.i32[0:1], self.i32[2:3])
+            u, u2 = u_all[:h * w], u_all[h * w:]
+        else:
+            u, sv = forward_raw(m.net, S.feat4.view(h * w, C), self.i32[0:1])
+        out = ms.forward_backward_uncertainty(S.cam, S.image4[0], S.depth4[0], S.ex[0:1], S.ex[1:2], m.bg,
+                                              u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
+                                              freeze_uncertainty_loss=False, median_depth=S.med,
+                                              pre_exposed=not refine, cap=self.cap, counts=self.counts,
+                                              need_tau=False)
+        du = out["uncertainty_grad"].reshape(-1).contiguous()
+        if ns > 0:
+            _, gu = dino_reg_raw(u2, sf)
+            G = backward_raw2(sv, du, gu, 1.0, float(c["reg_mult"]))
+        else:
+            G = backward_raw(sv, du)
         skip = self.counts[3:4]
         # Adam: the Gaussians, the keyframe's exposure on its bank row (skipped
         # unless the window optimiser holds it; also the overflow bookkeeping),
