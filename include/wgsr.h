@@ -258,6 +258,14 @@ int wgsr_gaussian_activate_backward(int P, const float* opacity_raw, const float
                                     const float* dL_dscales, const float* dL_drotations,
                                     float iso_weight, float* dL_dopacity_raw,
                                     float* dL_dscaling_raw, float* dL_drotation_raw, void* stream);
+/* ... and, in the same pass, wgsr_densification_stats' update of
+ * max_radii2D / grad_accum / denom (one launch instead of two). */
+int wgsr_gaussian_activate_backward_stats(int P, const float* opacity_raw, const float* scaling_raw,
+                                          const float* rotation_raw, const float* dL_dopacity,
+                                          const float* dL_dscales, const float* dL_drotations, float iso_weight,
+                                          float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+                                          const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
+                                          float* grad_accum, float* denom, void* stream);
 
 /* get_loss_mapping_rgbd (slam_utils.py:107-143) without its SSIM term:
  * image_ab = exp(exposure_a) image + exposure_b ([3,H,W], written for the
@@ -336,6 +344,14 @@ int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials,
                             const float* ssim_mean, const float* extra_partials, int n_extra, float extra_weight,
                             float alpha, float lambda_dssim, float ssim_mult, int ssim_loss, float* loss,
                             float* sums, float* ssim_scale, void* stream);
+/* wgsr_uncer_loss_combine taking the SSIM forward's tile partials
+ * (wgsr_ssim_forward_partials of the 3 planes) instead of its mean: the
+ * partials are reduced in this launch, in k_ssim_reduce's order (the same
+ * mean, bit for bit), and the mean written to ssim_mean (may be NULL). */
+int wgsr_uncer_loss_combine_ssim(const wgsr_uncer_params* prm, const float* partials, const float* small_partials,
+                                 const float* ssim_partials, float* ssim_mean, const float* extra_partials,
+                                 int n_extra, float extra_weight, float alpha, float lambda_dssim, float ssim_mult,
+                                 float* loss, float* sums, float* ssim_scale, void* stream);
 /* dL_dimage / dL_ddepth of loss_grad x (w_rgb sum(w rgb L1) + w_depth
  * sum(re-weighted depth L1)) + the SSIM term (ssim_grad: its gradient w.r.t.
  * image_ab, already scaled; NULL = none); loss_grad: device scalar (NULL = 1);
@@ -531,11 +547,13 @@ typedef struct wgsr_gather_job {
 int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, void* stream);
 /* The keyframe exposure optimiser's step (torch.optim.Adam arithmetic, as
  * wgsr_adam_step) on row idx[0] of bank [K][3][2] = (a, b), exp_avg,
- * exp_avg_sq, with grad [2] and scalars = (step_size, sqrt(1 - beta2^n));
- * skipped when *skip_a or *skip_b is non-zero.  With sticky and counts (the
+ * exp_avg_sq, with grad = the sum of nparts (a, b) rows (the loss
+ * backward's per-block partials, added in a fixed order; nparts = 1: the
+ * gradient itself) and scalars = (step_size, sqrt(1 - beta2^n)); skipped
+ * when *skip_a or *skip_b is non-zero.  With sticky and counts (the
  * capacity-mode forward's, or NULL): sticky[0] += counts[3], sticky[1] =
  * max(sticky[1], counts[0]). */
-int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, const float* scalars,
+int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, int nparts, const float* scalars,
                        const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
                        int64_t* sticky, const uint32_t* counts, void* stream);
 
@@ -655,6 +673,12 @@ size_t wgsr_ssim_scratch_bytes(int64_t planes, int H, int W);
 int wgsr_ssim_forward(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
                       float* dmap, float* plane_mean, float* mean, wgsr_alloc_fn scratch_alloc, void* alloc_ctx,
                       void* stream);
+/* The SSIM forward without its reduction launch: per-tile partial sums
+ * (wgsr_ssim_tiles(H, W) per plane, plane-major) into `partials`, for a
+ * consumer that reduces them itself (wgsr_uncer_loss_combine_ssim). */
+int wgsr_ssim_forward_partials(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
+                               float* dmap, float* partials, void* stream);
+int wgsr_ssim_tiles(int H, int W);
 /* dL/dimg1 of the forward above given plane_scale[p] = dL/dS for every pixel
  * of plane p (device array; e.g. dL/dmean / (planes*H*W)).  img2 gets no
  * gradient (the reference passes the ground-truth image there). */

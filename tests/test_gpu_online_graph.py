@@ -244,7 +244,7 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     counts = torch.tensor([1234, 0, 0, 0, 0], dtype=torch.int32, device=DEV)
     sticky = torch.tensor([0, 99], dtype=torch.int64, device=DEV)
     got = ex.clone()
-    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, p(sticky),
+    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, p(sticky),
                                     p(counts), st))
     # (the same arithmetic as the Adam kernel; the compiler may contract its
     # multiply-adds differently in the two kernels: a few ulp)
@@ -252,11 +252,21 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     assert torch.equal(got[:7], ex[:7]) and torch.equal(got[8:], ex[8:])  # only the indexed row moves
     before = got.clone()
     counts[3] = 1
-    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), p(sc), p(one), p(zero), 0.9, 0.999, 1e-8, p(sticky),
+    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(one), p(zero), 0.9, 0.999, 1e-8, p(sticky),
                                     p(counts), st))
-    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), p(sc), p(zero), p(one), 0.9, 0.999, 1e-8, None, None,
+    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(zero), p(one), 0.9, 0.999, 1e-8, None, None,
                                     st))
     assert torch.equal(got, before) and sticky.tolist() == [1, 1234]
+    # the gradient as per-block partial rows, summed inside the step
+    parts = torch.randn(768, 2, device=DEV, generator=g)
+    got = ex.clone()
+    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(parts), 768, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, None,
+                                    None, st))
+    ref2 = ex.clone()
+    gsum = parts.double().sum(0).float().contiguous()
+    _lib.check(L.wgsr_exposure_step(p(ref2), p(idx), p(gsum), 1, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, None,
+                                    None, st))
+    assert torch.allclose(got, ref2, rtol=1e-5, atol=1e-6)
     # MLP backward: scaled upstream gradient accumulated into an earlier one
     torch.manual_seed(1)
     net = UncertaintyMLP(384).to(DEV)

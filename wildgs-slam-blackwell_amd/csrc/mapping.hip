@@ -69,6 +69,24 @@ __global__ __launch_bounds__(kMapBlock) void k_activate(int P, const float* __re
 
 __device__ __forceinline__ float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
+// the densification statistics of k_densify_stats, fused into the
+// activation backward's pass over the Gaussians (radii null: none)
+struct DensifyJob {
+  const int32_t* radii;
+  const float* m2d_grad;
+  float* max_radii;
+  float* accum;
+  float* denom;
+};
+__device__ __forceinline__ void densify_stats_one(int i, const DensifyJob& J) {
+  const int r = J.radii[i];
+  if (r <= 0) return;
+  J.max_radii[i] = fmaxf(J.max_radii[i], (float)r);
+  const float gx = J.m2d_grad[3 * (size_t)i], gy = J.m2d_grad[3 * (size_t)i + 1];
+  J.accum[i] += sqrtf(gx * gx + gy * gy);
+  J.denom[i] += 1.f;
+}
+
 __global__ __launch_bounds__(kMapBlock) void k_activate_bwd(int P, const float* __restrict__ o_raw,
                                                             const float* __restrict__ s_raw,
                                                             const float* __restrict__ r_raw,
@@ -76,9 +94,10 @@ __global__ __launch_bounds__(kMapBlock) void k_activate_bwd(int P, const float* 
                                                             const float* __restrict__ g_sc,
                                                             const float* __restrict__ g_rot, float iso_w,
                                                             float* __restrict__ d_o, float* __restrict__ d_s,
-                                                            float* __restrict__ d_r) {
+                                                            float* __restrict__ d_r, const DensifyJob dj) {
   const int i = blockIdx.x * kMapBlock + threadIdx.x;
   if (i >= P) return;
+  if (dj.radii) densify_stats_one(i, dj);
   // sigmoid: grad * (1 - y) * y
   const float y = 1.f / (1.f + expf(-o_raw[i]));
   d_o[i] = g_op[i] * (1.f - y) * y;
@@ -180,12 +199,7 @@ __global__ __launch_bounds__(kMapBlock) void k_densify_stats(int P, const int32_
                                                              float* __restrict__ denom) {
   const int i = blockIdx.x * kMapBlock + threadIdx.x;
   if (i >= P) return;
-  const int r = radii[i];
-  if (r <= 0) return;
-  max_radii[i] = fmaxf(max_radii[i], (float)r);
-  const float gx = m2d_grad[3 * (size_t)i], gy = m2d_grad[3 * (size_t)i + 1];
-  accum[i] += sqrtf(gx * gx + gy * gy);
-  denom[i] += 1.f;
+  densify_stats_one(i, DensifyJob{radii, m2d_grad, max_radii, accum, denom});
 }
 
 }  // namespace
@@ -226,8 +240,29 @@ int wgsr_gaussian_activate_backward(int P, const float* opacity_raw, const float
     return set_error(WGSR_EINVAL, "wgsr_gaussian_activate_backward: null pointer");
   hipLaunchKernelGGL(k_activate_bwd, dim3(wgsr_map_blocks(P)), dim3(kMapBlock), 0, (hipStream_t)stream, P,
                      opacity_raw, scaling_raw, rotation_raw, dL_dopacity, dL_dscales, dL_drotations, iso_weight,
-                     dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw);
+                     dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw,
+                     DensifyJob{nullptr, nullptr, nullptr, nullptr, nullptr});
   MAPCHK("wgsr_gaussian_activate_backward");
+  return WGSR_OK;
+}
+
+int wgsr_gaussian_activate_backward_stats(int P, const float* opacity_raw, const float* scaling_raw,
+                                          const float* rotation_raw, const float* dL_dopacity,
+                                          const float* dL_dscales, const float* dL_drotations, float iso_weight,
+                                          float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+                                          const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
+                                          float* grad_accum, float* denom, void* stream) {
+  if (P < 0) return set_error(WGSR_EINVAL, "wgsr_gaussian_activate_backward_stats: negative P");
+  if (P == 0) return WGSR_OK;
+  if (!opacity_raw || !scaling_raw || !rotation_raw || !dL_dopacity || !dL_dscales || !dL_drotations ||
+      !dL_dopacity_raw || !dL_dscaling_raw || !dL_drotation_raw || !radii || !dL_dmeans2D || !max_radii2D ||
+      !grad_accum || !denom)
+    return set_error(WGSR_EINVAL, "wgsr_gaussian_activate_backward_stats: null pointer");
+  hipLaunchKernelGGL(k_activate_bwd, dim3(wgsr_map_blocks(P)), dim3(kMapBlock), 0, (hipStream_t)stream, P,
+                     opacity_raw, scaling_raw, rotation_raw, dL_dopacity, dL_dscales, dL_drotations, iso_weight,
+                     dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw,
+                     DensifyJob{radii, dL_dmeans2D, max_radii2D, grad_accum, denom});
+  MAPCHK("wgsr_gaussian_activate_backward_stats");
   return WGSR_OK;
 }
 

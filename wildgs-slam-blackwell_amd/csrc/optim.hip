@@ -268,17 +268,36 @@ __global__ __launch_bounds__(256) void k_gather_rows(GatherBatch b) {
 // k_adam_multi) unless either skip word is set, plus the overflow
 // bookkeeping of the capacity-mode forward: sticky[0] += counts[3],
 // sticky[1] = max(sticky[1], counts[0]).
+// The gradient is the sum of nparts (a, b) rows (the loss backward's
+// per-block partials), added in a fixed order: lane l sums rows l, l + 64,
+// ..., then a butterfly over the wave.
 __global__ __launch_bounds__(64) void k_exposure_step(float* __restrict__ bank, const int64_t* __restrict__ idx,
-                                                      const float* __restrict__ grad, const float* __restrict__ sc,
+                                                      const float* __restrict__ grad, int nparts,
+                                                      const float* __restrict__ sc,
                                                       const uint32_t* __restrict__ skip_a,
                                                       const uint32_t* __restrict__ skip_b, float w1, float beta2,
                                                       float w2, float eps, long long* __restrict__ sticky,
                                                       const uint32_t* __restrict__ counts) {
   const int l = threadIdx.x;
+  float ga = 0.f, gb = 0.f;
+  if (nparts == 1) {
+    ga = grad[0];
+    gb = grad[1];
+  } else {
+    for (int r = l; r < nparts; r += 64) {
+      ga += grad[2 * r];
+      gb += grad[2 * r + 1];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      ga += __shfl_xor(ga, off, 64);
+      gb += __shfl_xor(gb, off, 64);
+    }
+  }
   if (l < 2 && !(*skip_a | *skip_b)) {
     float* row = bank + 6 * idx[0];  // (a, b), exp_avg (a, b), exp_avg_sq (a, b)
     float p = row[l], m = row[2 + l], v = row[4 + l];
-    adam_elem(p, grad[l], m, v, w1, beta2, w2, eps, -sc[0], sc[1]);
+    adam_elem(p, l == 0 ? ga : gb, m, v, w1, beta2, w2, eps, -sc[0], sc[1]);
     row[l] = p;
     row[2 + l] = m;
     row[4 + l] = v;
@@ -360,12 +379,12 @@ int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, voi
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_gather_rows: %s", hipGetErrorString(e));
 }
 
-int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, const float* scalars,
+int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, int nparts, const float* scalars,
                        const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
                        int64_t* sticky, const uint32_t* counts, void* stream) {
-  if (!bank || !idx || !grad || !scalars || !skip_a || !skip_b)
-    return set_error(WGSR_EINVAL, "wgsr_exposure_step: null pointer");
-  hipLaunchKernelGGL(k_exposure_step, dim3(1), dim3(64), 0, (hipStream_t)stream, bank, idx, grad, scalars, skip_a,
+  if (!bank || !idx || !grad || !scalars || !skip_a || !skip_b || nparts < 1)
+    return set_error(WGSR_EINVAL, "wgsr_exposure_step: null pointer or no gradient rows");
+  hipLaunchKernelGGL(k_exposure_step, dim3(1), dim3(64), 0, (hipStream_t)stream, bank, idx, grad, nparts, scalars, skip_a,
                      skip_b, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
                      reinterpret_cast<long long*>(sticky), counts);
   const hipError_t e = hipGetLastError();

@@ -212,22 +212,8 @@ __global__ __launch_bounds__(256) void k_ssim_reduce(const float* __restrict__ p
                                                      int tiles, double inv_plane_px, float* __restrict__ plane_mean,
                                                      float* __restrict__ mean) {
   __shared__ double s_red[256];
-  double total = 0.0;
-  for (int64_t p = 0; p < planes; ++p) {
-    double v = 0.0;
-    for (int i = threadIdx.x; i < tiles; i += 256) v += partial[p * tiles + i];
-    s_red[threadIdx.x] = v;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if ((int)threadIdx.x < s) s_red[threadIdx.x] += s_red[threadIdx.x + s];
-      __syncthreads();
-    }
-    const double ps = s_red[0];
-    __syncthreads();
-    total += ps;
-    if (threadIdx.x == 0 && plane_mean) plane_mean[p] = (float)(ps * inv_plane_px);
-  }
-  if (threadIdx.x == 0) mean[0] = (float)(total * inv_plane_px / (double)planes);
+  const float m = ssim_partials_mean(partial, planes, tiles, inv_plane_px, plane_mean, s_red);
+  if (threadIdx.x == 0) mean[0] = m;
 }
 
 template <int R>
@@ -360,6 +346,22 @@ int wgsr_ssim_forward(const float* img1, const float* img2, int64_t planes, int 
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_ssim_forward: %s", hipGetErrorString(e));
 }
+
+int wgsr_ssim_forward_partials(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
+                               float* dmap, float* partials, void* stream) {
+  if (planes <= 0 || H <= 0 || W <= 0 || planes > 65535 || !window_ok(window_size))
+    return set_error(WGSR_EINVAL, "wgsr_ssim_forward_partials: bad shape or window %d", window_size);
+  if (!img1 || !img2 || !partials) return set_error(WGSR_EINVAL, "wgsr_ssim_forward_partials: null pointer");
+  const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, (unsigned)planes);
+  const Window win = make_window(window_size);
+  const int64_t all = planes * (int64_t)H * W;
+  WGSR_SSIM_DISPATCH(window_size, k_ssim_fwd, grid, dim3(256), 0, (hipStream_t)stream, img1, img2, H, W, win, dmap,
+                     all, partials);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_ssim_forward_partials: %s", hipGetErrorString(e));
+}
+
+int wgsr_ssim_tiles(int H, int W) { return (H > 0 && W > 0) ? ((W + kTW - 1) / kTW) * ((H + kTH - 1) / kTH) : 0; }
 
 int wgsr_ssim_backward(const float* img1, const float* img2, int64_t planes, int H, int W, int window_size,
                        const float* dmap, const float* plane_scale, float* grad_img1, void* stream) {

@@ -352,9 +352,16 @@ __global__ __launch_bounds__(kCombine) void k_unc_combine(int HW, int hw, const 
                                                           const float* __restrict__ extra, int nextra, float w_extra,
                                                           float alpha, float lam, float ssim_mult, int ssim_loss,
                                                           float* __restrict__ loss, float* __restrict__ sums,
-                                                          float* __restrict__ ssim_scale) {
+                                                          float* __restrict__ ssim_scale,
+                                                          const float* __restrict__ ssim_partials, int ssim_tiles,
+                                                          float* __restrict__ ssim_mean_out) {
   __shared__ float sred[5][kCombine / 64];
+  __shared__ double s_dred[256];
   const int t = threadIdx.x;
+  // (ssim_partials: the SSIM forward's 3-plane tile partials, reduced here
+  // as k_ssim_reduce would -- one launch fewer)
+  float smean = 0.f;
+  if (ssim_partials) smean = ssim_partials_mean(ssim_partials, 3, ssim_tiles, 1.0 / (double)HW, nullptr, s_dred);
   float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int i = t; i < nb; i += kCombine) {
     v[0] += lpart[3 * i];
@@ -379,7 +386,9 @@ __global__ __launch_bounds__(kCombine) void k_unc_combine(int HW, int hw, const 
   }
   const float s0 = r[0], s1 = r[1], s2 = r[2], u = r[3], x = r[4];
   const float n3 = 3.f * (float)HW;
-  const float rgb = ssim_loss ? ((1.f - lam) * s0 + 3.f * lam * (1.f - ssim_mean[0]) * s1) / n3 : s0 / n3;
+  if (ssim_partials && ssim_mean_out) ssim_mean_out[0] = smean;
+  const float sm = ssim_partials ? smean : (ssim_loss ? ssim_mean[0] : 0.f);
+  const float rgb = ssim_loss ? ((1.f - lam) * s0 + 3.f * lam * (1.f - sm) * s1) / n3 : s0 / n3;
   loss[0] = alpha * rgb + (1.f - alpha) * s2 / (float)HW + ssim_mult * (u / (float)hw) + w_extra * x;
   sums[0] = s0;
   sums[1] = s1;
@@ -473,8 +482,27 @@ int wgsr_uncer_loss_combine(const wgsr_uncer_params* prm, const float* partials,
   hipLaunchKernelGGL(k_unc_combine, dim3(1), dim3(kCombine), 0, (hipStream_t)stream, prm->H * prm->W,
                      prm->h * prm->w, partials, ublocks((int64_t)prm->H * prm->W), small_partials,
                      ublocks((int64_t)prm->h * prm->w), ssim_mean, n_extra > 0 ? extra_partials : nullptr, n_extra,
-                     extra_weight, alpha, lambda_dssim, ssim_mult, ssim_loss, loss, sums, ssim_scale);
+                     extra_weight, alpha, lambda_dssim, ssim_mult, ssim_loss, loss, sums, ssim_scale, nullptr, 0,
+                     nullptr);
   UNCCHK("wgsr_uncer_loss_combine");
+  return WGSR_OK;
+}
+
+int wgsr_uncer_loss_combine_ssim(const wgsr_uncer_params* prm, const float* partials, const float* small_partials,
+                                 const float* ssim_partials, float* ssim_mean, const float* extra_partials,
+                                 int n_extra, float extra_weight, float alpha, float lambda_dssim, float ssim_mult,
+                                 float* loss, float* sums, float* ssim_scale, void* stream) {
+  if (int e = check_params(prm, "wgsr_uncer_loss_combine_ssim")) return e;
+  if (!partials || !small_partials || !ssim_partials || !loss || !sums || !ssim_scale ||
+      (n_extra > 0 && !extra_partials))
+    return set_error(WGSR_EINVAL, "wgsr_uncer_loss_combine_ssim: null pointer");
+  const int tiles = wgsr_ssim_tiles(prm->H, prm->W);
+  hipLaunchKernelGGL(k_unc_combine, dim3(1), dim3(kCombine), 0, (hipStream_t)stream, prm->H * prm->W,
+                     prm->h * prm->w, partials, ublocks((int64_t)prm->H * prm->W), small_partials,
+                     ublocks((int64_t)prm->h * prm->w), nullptr, n_extra > 0 ? extra_partials : nullptr, n_extra,
+                     extra_weight, alpha, lambda_dssim, ssim_mult, 1, loss, sums, ssim_scale, ssim_partials, tiles,
+                     ssim_mean);
+  UNCCHK("wgsr_uncer_loss_combine_ssim");
   return WGSR_OK;
 }
 

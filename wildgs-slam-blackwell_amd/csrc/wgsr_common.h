@@ -44,6 +44,34 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// SSIM tile partials -> per-plane means and the overall mean, sums in double
+// in a fixed order: threads t < 256 stride over a plane's tiles, then a
+// tree over the 256 values (k_ssim_reduce; k_unc_combine runs the same
+// sequence, so both give the same bits).  Every thread of the block calls it
+// (blockDim >= 256); s_red: 256 doubles of LDS.  Returns the mean (all threads).
+__device__ __forceinline__ float ssim_partials_mean(const float* __restrict__ partial, int64_t planes, int tiles,
+                                                    double inv_plane_px, float* __restrict__ plane_mean,
+                                                    double* s_red) {
+  const int t = threadIdx.x;
+  double total = 0.0;
+  for (int64_t p = 0; p < planes; ++p) {
+    double v = 0.0;
+    if (t < 256)
+      for (int i = t; i < tiles; i += 256) v += partial[p * tiles + i];
+    if (t < 256) s_red[t] = v;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (t < st) s_red[t] += s_red[t + st];
+      __syncthreads();
+    }
+    const double ps = s_red[0];
+    __syncthreads();
+    total += ps;
+    if (t == 0 && plane_mean) plane_mean[p] = (float)(ps * inv_plane_px);
+  }
+  return (float)(total * inv_plane_px / (double)planes);
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);

@@ -142,6 +142,9 @@ def load():
         L.wgsr_map_blocks.argtypes = [c_i64]
         L.wgsr_gaussian_activate.restype = c_int
         L.wgsr_gaussian_activate.argtypes = [c_int] + [_fp] * 7 + [_fp]
+        L.wgsr_gaussian_activate_backward_stats.restype = c_int
+        L.wgsr_gaussian_activate_backward_stats.argtypes = ([c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 8
+                                                            + [_fp])
         L.wgsr_gaussian_activate_backward.restype = c_int
         L.wgsr_gaussian_activate_backward.argtypes = [c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 3 + [_fp]
         L.wgsr_mapping_loss_forward.restype = c_int
@@ -230,13 +233,20 @@ def load():
         L.wgsr_mlp_backward_seg2.restype = c_int
         L.wgsr_mlp_backward_seg2.argtypes = ([c_int, c_int, c_int] + [_fp] * 4 + [ctypes.c_float] + [_fp] * 5
                                              + [ctypes.c_float, ctypes.c_float, c_int, _fp, _fp, _fp])
+        L.wgsr_ssim_forward_partials.restype = c_int
+        L.wgsr_ssim_forward_partials.argtypes = [_fp, _fp, c_i64, c_int, c_int, c_int, _fp, _fp, _fp]
+        L.wgsr_ssim_tiles.restype = c_int
+        L.wgsr_ssim_tiles.argtypes = [c_int, c_int]
+        L.wgsr_uncer_loss_combine_ssim.restype = c_int
+        L.wgsr_uncer_loss_combine_ssim.argtypes = ([U] + [_fp] * 5 + [c_int] + [ctypes.c_float] * 4
+                                                   + [_fp] * 3 + [_fp])
         L.wgsr_mlp_backward_acc.restype = c_int
         L.wgsr_mlp_backward_acc.argtypes = ([c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 4
                                             + [ctypes.c_float, c_int, _fp, _fp, _fp])
         L.wgsr_gather_rows.restype = c_int
         L.wgsr_gather_rows.argtypes = [ctypes.POINTER(GatherJob), c_int, _fp, _fp]
         L.wgsr_exposure_step.restype = c_int
-        L.wgsr_exposure_step.argtypes = [_fp] * 6 + [ctypes.c_double] * 3 + [_fp, _fp, _fp]
+        L.wgsr_exposure_step.argtypes = [_fp] * 3 + [c_int] + [_fp] * 3 + [ctypes.c_double] * 3 + [_fp, _fp, _fp]
         L.wgsr_mlp_backward.restype = c_int
         L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
         L.wgsr_dino_reg.restype = c_int
@@ -305,7 +315,9 @@ EXPORTED_SYMBOLS = (
     "wgsr_adam_step", "wgsr_adam_step_dev", "wgsr_compact_rows",
     "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
     "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_random_perm_prefix_max_n", "wgsr_random_perm_prefix_max_k",
-    "wgsr_random_perm_prefix", "wgsr_mlp_forward_seg2", "wgsr_mlp_backward_seg2", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
+    "wgsr_random_perm_prefix", "wgsr_mlp_forward_seg2", "wgsr_mlp_backward_seg2",
+    "wgsr_gaussian_activate_backward_stats", "wgsr_ssim_forward_partials", "wgsr_ssim_tiles",
+    "wgsr_uncer_loss_combine_ssim", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",

@@ -260,12 +260,11 @@ class MappingStep:
             cam["campos"], geom, nr, binning, img, False, out=out)
         dL_dmeans2D, dL_dtau = g[0], g[8]
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_gaussian_activate_backward(
+            _lib.check(L.wgsr_gaussian_activate_backward_stats(
                 self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
                 p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
-                p(self.grad["scaling"]), p(self.grad["rotation"]), st))
-            _lib.check(L.wgsr_densification_stats(self.P, p(radii), p(dL_dmeans2D), p(self.max_radii2D),
-                                                  p(self.xyz_gradient_accum), p(self.denom), st))
+                p(self.grad["scaling"]), p(self.grad["rotation"]), p(radii), p(dL_dmeans2D), p(self.max_radii2D),
+                p(self.xyz_gradient_accum), p(self.denom), st))
         return dL_dmeans2D, (dL_dtau.sum(0) if need_tau else None)
 
     def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
@@ -328,7 +327,8 @@ class MappingStep:
                                      train_frac: float, ssim_frac: float, config: dict | None = None,
                                      initialization: bool = False, freeze_uncertainty_loss: bool = False,
                                      median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True,
-                                     cap: int | None = None, counts=None, need_tau: bool = True):
+                                     cap: int | None = None, counts=None, need_tau: bool = True,
+                                     exposure_partials: bool = False):
         """The reference's DEFAULT mapping iteration (uncertainty_params.activate):
         get_loss_mapping_uncertainty (slam_utils.py:146-258) + 10 * isotropic
         loss, and their backward.
@@ -356,7 +356,9 @@ class MappingStep:
         ``gt_depth.median()`` (constant per keyframe).  ``full_resolution``
         (depth rendered at another size) is not supported.  ``cap`` /
         ``counts``: the capacity-mode forward (no host wait; graph capture,
-        wgsr.online).  Returns the dict of
+        wgsr.online).  ``exposure_partials``: the exposure gradient as the loss
+        backward's per-block (a, b) partial sums (``dexposure_partials``
+        [n, 2], for wgsr_exposure_step) instead of its sum.  Returns the dict of
         ``forward_backward`` plus ``uncertainty_grad`` and ``uncertainty_loss``."""
         from . import uncertainty as U
         cfg = U.flatten_config(config)
@@ -368,10 +370,14 @@ class MappingStep:
         loss, state = U.loss_forward(image, depth, opac_img, gt_image, gt_depth, exposure_a, exposure_b, uncertainty,
                                      train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
                                      median_depth, extra=(self.iso_part, w_iso), pre_exposed=pre_exposed)
-        d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state)
+        d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state, exposure_partials=exposure_partials)
         _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso, need_tau)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:
             uncertainty.backward(d_unc.to(uncertainty.dtype))
+        if exposure_partials:
+            return {"loss": loss, "dexposure_partials": d_a, "radii": radii, "image": image, "depth": depth,
+                    "num_rendered": nr, "uncertainty_grad": d_unc, "uncertainty_loss": state.uncertainty_loss,
+                    "drho": tau[:3] if tau is not None else None, "dtheta": tau[3:] if tau is not None else None}
         return {"loss": loss, "dexposure_a": d_a, "dexposure_b": d_b,
                 "drho": tau[:3] if tau is not None else None, "dtheta": tau[3:] if tau is not None else None,
                 "radii": radii, "image": image, "depth": depth, "num_rendered": nr, "uncertainty_grad": d_unc,

@@ -317,7 +317,8 @@ class OnlineMapper:
         from . import _lib
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         L = _lib.load()
-        if k is not None and n <= int(L.wgsr_random_perm_prefix_max_n()) and k <= int(L.wgsr_random_perm_prefix_max_k()):
+        if (k is not None and n <= int(L.wgsr_random_perm_prefix_max_n())
+                and k <= int(L.wgsr_random_perm_prefix_max_k())):
             perm = torch.empty(max(k, 1), dtype=torch.int32, device=self.dev)
             with torch.cuda.device(self.dev):
                 _lib.check(L.wgsr_random_perm_prefix(n, k, seed, None, _lib.ptr(perm), _lib.stream_handle(self.dev)))
@@ -347,6 +348,42 @@ class OnlineMapper:
         sf = buf[perm].unsqueeze(0)
         (c["reg_mult"] * dino_regularization_loss(self.net(sf), sf)).backward()
 
+    def _mlp_pair_ok(self) -> bool:
+        """The MLP's two forwards / backwards batched into one launch each
+        (the graph-replayed iteration's arithmetic) unless a test feeds the
+        random draws."""
+        return self.net.seed_source is None and "_perm" not in self.__dict__ and self.dev.type == "cuda"
+
+    def _mlp_pair_loss(self, kf, neighbours, fb):
+        """One iteration's uncertainty MLP + loss + DINO term with both MLP
+        passes batched (wgsr.mlp.forward_raw2 / backward_raw2), the draws in
+        the eager order (the keyframe forward's dropout seed, the sample's
+        permutation seed, the sample forward's seed): ``fb(unc)`` runs the
+        rasteriser loss on the uncertainty map and returns its dict; the MLP
+        gradient (loss + reg_mult x DINO) lands in the parameters' .grad."""
+        from .mlp import backward_raw2, forward_raw2
+        from .uncertainty import dino_reg_raw
+        c = self.cfg
+        h, w, C = kf.features.shape
+        s1 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        buf = torch.stack([self.keyframes[k].features for k in neighbours]).view(-1, C)
+        ns = buf.shape[0] // (c["reg_stride"] ** 4)
+        perm = self._perm(buf.shape[0], ns)
+        s2 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        sf = buf[perm].contiguous()
+        seeds = torch.tensor([s1, s2], dtype=torch.int32).to(self.dev, non_blocking=True)
+        u_all, sv = forward_raw2(self.net, kf.features.reshape(h * w, C), sf, seeds[0:1], seeds[1:2])
+        out = fb(u_all[:h * w].view(h, w))
+        _, gu = dino_reg_raw(u_all[h * w:], sf)
+        G = backward_raw2(sv, out["uncertainty_grad"].reshape(-1).contiguous(), gu, 1.0, float(c["reg_mult"]))
+        off = 0
+        for prm in self.net.parameters():
+            k = prm.numel()
+            g = G[off:off + k].view_as(prm)
+            prm.grad = g if prm.grad is None else prm.grad + g
+            off += k
+        return out
+
     # ---- one optimisation iteration ------------------------------------------
     def _iteration(self, kf: Keyframe, neighbours, initialization: bool, update: bool, reset: str | None,
                    occ_window=None):
@@ -365,14 +402,18 @@ class OnlineMapper:
                                                       [kf.features[::st, ::st]])).backward(retain_graph=True)
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, ea, eb, self.bg, unc,
                                                   c["train_frac_fix"], c["train_frac_fix"], initialization=True,
-                                                  median_depth=kf.median_depth, need_tau=False)
+                                                  median_depth=kf.median_depth, need_tau=False, exposure_partials=True)
+        elif self.iterations_after_densify_or_reset >= 20 and self._mlp_pair_ok():
+            out = self._mlp_pair_loss(kf, neighbours, lambda unc: ms.forward_backward_uncertainty(
+                kf.cam, kf.image, kf.depth, ea, eb, self.bg, unc, c["train_frac_fix"], c["train_frac_fix"],
+                freeze_uncertainty_loss=False, median_depth=kf.median_depth, need_tau=False, exposure_partials=True))
         else:
             unc = self.net(kf.features)
             freeze = self.iterations_after_densify_or_reset < 20
             out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, ea, eb, self.bg, unc,
                                                   c["train_frac_fix"], c["train_frac_fix"],
                                                   freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
-                                                  need_tau=False)
+                                                  need_tau=False, exposure_partials=True)
             if self.iterations_after_densify_or_reset >= 20:
                 self._dino_term(neighbours, kf)
         self._max_nr = max(self._max_nr, int(out["num_rendered"]))
@@ -415,12 +456,24 @@ class OnlineMapper:
         from . import _lib
         self.kopt_steps[kf.uid] += 1
         n = self.kopt_steps[kf.uid]
+        lr = self.cfg["exposure_lr"]
+        L = _lib.load()
+        p = _lib.ptr
+        if "dexposure_partials" in out:  # the loss backward's per-block partials, summed in the step (as replays do)
+            g = out["dexposure_partials"]
+            hs = np.zeros(6, dtype=np.float32)
+            hs[0], hs[1] = lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)
+            hs[2:4].view(np.int64)[0] = self.bank.slots[kf.uid]
+            dv = torch.from_numpy(hs).to(self.dev, non_blocking=True)
+            with torch.cuda.device(self.dev):
+                _lib.check(L.wgsr_exposure_step(p(self.bank.ex), p(dv[2:4]), p(g), int(g.shape[0]), p(dv[0:2]),
+                                                p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None,
+                                                _lib.stream_handle(self.dev)))
+            return
         da, db = out["dexposure_a"], out["dexposure_b"]
         g = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
         prm, m, v = self.bank.ex_ptrs(kf.uid)
-        lr = self.cfg["exposure_lr"]
         t = _lib.AdamTensor(prm, g.data_ptr(), m, v, 2, lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n))
-        L = _lib.load()
         with torch.cuda.device(self.dev):
             _lib.check(L.wgsr_adam_step((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, _lib.stream_handle(self.dev)))
 
@@ -529,15 +582,23 @@ class OnlineMapper:
                 continue
             self.iteration_count += 1
             self.iterations_after_densify_or_reset += 1
-            unc = self.net(kf.features)
-            freeze = self.iterations_after_densify_or_reset < 200
-            out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg,
-                                                  unc, c["train_frac_fix"], c["train_frac_fix"],
-                                                  freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
-                                                  pre_exposed=False, need_tau=False)
-            self._max_nr = max(self._max_nr, int(out["num_rendered"]))
-            if self.iterations_after_densify_or_reset >= 200:
-                self._dino_term([stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))], kf)
+            nbrs = [stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))]
+            if self.iterations_after_densify_or_reset >= 200 and self._mlp_pair_ok():
+                out = self._mlp_pair_loss(kf, nbrs, lambda unc: ms.forward_backward_uncertainty(
+                    kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg, unc, c["train_frac_fix"],
+                    c["train_frac_fix"], freeze_uncertainty_loss=False, median_depth=kf.median_depth,
+                    pre_exposed=False, need_tau=False, exposure_partials=True))
+                self._max_nr = max(self._max_nr, int(out["num_rendered"]))
+            else:
+                unc = self.net(kf.features)
+                freeze = self.iterations_after_densify_or_reset < 200
+                out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b,
+                                                      self.bg, unc, c["train_frac_fix"], c["train_frac_fix"],
+                                                      freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
+                                                      pre_exposed=False, need_tau=False, exposure_partials=True)
+                self._max_nr = max(self._max_nr, int(out["num_rendered"]))
+                if self.iterations_after_densify_or_reset >= 200:
+                    self._dino_term(nbrs, kf)
             ms.optimizer_step()
             ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
                                      lr_delay_mult=c["position_lr_delay_mult"], max_steps=c["position_lr_max_steps"])

@@ -348,7 +348,7 @@ class IterationGraphs:
                                               u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
                                               freeze_uncertainty_loss=False, median_depth=S.med,
                                               pre_exposed=not refine, cap=self.cap, counts=self.counts,
-                                              need_tau=False)
+                                              need_tau=False, exposure_partials=True)
         du = out["uncertainty_grad"].reshape(-1).contiguous()
         if ns > 0:
             _, gu = dino_reg_raw(u2, sf)
@@ -360,10 +360,10 @@ class IterationGraphs:
         # unless the window optimiser holds it; also the overflow bookkeeping),
         # the MLP (L2 weight decay)
         ms.optimizer_step_dev(ms.adam_tensors(), self.f32[self.F_GAUSS:self.F_GAUSS + 15], skip)
-        da, db = out["dexposure_a"], out["dexposure_b"]
-        gex = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
+        gex = out["dexposure_partials"]  # (summed inside the exposure step)
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), p(self.f32[self.F_EXPO:self.F_EXPO + 2]),
+            _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), int(gex.shape[0]),
+                                            p(self.f32[self.F_EXPO:self.F_EXPO + 2]),
                                             p(skip), p(self.i32[self.F_EXSKIP:self.F_EXSKIP + 1]), 0.9, 0.999, 1e-8,
                                             p(self.sticky), p(self.counts), st))
         ts, off = [], 0

@@ -134,7 +134,7 @@ def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, u
     opacity = opacity.detach().contiguous()
     gt = gt.detach().contiguous()
     ref = ref_depth.detach().contiguous()
-    z = torch.zeros(1, device=dev)
+    z = torch.zeros(1, device=dev) if initialization else None  # (no fill launch otherwise)
     ea = z if initialization else exposure_a.detach().to(torch.float32).reshape(1).contiguous()
     eb = z if initialization else exposure_b.detach().to(torch.float32).reshape(1).contiguous()
     unc = uncertainty.detach().contiguous()
@@ -156,12 +156,11 @@ def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, u
         _lib.check(L.wgsr_uncer_loss_forward(ctypes.byref(prm), p(image), p(gt), p(depth), p(ref), p(ea), p(eb),
                                              p(unc), p(med), p(image_ab), p(lpart), st))
         if cfg["ssim_loss"]:
+            # (tile partials only: the epilogue launch below reduces them)
             ssim_dmap = torch.empty(3 * 3 * HW, device=dev)
-            ssim_plane = torch.empty(3, device=dev)
+            ssim_part = torch.empty(3 * int(L.wgsr_ssim_tiles(H, W)), device=dev)
             ssim_mean = torch.empty((), device=dev)
-            with _lib.AllocRequest(dev):
-                _lib.check(L.wgsr_ssim_forward(p(image_ab), p(gt), 3, H, W, 11, p(ssim_dmap), p(ssim_plane),
-                                               p(ssim_mean), _lib.ALLOC_SCRATCH, None, st))
+            _lib.check(L.wgsr_ssim_forward_partials(p(image_ab), p(gt), 3, H, W, 11, p(ssim_dmap), p(ssim_part), st))
         # compute_ssim_components(gt_img, rendered_img) at full resolution, then
         # the feature-resolution maps of the uncertainty loss
         _lib.check(L.wgsr_ssim_components(p(gt), p(image_ab), 1, 3, H, W, int(cfg["ssim_window_size"]),
@@ -176,19 +175,27 @@ def loss_forward(image, depth, opacity, gt, ref_depth, exposure_a, exposure_b, u
     ssim_scale = torch.empty(3, device=dev)
     ex, exw = (None, 0.0) if extra is None else (extra[0].contiguous(), float(extra[1]))
     with torch.cuda.device(dev):
-        _lib.check(L.wgsr_uncer_loss_combine(ctypes.byref(prm), p(lpart), p(upart), p(ssim_mean), p(ex),
-                                             0 if ex is None else ex.numel(), exw, float(cfg["alpha"]),
-                                             float(cfg["lambda_dssim"]), float(cfg["ssim_mult"]),
-                                             int(bool(cfg["ssim_loss"])), p(loss), p(sums), p(ssim_scale), st))
+        if cfg["ssim_loss"]:
+            _lib.check(L.wgsr_uncer_loss_combine_ssim(ctypes.byref(prm), p(lpart), p(upart), p(ssim_part),
+                                                      p(ssim_mean), p(ex), 0 if ex is None else ex.numel(), exw,
+                                                      float(cfg["alpha"]), float(cfg["lambda_dssim"]),
+                                                      float(cfg["ssim_mult"]), p(loss), p(sums), p(ssim_scale), st))
+        else:
+            _lib.check(L.wgsr_uncer_loss_combine(ctypes.byref(prm), p(lpart), p(upart), p(ssim_mean), p(ex),
+                                                 0 if ex is None else ex.numel(), exw, float(cfg["alpha"]),
+                                                 float(cfg["lambda_dssim"]), float(cfg["ssim_mult"]),
+                                                 int(bool(cfg["ssim_loss"])), p(loss), p(sums), p(ssim_scale), st))
     state = LossState(prm, cfg, image, image_ab, gt, depth, ref, ea, eb, unc, med, sums, ssim_dmap, d_unc, uloss,
                       ssim_scale)
     return loss, state
 
 
-def loss_backward(s: LossState, loss_grad=None):
+def loss_backward(s: LossState, loss_grad=None, exposure_partials: bool = False):
     """-> (dL/dimage [3,H,W], dL/ddepth [1,H,W], dL/dexposure_a [1],
     dL/dexposure_b [1], dL/duncertainty [h,w]) for dL/dloss = loss_grad
-    (0-d device tensor; None = 1)."""
+    (0-d device tensor; None = 1).  ``exposure_partials``: the exposure
+    gradient as its per-block (a, b) partial sums [n, 2] in place of
+    dL/dexposure_a, and None for dL/dexposure_b (no summing launch)."""
     L = _lib.load()
     dev = s.image.device
     st = _lib.stream_handle(dev)
@@ -213,8 +220,12 @@ def loss_backward(s: LossState, loss_grad=None):
                                               p(s.ref), p(s.ea), p(s.eb), p(s.unc), p(s.med), float(w_rgb),
                                               float((1.0 - alpha) / HW), p(lg), p(ssim_grad), p(d_image), p(d_depth),
                                               p(epart), st))
-    esum = epart.sum(0)
     d_unc = s.d_unc if lg is None else s.d_unc * lg[0]
+    if exposure_partials:
+        if s.prm.initialization:
+            epart.zero_()
+        return d_image, d_depth, epart, None, d_unc
+    esum = epart.sum(0)
     if s.prm.initialization:
         esum = torch.zeros_like(esum)
     return d_image, d_depth, esum[0:1], esum[1:2], d_unc
