@@ -467,7 +467,8 @@ int wgsr_mlp_backward(int N, int C, const float* X, const float* W2, const float
  * min(top_k, N) most similar samples with cosine similarity > thresh, and
  * grad_u [N] = d loss / d u (zeroed by the call; float atomics, so the
  * order of its adds is not fixed).  Scratch: fn [N, C], sim [N, N], row_var
- * [N].  N <= 16384, thresh > 0. */
+ * [N].  N <= 16384, thresh > 0.  loss may be NULL: the gradient only (one
+ * launch fewer). */
 int wgsr_dino_reg(const float* u, const float* feat, int N, int C, int top_k, float thresh, float eps,
                   float* fn_scratch, float* sim_scratch, float* row_var, float* grad_u, float* loss, void* stream);
 

@@ -223,6 +223,21 @@ def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
         np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6 * float(np.abs(b).max() + 1e-30), err_msg=k)
 
 
+@pytest.mark.parametrize("P", [300_000, 600_000])
+def test_compact_backward_large_workgroups(P, monkeypatch):
+    """k_gauss_bwd_compact with 512 / 1024 Gaussians per workgroup (chosen
+    from P so that the grid is one resident round) against the two-kernel
+    sparse path on the same records (no CPU restatement at this size)."""
+    inputs, settings, grads = _synthetic(P, 640, 480, 1, 1)
+    monkeypatch.setenv("WGSR_GB", "sparse")
+    a = run_c(inputs, settings, grads)
+    monkeypatch.setenv("WGSR_GB_COMPACT", "0")
+    b = run_c(inputs, settings, grads)
+    for k in GRAD_KEYS + ("dL_dtau", "dL_dcov3D"):
+        np.testing.assert_array_equal(a[k] == 0, b[k] == 0, err_msg=f"{k} zero rows")
+        np.testing.assert_allclose(a[k], b[k], rtol=2e-6, atol=2e-6 * float(np.abs(b[k]).max() + 1e-30), err_msg=k)
+
+
 @pytest.mark.parametrize("P,W,H,deg,view", [(20_000, 640, 480, 3, 2), (6_000, 200, 136, 1, 1),
                                             (30_000, 1000, 120, 0, 0)])
 def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):

@@ -252,7 +252,7 @@ int wgsr_dino_reg(const float* u, const float* feat, int N, int C, int top_k, fl
   if (N <= 0 || C <= 0 || top_k <= 0 || N > 16384)
     return set_error(WGSR_EINVAL, "wgsr_dino_reg: bad shape N=%d C=%d k=%d", N, C, top_k);
   if (!(thresh > 0.f)) return set_error(WGSR_EINVAL, "wgsr_dino_reg: the threshold must be positive");
-  if (!u || !feat || !fn_scratch || !sim_scratch || !row_var || !grad_u || !loss)
+  if (!u || !feat || !fn_scratch || !sim_scratch || !row_var || !grad_u)
     return set_error(WGSR_EINVAL, "wgsr_dino_reg: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int K = top_k < N ? top_k : N;
@@ -265,7 +265,7 @@ int wgsr_dino_reg(const float* u, const float* feat, int N, int C, int top_k, fl
     hipLaunchKernelGGL(k_dino_similarity, dim3(tiles, tiles), dim3(256), 0, s, fn_scratch, N, C, sim_scratch);
   hipLaunchKernelGGL(k_dino_select, dim3(rows4), dim3(256), 0, s, sim_scratch, u, N, K, thresh, eps,
                      1.f / (float)N, row_var, grad_u);
-  hipLaunchKernelGGL(k_dino_mean, dim3(1), dim3(256), 0, s, row_var, N, loss);
+  if (loss) hipLaunchKernelGGL(k_dino_mean, dim3(1), dim3(256), 0, s, row_var, N, loss);  // (NULL: the gradient only)
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_dino_reg: %s", hipGetErrorString(e));
 }

@@ -1529,13 +1529,8 @@ __global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8)))
 // kernel would need.  (WGSR_GBC_FLAT=0: 16-lane groups per listed Gaussian
 // with a dependent slot-range load per group pass: 75 vs 65 us at 1M/1080p.)
 constexpr int kGbcThreads = 256;
-// Gaussians per workgroup = kGbcThreads x kGbcRounds (measured at 1M/1080p:
-// 256 -> 86 us, 512 -> 72 us, 1024 -> 86 us, 2048 -> 113 us; the two-kernel
-// sparse path k_sum_active + k_gauss_bwd: 89 us)
-#ifndef WGSR_GBC_ROUNDS
-#define WGSR_GBC_ROUNDS 2
-#endif
-constexpr int kGbcRounds = WGSR_GBC_ROUNDS;
+// Gaussians per workgroup = kGbcThreads x kR, kR chosen per launch (below;
+// the two-kernel sparse path k_sum_active + k_gauss_bwd: 89 us at 1M)
 // WGSR_GBC_PREFETCH=1 (A/B): the listed Gaussians' parameters load before the
 // record sums instead of after them
 #ifndef WGSR_GBC_PREFETCH
@@ -1986,16 +1981,27 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, con
   const char* ce = getenv("WGSR_GB_COMPACT");  // read per call: tests compare the sparse kernels
   if (sparse && zeroed && !(ce && strcmp(ce, "0") == 0)) {
     // (no pair listed: gflag is all zero and nothing is written)
-    // one round (256 Gaussians per workgroup) when two rounds would leave
-    // fewer than two workgroups per CU (the mapper's ~100k-Gaussian maps):
-    // the per-workgroup chain of dependent loads is the kernel's time there
     // (WGSR_GBC_R = 1..4 forces the rounds per workgroup: A/B)
     static const int force_r = [] {
       const char* e = getenv("WGSR_GBC_R");
       const int v = e ? atoi(e) : 0;
       return v >= 1 && v <= 4 ? v : 0;
     }();
-    const int nr = force_r ? force_r : (a.P < 256 * 1024 && kGbcRounds >= 2) ? 1 : kGbcRounds;
+    // the fewest Gaussians per workgroup (256, 512 or 1024) whose grid is ONE
+    // resident round at four workgroups per CU (LDS-limited): the chain of
+    // dependent loads per workgroup is the kernel's time, a second round
+    // doubles it (measured at 1M / 1080p: 1024 per workgroup 57-58 us, 512
+    // 63-64 us (two rounds), 768 68 us)
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                  hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    int nr = 1;
+    while (nr < 4 && (a.P + kGbcThreads * nr - 1) / (kGbcThreads * nr) > 4 * ncu) nr *= 2;
+    if (force_r) nr = force_r;
     const int span = kGbcThreads * nr;
     hipLaunchKernelGGL(nr == 1 ? k_gauss_bwd_compact<1> : nr == 2 ? k_gauss_bwd_compact<2>
                        : nr == 3 ? k_gauss_bwd_compact<3> : k_gauss_bwd_compact<4>,

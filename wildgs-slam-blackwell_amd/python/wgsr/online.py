@@ -374,7 +374,7 @@ class OnlineMapper:
         seeds = torch.tensor([s1, s2], dtype=torch.int32).to(self.dev, non_blocking=True)
         u_all, sv = forward_raw2(self.net, kf.features.reshape(h * w, C), sf, seeds[0:1], seeds[1:2])
         out = fb(u_all[:h * w].view(h, w))
-        _, gu = dino_reg_raw(u_all[h * w:], sf)
+        _, gu = dino_reg_raw(u_all[h * w:], sf, want_loss=False)
         G = backward_raw2(sv, out["uncertainty_grad"].reshape(-1).contiguous(), gu, 1.0, float(c["reg_mult"]))
         off = 0
         for prm in self.net.parameters():

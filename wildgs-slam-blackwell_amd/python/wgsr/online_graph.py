@@ -351,7 +351,7 @@ class IterationGraphs:
                                               need_tau=False, exposure_partials=True)
         du = out["uncertainty_grad"].reshape(-1).contiguous()
         if ns > 0:
-            _, gu = dino_reg_raw(u2, sf)
+            _, gu = dino_reg_raw(u2, sf, want_loss=False)
             G = backward_raw2(sv, du, gu, 1.0, float(c["reg_mult"]))
         else:
             G = backward_raw(sv, du)

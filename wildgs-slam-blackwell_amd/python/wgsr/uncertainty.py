@@ -288,9 +288,10 @@ DINO_SIMILARITY_THRESHOLD = 0.75
 DINO_EPS = float(torch.finfo(torch.float32).eps)
 
 
-def dino_reg_raw(u, feat):
+def dino_reg_raw(u, feat, want_loss: bool = True):
     """wgsr_dino_reg (csrc/dino.hip) on u [N], feat [N, C] (device, fp32,
-    contiguous): -> (loss 0-d, d loss / d u [N]), no autograd."""
+    contiguous): -> (loss 0-d, d loss / d u [N]), no autograd; without
+    ``want_loss`` the loss launch is skipped and None returned for it."""
     L = _lib.load()
     N, C = feat.shape
     dev = feat.device
@@ -298,7 +299,7 @@ def dino_reg_raw(u, feat):
     sim = torch.empty(N, N, device=dev)
     row_var = torch.empty(N, device=dev)
     grad_u = torch.empty(N, device=dev)
-    loss = torch.empty((), device=dev)
+    loss = torch.empty((), device=dev) if want_loss else None
     pt = _lib.ptr
     with torch.cuda.device(dev):
         _lib.check(L.wgsr_dino_reg(pt(u), pt(feat), N, C, DINO_TOP_K, DINO_SIMILARITY_THRESHOLD, DINO_EPS,
