@@ -530,6 +530,13 @@ int wgsr_adam_step(const wgsr_adam_tensor* tensors, int n, double beta1, double 
  * used is grad + weight_decay * param (0: none). */
 int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps,
                        double weight_decay, const float* scalars, const uint32_t* skip, void* stream);
+/* Two optimisers sharing beta1 / beta2 in one launch (the Gaussians' and the
+ * uncertainty MLP's in the mapping iteration): tensors [0, n1) step with
+ * eps1 / weight_decay1 / scalars1, tensors [n1, n) with eps2 /
+ * weight_decay2 / scalars2 (3 floats per tensor, from tensor n1 on). */
+int wgsr_adam_step_dev2(const wgsr_adam_tensor* tensors, int n1, int n, double beta1, double beta2, double eps1,
+                        double weight_decay1, const float* scalars1, double eps2, double weight_decay2,
+                        const float* scalars2, const uint32_t* skip, void* stream);
 
 /* ---- The graph-replayed mapping iteration (wgsr/online_graph.py) -------
  * No reference counterpart: device-side steps that let one captured graph

@@ -321,3 +321,40 @@ def test_random_perm_prefix_and_mlp_two_segments():
     assert torch.allclose(G, want, rtol=1e-5, atol=1e-5 * float(want.abs().max()))
     Gacc = backward_raw2(sv, du1, du2, 1.0, 0.5, accumulate_into=want.clone())
     assert torch.allclose(Gacc, 2 * want, rtol=1e-5, atol=2e-5 * float(want.abs().max()))
+
+
+@pytest.mark.gpu
+def test_adam_two_optimisers_one_launch():
+    """wgsr_adam_step_dev2 == wgsr_adam_step_dev per group (the Gaussians'
+    eps / no decay, the MLP's eps / L2 decay), bit for bit."""
+    from wgsr import _lib
+    L = _lib.load()
+    st = _lib.stream_handle(DEV)
+    p = _lib.ptr
+    g = torch.Generator(device=DEV).manual_seed(5)
+    sizes = [(3000, 0), (4801, 3), (17, 0), (256, 0), (6, 0)]
+    def make():
+        out = []
+        for n, _ in sizes:
+            prm, grd = torch.randn(n, device=DEV, generator=g), torch.randn(n, device=DEV, generator=g)
+            m, v = torch.randn(n, device=DEV, generator=g), torch.rand(n, device=DEV, generator=g)
+            out.append([prm, grd, m, v])
+        return out
+    A, B = make(), make()
+    sc1 = torch.rand(3 * 3, device=DEV, generator=g) + 0.5
+    sc2 = torch.rand(2 * 3, device=DEV, generator=g) + 0.5
+    skip = torch.zeros(1, dtype=torch.int32, device=DEV)
+    def tens(T, lo, hi):
+        return [_lib.AdamTensor(p(T[i][0]), p(T[i][1]), p(T[i][2]), p(T[i][3]), T[i][0].numel(), 0.0, 1.0)
+                for i in range(lo, hi)]
+    ref = [[t.clone() for t in row] for row in A]
+    t1, t2 = tens(ref, 0, 3), tens(ref, 3, 5)
+    _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 3)(*t1), 3, 0.9, 0.999, 1e-15, 0.0, p(sc1), p(skip), st))
+    _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * 2)(*t2), 2, 0.9, 0.999, 1e-8, 1e-5, p(sc2), p(skip), st))
+    got = [[t.clone() for t in row] for row in A]
+    ta = tens(got, 0, 5)
+    _lib.check(L.wgsr_adam_step_dev2((_lib.AdamTensor * 5)(*ta), 3, 5, 0.9, 0.999, 1e-15, 0.0, p(sc1), 1e-8, 1e-5,
+                                     p(sc2), p(skip), st))
+    for r, q in zip(ref, got):
+        for a, b in zip(r, q):
+            assert torch.equal(a, b)

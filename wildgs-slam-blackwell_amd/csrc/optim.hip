@@ -32,6 +32,11 @@ struct AdamBatch {
   const float* sc;
   const uint32_t* skip;
   float wd;
+  // wgsr_adam_step_dev2: tensors [n1, n) are a second optimiser's (its own
+  // eps, weight decay and device scalars, indexed from n1)
+  int n1;
+  float eps2, wd2;
+  const float* sc2;
 };
 
 // tensor k's step scalars: its own fields, or the device triple
@@ -40,6 +45,10 @@ struct AdamScal {
 };
 __device__ __forceinline__ AdamScal adam_scal(const AdamBatch& b, int k) {
   const wgsr_adam_tensor& T = b.t[k];
+  if (k >= b.n1) {
+    const float* q = b.sc2 + 3 * (k - b.n1);
+    return {-q[0], -q[2], q[1]};
+  }
   if (b.sc) return {-b.sc[3 * k], -b.sc[3 * k + 2], b.sc[3 * k + 1]};
   return {-T.step_size, -T.step_size_tail, T.bias_correction2_sqrt};
 }
@@ -85,7 +94,7 @@ constexpr int kAdamU = 2;
 __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
   if (b.skip && *b.skip) return;  // (uniform: the whole grid leaves)
   const int64_t units = b.ustart[b.n];
-  const float w1 = b.w1, w2 = b.w2, beta2 = b.beta2, eps = b.eps, wd = b.wd;
+  const float w1 = b.w1, w2 = b.w2, beta2 = b.beta2;
   for (int64_t tile = (int64_t)blockIdx.x * (256 * kAdamU); tile < units; tile += (int64_t)gridDim.x * (256 * kAdamU)) {
     float4 p[kAdamU], g[kAdamU], m[kAdamU], v[kAdamU];
     int ti[kAdamU];
@@ -117,6 +126,8 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b) {
       if (u >= units) continue;
       const wgsr_adam_tensor& T = b.t[ti[j]];
       const AdamScal S = adam_scal(b, ti[j]);
+      const bool second = ti[j] >= b.n1;
+      const float eps = second ? b.eps2 : b.eps, wd = second ? b.wd2 : b.wd;
       if (!vec[j]) {
         adam_scalar(T, S, e0[j], w1, beta2, w2, eps, wd);
         continue;
@@ -317,13 +328,18 @@ using namespace wgsr;
 extern "C" {
 
 static int adam_step_impl(const wgsr_adam_tensor* tensors, int n, double beta1, double beta2, double eps, double wd,
-                          const float* scalars, const uint32_t* skip, void* stream) {
+                          const float* scalars, const uint32_t* skip, void* stream, int n1 = -1, double eps2 = 0.0,
+                          double wd2 = 0.0, const float* scalars2 = nullptr) {
   if (n < 0 || n > kAdamMax || (n > 0 && !tensors)) return set_error(WGSR_EINVAL, "wgsr_adam_step: 0..%d tensors", kAdamMax);
   AdamBatch b{};
   b.sc = scalars;
   b.skip = skip;
   b.wd = (float)wd;
   b.n = n;
+  b.n1 = n1 < 0 ? n : n1;
+  b.eps2 = (float)eps2;
+  b.wd2 = (float)wd2;
+  b.sc2 = scalars2;
   b.beta2 = (float)beta2;
   b.w1 = (float)(1.0 - beta1);
   b.w2 = (float)(1.0 - beta2);
@@ -352,6 +368,15 @@ int wgsr_adam_step_dev(const wgsr_adam_tensor* tensors, int n, double beta1, dou
                        double weight_decay, const float* scalars, const uint32_t* skip, void* stream) {
   if (!scalars) return set_error(WGSR_EINVAL, "wgsr_adam_step_dev: missing device scalars");
   return adam_step_impl(tensors, n, beta1, beta2, eps, weight_decay, scalars, skip, stream);
+}
+
+int wgsr_adam_step_dev2(const wgsr_adam_tensor* tensors, int n1, int n, double beta1, double beta2, double eps1,
+                        double weight_decay1, const float* scalars1, double eps2, double weight_decay2,
+                        const float* scalars2, const uint32_t* skip, void* stream) {
+  if (!scalars1 || (n > n1 && !scalars2) || n1 < 0 || n1 > n)
+    return set_error(WGSR_EINVAL, "wgsr_adam_step_dev2: 0 <= n1 <= n and device scalars for both groups");
+  return adam_step_impl(tensors, n, beta1, beta2, eps1, weight_decay1, scalars1, skip, stream, n1, eps2,
+                        weight_decay2, scalars2);
 }
 
 int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, void* stream) {

@@ -240,6 +240,9 @@ def load():
         L.wgsr_uncer_loss_combine_ssim.restype = c_int
         L.wgsr_uncer_loss_combine_ssim.argtypes = ([U] + [_fp] * 5 + [c_int] + [ctypes.c_float] * 4
                                                    + [_fp] * 3 + [_fp])
+        L.wgsr_adam_step_dev2.restype = c_int
+        L.wgsr_adam_step_dev2.argtypes = ([ctypes.POINTER(AdamTensor), c_int, c_int] + [ctypes.c_double] * 4
+                                          + [_fp] + [ctypes.c_double] * 2 + [_fp, _fp, _fp])
         L.wgsr_mlp_backward_acc.restype = c_int
         L.wgsr_mlp_backward_acc.argtypes = ([c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 4
                                             + [ctypes.c_float, c_int, _fp, _fp, _fp])
@@ -317,7 +320,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_random_perm_prefix_max_n", "wgsr_random_perm_prefix_max_k",
     "wgsr_random_perm_prefix", "wgsr_mlp_forward_seg2", "wgsr_mlp_backward_seg2",
     "wgsr_gaussian_activate_backward_stats", "wgsr_ssim_forward_partials", "wgsr_ssim_tiles",
-    "wgsr_uncer_loss_combine_ssim", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
+    "wgsr_uncer_loss_combine_ssim", "wgsr_adam_step_dev2", "wgsr_mlp_backward_acc", "wgsr_gather_rows", "wgsr_exposure_step",
     "wgsr_ssim_scratch_bytes", "wgsr_ssim_forward", "wgsr_ssim_backward", "wgsr_ssim_components",
     "wgsr_ply_pack", "wgsr_ply_unpack",
     "wgsr_pack_view_camera", "wgsr_rasterize_backward_records", "wgsr_gauss_backward_views_blocks",

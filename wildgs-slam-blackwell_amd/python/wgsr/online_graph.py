@@ -359,7 +359,6 @@ class IterationGraphs:
         # Adam: the Gaussians, the keyframe's exposure on its bank row (skipped
         # unless the window optimiser holds it; also the overflow bookkeeping),
         # the MLP (L2 weight decay)
-        ms.optimizer_step_dev(ms.adam_tensors(), self.f32[self.F_GAUSS:self.F_GAUSS + 15], skip)
         gex = out["dexposure_partials"]  # (summed inside the exposure step)
         with torch.cuda.device(dev):
             _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), int(gex.shape[0]),
@@ -374,10 +373,20 @@ class IterationGraphs:
             ts.append(_lib.AdamTensor(prm.data_ptr(), G.data_ptr() + 4 * off, sto["exp_avg"].data_ptr(),
                                       sto["exp_avg_sq"].data_ptr(), k, 0.0, 1.0))
             off += k
+        # the Gaussians' and the MLP's Adam in one launch (shared betas)
+        gts = ms.adam_tensors()
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * len(ts))(*ts), len(ts), S.mlp_betas[0], S.mlp_betas[1],
-                                            S.mlp_eps, S.mlp_wd, p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip),
-                                            st))
+            if tuple(ms.betas) == tuple(S.mlp_betas):
+                allt = gts + ts
+                _lib.check(L.wgsr_adam_step_dev2((_lib.AdamTensor * len(allt))(*allt), len(gts), len(allt),
+                                                 ms.betas[0], ms.betas[1], ms.eps, 0.0,
+                                                 p(self.f32[self.F_GAUSS:self.F_GAUSS + 15]), S.mlp_eps, S.mlp_wd,
+                                                 p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip), st))
+            else:
+                ms.optimizer_step_dev(gts, self.f32[self.F_GAUSS:self.F_GAUSS + 15], skip)
+                _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * len(ts))(*ts), len(ts), S.mlp_betas[0],
+                                                S.mlp_betas[1], S.mlp_eps, S.mlp_wd,
+                                                p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip), st))
         # the overflow bookkeeping, seen by the host through pinned memory
         self.sticky_host.copy_(self.sticky, non_blocking=True)
 
