@@ -540,10 +540,10 @@ constexpr int kSeg = 16;
 // (acc: the final sums are added to what `seg` / `grad` holds -- a second
 // backward accumulating into the first one's gradient, as autograd does)
 __global__ __launch_bounds__(256) void k_mlp_reduce_seg(int nblocks, int total, const float* __restrict__ part,
-                                                        float* __restrict__ seg, int acc) {
+                                                        float* __restrict__ seg, int acc, int seglen) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= total) return;
-  const int b0 = blockIdx.y * kSeg, b1 = min(nblocks, b0 + kSeg);
+  const int b0 = blockIdx.y * seglen, b1 = min(nblocks, b0 + seglen);
   float s = 0.f;
   for (int b = b0; b < b1; ++b) s += part[(size_t)b * total + e];
   float* d = &seg[(size_t)blockIdx.y * total + e];
@@ -783,12 +783,15 @@ static int mlp_backward_impl(int N, int C, const float* X, const float* W2, cons
   else
     hipLaunchKernelGGL(k_mlp_bwd, dim3(nb, C / 64), dim3(256), 0, (hipStream_t)stream, N, C, X, W2, W3, dropout_p,
                        h1d, h2d, o_pre, dL_du, scratch, du_scale);
-  const int nseg = (nb + kSeg - 1) / kSeg;
+  // (up to 64 row blocks -- the mapper's feature map plus the DINO sample --
+  // are one segment: the second stage would be a copy)
+  const int seglen = nb <= 64 ? nb : kSeg;
+  const int nseg = (nb + seglen - 1) / seglen;
   // one segment (<= 16 row blocks: the mapper's feature maps): its sum is
   // the gradient -- the second stage would be a copy
   float* seg = nseg == 1 ? grad : scratch + (size_t)nb * total;
   hipLaunchKernelGGL(k_mlp_reduce_seg, dim3((total + 255) / 256, nseg), dim3(256), 0, (hipStream_t)stream, nb, total,
-                     scratch, seg, nseg == 1 ? accumulate : 0);
+                     scratch, seg, nseg == 1 ? accumulate : 0, seglen);
   if (nseg > 1)
     hipLaunchKernelGGL(k_mlp_reduce, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, nseg, total, seg,
                        grad, accumulate);

@@ -762,6 +762,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
     float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
   __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
+  __shared__ uint32_t sG[kBatch];
   __shared__ float sP[4][kBatch][11];
   __shared__ uint64_t sHitW[4];
   __shared__ uint32_t sEnd[4];
@@ -808,24 +809,14 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
   __syncthreads();
   const uint32_t end = range.x + max(max(sEnd[0], sEnd[1]), max(sEnd[2], sEnd[3]));
 
-  // wave 0 lane j stages entry j of every batch and writes its record, so it
-  // also loads the entry's slot data (slot_start, rect, row table) with its
-  // splat record, one batch ahead: the record write at the end of a batch
-  // then waits for no load (a dependent round trip per batch otherwise, with
-  // the other three waves idle at the next barrier)
-  uint32_t gcur = 0, gnext = 0, ssN = 0, kC = 0, gC = 0;
+  uint32_t gcur = 0, gnext = 0;
   float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  uint2 rwN = make_uint2(0u, 0u);
-  uint4 tabN = make_uint4(0u, 0u, 0u, 0u);
   if (w == 0) {
     if (end >= range.x + 1 + lane) {
       gcur = point_g[end - 1 - lane];
       nA = splat[3 * (size_t)gcur];
       nB = splat[3 * (size_t)gcur + 1];
       nC = splat[3 * (size_t)gcur + 2];
-      ssN = slot_start[gcur];
-      rwN = *reinterpret_cast<const uint2*>(&lrec[gcur].w);
-      tabN = lrec[gcur].tab;
     }
     if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
   }
@@ -837,10 +828,7 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
       sA[lane] = nA;
       sB[lane] = nB;
       sC[lane] = nC;
-      // this lane's entry of the batch: its duplicate slot (loads issued a
-      // batch ago); lanes past the batch compute a slot they never write
-      gC = gcur;
-      kC = ssN + pair_local(nA, nB, lr_rect(make_uint4(rwN.x, rwN.y, 0u, 0u)), tabN, tx, ty);
+      sG[lane] = gcur;
     }
     __syncthreads();
     if (w == 0) {
@@ -849,9 +837,6 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
         nA = splat[3 * (size_t)gcur];
         nB = splat[3 * (size_t)gcur + 1];
         nC = splat[3 * (size_t)gcur + 2];
-        ssN = slot_start[gcur];
-        rwN = *reinterpret_cast<const uint2*>(&lrec[gcur].w);
-        tabN = lrec[gcur].tab;
       }
       if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
     }
@@ -913,14 +898,14 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
 #pragma unroll
             for (int k = 0; k < 10; ++k) sv[k] += sP[q][lane][k];
         }
-        const float4 eA = sA[lane], eB = sB[lane];
-        record_sums(eA, eB, sv);
-        const size_t k = kC;
+        const uint32_t gid = sG[lane];
+        record_sums(sA[lane], sB[lane], sv);
+        const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], lr_rect(lrec[gid].w), lrec[gid].tab, tx, ty);
         partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
         partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
         partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
         pflag[k] = 1;
-        gflag[gC] = 1;
+        gflag[gid] = 1;
       }
     }
   }
