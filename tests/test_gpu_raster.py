@@ -261,6 +261,25 @@ def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):
                 np.testing.assert_array_equal(outs[sh][k], v, err_msg=f"shift {sh} {k}")
 
 
+@pytest.mark.parametrize("P,W,H,view", [(20_000, 640, 480, 2), (50_001, 1000, 120, 0)])
+def test_preprocess_variants_bit_identical(P, W, H, view, monkeypatch):
+    """The SH-degree-3 preprocess variants (WGSR_PRE: 2 = chunk-major LDS
+    slab, the default; 4 = row-major slab; 5 = half slab, the colour chain
+    run in two halves) write the same bits: every forward and backward output
+    equal."""
+    inputs, settings, grads = _synthetic(P, W, H, 3, view)
+    outs = {}
+    for mode in ("2", "4", "5"):
+        monkeypatch.setenv("WGSR_PRE", mode)
+        outs[mode] = run_c(inputs, settings, grads)
+    for mode in ("4", "5"):
+        for k, v in outs["2"].items():
+            if k == "num_rendered":
+                assert outs[mode][k] == v
+            else:
+                np.testing.assert_array_equal(outs[mode][k], v, err_msg=f"WGSR_PRE={mode} {k}")
+
+
 @pytest.mark.parametrize("fwd_shift,bwd_shift", [("2", "0"), ("0", "2")])
 def test_backward_finds_lists_whatever_bin_shift(fwd_shift, bwd_shift, monkeypatch):
     """The backward locates the forward's tile lists through the image

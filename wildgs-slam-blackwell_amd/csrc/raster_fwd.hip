@@ -69,6 +69,39 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
+// sh_to_rgb(3, ...) in two halves of its chain (the first 8 coefficients,
+// then the last 8 and the clamp): the same operations in the same order, so
+// the colour and clamp bits are bit-identical (k_preprocess_half)
+__device__ __forceinline__ f3 sh3_first(const float* sh, f3 dir) {
+#pragma clang fp contract(off)
+  f3 r = scl3(SH_C0, ldc(sh, 0));
+  const float x = dir.x, y = dir.y, z = dir.z;
+  r = sub3(add3(sub3(r, scl3(SH_C1 * y, ldc(sh, 1))), scl3(SH_C1 * z, ldc(sh, 2))), scl3(SH_C1 * x, ldc(sh, 3)));
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+  r = add3(r, scl3(SH_C2[0] * xy, ldc(sh, 4)));
+  r = add3(r, scl3(SH_C2[1] * yz, ldc(sh, 5)));
+  r = add3(r, scl3(SH_C2[2] * (2.f * zz - xx - yy), ldc(sh, 6)));
+  r = add3(r, scl3(SH_C2[3] * xz, ldc(sh, 7)));
+  return r;
+}
+// sh: coefficients 8..15
+__device__ __forceinline__ f3 sh3_rest(f3 r, const float* sh, f3 dir, uint32_t& clamp_bits) {
+#pragma clang fp contract(off)
+  const float x = dir.x, y = dir.y, z = dir.z;
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y;
+  r = add3(r, scl3(SH_C2[4] * (xx - yy), ldc(sh, 0)));
+  r = add3(r, scl3(SH_C3[0] * y * (3.f * xx - yy), ldc(sh, 1)));
+  r = add3(r, scl3(SH_C3[1] * xy * z, ldc(sh, 2)));
+  r = add3(r, scl3(SH_C3[2] * y * (4.f * zz - xx - yy), ldc(sh, 3)));
+  r = add3(r, scl3(SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), ldc(sh, 4)));
+  r = add3(r, scl3(SH_C3[4] * x * (4.f * zz - xx - yy), ldc(sh, 5)));
+  r = add3(r, scl3(SH_C3[5] * z * (xx - yy), ldc(sh, 6)));
+  r = add3(r, scl3(SH_C3[6] * x * (xx - 3.f * yy), ldc(sh, 7)));
+  r = add3(r, mk3(0.5f, 0.5f, 0.5f));
+  clamp_bits = (r.x < 0 ? 1u : 0u) | (r.y < 0 ? 2u : 0u) | (r.z < 0 ? 4u : 0u);
+  return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
+}
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
 template <int I0, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -434,6 +467,109 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       dir = mk3(dir.x / len, dir.y / len, dir.z / len);
       uint32_t cbits = 0;
       const f3 rgb = sh_rgb_lds_deg<kCh>(D, s_sh, lane, dir, cbits);
+      splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
+      clamped[i] = cbits;
+    }
+  }
+  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
+  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
+}
+
+// ---- k_preprocess_half: SH degree 3 through HALF the LDS slab ----------------
+// k_preprocess2<4> with a 6 KB slab instead of 12 KB: the first 8
+// coefficients of each row are queued before the geometry (as there), the
+// colour chain is run through them, and only then are the last 8 loaded into
+// the same LDS (a round trip the now twice as many resident waves per CU
+// cover: 26 instead of 13 workgroups by LDS).  Bit-identical outputs
+// (sh3_first / sh3_rest).  SH degree 3, 16-byte aligned rows.
+__global__ __launch_bounds__(kPreWave) void k_preprocess_half(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
+    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
+    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
+    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
+    uint32_t* __restrict__ meta) {
+  __shared__ float4 s_h[6 * 64];  // chunk-major: chunk k of lane l at k * 64 + l
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k), (lds_ptr)(s_h + 64 * k), 16, 0, 0);
+  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  f3 sc = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  float o = 0.f;
+  if (i < P) {
+    if (!cov_pre) {
+      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+      q = reinterpret_cast<const float4*>(rots)[i];
+    }
+    o = opac[i];
+  }
+  uint3 ac = make_uint3(0u, 0u, 0u);
+  uint32_t khi = 0u, knlo = 0u;
+  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+  if (i < P) {
+    uint2 rcw;
+    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
+                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, false);
+    radii[i] = (int32_t)w.x;
+    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    if (bshift) tb[i] = w.z;
+    dkey[i] = w.w;
+    if (w.w != 0xFFFFFFFFu) {
+      khi = w.w;
+      knlo = ~w.w;
+    }
+    n_touched[i] = 0;
+    gflag[i] = 0;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the first half has landed (one wave per workgroup)
+  __syncthreads();
+  const bool vis = i < P && w.x != 0u;
+  f3 dir = mk3(0.f, 0.f, 1.f);
+  f3 r = mk3(0.f, 0.f, 0.f);
+  {
+#pragma clang fp contract(off)
+    dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+    const float len = sqrtf(dot3(dir, dir));
+    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+  }
+  float sh[24];
+  if (wave_any(vis)) {  // (uniform)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float4 v = s_h[k * 64 + lane];
+      sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+    }
+    if (vis) r = sh3_first(sh, dir);
+    // every lane's reads are done before the second half overwrites the slab
+    // (the wave's LDS reads complete before the DMA is issued)
+    __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 24 + 4 * k), (lds_ptr)(s_h + 64 * k), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float4 v = s_h[k * 64 + lane];
+      sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+    }
+    if (vis) {
+      uint32_t cbits = 0;
+      const f3 rgb = sh3_rest(r, sh, dir, cbits);
       splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
       clamped[i] = cbits;
     }
@@ -1929,10 +2065,9 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   // k_preprocess2 (LDS-DMA slab behind the geometry) unless WGSR_PRE=1
-  static const int pre_mode = [] {
-    const char* e = getenv("WGSR_PRE");
-    return e ? atoi(e) : 2;
-  }();
+  // (read per call: tests compare the variants in one process)
+  const char* pre_env = getenv("WGSR_PRE");
+  const int pre_mode = pre_env ? atoi(pre_env) : 2;
   if (pre_mode == 3 && a.shs && !a.colors && (a.M * 3) % 4 == 0 &&
       (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) {
     auto kern = a.D == 0 ? k_preprocess3<0> : a.D == 1 ? k_preprocess3<1> : a.D == 2 ? k_preprocess3<2>
@@ -1948,6 +2083,16 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (pre_mode != 1) {
     const bool sh_on = a.shs && !a.colors;
     const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
+    if (ch4 && a.D == 3 && pre_mode == 5) {  // (A/B: the half slab)
+      hipLaunchKernelGGL(k_preprocess_half, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), 0, s, a.P, a.D,
+                         a.M, a.means3D, a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp,
+                         a.scale_modifier, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx,
+                         gy, a.prefiltered, at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
+                         at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag,
+                         rect_pairs, list_pairs, bin_pairs, bshift, at<uint32_t>(geom, L.tb),
+                         at<uint8_t>(geom, L.gflag), drange, zero, meta);
+      return hipGetLastError();
+    }
     const int nf = 3 * (a.D + 1) * (a.D + 1);
     const int kch = ch4 ? 4 : 1;
     const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
