@@ -938,6 +938,9 @@ constexpr int kExpThreads = 256;
 #ifndef WGSR_EXP_ITEMS  // entries per thread per compaction step (1 or 2; A/B)
 #define WGSR_EXP_ITEMS 1
 #endif
+#ifndef WGSR_EXP_PACK  // packed per-wave counts, one barrier per step (0: the plain loop; A/B)
+#define WGSR_EXP_PACK 1
+#endif
 __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __restrict__ skeys,
                                                              const uint32_t* __restrict__ sgid,
                                                              const uint2* __restrict__ bounds, int gx, int gy,
@@ -946,7 +949,9 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
                                                              uint32_t* __restrict__ tile_len,
                                                              uint32_t* __restrict__ meta) {
   constexpr int NW = kExpThreads / 64;
+#if WGSR_EXP_ITEMS == 2 || !WGSR_EXP_PACK
   __shared__ uint32_t s_wc[NW][4];
+#endif
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (blockIdx.x == 0 && t == 0) meta[0] = 1u;  // the lists are the sort-bin region
   const int B = 1 << bshift;
@@ -1003,6 +1008,49 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
     }
     __syncthreads();
     asm volatile("" ::"v"(key), "v"(gid), "v"(key2), "v"(gid2));
+  }
+#elif WGSR_EXP_PACK
+  // the step's per-wave counts of each tile as four 16-bit fields of one
+  // 64-bit LDS word (<= 4 x 64 entries per field): each wave's cross-wave
+  // prefix is three conditional 64-bit adds instead of 16 LDS reads and 32
+  // adds; the words are double-buffered by step parity, so a step needs one
+  // barrier (a wave rewrites a buffer only after the next step's barrier,
+  // which every wave passes after reading it); stores through a uniform base
+  // pointer with 32-bit offsets.  Same positions as the loop below.
+  __shared__ unsigned long long s_wp[2][NW];
+  uint32_t* const out0 = lists + base0;
+  uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
+  asm volatile("" ::"v"(key), "v"(gid));
+  int par = 0;
+  for (uint32_t e0 = lo; e0 < hi; e0 += kExpThreads, par ^= 1) {
+    const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
+    const uint32_t e1 = e0 + kExpThreads + t;
+    key = e1 < hi ? skeys[e1] : 0u;
+    gid = e1 < hi ? sgid[e1] : 0u;
+    uint64_t m[4];
+    unsigned long long packed = 0ull;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m[c] = wave_ballot(c < B && ((bits >> c) & 1u));
+      packed |= (unsigned long long)__popcll(m[c]) << (16 * c);
+    }
+    if (lane == 0) s_wp[par][w] = packed;
+    __syncthreads();
+    unsigned long long off = 0ull, tot = 0ull;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const unsigned long long v = s_wp[par][k];
+      off += k < w ? v : 0ull;
+      tot += v;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= B) break;
+      if ((bits >> c) & 1u)
+        out0[(uint32_t)c * len + count[c] + (uint32_t)((off >> (16 * c)) & 0xFFFFull) + lanes_below(m[c])] = my_gid;
+      count[c] += (uint32_t)((tot >> (16 * c)) & 0xFFFFull);
+    }
+    asm volatile("" ::"v"(key), "v"(gid));
   }
 #else
   uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
