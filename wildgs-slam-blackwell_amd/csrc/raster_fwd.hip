@@ -901,8 +901,12 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
       rg.ok = __shfl(rr.ok, lo, 64);
     }
     const int bx0 = x0 >> bshift, bw = ((x1 - 1) >> bshift) - bx0 + 1;
-    const int row = (int)local / bw;
-    const int bx = bx0 + ((int)local - row * bw), by = (y0 >> bshift) + row;
+    // local / bw without the integer-division sequence: local < 2^16 (a
+    // Gaussian's bins), so the float estimate is within one of the quotient
+    int row = (int)((float)local * __builtin_amdgcn_rcpf((float)bw));
+    int col = (int)local - row * bw;
+    if (col < 0) { --row; col += bw; } else if (col >= bw) { ++row; col -= bw; }
+    const int bx = bx0 + col, by = (y0 >> bshift) + row;
     const uint32_t pd = pair_depth ? (uint32_t)__shfl((int)dk, lo, 64) : 0u;
     if (k < end && k < cap_pairs) {
       keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, tl, rg) << 16);
