@@ -584,10 +584,11 @@ __global__ __launch_bounds__(256) void k_random_keys(int64_t n, uint32_t seed, c
 // The first k entries of wgsr_random_perm's permutation -- the stable
 // ascending order of k_random_keys' keys -- in one workgroup, without sorting
 // all n: each index's 44-bit composite (key << 13 | index; unique, and
-// ascending composites are the stable key order) stays in registers, four
-// 11-bit radix-select passes (LDS histogram, block scan) find the k-th
-// smallest composite, the k composites at or below it are appended to LDS,
-// and each is placed by counting the smaller ones.
+// ascending composites are the stable key order) stays in registers; one
+// 2048-bucket histogram of the top 11 bits (LDS atomics, a block scan) finds
+// the bucket holding the k-th smallest; the composites of the buckets below
+// it are taken, the few in that bucket ranked among themselves, and the k
+// taken composites placed by counting the smaller ones.
 constexpr int kPpThreads = 1024, kPpItems = 8, kPpMaxN = kPpThreads * kPpItems, kPpMaxK = kPpThreads;
 static_assert(kPpMaxN <= 8192, "13 index bits");
 __global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32_t seed,
@@ -597,7 +598,8 @@ __global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32
   __shared__ uint32_t wsum[kPpThreads / 64];
   __shared__ uint32_t sel[2];
   __shared__ unsigned long long list[kPpMaxK];
-  __shared__ uint32_t cnt;
+  __shared__ unsigned long long bk[kPpMaxN];  // the k-th's bucket (a few entries for hash keys)
+  __shared__ uint32_t cnt, nbk;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t sd = seed_dev ? *seed_dev : seed;
   unsigned long long c[kPpItems];
@@ -607,18 +609,18 @@ __global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32
     const uint32_t key = mix32(sd ^ mix32((uint32_t)i * 0x9E3779B9U + 0x632BE5ABU)) >> 1;  // k_random_keys
     c[j] = i < n ? ((unsigned long long)key << 13) | (unsigned long long)i : ~0ull;
   }
-  unsigned long long prefix = 0ull, pmask = 0ull;
-  uint32_t want = (uint32_t)k;  // rank (1-based) of the wanted composite among those matching the prefix
-#pragma unroll 1
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 33 - 11 * pass;  // bits 43-33, 32-22, 21-11, 10-0
-    hist[t] = 0u;
-    hist[t + kPpThreads] = 0u;
-    __syncthreads();
+  hist[t] = 0u;
+  hist[t + kPpThreads] = 0u;
+  if (t == 0) {
+    cnt = 0u;
+    nbk = 0u;
+  }
+  __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPpItems; ++j)
-      if (c[j] != ~0ull && (c[j] & pmask) == prefix) atomicAdd(&hist[(uint32_t)(c[j] >> shift) & 2047u], 1u);
-    __syncthreads();
+  for (int j = 0; j < kPpItems; ++j)
+    if (c[j] != ~0ull) atomicAdd(&hist[(uint32_t)(c[j] >> 33)], 1u);
+  __syncthreads();
+  {
     const uint32_t h0 = hist[2 * t], h1 = hist[2 * t + 1], sm = h0 + h1;
     const uint32_t inc = wave_incl_scan(sm);
     if (lane == 63) wsum[w] = inc;
@@ -626,7 +628,7 @@ __global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32
     uint32_t base = 0;
 #pragma unroll
     for (int q = 0; q < kPpThreads / 64; ++q) base += q < w ? wsum[q] : 0u;
-    const uint32_t e0 = base + inc - sm, e1 = e0 + h0;
+    const uint32_t e0 = base + inc - sm, e1 = e0 + h0, want = (uint32_t)k;
     if (e0 < want && want <= e0 + h0) {
       sel[0] = 2u * t;
       sel[1] = want - e0;
@@ -634,19 +636,26 @@ __global__ __launch_bounds__(kPpThreads) void k_perm_prefix(int n, int k, uint32
       sel[0] = 2u * t + 1u;
       sel[1] = want - e1;
     }
-    __syncthreads();
-    prefix |= (unsigned long long)sel[0] << shift;
-    pmask |= 2047ull << shift;
-    want = sel[1];
-    __syncthreads();  // (sel and hist are rewritten by the next pass)
   }
-  if (t == 0) cnt = 0u;
   __syncthreads();
+  const uint32_t bsel = sel[0], want = sel[1];  // the bucket, and how many of it are taken
 #pragma unroll
-  for (int j = 0; j < kPpItems; ++j)
-    if (c[j] <= prefix) list[atomicAdd(&cnt, 1u)] = c[j];  // exactly k of them (prefix: the k-th smallest)
+  for (int j = 0; j < kPpItems; ++j) {
+    if (c[j] == ~0ull) continue;
+    const uint32_t bj = (uint32_t)(c[j] >> 33);
+    if (bj < bsel) list[atomicAdd(&cnt, 1u)] = c[j];
+    else if (bj == bsel) bk[atomicAdd(&nbk, 1u)] = c[j];
+  }
   __syncthreads();
-  if (t < k) {
+  const uint32_t nb = nbk;
+  for (uint32_t q = (uint32_t)t; q < nb; q += kPpThreads) {
+    const unsigned long long v = bk[q];
+    uint32_t r = 0;
+    for (uint32_t u = 0; u < nb; ++u) r += bk[u] < v ? 1u : 0u;
+    if (r < want) list[atomicAdd(&cnt, 1u)] = v;
+  }
+  __syncthreads();
+  if (t < k) {  // exactly k taken
     const unsigned long long v = list[t];
     uint32_t r = 0;
     for (int q = 0; q < k; ++q) r += list[q] < v ? 1u : 0u;
