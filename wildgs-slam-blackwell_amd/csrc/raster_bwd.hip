@@ -1527,6 +1527,9 @@ constexpr int kGbcThreads = 256;
 #define WGSR_GBC_FLAT 1
 #endif
 #if WGSR_GBC_FLAT
+#ifndef WGSR_GBC_PIPE  // the next record chunk's loads in flight during the current chunk's sums
+#define WGSR_GBC_PIPE 1
+#endif
 #ifndef WGSR_GBC_RECCHUNK
 #define WGSR_GBC_RECCHUNK 512
 #endif
@@ -1640,7 +1643,52 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   for (int r = 0; r < kR; ++r)
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[r][k] = 0.f;
+#if WGSR_GBC_PIPE
+  // software pipeline: this thread's slots of the NEXT chunk are loaded into
+  // registers while the current chunk is summed out of LDS (the loads' round
+  // trip overlaps the sums and barriers instead of following them); same
+  // slots, same order of the sums
+  constexpr int U = kRecChunk / kGbcThreads;
+  float4 ra0[U], ra1[U], ra2[U];
+  bool rf[U];
+  auto fetch = [&](uint32_t b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t q = b + u * kGbcThreads + t;
+      rf[u] = false;
+      ra0[u] = ra1[u] = ra2[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (q < total) {
+        uint32_t lo = 0, hi = nlive;  // s_off[lo] <= q < s_off[hi]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_off[mid] <= q) lo = mid; else hi = mid;
+        }
+        const size_t sl = (size_t)s_s0[lo] + (q - s_off[lo]);
+        rf[u] = pflag[sl] != 0;
+        ra0[u] = partial[3 * sl];
+        ra1[u] = partial[3 * sl + 1];
+        ra2[u] = partial[3 * sl + 2];
+      }
+    }
+  };
+  if (total > 0) fetch(0);
+#endif
   for (uint32_t base = 0; base < total; base += kRecChunk) {
+#if WGSR_GBC_PIPE
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t q = base + u * kGbcThreads + t;
+      if (q < total) {
+        const bool f = rf[u];
+        const float4 a0 = ra0[u], a1 = ra1[u], a2 = ra2[u];
+        float* d = s_rec[q - base];
+        d[0] = f ? a0.x : 0.f; d[1] = f ? a0.y : 0.f; d[2] = f ? a0.z : 0.f; d[3] = f ? a0.w : 0.f;
+        d[4] = f ? a1.x : 0.f; d[5] = f ? a1.y : 0.f; d[6] = f ? a1.z : 0.f; d[7] = f ? a1.w : 0.f;
+        d[8] = f ? a2.x : 0.f; d[9] = f ? a2.y : 0.f;
+      }
+    }
+    if (base + kRecChunk < total) fetch(base + kRecChunk);
+#else
 #pragma unroll
     for (int u = 0; u < kRecChunk / kGbcThreads; ++u) {
       const uint32_t q = base + u * kGbcThreads + t;
@@ -1659,6 +1707,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
         d[8] = f ? a2.x : 0.f; d[9] = f ? a2.y : 0.f;
       }
     }
+#endif
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
