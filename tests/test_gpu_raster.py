@@ -264,15 +264,14 @@ def test_render_bins_give_identical_results(P, W, H, deg, view, monkeypatch):
 @pytest.mark.parametrize("P,W,H,view", [(20_000, 640, 480, 2), (50_001, 1000, 120, 0)])
 def test_preprocess_variants_bit_identical(P, W, H, view, monkeypatch):
     """The SH-degree-3 preprocess variants (WGSR_PRE: 2 = chunk-major LDS
-    slab, the default; 4 = row-major slab; 5 = half slab, the colour chain
-    run in two halves) write the same bits: every forward and backward output
-    equal."""
+    slab, the default; 4 = row-major slab) write the same bits: every forward
+    and backward output equal."""
     inputs, settings, grads = _synthetic(P, W, H, 3, view)
     outs = {}
-    for mode in ("2", "4", "5"):
+    for mode in ("2", "4"):
         monkeypatch.setenv("WGSR_PRE", mode)
         outs[mode] = run_c(inputs, settings, grads)
-    for mode in ("4", "5"):
+    for mode in ("4",):
         for k, v in outs["2"].items():
             if k == "num_rendered":
                 assert outs[mode][k] == v

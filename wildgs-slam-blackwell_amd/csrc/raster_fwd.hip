@@ -69,39 +69,6 @@ __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
 
-// sh_to_rgb(3, ...) in two halves of its chain (the first 8 coefficients,
-// then the last 8 and the clamp): the same operations in the same order, so
-// the colour and clamp bits are bit-identical (k_preprocess_half)
-__device__ __forceinline__ f3 sh3_first(const float* sh, f3 dir) {
-#pragma clang fp contract(off)
-  f3 r = scl3(SH_C0, ldc(sh, 0));
-  const float x = dir.x, y = dir.y, z = dir.z;
-  r = sub3(add3(sub3(r, scl3(SH_C1 * y, ldc(sh, 1))), scl3(SH_C1 * z, ldc(sh, 2))), scl3(SH_C1 * x, ldc(sh, 3)));
-  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-  r = add3(r, scl3(SH_C2[0] * xy, ldc(sh, 4)));
-  r = add3(r, scl3(SH_C2[1] * yz, ldc(sh, 5)));
-  r = add3(r, scl3(SH_C2[2] * (2.f * zz - xx - yy), ldc(sh, 6)));
-  r = add3(r, scl3(SH_C2[3] * xz, ldc(sh, 7)));
-  return r;
-}
-// sh: coefficients 8..15
-__device__ __forceinline__ f3 sh3_rest(f3 r, const float* sh, f3 dir, uint32_t& clamp_bits) {
-#pragma clang fp contract(off)
-  const float x = dir.x, y = dir.y, z = dir.z;
-  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y;
-  r = add3(r, scl3(SH_C2[4] * (xx - yy), ldc(sh, 0)));
-  r = add3(r, scl3(SH_C3[0] * y * (3.f * xx - yy), ldc(sh, 1)));
-  r = add3(r, scl3(SH_C3[1] * xy * z, ldc(sh, 2)));
-  r = add3(r, scl3(SH_C3[2] * y * (4.f * zz - xx - yy), ldc(sh, 3)));
-  r = add3(r, scl3(SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), ldc(sh, 4)));
-  r = add3(r, scl3(SH_C3[4] * x * (4.f * zz - xx - yy), ldc(sh, 5)));
-  r = add3(r, scl3(SH_C3[5] * z * (xx - yy), ldc(sh, 6)));
-  r = add3(r, scl3(SH_C3[6] * x * (xx - 3.f * yy), ldc(sh, 7)));
-  r = add3(r, mk3(0.5f, 0.5f, 0.5f));
-  clamp_bits = (r.x < 0 ? 1u : 0u) | (r.y < 0 ? 2u : 0u) | (r.z < 0 ? 4u : 0u);
-  return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
-}
-
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
 template <int I0, int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -467,109 +434,6 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       dir = mk3(dir.x / len, dir.y / len, dir.z / len);
       uint32_t cbits = 0;
       const f3 rgb = sh_rgb_lds_deg<kCh>(D, s_sh, lane, dir, cbits);
-      splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
-      clamped[i] = cbits;
-    }
-  }
-  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
-  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
-}
-
-// ---- k_preprocess_half: SH degree 3 through HALF the LDS slab ----------------
-// k_preprocess2<4> with a 6 KB slab instead of 12 KB: the first 8
-// coefficients of each row are queued before the geometry (as there), the
-// colour chain is run through them, and only then are the last 8 loaded into
-// the same LDS (a round trip the now twice as many resident waves per CU
-// cover: 26 instead of 13 workgroups by LDS).  Bit-identical outputs
-// (sh3_first / sh3_rest).  SH degree 3, 16-byte aligned rows.
-__global__ __launch_bounds__(kPreWave) void k_preprocess_half(
-    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
-    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
-    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
-    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
-    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
-    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
-    uint32_t* __restrict__ meta) {
-  __shared__ float4 s_h[6 * 64];  // chunk-major: chunk k of lane l at k * 64 + l
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
-  typedef __attribute__((address_space(3))) void* lds_ptr;
-  const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
-#pragma unroll
-  for (int k = 0; k < 6; ++k)
-    __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k), (lds_ptr)(s_h + 64 * k), 16, 0, 0);
-  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
-  f3 sc = mk3(1.f, 1.f, 1.f);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  float o = 0.f;
-  if (i < P) {
-    if (!cov_pre) {
-      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-      q = reinterpret_cast<const float4*>(rots)[i];
-    }
-    o = opac[i];
-  }
-  uint3 ac = make_uint3(0u, 0u, 0u);
-  uint32_t khi = 0u, knlo = 0u;
-  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
-  if (i < P) {
-    uint2 rcw;
-    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
-                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, false);
-    radii[i] = (int32_t)w.x;
-    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
-    if (bshift) tb[i] = w.z;
-    dkey[i] = w.w;
-    if (w.w != 0xFFFFFFFFu) {
-      khi = w.w;
-      knlo = ~w.w;
-    }
-    n_touched[i] = 0;
-    gflag[i] = 0;
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // the first half has landed (one wave per workgroup)
-  __syncthreads();
-  const bool vis = i < P && w.x != 0u;
-  f3 dir = mk3(0.f, 0.f, 1.f);
-  f3 r = mk3(0.f, 0.f, 0.f);
-  {
-#pragma clang fp contract(off)
-    dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
-    const float len = sqrtf(dot3(dir, dir));
-    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-  }
-  float sh[24];
-  if (wave_any(vis)) {  // (uniform)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const float4 v = s_h[k * 64 + lane];
-      sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
-    }
-    if (vis) r = sh3_first(sh, dir);
-    // every lane's reads are done before the second half overwrites the slab
-    // (the wave's LDS reads complete before the DMA is issued)
-    __builtin_amdgcn_s_waitcnt(0);
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      __builtin_amdgcn_global_load_lds((const void*)(src + 24 + 4 * k), (lds_ptr)(s_h + 64 * k), 16, 0, 0);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const float4 v = s_h[k * 64 + lane];
-      sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
-    }
-    if (vis) {
-      uint32_t cbits = 0;
-      const f3 rgb = sh3_rest(r, sh, dir, cbits);
       splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
       clamped[i] = cbits;
     }
@@ -1118,14 +982,14 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 // spare key / payload buffers.  A bin of more than kBdsCap entries runs the
 // same passes chunk by chunk through global scratch (the sort-bin list
 // region, free until k_expand_bins writes it).
-#ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort (7 or 14)
-#define WGSR_BDS_ITEMS 7
+#ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort
+#define WGSR_BDS_ITEMS 10
 #endif
 #ifndef WGSR_BDS_FINE  // entries per lane in steps of one (0: 1, 2, 4, 7 only)
 #define WGSR_BDS_FINE 1
 #endif
 #ifndef WGSR_BDS_THREADS  // workgroup size (512 or 1024)
-#define WGSR_BDS_THREADS 1024
+#define WGSR_BDS_THREADS 512
 #endif
 constexpr int kBdsThreads = WGSR_BDS_THREADS, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
 constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
@@ -1141,10 +1005,24 @@ __device__ __forceinline__ bool bds_owns_digit() { return (int)threadIdx.x < kBd
 #ifndef WGSR_BDS_LDSMATCH
 #define WGSR_BDS_LDSMATCH 1
 #endif
+// WGSR_BDS_SHARE: the lane-mask table shares LDS with the staging buffer (a
+// pass ranks with the table, then scatters into the buffer; the table is
+// zeroed again before the next pass) -- 61 instead of 93 KB per 512-thread
+// workgroup, two workgroups per CU: the 1M frame's 510 bins in one round
+#ifndef WGSR_BDS_SHARE
+#define WGSR_BDS_SHARE 1
+#endif
 struct BdsLds {
+#if WGSR_BDS_LDSMATCH && WGSR_BDS_SHARE
+  union {
+    uint2 buf[kBdsCap];                                // (depth key, position in the bin)
+    unsigned long long match[kBdsWaves][kBdsDigits];  // lane masks per digit (zero between uses)
+  };
+#else
   uint2 buf[kBdsCap];                     // (depth key, position in the bin)
 #if WGSR_BDS_LDSMATCH
   unsigned long long match[kBdsWaves][kBdsDigits];  // lane masks per digit (zero between uses)
+#endif
 #endif
   uint32_t wcnt[kBdsWaves][kBdsDigits];   // per wave digit counts, then their prefix over waves
   uint32_t base[kBdsDigits];              // per digit: first slot
@@ -1392,6 +1270,12 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
 #pragma unroll
     for (int q = 0; q < kBdsWaves; ++q)
       if (bds_owns_digit()) L.wcnt[q][t] = 0u;
+#if WGSR_BDS_LDSMATCH && WGSR_BDS_SHARE
+    if (p + 1 < npass) {  // the next pass ranks with the table the buffer overwrote
+      __syncthreads();
+      for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
+    }
+#endif
     __syncthreads();
   }
   if (E) {  // the per-tile lists straight from the sorted bin
@@ -1571,7 +1455,7 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
 #if WGSR_BDS_LDSMATCH
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
 #endif
-  if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
+  if (n <= 1u * kBdsThreads)
     bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 2u * kBdsThreads)
     bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
@@ -1592,6 +1476,12 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
 #endif
   else if (n <= 7u * kBdsThreads)
     bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#if WGSR_BDS_FINE
+  else if (kBdsItems > 8 && n <= 8u * kBdsThreads)
+    bds_small<(kBdsItems > 8 ? 8 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+  else if (kBdsItems > 9 && n <= 9u * kBdsThreads)
+    bds_small<(kBdsItems > 9 ? 9 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+#endif
   else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
     bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else
@@ -2135,16 +2025,6 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (pre_mode != 1) {
     const bool sh_on = a.shs && !a.colors;
     const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
-    if (ch4 && a.D == 3 && pre_mode == 5) {  // (A/B: the half slab)
-      hipLaunchKernelGGL(k_preprocess_half, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), 0, s, a.P, a.D,
-                         a.M, a.means3D, a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp,
-                         a.scale_modifier, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx,
-                         gy, a.prefiltered, at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
-                         at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag,
-                         rect_pairs, list_pairs, bin_pairs, bshift, at<uint32_t>(geom, L.tb),
-                         at<uint8_t>(geom, L.gflag), drange, zero, meta);
-      return hipGetLastError();
-    }
     const int nf = 3 * (a.D + 1) * (a.D + 1);
     const int kch = ch4 ? 4 : 1;
     const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
