@@ -68,3 +68,17 @@ def test_rigid_deformation_host_restatement():
         assert (got_r - want_r[rows]).abs().max() <= 2e-6
         assert not F[f"{after}_m_xyz"].any() and not F[f"{after}_m_rotation"].any()
         assert np.array_equal(F[f"{after}_m_scaling"], F[f"{before}_m_scaling"])
+
+
+def test_view_draw_matches_generator_choice():
+    """map_opt_online's per-iteration view pick restates numpy's
+    Generator.choice(n, p=prob) as its inverse-CDF draw (one random() per
+    call): the same indices from the same generator state."""
+    prob = np.array([0.05, 0.3, 0.1, 0.25, 0.2, 0.1])
+    prob /= prob.sum()
+    r1, r2 = np.random.default_rng(11), np.random.default_rng(11)
+    cdf = prob.cumsum()
+    cdf /= cdf[-1]
+    a = [int(r1.choice(len(prob), p=prob)) for _ in range(20000)]
+    b = [int(cdf.searchsorted(r2.random(), side="right")) for _ in range(20000)]
+    assert a == b

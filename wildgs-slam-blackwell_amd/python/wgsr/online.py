@@ -620,11 +620,19 @@ class OnlineMapper:
         if prob.sum() == 0:
             prob[:] = 1.0
         prob /= prob.sum()
+        # rng.choice(len(stack), p=prob) per iteration, restated: numpy's own
+        # inverse-CDF draw (the same single random() per call, the same
+        # indices) without its per-call checks of p
+        # (a test's scripted stand-in for the generator still gets choice())
+        cdf = prob.cumsum()
+        cdf /= cdf[-1]
+        fast = isinstance(self.rng, np.random.Generator)
         split = False
         self.bank.sync(self.keyframes)
         ms = self.ms
         for it in range(iters):
-            ci = int(self.rng.choice(len(stack), p=prob))
+            ci = (int(cdf.searchsorted(self.rng.random(), side="right")) if fast
+                  else int(self.rng.choice(len(stack), p=prob)))
             kf = self.keyframes[stack[ci]]
             nb = [stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))]
             nxt = self.iteration_count + 1
