@@ -223,6 +223,26 @@ def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
         np.testing.assert_allclose(a, b, rtol=2e-6, atol=2e-6 * float(np.abs(b).max() + 1e-30), err_msg=k)
 
 
+@pytest.mark.parametrize("P,W,H,deg,view,bg", [(20_000, 640, 480, 3, 2, 0.0), (30_000, 512, 384, 0, 1, 0.4),
+                                               (6_000, 200, 136, 1, 0, 0.0)])
+def test_split_backward_decoupled_waves_bit_identical(P, W, H, deg, view, bg, monkeypatch):
+    """The few-tile backward with decoupled quadrant waves (k_render_bwd_seg,
+    WGSR_BWD_SEG=1, the default) against the batch-synchronous one
+    (k_render_bwd_split): every gradient output bit-identical."""
+    inputs, settings, grads = _synthetic(P, W, H, deg, view)
+    settings = dict(settings, bg=torch.tensor([bg, bg * 0.5, bg * 0.25]))
+    monkeypatch.setenv("WGSR_BWD_SPLIT_BELOW", "1000000")
+    outs = {}
+    for seg in ("0", "1"):
+        monkeypatch.setenv("WGSR_BWD_SEG", seg)
+        outs[seg] = run_c(inputs, settings, grads)
+    for k, v in outs["0"].items():
+        if k == "num_rendered":
+            assert outs["1"][k] == v
+        else:
+            np.testing.assert_array_equal(outs["1"][k], v, err_msg=k)
+
+
 @pytest.mark.parametrize("P", [300_000, 600_000])
 def test_compact_backward_large_workgroups(P, monkeypatch):
     """k_gauss_bwd_compact with 512 / 1024 Gaussians per workgroup (chosen

@@ -647,14 +647,14 @@ struct BwdPairRec {
   uint32_t pad[2];
 };
 
-__device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cfirst, const float4* sA, const float4* sB,
-                                                      const float4* sC, BwdPairRec* R, float (*sPw)[11], v2f p0,
+// (A, B, C: this lane's entry of the batch -- lane j holds entry j)
+__device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cfirst, const float4 A, const float4 B,
+                                                      const float4 C, BwdPairRec* R, float (*sPw)[11], v2f p0,
                                                       uint32_t last, const v2f& dp01, const v2f& dp2d, float& T,
                                                       float& accd, int lane) {
   const int n = __popcll(todo);
   const uint32_t k = lanes_below(todo);
   if ((todo >> lane) & 1) {
-    const float4 A = sA[lane], B = sB[lane], C = sC[lane];
     BwdPairRec& r = R[k >> 1];
     float* q = &r.q[0].x + (k & 1);
     q[0] = A.x; q[2] = A.y; q[4] = A.z; q[6] = A.w; q[8] = B.x; q[10] = B.y;
@@ -844,8 +844,8 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
     uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < mq &&
                                 ellipse_hits(sA[lane], sB[lane], qx0, qx0 + 7, qy0, qy0 + 7));
 #if WGSR_BWD_SPLIT_EPAIR
-    const uint64_t hits = split_batch_pairs(todo, cfirst, sA, sB, sC, sPairs[w], sP[w], p0, last, dp01, dp2d, T,
-                                            accd, lane);
+    const uint64_t hits = split_batch_pairs(todo, cfirst, sA[lane], sB[lane], sC[lane], sPairs[w], sP[w], p0, last,
+                                            dp01, dp2d, T, accd, lane);
 #else
     uint64_t hits = 0;
     while (todo) {
@@ -908,6 +908,145 @@ __global__ __launch_bounds__(256) void k_render_bwd_split(
         gflag[gid] = 1;
       }
     }
+  }
+  zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
+}
+
+// k_render_bwd_split with the quadrant waves decoupled (the default below
+// 3072 tiles; WGSR_BWD_SEG=0 keeps k_render_bwd_split): every wave fetches
+// the batch records itself (lane j entry j, one batch ahead in registers)
+// instead of wave 0 staging them for all four behind two barriers per batch,
+// and leaves its per-entry quadrant sums in a segment table of kSegBatches
+// batches; the four waves meet only once per segment, where the workgroup
+// adds each entry's (up to four) quadrant sums in quadrant order and writes
+// its record (that entry's slot data loaded at the segment's start).  A
+// quadrant wave with less work no longer waits for the slowest one at every
+// batch.  Same per-pixel arithmetic, same sums in the same order:
+// bit-identical records.
+constexpr int kSegBatches = 3, kSegCap = kSegBatches * kBatch;
+#ifndef WGSR_BWD_SEG
+#define WGSR_BWD_SEG 1
+#endif
+__global__ __launch_bounds__(256) void k_render_bwd_seg(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
+    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ lists_exact,
+    const uint32_t* __restrict__ lists_bins, const float4* __restrict__ splat,
+    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
+    int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
+    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
+  __shared__ float sS[4][kSegCap][11];              // per quadrant: the segment's entry sums
+  __shared__ uint64_t sHit[4][kSegBatches];         // per quadrant and batch: the entries it summed
+  __shared__ BwdPairRec sPairs[4][kBatch / 2];      // per wave: the batch's compacted survivors
+  __shared__ uint32_t sEnd[4];
+  if (meta[1]) {  // overflowed capacity-mode forward (see k_render_bwd_quad)
+    zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
+    return;
+  }
+  const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
+  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int tx = (int)(tile % gx), ty = (int)(tile / gx);
+  const int qx0 = tx * kTile + (w & 1) * 8, qy0 = ty * kTile + (w >> 1) * 8;  // this wave's quadrant
+  const size_t HW = (size_t)H * W;
+  const uint2 range = ranges[tile];
+  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+
+  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+  const v2f p0{(float)px, (float)py};
+  const bool inside = px < W && py < H;
+  const size_t pid = (size_t)py * W + px;
+  const float Tf = inside ? final_Ts[pid] : 0.f;
+  const uint32_t last = inside ? n_contrib[pid] : 0u;
+  const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
+  const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
+  const v2f dp01{d0, d1}, dp2d{d2, dd};
+  float accd = bg0 * d0 + bg1 * d1 + bg2 * d2;  // the background as the colour behind the last contributor
+  float T = Tf;
+  uint32_t x = last;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
+  const uint32_t mq = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+  if (lane == 0) sEnd[w] = mq;
+  __syncthreads();
+  const uint32_t end = range.x + max(max(sEnd[0], sEnd[1]), max(sEnd[2], sEnd[3]));
+
+  // this wave's batch records, one batch ahead (lanes past the list hold
+  // entry 0's: valid rows, culled by lane < cnt)
+  uint32_t gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (end > range.x) {
+    const uint32_t g0 = point_g[end >= range.x + 1 + lane ? end - 1 - lane : range.x];
+    nA = splat[3 * (size_t)g0];
+    nB = splat[3 * (size_t)g0 + 1];
+    nC = splat[3 * (size_t)g0 + 2];
+    gnext = point_g[end >= range.x + 1 + kBatch + lane ? end - 1 - kBatch - lane : range.x];
+  }
+  for (uint32_t s_end = end; s_end > range.x;) {  // segments, back to front (block-uniform)
+    const uint32_t s_beg = s_end - range.x > (uint32_t)kSegCap ? s_end - kSegCap : range.x;
+    const uint32_t scnt = s_end - s_beg;
+    // the record writer's slot data of segment entry t (list index s_end - 1 - t),
+    // in flight during the walk
+    uint32_t rg = 0, rss = 0;
+    float4 rA = make_float4(0, 0, 0, 0), rB = rA;
+    uint2 rrw = make_uint2(0u, 0u);
+    uint4 rtab = make_uint4(0u, 0u, 0u, 0u);
+    if ((uint32_t)t < scnt) {
+      rg = point_g[s_end - 1 - t];
+      rA = splat[3 * (size_t)rg];
+      rB = splat[3 * (size_t)rg + 1];
+      rss = slot_start[rg];
+      rrw = *reinterpret_cast<const uint2*>(&lrec[rg].w);
+      rtab = lrec[rg].tab;
+    }
+    int bi = 0;
+    for (uint32_t b_end = s_end; b_end > s_beg; b_end = b_end - s_beg > (uint32_t)kBatch ? b_end - kBatch : s_beg, ++bi) {
+      const int cnt = (int)min((uint32_t)kBatch, b_end - s_beg);
+      const float4 A = nA, B = nB, C = nC;
+      // next batch (possibly the next segment's first)
+      const uint32_t nb_end = b_end - range.x > (uint32_t)kBatch ? b_end - kBatch : range.x;
+      if (nb_end > range.x) {
+        const uint32_t g = gnext;
+        nA = splat[3 * (size_t)g];
+        nB = splat[3 * (size_t)g + 1];
+        nC = splat[3 * (size_t)g + 2];
+        gnext = point_g[nb_end >= range.x + 1 + kBatch + lane ? nb_end - 1 - kBatch - lane : range.x];
+      }
+      const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
+      const uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < mq &&
+                                        ellipse_hits(A, B, qx0, qx0 + 7, qy0, qy0 + 7));
+      const uint64_t hits = split_batch_pairs(todo, cfirst, A, B, C, sPairs[w], &sS[w][bi * kBatch], p0, last, dp01,
+                                              dp2d, T, accd, lane);
+      if (lane == 0) sHit[w][bi] = hits;
+    }
+    __syncthreads();
+    // entry t of the segment: its quadrant sums in quadrant order, its record
+    if ((uint32_t)t < scnt) {
+      const int b = t >> 6;
+      const uint64_t bit = 1ull << (t & 63);
+      const uint64_t h0 = sHit[0][b], h1 = sHit[1][b], h2 = sHit[2][b], h3 = sHit[3][b];
+      if ((h0 | h1 | h2 | h3) & bit) {
+        float sv[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) sv[k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t hq = q == 0 ? h0 : (q == 1 ? h1 : (q == 2 ? h2 : h3));
+          if (hq & bit)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) sv[k] += sS[q][t][k];
+        }
+        record_sums(rA, rB, sv);
+        const size_t k = rss + pair_local(rA, rB, lr_rect(make_uint4(rrw.x, rrw.y, 0u, 0u)), rtab, tx, ty);
+        partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
+        partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
+        pflag[k] = 1;
+        gflag[rg] = 1;
+      }
+    }
+    __syncthreads();  // (the table is rewritten by the next segment)
+    s_end = s_beg;
   }
   zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
 }
@@ -1968,7 +2107,9 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const char* env = getenv("WGSR_BWD_SPLIT_BELOW");  // read per launch: tests switch kernels
   const int split_below = env ? atoi(env) : kBwdSplitBelowTiles;
   if (nt < split_below) {
-    hipLaunchKernelGGL(k_render_bwd_split, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), meta,
+    const char* segenv = getenv("WGSR_BWD_SEG");  // (read per launch: tests compare the two)
+    auto kern = (segenv ? atoi(segenv) != 0 : WGSR_BWD_SEG != 0) ? k_render_bwd_seg : k_render_bwd_split;
+    hipLaunchKernelGGL(kern, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), meta,
                        lists_exact, lists_bins,
                        at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
