@@ -224,6 +224,25 @@ def test_per_gaussian_backward_modes_agree(P, W, H, deg, view, monkeypatch):
 
 
 @pytest.mark.parametrize("P,W,H,deg,view,bg", [(20_000, 640, 480, 3, 2, 0.0), (30_000, 512, 384, 0, 1, 0.4),
+                                               (6_000, 200, 136, 1, 0, 0.0), (50_000, 1000, 120, 0, 0, 0.2)])
+def test_forward_decoupled_waves_bit_identical(P, W, H, deg, view, bg, monkeypatch):
+    """The forward with decoupled quadrant waves (k_render_fwd_dec,
+    WGSR_FWD_DEC=1, the default) against the batch-synchronous k_render_fwd1:
+    image, depth, opacity, n_touched, radii and every gradient bit-identical."""
+    inputs, settings, grads = _synthetic(P, W, H, deg, view)
+    settings = dict(settings, bg=torch.tensor([bg, bg * 0.5, bg * 0.25]))
+    outs = {}
+    for dec in ("0", "1"):
+        monkeypatch.setenv("WGSR_FWD_DEC", dec)
+        outs[dec] = run_c(inputs, settings, grads)
+    for k, v in outs["0"].items():
+        if k == "num_rendered":
+            assert outs["1"][k] == v
+        else:
+            np.testing.assert_array_equal(outs["1"][k], v, err_msg=k)
+
+
+@pytest.mark.parametrize("P,W,H,deg,view,bg", [(20_000, 640, 480, 3, 2, 0.0), (30_000, 512, 384, 0, 1, 0.4),
                                                (6_000, 200, 136, 1, 0, 0.0)])
 def test_split_backward_decoupled_waves_bit_identical(P, W, H, deg, view, bg, monkeypatch):
     """The few-tile backward with decoupled quadrant waves (k_render_bwd_seg,

@@ -1951,6 +1951,113 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
   out_opac[pid] = 1.f - T;
 }
 
+// k_render_fwd1 with the quadrant waves decoupled (the default;
+// WGSR_FWD_DEC=0 keeps k_render_fwd1): every wave prefetches its own batch
+// records into registers one batch ahead (lane j entry j) instead of wave 0
+// streaming them into shared LDS behind a barrier per batch, and stops as
+// soon as its own 64 pixels are done -- no wave waits for its tile's
+// slowest quadrant.  Same blend per pixel in the same order, n_touched as
+// integer atomics: bit-identical outputs.
+#ifndef WGSR_FWD_DEC
+#define WGSR_FWD_DEC 1
+#endif
+__global__ __launch_bounds__(256) void k_render_fwd_dec(
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, const uint32_t* __restrict__ point_g,
+    const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
+    float* __restrict__ out_color, float* __restrict__ out_depth, float* __restrict__ out_opac,
+    float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched,
+    uint32_t* __restrict__ tile_m4) {
+  __shared__ FwdPairLds sPair[4];  // per wave: the batch's surviving entries, compacted
+  const uint32_t slot = xcd_remap(blockIdx.x, (uint32_t)ntiles);
+  const uint32_t tile = order ? order[slot] : slot;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
+  int ox, oy;
+  tile_pixel<1>(w, lane, 0, ox, oy);
+  const int px = tx0 + ox, py = ty0 + oy;
+  const v2f pxy{(float)px, (float)py};
+  uint64_t dm = wave_ballot(!(px < W && py < H));
+  const uint2 range = ranges[tile];
+  int wx0, wx1, wy0, wy1;
+  wave_box<1>(w, tx0, ty0, wx0, wx1, wy0, wy1);
+  float T = 1.f;
+  v2f c01{0.f, 0.f}, c2d{0.f, 0.f};
+  uint32_t last = 0;
+  (void)t;
+  const uint32_t last_i = range.y > range.x ? range.y - 1 : range.x;
+  uint32_t gcur = 0, gnext = 0;
+  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
+  if (range.x < range.y) {
+    gcur = point_g[min(range.x + lane, last_i)];
+    nA = splat[3 * (size_t)gcur];
+    nB = splat[3 * (size_t)gcur + 1];
+    nC = splat[3 * (size_t)gcur + 2];
+    if (range.x + kFwdBatch < range.y) gnext = point_g[min(range.x + kFwdBatch + lane, last_i)];
+  }
+  uint32_t fl_gid = 0, fl_tv = 0;  // this lane's n_touched increment of the previous batch
+  for (uint32_t b0 = range.x; b0 < range.y && dm != ~0ull; b0 += kFwdBatch) {  // (wave-uniform)
+    const float4 pre[3] = {nA, nB, nC};
+    const uint32_t gme = gcur;
+    if (b0 + kFwdBatch < range.y) {  // the next batch's records, the one after's ids
+      gcur = gnext;
+      nA = splat[3 * (size_t)gcur];
+      nB = splat[3 * (size_t)gcur + 1];
+      nC = splat[3 * (size_t)gcur + 2];
+      if (b0 + 2 * kFwdBatch < range.y) gnext = point_g[min(b0 + 2 * kFwdBatch + lane, last_i)];
+    }
+    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
+    // cull against the wave's pixel box, compact the survivors in pairs, blend
+    // (fwd_blend_batch_pairs on register-held records)
+    FwdPairLds& L = sPair[w];
+    const bool mine = lane < cnt && ellipse_hits(pre[0], pre[1], wx0, wx1, wy0, wy1);
+    const uint64_t todo = wave_ballot(mine);
+    const int n = __popcll(todo);
+    const uint32_t k = lanes_below(todo);
+    const bool touch = (wave_ballot(T > 0.5f) & ~dm) != 0;  // (uniform)
+    if (mine) {
+      FwdPairRec& R = L.p[k >> 1];
+      float* q = &R.q[0].x + (k & 1);
+      q[0] = pre[0].x; q[2] = pre[0].y; q[4] = pre[0].z; q[6] = pre[0].w; q[8] = pre[1].x; q[10] = pre[1].y;
+      R.c[k & 1] = pre[2];
+      R.n[k & 1] = b0 - range.x + 1 + (uint32_t)lane;
+    }
+    if (touch) L.touch[lane] = 0;
+    if (lane == 63 && (n & 1)) {  // the unused half of an odd last pair: finite operands
+      FwdPairRec& R = L.p[n >> 1];
+      float* q = &R.q[0].x + 1;
+      q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
+      R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);  // the previous batch's
+    fl_tv = 0;
+    if (touch) {
+      fwd_blend_pairs<true>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
+      fl_gid = gme;
+      fl_tv = mine ? L.touch[k] : 0u;
+    } else {
+      fwd_blend_pairs<false>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
+    }
+  }
+  if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
+  {  // this quadrant's deepest contributor: tile_m4[4 tile + w]
+    uint32_t mx = last;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if (lane == 0) tile_m4[4 * tile + w] = mx;
+  }
+  if (!(px < W && py < H)) return;
+  const size_t HW = (size_t)H * W;
+  const size_t pid = (size_t)py * W + px;
+  final_T[pid] = T;
+  n_contrib[pid] = last;
+  out_color[pid] = c01.x + T * bg[0];
+  out_color[HW + pid] = c01.y + T * bg[1];
+  out_color[2 * HW + pid] = c2d.x + T * bg[2];
+  out_depth[pid] = c2d.y;
+  out_opac[pid] = 1.f - T;
+}
+
+
 
 __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means,
                                                       const float* __restrict__ viewm, uint8_t* __restrict__ present) {
@@ -2172,7 +2279,9 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
   const int nt = gx * gy;
-  hipLaunchKernelGGL(k_render_fwd1, dim3(nt), dim3(256), 0, s, ranges, nullptr, point_g,
+  const char* dec = getenv("WGSR_FWD_DEC");  // (read per launch: tests compare the two)
+  auto kern = (dec ? atoi(dec) != 0 : WGSR_FWD_DEC != 0) ? k_render_fwd_dec : k_render_fwd1;
+  hipLaunchKernelGGL(kern, dim3(nt), dim3(256), 0, s, ranges, nullptr, point_g,
                      at<float4>(geom, L.splat), a.W, a.H, gx, nt, a.bg, out_color, out_depth, out_opacity, final_T,
                      n_contrib, n_touched, tile_m);
   return hipGetLastError();
