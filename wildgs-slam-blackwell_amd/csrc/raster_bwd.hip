@@ -57,7 +57,9 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 //   g2, g3, g4 = o x moments                                         -- dL/dconic / (-1/2)
 //   g5 = S G dL/dalpha                                               -- dL/dopacity
 // (A.z, A.w, B.x: the log2(e)-scaled conic of the splat record, o = B.y.)
+// (no contraction: every kernel that writes records rounds them alike)
 __device__ __forceinline__ void record_sums(const float4& A, const float4& B, float (&g)[10]) {
+#pragma clang fp contract(off)
   const float o = B.y, ux = g[0], uy = g[1];
   g[0] = o * (2.f * A.z * ux + B.x * uy);
   g[1] = o * (2.f * A.w * uy + B.x * ux);
