@@ -59,6 +59,9 @@ for s in $STEPS; do
     pmc_sq2)
       # VALU pipe occupancy (SQ_ACTIVE_INST_VALU, quad-cycles incl. multi-cycle ops) and the SQ clock (SQ_BUSY_CYCLES per SE)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_INSTS_VALU_TRANS_F32 SQ_THREAD_CYCLES_VALU SQ_LDS_BANK_CONFLICT --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_sq2${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_sq2${SFX:-}.err); rc=$? ;;
+    pmc_ta)
+      # the vector memory path: TA (address) / TD (data) busy and stalls, TCP (L1) tag accesses and L2 waits
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_LATENCY_sum GRBM_GUI_ACTIVE --kernel-trace -d $GRAFT_REPO_ROOT/$OUT/pmc_ta${SFX:-} -o run --output-format csv -- python $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-knn ${BENCH_ARGS:-} > /dev/null 2> $GRAFT_REPO_ROOT/$OUT/pmc_ta${SFX:-}.err); rc=$? ;;
     ab)
       # AB_LIBS="name ...": bench each lib/variants/<name>.so ("base" = lib/libwgsr.so), twice, interleaved
       rc=0

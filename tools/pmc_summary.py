@@ -41,6 +41,8 @@ STAGE_OF = {
     "k_render_bwd_split": "render_bwd", "k_sum_active": "gauss_bwd", "k_gauss_bwd_compact": "gauss_bwd",
     "k_depth_hist": "depth_sort", "k_depth_scatter": "depth_sort",
     "k_bin_depth_sort": "tile_sort",  # (per-bin depth order: small frames)
+    "k_preprocess2": "preprocess", "k_preprocess3": "preprocess",
+    "k_render_fwd_dec": "render_fwd", "k_render_bwd_seg": "render_bwd",
 }
 
 
