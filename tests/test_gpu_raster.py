@@ -318,6 +318,30 @@ def test_preprocess_variants_bit_identical(P, W, H, view, monkeypatch):
                 np.testing.assert_array_equal(outs[mode][k], v, err_msg=f"WGSR_PRE={mode} {k}")
 
 
+@pytest.mark.parametrize("deg,active,P,pre", [(3, 3, 20_001, "2"), (3, 1, 9_999, "2"), (2, 2, 5_000, "2"),
+                                               (1, 1, 7_777, "2"), (0, 0, 30_000, "2"), (3, 3, 12_345, "4")])
+def test_preprocess_one_round_trip_bit_identical(deg, active, P, pre, monkeypatch):
+    """k_preprocess2e (every load of a wave in flight at once, one wait, the
+    stores after the colour; WGSR_PRE_EARLY=1, the default) writes the same
+    bits as k_preprocess2 (WGSR_PRE_EARLY=0): every forward and backward
+    output, at every SH degree, an active degree below the table's, ragged P
+    and both slab layouts.  (The SH colour is contraction-free in every
+    kernel, sh_to_rgb: an FMA fused in one inlining context and not in
+    another once made them differ in the colour's last bit.)"""
+    inputs, settings, grads = _synthetic(P, 640, 480, deg, 1)
+    settings = dict(settings, sh_degree=active)
+    monkeypatch.setenv("WGSR_PRE", pre)
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("WGSR_PRE_EARLY", mode)
+        outs[mode] = run_c(inputs, settings, grads)
+    for k, v in outs["0"].items():
+        if k == "num_rendered":
+            assert outs["1"][k] == v
+        else:
+            np.testing.assert_array_equal(outs["1"][k], v, err_msg=f"deg {deg}/{active} {k}")
+
+
 @pytest.mark.parametrize("fwd_shift,bwd_shift", [("2", "0"), ("0", "2")])
 def test_backward_finds_lists_whatever_bin_shift(fwd_shift, bwd_shift, monkeypatch):
     """The backward locates the forward's tile lists through the image

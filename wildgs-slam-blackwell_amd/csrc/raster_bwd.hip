@@ -1701,11 +1701,13 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   // compaction of the live Gaussians (list order = index order)
   bool live[kR];
   uint64_t bal[kR];
+  // (unconditional loads of clamped rows: a short-circuit load would be
+  // waited for at its join, one round trip per r instead of one in all)
+  uint8_t gf[kR];
 #pragma unroll
-  for (int r = 0; r < kR; ++r) {
-    const int i = i0 + r * kGbcThreads + t;
-    live[r] = i < P && gflag[i] != 0;
-  }
+  for (int r = 0; r < kR; ++r) gf[r] = gflag[min(i0 + r * kGbcThreads + t, P - 1)];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) live[r] = i0 + r * kGbcThreads + t < P && gf[r] != 0;
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     bal[r] = wave_ballot(live[r]);

@@ -39,32 +39,38 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 
 __device__ __forceinline__ f3 ldc(const float* sh, int k) { return mk3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]); }
 
-// SH -> RGB (upstream computeColorFromSH forward), clamp flags in bits 0..2
+// SH -> RGB (upstream computeColorFromSH forward), clamp flags in bits 0..2.
+// Every product and sum is written here, under contract(off) (the local
+// lambdas included): no multiply-add of the colour can be fused, whatever the
+// inlining context, so every preprocess kernel rounds the colour alike.
 __device__ __forceinline__ f3 sh_to_rgb(int deg, const float* sh, f3 dir, uint32_t& clamp_bits) {
 #pragma clang fp contract(off)
-  f3 r = scl3(SH_C0, ldc(sh, 0));
+  auto term = [](float c, const float* v) -> f3 { return {c * v[0], c * v[1], c * v[2]}; };
+  auto plus = [](f3 a, f3 b) -> f3 { return {a.x + b.x, a.y + b.y, a.z + b.z}; };
+  auto minus = [](f3 a, f3 b) -> f3 { return {a.x - b.x, a.y - b.y, a.z - b.z}; };
+  f3 r = term(SH_C0, sh);
   if (deg > 0) {
     const float x = dir.x, y = dir.y, z = dir.z;
-    r = sub3(add3(sub3(r, scl3(SH_C1 * y, ldc(sh, 1))), scl3(SH_C1 * z, ldc(sh, 2))), scl3(SH_C1 * x, ldc(sh, 3)));
+    r = minus(plus(minus(r, term(SH_C1 * y, sh + 3)), term(SH_C1 * z, sh + 6)), term(SH_C1 * x, sh + 9));
     if (deg > 1) {
       const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-      r = add3(r, scl3(SH_C2[0] * xy, ldc(sh, 4)));
-      r = add3(r, scl3(SH_C2[1] * yz, ldc(sh, 5)));
-      r = add3(r, scl3(SH_C2[2] * (2.f * zz - xx - yy), ldc(sh, 6)));
-      r = add3(r, scl3(SH_C2[3] * xz, ldc(sh, 7)));
-      r = add3(r, scl3(SH_C2[4] * (xx - yy), ldc(sh, 8)));
+      r = plus(r, term(SH_C2[0] * xy, sh + 12));
+      r = plus(r, term(SH_C2[1] * yz, sh + 15));
+      r = plus(r, term(SH_C2[2] * (2.f * zz - xx - yy), sh + 18));
+      r = plus(r, term(SH_C2[3] * xz, sh + 21));
+      r = plus(r, term(SH_C2[4] * (xx - yy), sh + 24));
       if (deg > 2) {
-        r = add3(r, scl3(SH_C3[0] * y * (3.f * xx - yy), ldc(sh, 9)));
-        r = add3(r, scl3(SH_C3[1] * xy * z, ldc(sh, 10)));
-        r = add3(r, scl3(SH_C3[2] * y * (4.f * zz - xx - yy), ldc(sh, 11)));
-        r = add3(r, scl3(SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), ldc(sh, 12)));
-        r = add3(r, scl3(SH_C3[4] * x * (4.f * zz - xx - yy), ldc(sh, 13)));
-        r = add3(r, scl3(SH_C3[5] * z * (xx - yy), ldc(sh, 14)));
-        r = add3(r, scl3(SH_C3[6] * x * (xx - 3.f * yy), ldc(sh, 15)));
+        r = plus(r, term(SH_C3[0] * y * (3.f * xx - yy), sh + 27));
+        r = plus(r, term(SH_C3[1] * xy * z, sh + 30));
+        r = plus(r, term(SH_C3[2] * y * (4.f * zz - xx - yy), sh + 33));
+        r = plus(r, term(SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), sh + 36));
+        r = plus(r, term(SH_C3[4] * x * (4.f * zz - xx - yy), sh + 39));
+        r = plus(r, term(SH_C3[5] * z * (xx - yy), sh + 42));
+        r = plus(r, term(SH_C3[6] * x * (xx - 3.f * yy), sh + 45));
       }
     }
   }
-  r = add3(r, mk3(0.5f, 0.5f, 0.5f));
+  r = plus(r, f3{0.5f, 0.5f, 0.5f});
   clamp_bits = (r.x < 0 ? 1u : 0u) | (r.y < 0 ? 2u : 0u) | (r.z < 0 ? 4u : 0u);
   return mk3(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f));
 }
@@ -83,6 +89,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 // list length, tb, depth key) are returned in `w` (radius, cnt, tb, key) and
 // stored once by the caller; the splat record, rect, row table and clamp bits
 // only for visible Gaussians.
+// records of a visible Gaussian kept in registers instead of stored
+// (k_preprocess2's deferred-store form: every store after the colour)
+struct PreDefer {
+  float4 A, B;
+  uint4 tab;
+};
 __device__ __forceinline__ uint3 preprocess_one(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
@@ -92,7 +104,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
     int i, const Cam& c, const f3 p, const f3 sc, const float4 q, const float o, const f3 sh_rgb,
-    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true) {
+    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true, PreDefer* dfr = nullptr) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
   rcw = make_uint2(0u, 0u);
@@ -150,8 +162,13 @@ __device__ __forceinline__ uint3 preprocess_one(
   // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
   const float4 A = make_float4(px, py, kConicSq * (cc * det_inv), kConicSq * (a * det_inv));
   const float4 B = make_float4(kConicXY * (-b * det_inv), o, lim, 0.f);
-  splat[3 * (size_t)i + 0] = A;
-  splat[3 * (size_t)i + 1] = B;
+  if (dfr) {
+    dfr->A = A;
+    dfr->B = B;
+  } else {
+    splat[3 * (size_t)i + 0] = A;
+    splat[3 * (size_t)i + 1] = B;
+  }
   if (write_color) splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rcw = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
   // exact tile list length (row_span); upstream's num_rendered counts the rect
@@ -171,7 +188,10 @@ __device__ __forceinline__ uint3 preprocess_one(
     }
     cnt += len;
   }
-  lrec[i].tab = tab;
+  if (dfr)
+    dfr->tab = tab;
+  else
+    lrec[i].tab = tab;
   if (write_color) clamped[i] = cbits;
   // bins of the rect (exact lists are per tile; a bin list holds every
   // Gaussian whose rect meets the bin, and the render waves cull the rest)
@@ -351,6 +371,122 @@ __device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_
     case 2: return sh_rgb_lds<2, kCh>(s_sh, lane, dir, cbits);
     default: return sh_rgb_lds<3, kCh>(s_sh, lane, dir, cbits);
   }
+}
+
+// k_preprocess2e (the default; WGSR_PRE_EARLY=0 runs k_preprocess2): the
+// same work with ONE memory round trip per wave.  k_preprocess2 as compiled
+// waits three times (vmcnt(0) after the means load -- slab included --, then
+// for scales / rotation, then for the opacity the compiler had sunk to its
+// use): here the slab and every parameter (unconditional, clamped row) are
+// issued together and waited for once, the SH degree is a template argument
+// (a fixed run of slab loads), and every store of the Gaussian is held back
+// to after the colour.
+// queue a wave's SH slab (64 rows' evaluated coefficients) into LDS:
+// chunk-major (kCh 4 / 1) or row-major (kCh 8), see k_preprocess2
+template <int kCh, int kD>
+__device__ __forceinline__ void queue_sh_slab(int P, int M, const float* __restrict__ shs, float* s_sh, int lane,
+                                              int i0, int i) {
+  constexpr int nf = 3 * (kD + 1) * (kD + 1), nch = (nf + (kCh == 8 ? 4 : kCh) - 1) / (kCh == 8 ? 4 : kCh);
+  const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
+  const size_t c_end = (size_t)P * (3 * M) / 4;  // chunks in the whole table
+#pragma unroll
+  for (int k = 0; k < nch; ++k) {
+    if constexpr (kCh == 8) {
+      const size_t c = min((size_t)i0 * (3 * M) / 4 + (size_t)(64 * k + lane), c_end - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(shs + 4 * c),
+                                       (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+    } else if constexpr (kCh == 4)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
+                                       (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(src + k),
+                                       (__attribute__((address_space(3))) void*)(s_sh + 64 * k), 4, 0, 0);
+  }
+}
+
+// kD < 0: no SH colour (colours given, or no SH table)
+template <int kCh, int kD>
+__global__ __launch_bounds__(kPreWave) void k_preprocess2e(
+    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
+    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
+    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
+    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped, uint32_t* __restrict__ dkey,
+    int32_t* __restrict__ radii, int32_t* __restrict__ n_touched, uint32_t* __restrict__ err_flag,
+    unsigned long long* __restrict__ rect_pairs, unsigned long long* __restrict__ list_pairs,
+    unsigned long long* __restrict__ bin_pairs, int bshift, uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag,
+    uint32_t* __restrict__ drange, const ZeroJob zero, uint32_t* __restrict__ meta) {
+  extern __shared__ float s_sh[];  // nch x 64 x kCh floats (chunk-major), as k_preprocess2
+  constexpr bool sh_on = kD >= 0;
+  const int lane = threadIdx.x;
+  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
+  // every load of the Gaussian in flight at once: the slab, then the
+  // parameters (unconditional, clamped row: lanes past P compute nothing)
+  if constexpr (sh_on) queue_sh_slab<kCh, kD>(P, M, shs, s_sh, lane, i0, i);
+  const int ic = min(i, P - 1);
+  f3 p = mk3(means[3 * ic], means[3 * ic + 1], means[3 * ic + 2]);
+  f3 sc = mk3(1.f, 1.f, 1.f);
+  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+  if (!cov_pre) {  // (uniform)
+    sc = mk3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
+    q = reinterpret_cast<const float4*>(rots)[ic];
+  }
+  const float o = opac[ic];
+  // ONE wait for all of them, here: without this use the compiler sinks
+  // loads to their first use and waits at each (three round trips, each
+  // counting the slab too, since LDS-DMA loads are not counted past)
+  asm volatile("" ::"v"(p.x), "v"(p.y), "v"(p.z), "v"(sc.x), "v"(sc.y), "v"(sc.z), "v"(q.x), "v"(q.y), "v"(q.z),
+               "v"(q.w), "v"(o));
+  Cam c;
+  load_cam(c, viewm, projm, W, H, tanx, tany);
+  uint3 ac = make_uint3(0u, 0u, 0u);
+  uint32_t khi = 0u, knlo = 0u;
+  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+  uint2 rcw = make_uint2(0u, 0u);
+  PreDefer dfr;
+  if (i < P)
+    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
+                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p, sc,
+                        q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, !sh_on, &dfr);
+  float4 C = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t cbits = 0;
+  if constexpr (sh_on) {
+    __builtin_amdgcn_s_waitcnt(0);  // the slab has landed (no store issued since; one wave per workgroup)
+    __syncthreads();
+    if (i < P && w.x != 0u) {  // visible: the colour record
+#pragma clang fp contract(off)
+      f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
+      const float len = sqrtf(dot3(dir, dir));
+      dir = mk3(dir.x / len, dir.y / len, dir.z / len);
+      const f3 rgb = sh_rgb_lds<(kD < 0 ? 0 : kD), kCh>(s_sh, lane, dir, cbits);
+      C = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
+    }
+  }
+  if (i < P) {
+    if (ac.x != 0u) {  // preprocess_one reached its records (rect area > 0)
+      splat[3 * (size_t)i + 0] = dfr.A;
+      splat[3 * (size_t)i + 1] = dfr.B;
+      lrec[i].tab = dfr.tab;
+    }
+    if (sh_on && w.x != 0u) {  // (uniform sh_on)
+      splat[3 * (size_t)i + 2] = C;
+      clamped[i] = cbits;
+    }
+    radii[i] = (int32_t)w.x;
+    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    if (bshift) tb[i] = w.z;
+    dkey[i] = w.w;
+    if (w.w != 0xFFFFFFFFu) {
+      khi = w.w;
+      knlo = ~w.w;
+    }
+    n_touched[i] = 0;
+    gflag[i] = 0;
+  }
+  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
+  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
 }
 
 template <int kCh>
@@ -1231,11 +1367,15 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
   constexpr uint32_t kPosMask = (1u << kBdsPosBits) - 1u;
   uint32_t k[JN], pk[JN];
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  // (loads of clamped positions, all issued before any is used: a load under
+  // `le < n` is waited for at its join, one round trip per j)
+#pragma unroll
+  for (int j = 0; j < JN; ++j) k[j] = sdep[lo + min((uint32_t)(w * JN + j) * 64u + (uint32_t)lane, n - 1u)];
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     pk[j] = le;
-    k[j] = le < n ? sdep[lo + le] : 0u;
+    k[j] = le < n ? k[j] : 0u;
     if (le < n) {
       mn = min(mn, k[j]);
       mx = max(mx, k[j]);
@@ -1284,26 +1424,37 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
 #pragma unroll
     for (int j = 0; j < JN; ++j) {
       const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
-      m[j] = 0u;
-      g[j] = 0u;
-      if (le < n) {
-        const uint32_t q = pk[j] & kPosMask;
-        m[j] = (skeys[lo + q] >> 16) & tmask;
-        g[j] = sgid[lo + q];
-      }
+      const uint32_t q = le < n ? pk[j] & kPosMask : 0u;  // (unconditional loads, as above)
+      m[j] = skeys[lo + q];
+      g[j] = sgid[lo + q];
+    }
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+      const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+      m[j] = le < n ? (m[j] >> 16) & tmask : 0u;
+      g[j] = le < n ? g[j] : 0u;
     }
     if (t < 16) L.erun[t] = 0u;
     __syncthreads();
     bds_emit_chunk<JN>(L, m, g, n, 1 << (2 * EM.bshift), EM.lists + ((size_t)lo << (2 * EM.bshift)), n);
     return;
   }
+  // every gather load issued before the first store (unconditional, clamped)
+  uint32_t ok[JN], og[JN];
+#pragma unroll
+  for (int j = 0; j < JN; ++j) {
+    const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
+    const uint32_t q = le < n ? pk[j] & kPosMask : 0u;
+    pk[j] = q;
+    ok[j] = okeys ? skeys[lo + q] : 0u;  // (uniform; null: the stable argsort of k_argsort_small)
+    og[j] = sgid ? sgid[lo + q] : q;
+  }
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     if (le < n) {
-      const uint32_t q = pk[j] & kPosMask;
-      if (okeys) okeys[lo + le] = skeys[lo + q];  // (uniform; null: the stable argsort of k_argsort_small)
-      ogid[lo + le] = sgid ? sgid[lo + q] : q;
+      if (okeys) okeys[lo + le] = ok[j];
+      ogid[lo + le] = og[j];
     }
   }
 }
@@ -2138,7 +2289,23 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
     // (WGSR_PRE=4, A/B, whole rows evaluated only: the coalesced row-major
     // slab k_preprocess2<8> -- 112 vs 102 us at 1M / SH3: the strided
     // chunk-major gather is not the limit)
+    const char* early_env = getenv("WGSR_PRE_EARLY");  // (read per call: tests compare the orders)
+    const bool early = early_env ? atoi(early_env) != 0 : true;
     auto kern = ch4 ? ((nf == 3 * a.M && pre_mode == 4) ? k_preprocess2<8> : k_preprocess2<4>) : k_preprocess2<1>;
+    if (early) {
+      // (the SH degree and slab layout as template arguments: the slab is a
+      // fixed run of loads, so the geometry's wait can count past it)
+      const int d = sh_on ? a.D : -1;
+      if (pre_mode == 4 && ch4 && nf == 3 * a.M)
+        kern = d < 0 ? k_preprocess2e<8, -1> : d == 0 ? k_preprocess2e<8, 0> : d == 1 ? k_preprocess2e<8, 1>
+             : d == 2 ? k_preprocess2e<8, 2> : k_preprocess2e<8, 3>;
+      else if (ch4 || !sh_on)
+        kern = d < 0 ? k_preprocess2e<4, -1> : d == 0 ? k_preprocess2e<4, 0> : d == 1 ? k_preprocess2e<4, 1>
+             : d == 2 ? k_preprocess2e<4, 2> : k_preprocess2e<4, 3>;
+      else
+        kern = d == 0 ? k_preprocess2e<1, 0> : d == 1 ? k_preprocess2e<1, 1> : d == 2 ? k_preprocess2e<1, 2>
+                                                                          : k_preprocess2e<1, 3>;
+    }
     hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds2, s, a.P, a.D, a.M, a.means3D,
                        a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
                        a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
