@@ -322,7 +322,7 @@ def test_preprocess_variants_bit_identical(P, W, H, view, monkeypatch):
                                                (1, 1, 7_777, "2"), (0, 0, 30_000, "2"), (3, 3, 12_345, "4")])
 def test_preprocess_one_round_trip_bit_identical(deg, active, P, pre, monkeypatch):
     """k_preprocess2e (every load of a wave in flight at once, one wait, the
-    stores after the colour; WGSR_PRE_EARLY=1, the default) writes the same
+    stores after the colour; WGSR_PRE_EARLY=1, an A/B variant) writes the same
     bits as k_preprocess2 (WGSR_PRE_EARLY=0): every forward and backward
     output, at every SH degree, an active degree below the table's, ragged P
     and both slab layouts.  (The SH colour is contraction-free in every

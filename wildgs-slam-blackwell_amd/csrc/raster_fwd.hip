@@ -373,8 +373,10 @@ __device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_
   }
 }
 
-// k_preprocess2e (the default; WGSR_PRE_EARLY=0 runs k_preprocess2): the
-// same work with ONE memory round trip per wave.  k_preprocess2 as compiled
+// k_preprocess2e (WGSR_PRE_EARLY=1, A/B; measured SLOWER at 1M / SH3: 106.7
+// vs 103.4 us -- the vector memory path, not the wait structure, bounds the
+// preprocess: TD busy 78 %, 71 % of it stalled on L2 data, tools/pmc_ta.py):
+// the same work with ONE memory round trip per wave.  k_preprocess2 as compiled
 // waits three times (vmcnt(0) after the means load -- slab included --, then
 // for scales / rotation, then for the opacity the compiler had sunk to its
 // use): here the slab and every parameter (unconditional, clamped row) are
@@ -2290,7 +2292,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
     // slab k_preprocess2<8> -- 112 vs 102 us at 1M / SH3: the strided
     // chunk-major gather is not the limit)
     const char* early_env = getenv("WGSR_PRE_EARLY");  // (read per call: tests compare the orders)
-    const bool early = early_env ? atoi(early_env) != 0 : true;
+    const bool early = early_env ? atoi(early_env) != 0 : false;  // (A/B: 106.7 vs 103.4 us at 1M)
     auto kern = ch4 ? ((nf == 3 * a.M && pre_mode == 4) ? k_preprocess2<8> : k_preprocess2<4>) : k_preprocess2<1>;
     if (early) {
       // (the SH degree and slab layout as template arguments: the slab is a
