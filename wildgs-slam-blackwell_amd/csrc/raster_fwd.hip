@@ -375,7 +375,7 @@ __device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_
 
 // k_preprocess2e (WGSR_PRE_EARLY=1, A/B; measured SLOWER at 1M / SH3: 106.7
 // vs 103.4 us -- the vector memory path, not the wait structure, bounds the
-// preprocess: TD busy 78 %, 71 % of it stalled on L2 data, tools/pmc_ta.py):
+// preprocess: TD busy 80 %, 74 % of it stalled on L2 data, tools/pmc_ta.py):
 // the same work with ONE memory round trip per wave.  k_preprocess2 as compiled
 // waits three times (vmcnt(0) after the means load -- slab included --, then
 // for scales / rotation, then for the opacity the compiler had sunk to its
