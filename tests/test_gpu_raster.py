@@ -319,18 +319,21 @@ def test_preprocess_variants_bit_identical(P, W, H, view, monkeypatch):
 
 
 @pytest.mark.parametrize("deg,active,P,pre", [(3, 3, 20_001, "2"), (3, 1, 9_999, "2"), (2, 2, 5_000, "2"),
-                                               (1, 1, 7_777, "2"), (0, 0, 30_000, "2"), (3, 3, 12_345, "4")])
+                                               (1, 1, 7_777, "2"), (0, 0, 30_000, "2"), (3, 3, 12_345, "4"),
+                                               (3, 3, 20_001, "2:0"), (0, 0, 3_333, "2:0")])
 def test_preprocess_one_round_trip_bit_identical(deg, active, P, pre, monkeypatch):
     """k_preprocess2e (every load of a wave in flight at once, one wait, the
     stores after the colour; WGSR_PRE_EARLY=1, an A/B variant) writes the same
     bits as k_preprocess2 (WGSR_PRE_EARLY=0): every forward and backward
-    output, at every SH degree, an active degree below the table's, ragged P
-    and both slab layouts.  (The SH colour is contraction-free in every
+    output, at every SH degree, an active degree below the table's, ragged P,
+    both slab layouts, with and without the LDS-staged record stores.  (The SH colour is contraction-free in every
     kernel, sh_to_rgb: an FMA fused in one inlining context and not in
     another once made them differ in the colour's last bit.)"""
     inputs, settings, grads = _synthetic(P, 640, 480, deg, 1)
     settings = dict(settings, sh_degree=active)
+    pre, _, stage = pre.partition(":")  # "2:0": without the staged record stores (WGSR_PRE_STAGE)
     monkeypatch.setenv("WGSR_PRE", pre)
+    monkeypatch.setenv("WGSR_PRE_STAGE", stage or "1")  # (staging on unless ":0"; off by default in the library)
     outs = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("WGSR_PRE_EARLY", mode)

@@ -406,8 +406,14 @@ __device__ __forceinline__ void queue_sh_slab(int P, int M, const float* __restr
   }
 }
 
-// kD < 0: no SH colour (colours given, or no SH table)
-template <int kCh, int kD>
+// kD < 0: no SH colour (colours given, or no SH table).  kStage (SH only;
+// WGSR_PRE_STAGE=1 with WGSR_PRE_EARLY=1, A/B: measured slower, 115.8 vs
+// 106.7 us at 1M / SH3):
+// the wave's 64 splat records (48 B each) and list records (32 B) leave as
+// whole contiguous runs -- staged in the slab's LDS, 1 KB per store
+// instruction -- instead of 16-byte stores strided by 48 / 32 bytes (rows
+// of culled Gaussians are written as zeros; nothing reads them)
+template <int kCh, int kD, bool kStage = false>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2e(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2e(
   uint32_t khi = 0u, knlo = 0u;
   uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
   uint2 rcw = make_uint2(0u, 0u);
-  PreDefer dfr;
+  PreDefer dfr{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f), make_uint4(0u, 0u, 0u, 0u)};
   if (i < P)
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
                         W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p, sc,
@@ -466,18 +472,42 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2e(
       C = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
     }
   }
+  constexpr bool stage = kStage && sh_on;
+  if constexpr (stage) {
+    float4* sb = reinterpret_cast<float4*>(s_sh);  // 64 x 3 splat rows, then 64 x 2 list rows
+    __syncthreads();  // every lane's slab reads are done
+    const bool rec = i < P && ac.x != 0u;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    sb[3 * lane] = rec ? dfr.A : z4;
+    sb[3 * lane + 1] = rec ? dfr.B : z4;
+    sb[3 * lane + 2] = rec && w.x != 0u ? C : z4;
+    reinterpret_cast<uint4*>(sb)[192 + 2 * lane] = rec ? dfr.tab : make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(sb)[192 + 2 * lane + 1] = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    __syncthreads();
+    const int nrow = min(kPreWave, P - i0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int idx = 64 * k + lane;
+      if (idx < 3 * nrow) splat[3 * (size_t)i0 + idx] = sb[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = 64 * k + lane;
+      if (idx < 2 * nrow) reinterpret_cast<uint4*>(lrec + i0)[idx] = reinterpret_cast<const uint4*>(sb)[192 + idx];
+    }
+  }
   if (i < P) {
-    if (ac.x != 0u) {  // preprocess_one reached its records (rect area > 0)
+    if (!stage && ac.x != 0u) {  // preprocess_one reached its records (rect area > 0)
       splat[3 * (size_t)i + 0] = dfr.A;
       splat[3 * (size_t)i + 1] = dfr.B;
       lrec[i].tab = dfr.tab;
     }
     if (sh_on && w.x != 0u) {  // (uniform sh_on)
-      splat[3 * (size_t)i + 2] = C;
+      if (!stage) splat[3 * (size_t)i + 2] = C;
       clamped[i] = cbits;
     }
     radii[i] = (int32_t)w.x;
-    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
+    if (!stage) lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
     if (bshift) tb[i] = w.z;
     dkey[i] = w.w;
     if (w.w != 0xFFFFFFFFu) {
@@ -2287,7 +2317,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
     const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
     const int nf = 3 * (a.D + 1) * (a.D + 1);
     const int kch = ch4 ? 4 : 1;
-    const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
+    size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
     // (WGSR_PRE=4, A/B, whole rows evaluated only: the coalesced row-major
     // slab k_preprocess2<8> -- 112 vs 102 us at 1M / SH3: the strided
     // chunk-major gather is not the limit)
@@ -2298,7 +2328,14 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
       // (the SH degree and slab layout as template arguments: the slab is a
       // fixed run of loads, so the geometry's wait can count past it)
       const int d = sh_on ? a.D : -1;
-      if (pre_mode == 4 && ch4 && nf == 3 * a.M)
+      const char* st_env = getenv("WGSR_PRE_STAGE");  // (read per call: tests compare)
+      // (A/B: 115.8 vs 106.7 us without staging at 1M / SH3 -- rejected)
+      const bool stage = sh_on && ch4 && (st_env ? atoi(st_env) != 0 : false) && pre_mode != 4;
+      if (stage) {
+        kern = d == 0 ? k_preprocess2e<4, 0, true> : d == 1 ? k_preprocess2e<4, 1, true>
+             : d == 2 ? k_preprocess2e<4, 2, true> : k_preprocess2e<4, 3, true>;
+        lds2 = std::max(lds2, sizeof(float4) * 5 * 64);
+      } else if (pre_mode == 4 && ch4 && nf == 3 * a.M)
         kern = d < 0 ? k_preprocess2e<8, -1> : d == 0 ? k_preprocess2e<8, 0> : d == 1 ? k_preprocess2e<8, 1>
              : d == 2 ? k_preprocess2e<8, 2> : k_preprocess2e<8, 3>;
       else if (ch4 || !sh_on)
