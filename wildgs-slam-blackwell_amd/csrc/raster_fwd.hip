@@ -835,17 +835,23 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
-  const uint32_t g = in ? (sorted_g ? sorted_g[r] : r) : 0u;  // (null: index order)
+  // (unconditional loads of a clamped rank, the selects after: a load under
+  // `in` would be waited for at its join.  The depth key rides in the same
+  // round trip as the list record.)
+  const uint32_t rc = min(r, P - 1u);
+  const uint32_t g0 = sorted_g ? sorted_g[rc] : rc;  // (null: index order)
   // the whole 32-byte list record in one round trip (row table + rect, tb,
   // list length: one cache line)
-  uint4 lw = make_uint4(0u, 0u, 0u, 0u), tab = lw;
-  if (in) {
-    lw = lrec[g].w;
-    tab = lrec[g].tab;
+  uint4 lw = lrec[g0].w, tab = lrec[g0].tab;
+  const uint32_t dk0 = pair_depth ? dkey[g0] : 0u;
+  const uint32_t g = in ? g0 : 0u;
+  if (!in) {
+    lw = make_uint4(0u, 0u, 0u, 0u);
+    tab = lw;
   }
   const uint32_t v = lw.z;
   const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
-  const uint32_t dk = pair_depth && in && nb ? dkey[g] : 0u;  // (per-bin depth sort input)
+  const uint32_t dk = in && nb ? dk0 : 0u;  // (per-bin depth sort input)
   uint32_t rlo = 0, rhi = 0;
   bool tall = false;
   if (nb) {
