@@ -259,13 +259,16 @@ int wgsr_gaussian_activate_backward(int P, const float* opacity_raw, const float
                                     float iso_weight, float* dL_dopacity_raw,
                                     float* dL_dscaling_raw, float* dL_drotation_raw, void* stream);
 /* ... and, in the same pass, wgsr_densification_stats' update of
- * max_radii2D / grad_accum / denom (one launch instead of two). */
+ * max_radii2D / grad_accum / denom (one launch instead of two).  skip
+ * (nullable device word): when non-zero the statistics are left unchanged --
+ * pass the capacity-mode forward's overflow word (counts[3]), whose iteration
+ * produced no gradient. */
 int wgsr_gaussian_activate_backward_stats(int P, const float* opacity_raw, const float* scaling_raw,
                                           const float* rotation_raw, const float* dL_dopacity,
                                           const float* dL_dscales, const float* dL_drotations, float iso_weight,
                                           float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
                                           const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
-                                          float* grad_accum, float* denom, void* stream);
+                                          float* grad_accum, float* denom, const uint32_t* skip, void* stream);
 
 /* get_loss_mapping_rgbd (slam_utils.py:107-143) without its SSIM term:
  * image_ab = exp(exposure_a) image + exposure_b ([3,H,W], written for the
@@ -560,10 +563,12 @@ int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, voi
  * gradient itself) and scalars = (step_size, sqrt(1 - beta2^n)); skipped
  * when *skip_a or *skip_b is non-zero.  With sticky and counts (the
  * capacity-mode forward's, or NULL): sticky[0] += counts[3], sticky[1] =
- * max(sticky[1], counts[0]). */
+ * max(sticky[1], counts[0]).  slot_skips (nullable, one word per bank row):
+ * slot_skips[idx[0]] += 1 when the step was meant to run (*skip_b == 0) but
+ * *skip_a held it back, so the host can roll back that row's step count. */
 int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, int nparts, const float* scalars,
                        const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
-                       int64_t* sticky, const uint32_t* counts, void* stream);
+                       int64_t* sticky, const uint32_t* counts, int64_t* slot_skips, void* stream);
 
 /* One row-major tensor for row compaction: rows of `row_bytes` (a multiple
  * of 4) from `src` [P rows]; `dst` receives the kept rows in order. */

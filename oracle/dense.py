@@ -292,7 +292,11 @@ def rasterize_dense(means3D, means2D, opacities, shs, colors_precomp, scales, ro
     T_img = assemble(out_t, 1)
     return dict(color=color, depth=depth_img, opacity=1.0 - T_img,
                 radii=radii.to(torch.int32), n_touched=n_touched.to(torch.int32),
-                num_rendered=int(tiles.sum()), tiles_touched=tiles)
+                num_rendered=int(tiles.sum()), tiles_touched=tiles,
+                # per-Gaussian geometry (detached; tests cross-check it against
+                # the reference-held shader text, tests/test_shader_crosscheck.py)
+                cov2d=torch.stack([a, b, c], dim=1).detach(), conic=conic.detach(), xy=xy.detach(),
+                rgb=rgb.detach(), visible=visible)
 
 
 def dense_forward_backward(scene: dict, settings: dict, grad_color, grad_depth):

@@ -79,6 +79,30 @@ def test_capacity_forward_matches_and_overflow_zeroes_gradients():
     go = _backward(args, cam, small, W, H, dcol, ddep)
     for t in go:
         assert not t.any()
+    # the activation backward's densification statistics skip on the same word
+    # (an overflowed replay must not count denom / max_radii2D)
+    from wgsr import _lib
+    L = _lib.load()
+    P = xyz.shape[0]
+    p = _lib.ptr
+    raw_o, raw_s, raw_r = torch.randn(P, 1, device=DEV), torch.randn(P, 3, device=DEV), torch.randn(P, 4, device=DEV)
+    g_o, g_s, g_r = torch.randn(P, 1, device=DEV), torch.randn(P, 3, device=DEV), torch.randn(P, 4, device=DEV)
+    d_o, d_s, d_r = torch.empty_like(g_o), torch.empty_like(g_s), torch.empty_like(g_r)
+    for skip_set, radii, m2d in ((True, small[2], go[0]), (False, ref[2], gr[0])):
+        mr, acc, den = torch.full((P,), 2.0, device=DEV), torch.full((P, 1), 0.5, device=DEV), torch.ones(P, 1,
+                                                                                                         device=DEV)
+        word = counts[3:4] if skip_set else torch.zeros(1, dtype=torch.int32, device=DEV)
+        _lib.check(L.wgsr_gaussian_activate_backward_stats(
+            P, p(raw_o), p(raw_s), p(raw_r), p(g_o), p(g_s), p(g_r), 0.0, p(d_o), p(d_s), p(d_r), p(radii), p(m2d),
+            p(mr), p(acc), p(den), p(word), _lib.stream_handle(DEV)))
+        torch.cuda.synchronize()
+        vis = radii > 0
+        assert vis.any()
+        if skip_set:
+            assert (mr == 2.0).all() and (acc == 0.5).all() and (den == 1.0).all()
+        else:
+            assert (den[vis] == 2.0).all() and (den[~vis] == 1.0).all()
+            assert torch.equal(mr[vis], torch.maximum(radii[vis].float(), torch.tensor(2.0, device=DEV)))
 
 
 def test_adam_step_dev_matches_host_scalars_and_torch_weight_decay():
@@ -245,27 +269,34 @@ def test_random_perm_gather_exposure_step_and_mlp_accumulate():
     sticky = torch.tensor([0, 99], dtype=torch.int64, device=DEV)
     got = ex.clone()
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, p(sticky),
-                                    p(counts), st))
+                                    p(counts), None, st))
     # (the same arithmetic as the Adam kernel; the compiler may contract its
     # multiply-adds differently in the two kernels: a few ulp)
     assert torch.allclose(got, ref, rtol=1e-6, atol=1e-7) and sticky.tolist() == [0, 1234]
     assert torch.equal(got[:7], ex[:7]) and torch.equal(got[8:], ex[8:])  # only the indexed row moves
     before = got.clone()
     counts[3] = 1
+    slot_skips = torch.zeros(ex.shape[0], dtype=torch.int64, device=DEV)
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(one), p(zero), 0.9, 0.999, 1e-8, p(sticky),
-                                    p(counts), st))
+                                    p(counts), p(slot_skips), st))
+    # (a step the host did not count -- skip_b set -- is not a held-back one)
+    _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(one), p(one), 0.9, 0.999, 1e-8, None, None,
+                                    p(slot_skips), st))
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(grad), 1, p(sc), p(zero), p(one), 0.9, 0.999, 1e-8, None, None,
-                                    st))
+                                    None, st))
     assert torch.equal(got, before) and sticky.tolist() == [1, 1234]
+    want_sk = torch.zeros_like(slot_skips)
+    want_sk[int(idx[0])] = 1
+    assert torch.equal(slot_skips, want_sk)
     # the gradient as per-block partial rows, summed inside the step
     parts = torch.randn(768, 2, device=DEV, generator=g)
     got = ex.clone()
     _lib.check(L.wgsr_exposure_step(p(got), p(idx), p(parts), 768, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, None,
-                                    None, st))
+                                    None, None, st))
     ref2 = ex.clone()
     gsum = parts.double().sum(0).float().contiguous()
     _lib.check(L.wgsr_exposure_step(p(ref2), p(idx), p(gsum), 1, p(sc), p(zero), p(zero), 0.9, 0.999, 1e-8, None,
-                                    None, st))
+                                    None, None, st))
     assert torch.allclose(got, ref2, rtol=1e-5, atol=1e-6)
     # MLP backward: scaled upstream gradient accumulated into an earlier one
     torch.manual_seed(1)

@@ -77,6 +77,10 @@ struct DensifyJob {
   float* max_radii;
   float* accum;
   float* denom;
+  // a capacity-mode forward's overflow word (counts[3] / ImageLayout::meta[1];
+  // null: none): set, the iteration left no gradient and the statistics keep
+  // their values (the render backward wrote only the zero fill)
+  const uint32_t* skip;
 };
 __device__ __forceinline__ void densify_stats_one(int i, const DensifyJob& J) {
   const int r = J.radii[i];
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(kMapBlock) void k_activate_bwd(int P, const float* 
                                                             float* __restrict__ d_r, const DensifyJob dj) {
   const int i = blockIdx.x * kMapBlock + threadIdx.x;
   if (i >= P) return;
-  if (dj.radii) densify_stats_one(i, dj);
+  if (dj.radii && !(dj.skip && *dj.skip)) densify_stats_one(i, dj);
   // sigmoid: grad * (1 - y) * y
   const float y = 1.f / (1.f + expf(-o_raw[i]));
   d_o[i] = g_op[i] * (1.f - y) * y;
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(kMapBlock) void k_densify_stats(int P, const int32_
                                                              float* __restrict__ denom) {
   const int i = blockIdx.x * kMapBlock + threadIdx.x;
   if (i >= P) return;
-  densify_stats_one(i, DensifyJob{radii, m2d_grad, max_radii, accum, denom});
+  densify_stats_one(i, DensifyJob{radii, m2d_grad, max_radii, accum, denom, nullptr});
 }
 
 }  // namespace
@@ -241,7 +245,7 @@ int wgsr_gaussian_activate_backward(int P, const float* opacity_raw, const float
   hipLaunchKernelGGL(k_activate_bwd, dim3(wgsr_map_blocks(P)), dim3(kMapBlock), 0, (hipStream_t)stream, P,
                      opacity_raw, scaling_raw, rotation_raw, dL_dopacity, dL_dscales, dL_drotations, iso_weight,
                      dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw,
-                     DensifyJob{nullptr, nullptr, nullptr, nullptr, nullptr});
+                     DensifyJob{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr});
   MAPCHK("wgsr_gaussian_activate_backward");
   return WGSR_OK;
 }
@@ -251,7 +255,7 @@ int wgsr_gaussian_activate_backward_stats(int P, const float* opacity_raw, const
                                           const float* dL_dscales, const float* dL_drotations, float iso_weight,
                                           float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
                                           const int32_t* radii, const float* dL_dmeans2D, float* max_radii2D,
-                                          float* grad_accum, float* denom, void* stream) {
+                                          float* grad_accum, float* denom, const uint32_t* skip, void* stream) {
   if (P < 0) return set_error(WGSR_EINVAL, "wgsr_gaussian_activate_backward_stats: negative P");
   if (P == 0) return WGSR_OK;
   if (!opacity_raw || !scaling_raw || !rotation_raw || !dL_dopacity || !dL_dscales || !dL_drotations ||
@@ -261,7 +265,7 @@ int wgsr_gaussian_activate_backward_stats(int P, const float* opacity_raw, const
   hipLaunchKernelGGL(k_activate_bwd, dim3(wgsr_map_blocks(P)), dim3(kMapBlock), 0, (hipStream_t)stream, P,
                      opacity_raw, scaling_raw, rotation_raw, dL_dopacity, dL_dscales, dL_drotations, iso_weight,
                      dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw,
-                     DensifyJob{radii, dL_dmeans2D, max_radii2D, grad_accum, denom});
+                     DensifyJob{radii, dL_dmeans2D, max_radii2D, grad_accum, denom, skip});
   MAPCHK("wgsr_gaussian_activate_backward_stats");
   return WGSR_OK;
 }

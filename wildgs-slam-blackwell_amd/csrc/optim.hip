@@ -288,7 +288,8 @@ __global__ __launch_bounds__(64) void k_exposure_step(float* __restrict__ bank, 
                                                       const uint32_t* __restrict__ skip_a,
                                                       const uint32_t* __restrict__ skip_b, float w1, float beta2,
                                                       float w2, float eps, long long* __restrict__ sticky,
-                                                      const uint32_t* __restrict__ counts) {
+                                                      const uint32_t* __restrict__ counts,
+                                                      long long* __restrict__ slot_skips) {
   const int l = threadIdx.x;
   float ga = 0.f, gb = 0.f;
   if (nparts == 1) {
@@ -317,6 +318,8 @@ __global__ __launch_bounds__(64) void k_exposure_step(float* __restrict__ bank, 
     sticky[0] += (long long)counts[3];
     sticky[1] = max(sticky[1], (long long)counts[0]);
   }
+  // a step the host counted (skip_b clear) that the overflow word held back
+  if (l == 0 && slot_skips && *skip_a && !*skip_b) slot_skips[idx[0]] += 1;
 }
 
 }  // namespace
@@ -406,12 +409,12 @@ int wgsr_gather_rows(const wgsr_gather_job* jobs, int n, const int64_t* idx, voi
 
 int wgsr_exposure_step(float* bank, const int64_t* idx, const float* grad, int nparts, const float* scalars,
                        const uint32_t* skip_a, const uint32_t* skip_b, double beta1, double beta2, double eps,
-                       int64_t* sticky, const uint32_t* counts, void* stream) {
+                       int64_t* sticky, const uint32_t* counts, int64_t* slot_skips, void* stream) {
   if (!bank || !idx || !grad || !scalars || !skip_a || !skip_b || nparts < 1)
     return set_error(WGSR_EINVAL, "wgsr_exposure_step: null pointer or no gradient rows");
   hipLaunchKernelGGL(k_exposure_step, dim3(1), dim3(64), 0, (hipStream_t)stream, bank, idx, grad, nparts, scalars, skip_a,
                      skip_b, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
-                     reinterpret_cast<long long*>(sticky), counts);
+                     reinterpret_cast<long long*>(sticky), counts, reinterpret_cast<long long*>(slot_skips));
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? WGSR_OK : set_error(WGSR_EHIP, "wgsr_exposure_step: %s", hipGetErrorString(e));
 }

@@ -672,6 +672,9 @@ __device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cf
     c[0] = 0.f; c[2] = 0.f; c[4] = 0.f; c[6] = 0.f;
     r.j[1] = 0u;
   }
+  // (the wave's own LDS accesses complete in order; the instruction-free wave
+  // barrier keeps the compiler from hoisting the cross-lane reads below)
+  __builtin_amdgcn_wave_barrier();
   // per-lane targets of the two-entry sums (constants of the lane)
   const int yv = sum20_y_value(lane), zv = sum20_z_value(lane);
   const int yk = yv >> 1, ye = yv & 1, zk = zv >> 1, ze = zv & 1;
@@ -745,6 +748,7 @@ __device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cf
       hits |= 1ull << jj.y;
     }
   }
+  __builtin_amdgcn_wave_barrier();  // (the next batch's compaction writes stay behind these reads)
   return hits;
 }
 

@@ -1942,7 +1942,10 @@ __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, c
     q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
     R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // (a wave's own LDS writes are visible to its later reads: no barrier)
+  // (a wave's own LDS accesses complete in order; the wave barrier -- no
+  // instruction -- keeps the compiler from moving the cross-lane reads below
+  // above these writes)
+  __builtin_amdgcn_wave_barrier();
   after();
   if (touch) {
     fwd_blend_pairs<true>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
@@ -1956,6 +1959,7 @@ __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, c
   } else {
     fwd_blend_pairs<false>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
   }
+  __builtin_amdgcn_wave_barrier();  // (the next batch's compaction writes stay behind these reads)
 }
 
 // One 16x16 tile per workgroup of 4 waves; wave w owns the 8x8 quadrant w,
@@ -2217,6 +2221,9 @@ __global__ __launch_bounds__(256) void k_render_fwd_dec(
       q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
       R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // cross-lane LDS traffic of one wave: ordered by the hardware, and kept in
+    // program order by the (instruction-free) wave barriers here and below
+    __builtin_amdgcn_wave_barrier();
     if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);  // the previous batch's
     fl_tv = 0;
     if (touch) {
@@ -2226,6 +2233,7 @@ __global__ __launch_bounds__(256) void k_render_fwd_dec(
     } else {
       fwd_blend_pairs<false>(n, L, L.touch, pxy, T, c01, c2d, last, dm);
     }
+    __builtin_amdgcn_wave_barrier();
   }
   if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w]

@@ -143,7 +143,7 @@ def load():
         L.wgsr_gaussian_activate.restype = c_int
         L.wgsr_gaussian_activate.argtypes = [c_int] + [_fp] * 7 + [_fp]
         L.wgsr_gaussian_activate_backward_stats.restype = c_int
-        L.wgsr_gaussian_activate_backward_stats.argtypes = ([c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 8
+        L.wgsr_gaussian_activate_backward_stats.argtypes = ([c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 9
                                                             + [_fp])
         L.wgsr_gaussian_activate_backward.restype = c_int
         L.wgsr_gaussian_activate_backward.argtypes = [c_int] + [_fp] * 6 + [ctypes.c_float] + [_fp] * 3 + [_fp]
@@ -249,7 +249,7 @@ def load():
         L.wgsr_gather_rows.restype = c_int
         L.wgsr_gather_rows.argtypes = [ctypes.POINTER(GatherJob), c_int, _fp, _fp]
         L.wgsr_exposure_step.restype = c_int
-        L.wgsr_exposure_step.argtypes = [_fp] * 3 + [c_int] + [_fp] * 3 + [ctypes.c_double] * 3 + [_fp, _fp, _fp]
+        L.wgsr_exposure_step.argtypes = [_fp] * 3 + [c_int] + [_fp] * 3 + [ctypes.c_double] * 3 + [_fp] * 4
         L.wgsr_mlp_backward.restype = c_int
         L.wgsr_mlp_backward.argtypes = [c_int, c_int] + [_fp] * 3 + [ctypes.c_float] + [_fp] * 6 + [_fp]
         L.wgsr_dino_reg.restype = c_int

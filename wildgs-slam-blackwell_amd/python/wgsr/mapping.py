@@ -240,10 +240,13 @@ class MappingStep:
             cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
             self.D, cam["campos"], False, False)
 
-    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True):
+    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True, skip=None):
         """Rasteriser backward straight into the gradient storage, activation
         backward (isotropic term folded in), densification statistics.
-        -> (dL/dmeans2D, dL/dtau summed over P, or None without need_tau)."""
+        ``skip``: a capacity-mode forward's overflow word (counts[3:4]); when
+        set on the device the statistics stay unchanged (that iteration has no
+        gradient).  -> (dL/dmeans2D, dL/dtau summed over P, or None without
+        need_tau)."""
         from diff_gaussian_rasterization import _C
         L = _lib.load()
         dev = self.xyz.device
@@ -264,7 +267,7 @@ class MappingStep:
                 self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
                 p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
                 p(self.grad["scaling"]), p(self.grad["rotation"]), p(radii), p(dL_dmeans2D), p(self.max_radii2D),
-                p(self.xyz_gradient_accum), p(self.denom), st))
+                p(self.xyz_gradient_accum), p(self.denom), p(skip) if skip is not None else None, st))
         return dL_dmeans2D, (dL_dtau.sum(0) if need_tau else None)
 
     def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
@@ -371,16 +374,19 @@ class MappingStep:
                                      train_frac, ssim_frac, cfg, initialization, freeze_uncertainty_loss,
                                      median_depth, extra=(self.iso_part, w_iso), pre_exposed=pre_exposed)
         d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state, exposure_partials=exposure_partials)
-        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso, need_tau)
+        _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso, need_tau,
+                                skip=counts[3:4] if cap is not None else None)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:
             uncertainty.backward(d_unc.to(uncertainty.dtype))
         if exposure_partials:
             return {"loss": loss, "dexposure_partials": d_a, "radii": radii, "image": image, "depth": depth,
-                    "num_rendered": nr, "uncertainty_grad": d_unc, "uncertainty_loss": state.uncertainty_loss,
+                    "n_touched": fwd[8], "num_rendered": nr, "uncertainty_grad": d_unc,
+                    "uncertainty_loss": state.uncertainty_loss,
                     "drho": tau[:3] if tau is not None else None, "dtheta": tau[3:] if tau is not None else None}
         return {"loss": loss, "dexposure_a": d_a, "dexposure_b": d_b,
                 "drho": tau[:3] if tau is not None else None, "dtheta": tau[3:] if tau is not None else None,
-                "radii": radii, "image": image, "depth": depth, "num_rendered": nr, "uncertainty_grad": d_unc,
+                "radii": radii, "image": image, "depth": depth, "n_touched": fwd[8], "num_rendered": nr,
+                "uncertainty_grad": d_unc,
                 "uncertainty_loss": state.uncertainty_loss}
 
     @torch.no_grad()

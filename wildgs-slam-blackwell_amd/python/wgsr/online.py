@@ -467,7 +467,7 @@ class OnlineMapper:
             dv = torch.from_numpy(hs).to(self.dev, non_blocking=True)
             with torch.cuda.device(self.dev):
                 _lib.check(L.wgsr_exposure_step(p(self.bank.ex), p(dv[2:4]), p(g), int(g.shape[0]), p(dv[0:2]),
-                                                p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None,
+                                                p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None, None,
                                                 _lib.stream_handle(self.dev)))
             return
         da, db = out["dexposure_a"], out["dexposure_b"]
@@ -477,9 +477,16 @@ class OnlineMapper:
         with torch.cuda.device(self.dev):
             _lib.check(L.wgsr_adam_step((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, _lib.stream_handle(self.dev)))
 
+    def _settle_replays(self):
+        """The graph replays' overflow bookkeeping (IterationGraphs.account)
+        before the host resets or reads optimiser step counts."""
+        if self.graphs is not None:
+            self.graphs.account()
+
     def _new_exposure_optimizer(self):
         """mapper.py:219-241: a fresh Adam over the window's exposures (not kf
         0): zero moments and step counts on their exposure-bank rows."""
+        self._settle_replays()
         self.bank.sync(self.keyframes)
         uids = {k for k in self.window if k != 0 and k in self.keyframes}
         if uids:
@@ -526,7 +533,10 @@ class OnlineMapper:
         """Mapper._update_keyframes_from_frontend (mapper.py:365-429): the
         tracker's new poses (and, in the reference's ablation without metric
         depth, new depths) of existing keyframes.  ``updates``: {kf uid:
-        (w2c [4, 4], depth [1, H, W] or None)}.  A keyframe whose pose is
+        (w2c [4, 4], depth [1, H, W] or None[, invalid])} -- ``invalid`` is
+        get_w2c_and_depth's flag (too few valid frontend depths): the new
+        depth is still stored, but the map moves rigidly (mapper.py:413-421).
+        A keyframe whose pose is
         unchanged (allclose, atol 1e-6) and that has no new depth is skipped;
         the others get the new pose (and depth) and, with ``deform``
         (mapping.deform_gaussians, default True), their anchored Gaussians
@@ -536,7 +546,9 @@ class OnlineMapper:
         (mapper.py:399-401 then 423-429), so its rescale factor is 1.
         Returns the number of keyframes moved."""
         frames = []
-        for k, (w2c, depth) in updates.items():
+        for k, upd in updates.items():
+            w2c, depth = upd[0], upd[1]
+            invalid = bool(upd[2]) if len(upd) > 2 else False
             kf = self.keyframes[k]
             w2c = torch.as_tensor(w2c, dtype=torch.float32).cpu()
             w2c_old = kf.w2c()
@@ -547,8 +559,10 @@ class OnlineMapper:
                 kf.depth = depth.to(kf.image.device, torch.float32).reshape(1, kf.H, kf.W).contiguous()
                 kf.median_depth = kf.depth.median()
             fr = {"kf_id": k, "w2c": w2c, "w2c_old": w2c_old}
-            if depth is not None:
+            if depth is not None and not invalid:
                 fr.update(method="depth", depth=kf.depth[0], depth_old=kf.depth[0])
+            else:
+                fr["method"] = "rigid"
             frames.append(fr)
         if deform and frames and self.ms is not None:
             K = self.keyframes[frames[0]["kf_id"]].K
@@ -605,6 +619,7 @@ class OnlineMapper:
             self._exposure_step(kf, out)
             self.uopt.step()
             self.uopt.zero_grad()
+        self._settle_replays()
 
     def map_opt_online(self, window, iters: int = 1):
         """mapper.py:1049-1219."""
@@ -651,4 +666,5 @@ class OnlineMapper:
                 continue
             self._iteration(kf, nb, False, update, reset, occ_window=window if last else None)
             split = split or update or reset is not None
+        self._settle_replays()
         return split

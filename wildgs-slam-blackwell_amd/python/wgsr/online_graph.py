@@ -227,6 +227,11 @@ class IterationGraphs:
         self.sticky = torch.zeros(2, dtype=torch.int64, device=dev)   # overflowed replays, max N_rect
         self.sticky_host = torch.zeros(2, dtype=torch.int64).pin_memory()
         self.sticky_np = self.sticky_host.numpy()
+        # per exposure-bank row: replayed exposure steps the overflow word held
+        # back (the host had already counted them in kopt_steps)
+        self.slot_skips = torch.zeros(0, dtype=torch.int64, device=dev)
+        self.replays_since_account = 0
+        self.pending_mx = 0          # largest N_rect of replays already accounted
         self.graphs = {}
         self.key = None
         self.pool = None
@@ -292,6 +297,8 @@ class IterationGraphs:
         g = opt.param_groups[0]
         S.mlp_lr, S.mlp_betas, S.mlp_eps, S.mlp_wd = g["lr"], g["betas"], g["eps"], g.get("weight_decay", 0.0)
         m.ms.iso_part  # noqa: B018  (allocated outside the capture)
+        if self.slot_skips.numel() < B.ex.shape[0]:
+            self.slot_skips = torch.zeros(B.ex.shape[0], dtype=torch.int64, device=dev)
         self.S = S
 
     def _gather_jobs(self, nbc: int):
@@ -364,7 +371,7 @@ class IterationGraphs:
             _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), int(gex.shape[0]),
                                             p(self.f32[self.F_EXPO:self.F_EXPO + 2]),
                                             p(skip), p(self.i32[self.F_EXSKIP:self.F_EXSKIP + 1]), 0.9, 0.999, 1e-8,
-                                            p(self.sticky), p(self.counts), st))
+                                            p(self.sticky), p(self.counts), p(self.slot_skips), st))
         ts, off = [], 0
         opt = m.uopt
         for prm in S.mlp_params:
@@ -426,19 +433,25 @@ class IterationGraphs:
         return g
 
     # -- the step ----------------------------------------------------------------
-    def _check_capacity(self, new_generation: bool):
-        """The pair capacity: twice the largest upstream num_rendered seen since
-        the last check (replays through the pinned copy of the device maximum,
-        eager iterations through the mapper's own record) + 4096.  Changed --
-        and the graphs recaptured -- after an overflow, when the maximum comes
-        within 3/4 of the capacity, or, for a new map state, when it is more
-        than twice what is needed (the map shrank after a prune)."""
-        ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
-        if not new_generation and self.cap is not None and not ovf and mx <= 0.75 * self.cap:
-            return
+    def account(self, consume: bool = False):
+        """Settle the overflow bookkeeping of the replays so far: wait for them
+        (so no in-flight replay is missed), roll back the step counts of the
+        optimiser steps an overflow held back -- the Gaussians' and the MLP's
+        by the overflow count, each keyframe's exposure by its row's count in
+        ``slot_skips`` -- and zero the device words.  Called before the
+        capacity changes and whenever the host is about to reset or read the
+        step counts (the end of a map_opt_online / final_refine call, a new
+        exposure optimiser).  Returns (overflowed replays, largest N_rect);
+        the latter is kept for the next capacity check unless ``consume``."""
+        if self.replays_since_account == 0:
+            mx = self.pending_mx
+            if consume:
+                self.pending_mx = 0
+            return 0, mx
+        torch.cuda.synchronize(self.dev)
+        self.replays_since_account = 0
+        ovf, mx = int(self.sticky_np[0]), max(int(self.sticky_np[1]), self.pending_mx)
         if ovf:
-            torch.cuda.synchronize(self.dev)
-            ovf, mx = int(self.sticky_np[0]), int(self.sticky_np[1])
             self.stats["overflows"] += 1
             self.stats["skipped_iterations"] += ovf
             # the skipped steps advanced no moments on the device: undo their counts
@@ -447,7 +460,31 @@ class IterationGraphs:
             if self.S is not None:
                 for t in self.S.mlp_steps:
                     t -= ovf
+            sk = self.slot_skips.cpu().numpy()
+            if sk.any():
+                by_slot = {s_: u for u, s_ in self.m.bank.slots.items()}
+                for s_ in np.nonzero(sk)[0]:
+                    uid = by_slot.get(int(s_))
+                    if uid in self.m.kopt_steps:
+                        self.m.kopt_steps[uid] -= int(sk[s_])
+                self.slot_skips.zero_()
             self.m.events.append((self.m.iteration_count, "capacity_overflow", {"cap": self.cap, "skipped": ovf}))
+        self.sticky.zero_()
+        self.sticky_np[:] = 0
+        self.pending_mx = 0 if consume else mx
+        return ovf, mx
+
+    def _check_capacity(self, new_generation: bool):
+        """The pair capacity: twice the largest upstream num_rendered seen since
+        the last check (replays through the pinned copy of the device maximum,
+        eager iterations through the mapper's own record) + 4096.  Changed --
+        and the graphs recaptured -- after an overflow, when the maximum comes
+        within 3/4 of the capacity, or, for a new map state, when it is more
+        than twice what is needed (the map shrank after a prune)."""
+        ovf, mx = int(self.sticky_np[0]), max(int(self.sticky_np[1]), self.pending_mx)
+        if not new_generation and self.cap is not None and not ovf and mx <= 0.75 * self.cap:
+            return
+        ovf, mx = self.account(consume=True)
         want = max(self.min_cap, int(self.cap_scale * max(mx, int(self.m._max_nr))) + self.cap_margin)
         if ovf and self.cap is not None:
             want = max(want, 2 * self.cap)
@@ -456,8 +493,6 @@ class IterationGraphs:
                 self.invalidate()
             self.cap = want
         self.m._max_nr = 0
-        self.sticky.zero_()
-        self.sticky_np[:] = 0
 
     def step(self, kf, neighbours, refine: bool = False) -> bool:
         """Run one steady-state iteration on keyframe ``kf`` as a graph replay;
@@ -516,6 +551,7 @@ class IterationGraphs:
         t_end = time.perf_counter()
         torch._foreach_add_(S.mlp_steps, 1.0)
         self.stats["replays"] += 1
+        self.replays_since_account += 1
         self.stats["replay_call_s"] += t_end - t_rep
         self.stats["step_host_s"] += time.perf_counter() - t_step
         return True
