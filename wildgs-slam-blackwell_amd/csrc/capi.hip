@@ -27,8 +27,8 @@ struct HostCounters {
   // the D->H copy runs on a side stream behind `pre` (recorded after
   // k_preprocess), so the forward's stream goes straight on to the depth
   // sort instead of waiting out the copy and its host-visible release
-  // (~10 us of the stream's time per forward); WGSR_COUNTER_SIDE=0 keeps
-  // the copy on the forward's stream
+  // (~10 us of the stream's time per forward; used when the Gaussian-level
+  // depth sort runs, which the copy then overlaps)
   hipStream_t side = nullptr;
   hipEvent_t pre = nullptr;
 };
@@ -45,15 +45,9 @@ HostCounters& host_counters() {
     if (hipHostMalloc(&p, kCounterBytes, hipHostMallocDefault) != hipSuccess) p = nullptr;
     hc.buf = static_cast<uint32_t*>(p);
     if (hipEventCreateWithFlags(&hc.ev, hipEventDisableTiming) != hipSuccess) hc.ev = nullptr;
-    static const bool side_off = [] {
-      const char* e = getenv("WGSR_COUNTER_SIDE");
-      return e && strcmp(e, "0") == 0;
-    }();
-    if (!side_off) {
-      if (hipStreamCreateWithFlags(&hc.side, hipStreamNonBlocking) != hipSuccess) hc.side = nullptr;
-      if (hc.side && hipEventCreateWithFlags(&hc.pre, hipEventDisableTiming) != hipSuccess) hc.pre = nullptr;
-      if (!hc.pre) hc.side = nullptr;
-    }
+    if (hipStreamCreateWithFlags(&hc.side, hipStreamNonBlocking) != hipSuccess) hc.side = nullptr;
+    if (hc.side && hipEventCreateWithFlags(&hc.pre, hipEventDisableTiming) != hipSuccess) hc.pre = nullptr;
+    if (!hc.pre) hc.side = nullptr;
   }
   return hc;
 }
@@ -63,29 +57,20 @@ HostCounters& host_counters() {
 // and its k_preprocess zeroes the other for the next forward on this thread.
 // The previous forward's block was last touched by its D->H copy, which the
 // host waited for before that call returned, so no stream (ours or another)
-// can still be reading it.  WGSR_COUNTER_MEMSET=1 keeps the memset of the
-// geometry buffer's counter block.
+// can still be reading it.  (If the two blocks cannot be allocated, the
+// geometry buffer's counter block is zeroed by a memset per call.)
 struct DevCounters {
   uint32_t* buf = nullptr;  // 2 x kCounterBytes, zeroed once
   int parity = 0;
   bool failed = false;
 };
-// WGSR_BDS_EMIT: 1 / 0 forces the per-tile list emit of the per-bin depth
-// sort on / off (-1: by bin size)
-int bds_emit_mode() {
-  static const int m = [] {
-    const char* e = getenv("WGSR_BDS_EMIT");
-    return e ? (atoi(e) ? 1 : 0) : -1;
-  }();
-  return m;
-}
+// The per-bin depth sort emits the per-tile lists itself for small bins
+// (2 x 2 tiles: TUM 512 x 384, 35.4 -> 33.8 us for sort + lists); with 4 x 4-
+// tile bins (1080p) the 16-tile compaction inside the one-workgroup-per-CU
+// sort costs more than k_expand_bins' 4x wider grid (140.8 vs 131.3 us).
+bool bds_emit(int bshift) { return bshift <= 1; }
 
 DevCounters* dev_counters(hipStream_t s) {
-  static const bool off = [] {
-    const char* e = getenv("WGSR_COUNTER_MEMSET");
-    return e && strcmp(e, "1") == 0;
-  }();
-  if (off) return nullptr;
   thread_local DevCounters per_dev[kMaxDevices];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
@@ -111,12 +96,6 @@ int set_error(int code, const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
   return code;
-}
-
-// WGSR_SCAN_SUP=0: the dual scan's block prefix by its own scan kernel
-static bool scan_sup_mode() {
-  const char* e = getenv("WGSR_SCAN_SUP");  // read per call: tests compare both
-  return !(e && strcmp(e, "0") == 0);
 }
 
 int num_bits(uint32_t n) {
@@ -369,7 +348,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     zj.n[zj.count++] = sup_words;
   }
   // ... and, with sort bins, the dual scan's superblock sums
-  const bool scan_sup = bshift && scan_sup_mode();
+  const bool scan_sup = bshift != 0;
   if (scan_sup) {
     zj.p[zj.count] = at<float>(geom, GL.bsup);
     zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
@@ -569,12 +548,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       StageTimer T(4, s);
       uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
       uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
-      // Emitting the lists from the sort kernel pays for small bins (2 x 2
-      // tiles: TUM 512 x 384, 35.4 -> 33.8 us for sort + lists); with 4 x 4-tile
-      // bins (1080p) the 16-tile compaction inside the one-workgroup-per-CU
-      // sort costs more than k_expand_bins' 4x wider grid (140.8 vs 131.3 us).
-      // WGSR_BDS_EMIT=0 / 1 forces either.
-      const bool emit = bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1);
+      const bool emit = bds_emit(bshift);
       STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift, at<uint2>(image, IL.tile_m),
                                         bounds_done, pdep, okeys, ogid, bds_scratch, s, emit ? lists : nullptr,
                                         ranges, at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta)));
@@ -585,7 +559,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       }
     }
     StageTimer T(5, s);
-    if (bin_depth && (bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1))) {
+    if (bin_depth && bds_emit(bshift)) {
       // (lists and ranges written by the per-bin depth sort)
     } else if (bshift) {
       STAGE(a, s, launch_expand_bins(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift,
@@ -679,7 +653,7 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   uint32_t* meta = at<uint32_t>(image, IL.meta);
   HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
   ZeroJob zj{};
-  const bool scan_sup = scan_sup_mode();
+  const bool scan_sup = true;
   if (scan_sup) {
     zj.p[zj.count] = at<float>(geom, GL.bsup);
     zj.n[zj.count++] = 2 * kScanSupStride * packed_scan_supers((size_t)a.P);
@@ -719,7 +693,7 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
   const uint32_t* sorted_gid = at<uint32_t>(binning, BL.point_g);
   uint2* ranges = at<uint2>(image, IL.ranges);
-  const bool emit = bds_emit_mode() == 1 || (bds_emit_mode() < 0 && bshift <= 1);
+  const bool emit = bds_emit(bshift);
   uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
   uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
   { StageTimer T(4, s);
@@ -753,14 +727,13 @@ int render_backward_pairs(const wgsr_raster_args& a, const void* geom, void* bin
   const Grid grid(a);
   const ImageLayout IL(a.W, a.H);
   const size_t N = (size_t)num_rendered;
-  // scratch: 48-byte partial record per pair + per-Gaussian partial sums
-  // gsum[10][P] (used by the split per-Gaussian backward).  The 1-byte
-  // "record written" flag per pair lives in the binning buffer, zeroed by the
-  // forward's k_duplicate (render_bwd sets it for the same pairs on every
-  // backward call of that forward, so repeated backwards agree).
+  // scratch: 48-byte partial record per pair.  The 1-byte "record written"
+  // flag per pair lives in the binning buffer, zeroed by the forward's
+  // k_duplicate (render_bwd sets it for the same pairs on every backward call
+  // of that forward, so repeated backwards agree).
   const size_t rec_bytes = align256(48 * N);
-  void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes + align256(40 * (size_t)a.P));
-  if (!scratch) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
+  void* scratch = call_alloc(scratch_alloc, ctx, rec_bytes);
+  if (!scratch && rec_bytes) return set_error(WGSR_EALLOC, "backward scratch allocation failed");
   float4* partial = N > 0 ? static_cast<float4*>(scratch) : nullptr;
   const BinLayout BL(N);
   uint8_t* pflag = N > 0 ? at<uint8_t>(binning, BL.flag) : nullptr;
@@ -800,11 +773,10 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   hipStream_t s = (hipStream_t)stream;
   float4* partial = nullptr;
   uint8_t* pflag = nullptr;
-  // sparse per-Gaussian backward: the render backward zero-fills the outputs
-  // and k_gauss_bwd writes only the rows that received gradient
-  const GbMode mode = gauss_bwd_mode();
+  // the render backward zero-fills the outputs and k_gauss_bwd_compact writes
+  // only the rows of the Gaussians that received gradient
   ZeroJob zero{};
-  if (mode == kGbSparse) {
+  {
     const uint64_t P = (uint64_t)a.P;
     auto add = [&](float* p, uint64_t n) {
       if (p && n) { zero.p[zero.count] = p; zero.n[zero.count] = n; ++zero.count; }
@@ -818,11 +790,9 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
   if (int e = render_backward_pairs(a, geom, binning, image, num_rendered, dL_dcolor, dL_ddepth, scratch_alloc, ctx,
                                     zero, s, &partial, &pflag))
     return e;
-  float* gsum = partial ? reinterpret_cast<float*>(reinterpret_cast<char*>(partial) + align256(48 * (size_t)num_rendered))
-                        : nullptr;
   StageTimer T(8, s);
-  STAGE(a, s, launch_gauss_bwd(a, radii, geom, partial, pflag, gsum, dL_dmeans2D, dL_dcolors, dL_dopacity,
-                               dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dL_dtau, mode, true, s));
+  STAGE(a, s, launch_gauss_bwd(a, geom, partial, pflag, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                               dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
   return WGSR_OK;
 }
 

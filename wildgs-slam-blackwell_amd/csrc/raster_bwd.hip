@@ -25,11 +25,6 @@ namespace wgsr {
 namespace {
 
 constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
-// the quad backward keeps its "entry left a partial" flags as one SGPR mask
-// instead of an LDS array (one VALU move and one LDS store fewer per entry)
-#ifndef WGSR_BWD_HITMASK
-#define WGSR_BWD_HITMASK 1
-#endif
 // diagnostic build: histogram of (quadrants reached, quadrants evaluated in
 // phase 2) per entry over the quad backward (wgsr_debug_bwd_stats)
 #ifndef WGSR_BWD_STATS
@@ -38,7 +33,7 @@ constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 #if WGSR_BWD_STATS
 __device__ unsigned long long g_bwd_stats[32];
 #endif
-// below this many tiles the backward runs k_render_bwd_split (four waves per
+// below this many tiles the backward runs k_render_bwd_seg (four waves per
 // tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
 constexpr int kBwdSplitBelowTiles = 3072;
 
@@ -201,9 +196,6 @@ __device__ __forceinline__ void render_bwd_quad_tile(
     sA[lane] = nA;
     sB[lane] = nB;
     sC[lane] = nC;
-#if !WGSR_BWD_HITMASK
-    sHit[lane] = 0;
-#endif
     __syncthreads();
     if (phit) {
       const size_t k = ss_prev + pair_local(pA, pB, lr_rect(make_uint4(rw_prev.x, rw_prev.y, 0u, 0u)), tab_prev,
@@ -245,9 +237,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       }
     }
     uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
-#if WGSR_BWD_HITMASK
-    uint64_t hitm = 0;  // entries that left a partial (wave-uniform: SGPRs)
-#endif
+    uint64_t hitm = 0;  // entries that left a partial (wave-uniform: SGPRs, not an LDS array)
     while (todo) {
       const int j = __builtin_ctzll(todo);
       todo &= todo - 1;
@@ -320,270 +310,15 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       if (!hit) continue;  // no pixel of the tile: no partial
       const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g45.x, g45.y, g67.x, g67.y, g89.x, g89.y};
       wave_sum10_store_m(gv, sPm + 11 * j);
-#if WGSR_BWD_HITMASK
       hitm |= 1ull << j;
-#else
-      if (lane == 0) sHit[j] = 1;
-#endif
     }
-#if WGSR_BWD_HITMASK
     hit_prev = hitm & (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull));
-#else
-    __syncthreads();
-    hit_prev = wave_ballot(lane < cnt && sHit[lane]);
-#endif
   }
   write_records();  // the last batch's
 #if WGSR_BWD_STATS
   __syncthreads();
   if (lane < 32) atomicAdd(&g_bwd_stats[lane], (unsigned long long)sStat[lane]);
 #endif
-}
-
-// Pixel-pair variant of render_bwd_quad_tile (WGSR_BWD_PAIR=1; off by
-// default: measured 340 vs 306 us at 1M / 1080p -- 18.5k vs 17.6k VALU per
-// wave, since an entry reaching one quadrant of a row pair still pays both
-// pixels' exp2 and a row pair runs phase 2 whenever any lane of the tile
-// took the entry):
-// the same wave per tile and per-quadrant culling, but the lane's pixels of
-// horizontally adjacent quadrants (0, 1) and (2, 3) -- same row, x and x + 8
-// -- are evaluated TOGETHER in packed-FP32 math whenever the entry reaches
-// both (most entries reach 3-4 quadrants): every per-pixel operation of the
-// two evaluations except the transcendentals and compares is one v_pk_*
-// instruction, and the two pixels share dy.  The per-pixel arithmetic is the
-// forward's own operation sequence (dx = mean - (x0 + 8), power =
-// dx (A.z dx + B.x dy) + (A.w dy) dy), so alpha is bitwise the forward's.
-// A pair runs branch-free: a pixel the entry misses gets G = 0 and alpha = 0
-// (T, the accumulated colour and every sum pass through exactly).  An entry
-// reaching only one quadrant of a row pair evaluates that pixel alone
-// (exec-masked, as the quad tile).  Per-entry sums are pairs (one half per
-// pixel of the pair), added together once before the wave reduction; the
-// first evaluation of an entry writes them, later ones accumulate.
-// The background enters as the accumulated colour's starting value: upstream's
-// dL/dalpha term -T_final / (1 - alpha) (bg . dL/dpix) equals
-// -T (prod of (1 - alpha) behind the entry) (bg . dL/dpix), which is what the
-// accum_rec recurrence adds when it starts from bg instead of 0 -- so one
-// code path serves every background (a black one starts from 0).
-#ifndef WGSR_BWD_PAIR
-#define WGSR_BWD_PAIR 0
-#endif
-
-// phase 1 of one row pair (the lane's pixels at x and x + 8, same y) for
-// one entry: the forward's power / alpha and the per-pixel contribution tests
-// (reach: the entry reaches that quadrant at all, wave-uniform)
-struct PairP1 {
-  v2f G, av;
-  uint64_t mA, mB;  // lanes whose pixel takes this entry (SGPR lane masks)
-};
-__device__ __forceinline__ PairP1 bwd_pair_p1(v2f dX, v2f tX, float dy, float w, float cxy, float op, uint32_t cidx,
-                                              uint32_t lastA, uint32_t lastB, bool reachA, bool reachB) {
-  PairP1 r;
-  const v2f in = pfma(v2f{cxy, cxy}, v2f{dy, dy}, tX);
-  const v2f pw = pfma(dX, in, v2f{w, w});
-  r.G = v2f{__builtin_amdgcn_exp2f(pw.x), __builtin_amdgcn_exp2f(pw.y)};
-  const v2f ag = v2f{op, op} * r.G;
-  r.av = v2f{fminf(kMaxAlpha, ag.x), fminf(kMaxAlpha, ag.y)};
-  // each test its own ballot, combined by scalar ops (a ballot of the
-  // compound predicate would go through a VGPR)
-  const uint64_t mA = wave_ballot(cidx < lastA) & wave_ballot(pw.x <= 0.0f) & wave_ballot(r.av.x >= kMinAlpha);
-  const uint64_t mB = wave_ballot(cidx < lastB) & wave_ballot(pw.y <= 0.0f) & wave_ballot(r.av.y >= kMinAlpha);
-  r.mA = reachA ? mA : 0ull;
-  r.mB = reachB ? mB : 0ull;
-  return r;
-}
-
-// phase 2 of one row pair, branch-free: a pixel the entry does not reach
-// (v false) runs with alpha = 0 and G = 0, which passes T and the
-// accumulated colour through exactly (1 / (1 - 0) = 1) and adds 0 to every
-// sum.  kInit: write the sums instead of adding to them.
-template <bool kInit>
-__device__ __forceinline__ void bwd_pair_p2(const PairP1& q, v2f dX, float dy, v2f c01, v2f c2d, v2f& T, v2f& acc,
-                                            const v2f (&dp)[4], v2f (&S)[10]) {
-  const bool vA = __builtin_amdgcn_inverse_ballot_w64(q.mA), vB = __builtin_amdgcn_inverse_ballot_w64(q.mB);
-  const v2f a{vA ? q.av.x : 0.f, vB ? q.av.y : 0.f};
-  const v2f Ge{vA ? q.G.x : 0.f, vB ? q.G.y : 0.f};
-  const v2f om = v2f{1.f, 1.f} - a;
-  const v2f rinv{__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};  // alpha <= 0.99
-  const v2f Tn = T * rinv;
-  T = Tn;
-  const v2f dch = a * Tn;
-  // c . dL/d(colour, depth) per pixel: upstream's accum_rec recurrence, dotted
-  const v2f cp = pfma(v2f{c2d.y, c2d.y}, dp[3],
-                      pfma(v2f{c2d.x, c2d.x}, dp[2], pfma(v2f{c01.y, c01.y}, dp[1], v2f{c01.x, c01.x} * dp[0])));
-  const v2f sd = cp - acc;
-  const v2f dLda = sd * Tn;
-  acc = pfma(a, sd, acc);
-  const v2f gl = Ge * dLda;
-  const v2f dyy{dy, dy};
-  const v2f ux = gl * dX, uy = gl * dyy;
-  if (kInit) {
-    S[0] = ux; S[1] = uy; S[2] = ux * dX; S[3] = ux * dyy; S[4] = uy * dyy; S[5] = gl;
-    S[6] = dch * dp[0]; S[7] = dch * dp[1]; S[8] = dch * dp[2]; S[9] = dch * dp[3];
-  } else {
-    S[0] += ux; S[1] += uy;
-    S[2] = pfma(ux, dX, S[2]); S[3] = pfma(ux, dyy, S[3]); S[4] = pfma(uy, dyy, S[4]);
-    S[5] += gl;
-    S[6] = pfma(dch, dp[0], S[6]); S[7] = pfma(dch, dp[1], S[7]);
-    S[8] = pfma(dch, dp[2], S[8]); S[9] = pfma(dch, dp[3], S[9]);
-  }
-}
-
-__device__ __forceinline__ void render_bwd_pair_tile(
-    const uint32_t tile, const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_g,
-    const float4* __restrict__ splat, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
-    int H, int gx, float bg0, float bg1, float bg2, const float* __restrict__ final_Ts,
-    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
-    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, float4 (*sA2)[kBatch],
-    float4 (*sB2)[kBatch], float4 (*sC2)[kBatch], float (*sP)[11]) {
-  constexpr int Q = 4;
-  const int lane = threadIdx.x;
-  const int tx0 = (int)(tile % gx) * kTile, ty0 = (int)(tile / gx) * kTile;
-  const size_t HW = (size_t)H * W;
-  const uint2 range = ranges[tile];
-  // pixel x of the lane in quadrants (0 | 2) and (1 | 3); rows y and y + 8
-  const v2f PX{(float)(tx0 + (lane & 7)), (float)(tx0 + 8 + (lane & 7))};
-  const float PY0 = (float)(ty0 + (lane >> 3)), PY1 = (float)(ty0 + 8 + (lane >> 3));
-  // row pair r: T, accd, dL/dpix channels as (pixel of quadrant 2r, of 2r + 1)
-  v2f T[2], acc[2], dp[2][4];
-  uint32_t last[Q];
-  uint32_t m = 0, mq[Q];
-  {
-    float Tq[Q], dq[Q][4];
-    bool inside[Q];
-#pragma unroll
-    for (int p = 0; p < Q; ++p) {
-      const int px = tx0 + (p & 1) * 8 + (lane & 7), py = ty0 + (p >> 1) * 8 + (lane >> 3);
-      inside[p] = px < W && py < H;
-      const size_t pid = inside[p] ? (size_t)py * W + px : 0;
-      Tq[p] = final_Ts[pid];
-      last[p] = n_contrib[pid];
-      dq[p][0] = dL_dpix[pid];
-      dq[p][1] = dL_dpix[HW + pid];
-      dq[p][2] = dL_dpix[2 * HW + pid];
-      dq[p][3] = dL_ddep[pid];
-    }
-#pragma unroll
-    for (int p = 0; p < Q; ++p) {
-      Tq[p] = inside[p] ? Tq[p] : 0.f;
-      last[p] = inside[p] ? last[p] : 0u;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) dq[p][c] = inside[p] ? dq[p][c] : 0.f;
-      uint32_t x = last[p];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
-      mq[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);  // wave-uniform: an SGPR
-      m = max(m, mq[p]);
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      T[r] = v2f{Tq[2 * r], Tq[2 * r + 1]};
-      // the background as the colour behind the last contributor (see above)
-      acc[r] = v2f{bg0 * dq[2 * r][0] + bg1 * dq[2 * r][1] + bg2 * dq[2 * r][2],
-                   bg0 * dq[2 * r + 1][0] + bg1 * dq[2 * r + 1][1] + bg2 * dq[2 * r + 1][2]};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) dp[r][c] = v2f{dq[2 * r][c], dq[2 * r + 1][c]};
-    }
-  }
-  const uint32_t end = range.x + m;
-  float* const sPm = &sP[0][0] + sum10_slot(lane);
-
-  // records stream straight into LDS (global_load_lds_dwordx4: no VGPRs held
-  // for the prefetch), double buffered; Gaussian ids one batch ahead
-  auto fetch = [&](uint32_t g, int buf) {
-    const float4* src = splat + 3 * (size_t)g;
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)&sA2[buf][0], 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + 1), (__attribute__((address_space(3))) void*)&sB2[buf][0], 16,
-                                     0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(src + 2), (__attribute__((address_space(3))) void*)&sC2[buf][0], 16,
-                                     0, 0);
-  };
-  uint32_t gcur = 0, gnext = 0;
-  int buf = 0;
-  if (end >= range.x + 1 + lane) {
-    gcur = point_g[end - 1 - lane];
-    fetch(gcur, 0);
-  }
-  if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
-
-  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
-    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
-    __builtin_amdgcn_s_waitcnt(0);  // this batch's records (and the next ids) have landed
-    __syncthreads();
-    const float4* sA = sA2[buf];
-    const float4* sB = sB2[buf];
-    const float4* sC = sC2[buf];
-    const uint32_t gmine = gcur;  // this lane's entry of the batch
-    gcur = gnext;
-    if (b_end >= range.x + 1 + kBatch + lane) fetch(gcur, buf ^ 1);
-    if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
-
-    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
-    uint64_t qb[Q];
-    {
-      const uint32_t myidx = cfirst - (uint32_t)lane;
-      const float4 a = sA[lane], b = sB[lane];
-#pragma unroll
-      for (int p = 0; p < Q; ++p) {
-        const int x0 = tx0 + (p & 1) * 8, y0 = ty0 + (p >> 1) * 8;
-        qb[p] = wave_ballot(lane < cnt && myidx < mq[p] && ellipse_hits(a, b, x0, x0 + 7, y0, y0 + 7));
-      }
-    }
-    uint64_t todo = qb[0] | qb[1] | qb[2] | qb[3];
-    uint64_t hitm = 0;
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint32_t cidx = cfirst - j;
-      const float4 A = sA[j];
-      const float4 B = sB[j];
-      const float4 Cc = sC[j];
-      const v2f c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
-      const float cxy = B.x, op = B.y;
-      const v2f dX = v2f{A.x, A.x} - PX;     // mean.x - pixel x, both quadrant columns
-      const v2f tX = v2f{A.z, A.z} * dX;     // (A.z dx) of both
-      const bool r0 = (qb[0] >> j) & 1, r1 = (qb[1] >> j) & 1, r2 = (qb[2] >> j) & 1, r3 = (qb[3] >> j) & 1;
-      const float dy0 = A.y - PY0, w0 = (A.w * dy0) * dy0;
-      const float dy1 = A.y - PY1, w1 = (A.w * dy1) * dy1;
-      v2f S[10];
-      // straight-line code per case (wave-uniform): both row pairs, or one
-      if ((r0 || r1) && (r2 || r3)) {
-        const PairP1 q0 = bwd_pair_p1(dX, tX, dy0, w0, cxy, op, cidx, last[0], last[1], r0, r1);
-        const PairP1 q1 = bwd_pair_p1(dX, tX, dy1, w1, cxy, op, cidx, last[2], last[3], r2, r3);
-        if ((q0.mA | q0.mB | q1.mA | q1.mB) == 0) continue;  // no pixel of the tile: no partial
-        bwd_pair_p2<true>(q0, dX, dy0, c01, c2d, T[0], acc[0], dp[0], S);
-        bwd_pair_p2<false>(q1, dX, dy1, c01, c2d, T[1], acc[1], dp[1], S);
-      } else if (r0 || r1) {
-        const PairP1 q0 = bwd_pair_p1(dX, tX, dy0, w0, cxy, op, cidx, last[0], last[1], r0, r1);
-        if ((q0.mA | q0.mB) == 0) continue;
-        bwd_pair_p2<true>(q0, dX, dy0, c01, c2d, T[0], acc[0], dp[0], S);
-      } else {
-        const PairP1 q1 = bwd_pair_p1(dX, tX, dy1, w1, cxy, op, cidx, last[2], last[3], r2, r3);
-        if ((q1.mA | q1.mB) == 0) continue;
-        bwd_pair_p2<true>(q1, dX, dy1, c01, c2d, T[1], acc[1], dp[1], S);
-      }
-      float gv[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) gv[k] = S[k].x + S[k].y;
-      wave_sum10_store_m(gv, sPm + 11 * j);
-      hitm |= 1ull << j;
-    }
-    if (lane < cnt && ((hitm >> lane) & 1)) {
-      const uint32_t gid = gmine;
-      const float4 A = sA[lane], B = sB[lane];
-      const size_t k =
-          slot_start[gid] + pair_local(A, B, lr_rect(lrec[gid].w), lrec[gid].tab, (int)(tile % gx), (int)(tile / gx));
-      float sv[10];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) sv[q] = sP[lane][q];
-      record_sums(A, B, sv);
-      partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-      partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
-      partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
-      pflag[k] = 1;
-      gflag[gid] = 1;  // same value from every tile: a benign race
-    }
-    buf ^= 1;
-  }
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd_quad(
@@ -610,27 +345,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
   const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-#if WGSR_BWD_PAIR
-  __shared__ float4 sA2[2][kBatch], sB2[2][kBatch], sC2[2][kBatch];
-  (void)sHit; (void)sA; (void)sB; (void)sC; (void)sG;
-  render_bwd_pair_tile(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts, n_contrib,
-                       dL_dpix, dL_ddep, partial, pflag, gflag, sA2, sB2, sC2, sP);
-#else
   if (bg0 == 0.f && bg1 == 0.f && bg2 == 0.f)  // (uniform)
     render_bwd_quad_tile<false>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
                                 n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
   else
     render_bwd_quad_tile<true>(tile, ranges, point_g, splat, lrec, slot_start, W, H, gx, bg0, bg1, bg2, final_Ts,
                                n_contrib, dL_dpix, dL_ddep, partial, pflag, gflag, sA, sB, sC, sG, sP, sHit);
-#endif
   // this tile's share of the per-Gaussian outputs' zero fill (HBM is idle
   // here; measured at 1M/1080p: render_bwd +2 % with the fill after the walk,
   // +4.5 % before it, while k_gauss_bwd drops from 86 to 49 us)
   zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
 }
 
-// Entry pairs in the four-wave backward (WGSR_BWD_SPLIT_EPAIR, the default):
-// a wave owns one 8x8 quadrant, so the batch's entries that reach it are
+// Entry pairs in the four-wave backward (k_render_bwd_seg): a wave owns one
+// 8x8 quadrant, so the batch's entries that reach it are
 // compacted (two consecutive survivors interleaved per field, as the
 // forward's FwdPairRec) and walked in pairs: both entries' power, alpha,
 // 1 / (1 - alpha), colour dot products and gradient terms in packed-FP32
@@ -638,10 +366,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // entries' 10 sums reduced together (wave_sum20: two independent chains in
 // flight, 42 instead of 46 VALU).  A pixel an entry does not reach runs it
 // with alpha = 0 and G = 0 (pass-through, zero sums).  The background enters
-// as the accumulated colour's starting value (render_bwd_pair_tile).
-#ifndef WGSR_BWD_SPLIT_EPAIR
-#define WGSR_BWD_SPLIT_EPAIR 1
-#endif
+// as the accumulated colour's starting value: upstream's dL/dalpha term
+// -T_final / (1 - alpha) (bg . dL/dpix) equals -T (prod of (1 - alpha) behind
+// the entry) (bg . dL/dpix), which is what the accum_rec recurrence adds when
+// it starts from bg instead of 0 -- one code path for every background.
 struct BwdPairRec {
   float4 q[3];   // {x, x', y, y'}, {A.z, A.z', A.w, A.w'}, {B.x, B.x', o, o'}
   float4 c[2];   // {c0, c0', c1, c1'}, {c2, c2', depth, depth'}
@@ -754,185 +482,20 @@ __device__ __forceinline__ uint64_t split_batch_pairs(uint64_t todo, uint32_t cf
 
 // Small images (few tiles: TUM's 512x384 has 768) leave most SIMDs without a
 // wave under k_render_bwd_quad, and each tile's serial walk sets the time.
-// This variant gives a tile FOUR waves, one per 8x8 quadrant: wave 0 stages
-// the batch records for all of them, each wave culls and evaluates only its
-// quadrant and reduces its own sums, and wave 0 adds the (up to) four
-// quadrant sums of each hit entry into the pair's record.  Same arithmetic per
-// pixel; only the order of the final cross-quadrant sum differs.
-__global__ __launch_bounds__(256) void k_render_bwd_split(
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
-    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ lists_exact,
-    const uint32_t* __restrict__ lists_bins, const float4* __restrict__ splat,
-    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ slot_start, int W,
-    int H, int gx, int ntiles, const float* __restrict__ bg, const float* __restrict__ final_Ts,
-    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpix, const float* __restrict__ dL_ddep,
-    float4* __restrict__ partial, uint8_t* __restrict__ pflag, uint8_t* __restrict__ gflag, const ZeroJob zero) {
-  __shared__ float4 sA[kBatch], sB[kBatch], sC[kBatch];
-  __shared__ uint32_t sG[kBatch];
-  __shared__ float sP[4][kBatch][11];
-  __shared__ uint64_t sHitW[4];
-  __shared__ uint32_t sEnd[4];
-#if WGSR_BWD_SPLIT_EPAIR
-  __shared__ BwdPairRec sPairs[4][kBatch / 2];
-#endif
-  if (meta[1]) {  // overflowed capacity-mode forward (see k_render_bwd_quad)
-    zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
-    return;
-  }
-  // where the forward left the tile lists (ImageLayout::meta)
-  const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
-  const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tx = (int)(tile % gx), ty = (int)(tile / gx);
-  const int qx0 = tx * kTile + (w & 1) * 8, qy0 = ty * kTile + (w >> 1) * 8;  // this wave's quadrant
-  const size_t HW = (size_t)H * W;
-  const uint2 range = ranges[tile];
-  const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-
-  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
-  const v2f p0{(float)px, (float)py};
-  const bool inside = px < W && py < H;
-  const size_t pid = (size_t)py * W + px;
-  const float Tf = inside ? final_Ts[pid] : 0.f;
-  const uint32_t last = inside ? n_contrib[pid] : 0u;
-  const float d0 = inside ? dL_dpix[pid] : 0.f, d1 = inside ? dL_dpix[HW + pid] : 0.f;
-  const float d2 = inside ? dL_dpix[2 * HW + pid] : 0.f, dd = inside ? dL_ddep[pid] : 0.f;
-  const v2f dp01{d0, d1}, dp2d{d2, dd};
-#if WGSR_BWD_SPLIT_EPAIR
-  // the background as the colour behind the last contributor (see render_bwd_pair_tile)
-  float accd = bg0 * d0 + bg1 * d1 + bg2 * d2;
-  (void)Tf;
-#else
-  const float tb = -Tf * (bg0 * d0 + bg1 * d1 + bg2 * d2);
-  float accd = 0.f;  // accum_rec . dL/d(colour, depth), as k_render_bwd_quad
-#endif
-  float T = Tf;
-  uint32_t x = last;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
-  const uint32_t mq = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
-  if (lane == 0) sEnd[w] = mq;
-  __syncthreads();
-  const uint32_t end = range.x + max(max(sEnd[0], sEnd[1]), max(sEnd[2], sEnd[3]));
-
-  uint32_t gcur = 0, gnext = 0;
-  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (w == 0) {
-    if (end >= range.x + 1 + lane) {
-      gcur = point_g[end - 1 - lane];
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
-    }
-    if (end >= range.x + 1 + kBatch + lane) gnext = point_g[end - 1 - kBatch - lane];
-  }
-
-  for (uint32_t b_end = end; b_end > range.x; b_end = (b_end - range.x > (uint32_t)kBatch) ? b_end - kBatch : range.x) {
-    const int cnt = (int)min((uint32_t)kBatch, b_end - range.x);
-    __syncthreads();
-    if (w == 0) {
-      sA[lane] = nA;
-      sB[lane] = nB;
-      sC[lane] = nC;
-      sG[lane] = gcur;
-    }
-    __syncthreads();
-    if (w == 0) {
-      gcur = gnext;
-      if (b_end >= range.x + 1 + kBatch + lane) {
-        nA = splat[3 * (size_t)gcur];
-        nB = splat[3 * (size_t)gcur + 1];
-        nC = splat[3 * (size_t)gcur + 2];
-      }
-      if (b_end >= range.x + 1 + 2 * kBatch + lane) gnext = point_g[b_end - 1 - 2 * kBatch - lane];
-    }
-    const uint32_t cfirst = b_end - range.x - 1;  // tile-list index of entry j = cfirst - j
-    uint64_t todo = wave_ballot(lane < cnt && cfirst - (uint32_t)lane < mq &&
-                                ellipse_hits(sA[lane], sB[lane], qx0, qx0 + 7, qy0, qy0 + 7));
-#if WGSR_BWD_SPLIT_EPAIR
-    const uint64_t hits = split_batch_pairs(todo, cfirst, sA[lane], sB[lane], sC[lane], sPairs[w], sP[w], p0, last,
-                                            dp01, dp2d, T, accd, lane);
-#else
-    uint64_t hits = 0;
-    while (todo) {
-      const int j = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint32_t cidx = cfirst - j;
-      const float4 A = sA[j];
-      const float4 B = sB[j];
-      const float4 Cc = sC[j];
-      const v2f mxy{A.x, A.y}, cd{A.z, A.w}, c01{Cc.x, Cc.y}, c2d{Cc.z, Cc.w};
-      const float cxy = B.x, op = B.y;
-      const v2f d = mxy - p0;
-      const float power = splat_power(cd, cxy, d);
-      const float G = __builtin_amdgcn_exp2f(power);
-      const float av = fminf(kMaxAlpha, op * G);
-      const bool v = cidx < last && power <= 0.0f && av >= kMinAlpha;
-      if (!wave_any(v)) continue;
-      const float alpha = v ? av : 0.f;
-      const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
-      const float Tn = T * rinv;
-      T = Tn;
-      const float dch = alpha * Tn;
-      const v2f cp = c01 * dp01 + c2d * dp2d;
-      const float sd = (cp.x + cp.y) - accd;
-      float dLda = sd * Tn + tb * rinv;
-      dLda = v ? dLda : 0.f;
-      accd += alpha * sd;
-      const float gl = G * dLda;  // as k_render_bwd_quad: the entry's constants apply after the sums
-      const v2f u = gl * d;
-      const v2f g23 = u.x * d;
-      const float gv[10] = {u.x, u.y, g23.x, g23.y, u.y * d.y, gl, dch * dp01.x, dch * dp01.y,
-                            dch * dp2d.x, dch * dp2d.y};
-      wave_sum10_store(gv, &sP[w][j][0]);
-      hits |= 1ull << j;
-    }
-#endif
-    if (lane == 0) sHitW[w] = hits;
-    __syncthreads();
-    if (w == 0 && lane < cnt) {
-      const uint64_t h0 = sHitW[0], h1 = sHitW[1], h2 = sHitW[2], h3 = sHitW[3];
-      const uint64_t bit = 1ull << lane;
-      if ((h0 | h1 | h2 | h3) & bit) {
-        float sv[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) sv[k] = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint64_t hq = q == 0 ? h0 : (q == 1 ? h1 : (q == 2 ? h2 : h3));
-          if (hq & bit)
-#pragma unroll
-            for (int k = 0; k < 10; ++k) sv[k] += sP[q][lane][k];
-        }
-        const uint32_t gid = sG[lane];
-        record_sums(sA[lane], sB[lane], sv);
-        const size_t k = slot_start[gid] + pair_local(sA[lane], sB[lane], lr_rect(lrec[gid].w), lrec[gid].tab, tx, ty);
-        partial[3 * k] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-        partial[3 * k + 1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
-        partial[3 * k + 2] = make_float4(sv[8], sv[9], 0.f, 0.f);
-        pflag[k] = 1;
-        gflag[gid] = 1;
-      }
-    }
-  }
-  zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 256);
-}
-
-// k_render_bwd_split with the quadrant waves decoupled (the default below
-// 3072 tiles; WGSR_BWD_SEG=0 keeps k_render_bwd_split): every wave fetches
-// the batch records itself (lane j entry j, one batch ahead in registers)
-// instead of wave 0 staging them for all four behind two barriers per batch,
-// and leaves its per-entry quadrant sums in a segment table of kSegBatches
-// batches; the four waves meet only once per segment, where the workgroup
-// adds each entry's (up to four) quadrant sums in quadrant order and writes
-// its record (that entry's slot data loaded at the segment's start).  A
-// quadrant wave with less work no longer waits for the slowest one at every
-// batch.  Same per-pixel arithmetic, same sums in the same order:
-// bit-identical records.
+// Below kBwdSplitBelowTiles tiles a tile gets FOUR waves, one per 8x8
+// quadrant, with the quadrant waves decoupled: every wave fetches the batch
+// records itself (lane j entry j, one batch ahead in registers), culls and
+// evaluates only its quadrant (entry pairs, split_batch_pairs), and leaves its
+// per-entry quadrant sums in a segment table of kSegBatches batches; the four
+// waves meet only once per segment, where the workgroup adds each entry's (up
+// to four) quadrant sums in quadrant order and writes its record (that
+// entry's slot data loaded at the segment's start).  A quadrant wave with
+// less work never waits for the slowest one at a batch.  Same per-pixel
+// arithmetic as the one-wave kernel; only the order of the final
+// cross-quadrant sum differs.  (The batch-synchronous four-wave form, wave 0
+// staging every batch for all four behind two barriers, measured 71.5-71.8
+// vs 69.8-70.4 us at TUM scale and was removed in round 5.)
 constexpr int kSegBatches = 3, kSegCap = kSegBatches * kBatch;
-#ifndef WGSR_BWD_SEG
-#define WGSR_BWD_SEG 1
-#endif
 __global__ __launch_bounds__(256) void k_render_bwd_seg(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, bool global_order,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ lists_exact,
@@ -1206,107 +769,6 @@ __device__ __forceinline__ void scale_partial_sums(float g[10], int W, int H) {
   g[4] *= -0.5f;
 }
 
-// Optional first half of the per-Gaussian backward (WGSR_GB_SPLIT=1): a lean,
-// high-occupancy kernel sums each Gaussian's partial records into
-// gsum[10][P] (coalesced SoA), so k_gauss_bwd starts without the record walk.
-__global__ __launch_bounds__(256) void k_sum_partials(int P, const int32_t* __restrict__ radii,
-                                                      const uint32_t* __restrict__ slot_start,
-                                                      const ListRec* __restrict__ lrec,
-                                                      const uint8_t* __restrict__ pflag,
-                                                      const float4* __restrict__ partial, int W, int H,
-                                                      float* __restrict__ gsum) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
-  const bool live = radii[i] > 0;
-  const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + lrec[i].w.w : 0u;
-  float g[10];
-  sum_partials(s0, s1, pflag, partial, g);
-  scale_partial_sums(g, W, H);
-#pragma unroll
-  for (int q = 0; q < 10; ++q) gsum[(size_t)q * P + i] = g[q];
-}
-
-// First half of the sparse per-Gaussian backward: the record sums of the
-// Gaussians the render backward marked (gflag), 16 lanes per Gaussian, four
-// Gaussians per round, into gsum[10][P] (live rows only).  Lane l of a group
-// reads slots 4l .. 4l + 3 of each 64-slot pass, flags and records in ONE
-// round trip, and a DPP row reduction sums the group.  A per-lane walk
-// (sum_partials) pays about one round trip per 4 records and the wave waits
-// for its largest splat (foreground Gaussians cover ~100 tiles); done here,
-// in a lean kernel with many waves in flight, k_gauss_bwd's waves start from
-// independent loads (sums, parameters, SH row).
-__global__ __launch_bounds__(64) void k_sum_active(int P, const uint8_t* __restrict__ gflag,
-                                                   const uint32_t* __restrict__ slot_start,
-                                                   const ListRec* __restrict__ lrec,
-                                                   const uint8_t* __restrict__ pflag,
-                                                   const float4* __restrict__ partial, int W, int H,
-                                                   float* __restrict__ gsum) {
-  __shared__ float s_g[64][11];
-  const int lane = threadIdx.x, i0 = blockIdx.x * 64, i = i0 + lane;
-  const int q = lane >> 4, l = lane & 15;
-  // flag, slot range and list length in one round trip (coalesced)
-  const bool in = i < P;
-  const bool live = in && gflag[i] != 0;
-  const uint32_t my_s0 = in ? slot_start[i] : 0u, my_n = in ? lrec[i].w.w : 0u;
-  uint64_t act = wave_ballot(live);
-  if (!act) return;  // wave-uniform
-  while (act) {
-    int jq[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      jq[k] = act ? __builtin_ctzll(act) : -1;
-      act &= act - 1;
-    }
-    const int j = q == 0 ? jq[0] : q == 1 ? jq[1] : q == 2 ? jq[2] : jq[3];
-    // every lane takes part in both shuffles (a ds_bpermute from a lane
-    // outside EXEC reads 0): the group's slot range comes from lane j
-    const int src = j < 0 ? 0 : j;
-    const uint32_t s0 = (uint32_t)__shfl((int)my_s0, src, 64);
-    const uint32_t nj = (uint32_t)__shfl((int)my_n, src, 64);
-    const uint32_t n = j < 0 ? 0u : nj;
-    float acc[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-    for (uint32_t b = 0; b < n; b += 64) {
-      // flags and records of the lane's 4 slots in one round trip: records of
-      // unflagged slots are stale bytes, dropped by a select (never a multiply)
-      bool f[4];
-      float4 r[4][3];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t k = b + 4 * l + u;
-        const bool ok = k < n;
-        const size_t sl = (size_t)s0 + (ok ? k : 0u);
-        f[u] = ok && pflag[sl] != 0;
-#pragma unroll
-        for (int h = 0; h < 3; ++h) r[u][h] = ok ? partial[3 * sl + h] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 a0 = r[u][0], a1 = r[u][1], a2 = r[u][2];
-        acc[0] += f[u] ? a0.x : 0.f; acc[1] += f[u] ? a0.y : 0.f;
-        acc[2] += f[u] ? a0.z : 0.f; acc[3] += f[u] ? a0.w : 0.f;
-        acc[4] += f[u] ? a1.x : 0.f; acc[5] += f[u] ? a1.y : 0.f;
-        acc[6] += f[u] ? a1.z : 0.f; acc[7] += f[u] ? a1.w : 0.f;
-        acc[8] += f[u] ? a2.x : 0.f; acc[9] += f[u] ? a2.y : 0.f;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) acc[k] = dpp_row_sum16(acc[k]);
-    if (l == 15 && j >= 0)
-#pragma unroll
-      for (int k = 0; k < 10; ++k) s_g[j][k] = acc[k];
-  }
-  __syncthreads();
-  if (!live) return;
-  float g[10];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) g[k] = s_g[lane][k];
-  scale_partial_sums(g, W, H);
-#pragma unroll
-  for (int k = 0; k < 10; ++k) gsum[(size_t)k * P + i] = g[k];
-}
-
 // Camera-side backward of one Gaussian in one view (upstream
 // computeCov2DCUDA + the projection / depth terms of preprocessCUDA backward,
 // plus the w-pose gradient): from its screen-space partial sums g[10] to
@@ -1448,44 +910,23 @@ __device__ __forceinline__ void cov_to_scale_rot(float4 q, f3 sv, float scale_mo
           4 * z * (G[1][1] + G[0][0]));
 }
 
-// Per-Gaussian backward of Gaussian i.  `shrow` (LDS, or null without SH)
-// holds its 3M SH coefficients on entry and its dL/dsh row on exit.
-// a listed Gaussian's parameters, loaded ahead of its record sums
-// (k_gauss_bwd_compact with WGSR_GBC_PREFETCH)
-struct GbPre {
-  f3 mean, sv;
-  float4 q;
-};
+// Per-Gaussian backward of a Gaussian that received gradient: from its
+// screen-space sums g[10] through the camera-side backward to every output
+// row (the render backward zero-filled the rows of the others).  dm_sh: the
+// SH term of dL/dmean (the caller ran sh_backward first).
 __device__ __forceinline__ void gauss_bwd_one(
-    int i, int D, int M, bool live, const uint32_t* __restrict__ clamped, const float g[10],
-    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
-    const float* __restrict__ cov_pre, float* shrow, f3 dm_sh, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
-    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
-    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau, bool have_pre = false,
-    GbPre pre = GbPre{}) {
-  // dm_sh: the SH term of dL/dmean when the caller ran sh_backward itself
-  // (shrow null); zero otherwise.  pre: the parameters, already loaded
-  // (no cov3D_precomp then).
+    int i, const float g[10], const float* __restrict__ means, const float* __restrict__ scales,
+    const float* __restrict__ rots, const float* __restrict__ cov_pre, f3 dm_sh, float scale_mod,
+    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw, int W, int H,
+    float tanx, float tany, float* __restrict__ o_m2d, float* __restrict__ o_col, float* __restrict__ o_opac,
+    float* __restrict__ o_m3d, float* __restrict__ o_cov, float* __restrict__ o_sc, float* __restrict__ o_rot,
+    float* __restrict__ o_tau) {
   const size_t i3 = 3 * (size_t)i, i6 = 6 * (size_t)i;
-  if (!live) {  // culled, or (sparse) no partial record: every output is zero
-    for (int k = 0; k < 3; ++k) { o_m2d[i3 + k] = 0.f; o_col[i3 + k] = 0.f; o_m3d[i3 + k] = 0.f; o_sc[i3 + k] = 0.f; }
-    for (int k = 0; k < 6; ++k) { o_cov[i6 + k] = 0.f; o_tau[i6 + k] = 0.f; }
-    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (shrow) for (int k = 0; k < 3 * M; ++k) shrow[k] = 0.f;
-    o_opac[i] = 0.f;
-    return;
-  }
-  // parameters first: their loads overlap the partial-record walk below
-  const f3 mean = have_pre ? pre.mean : mk3(means[i3], means[i3 + 1], means[i3 + 2]);
+  const f3 mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
   float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
   f3 sv = mk3(0.f, 0.f, 0.f);
   float cv[6];
-  if (have_pre) {
-    sv = pre.sv;
-    q = pre.q;
-  } else if (cov_pre) {
+  if (cov_pre) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) cv[k] = cov_pre[i6 + k];
   } else {
@@ -1503,183 +944,32 @@ __device__ __forceinline__ void gauss_bwd_one(
   cam_backward(c, praw[0], praw[5], praw[11], mean, cv, g, cb);
 #pragma unroll
   for (int k = 0; k < 6; ++k) o_cov[i6 + k] = cb.ocov[k];
-  f3 dm = add3(cb.dm, dm_sh);
+  const f3 dm = add3(cb.dm, dm_sh);
   const f3 tau_rho = cb.rho, tau_theta = cb.theta;
-  if (shrow) {
-    const f3 dmsh = sh_backward(D, M, shrow, mean, mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i],
-                                mk3(g[6], g[7], g[8]), shrow);
-    dm = add3(dm, dmsh);
-  }
-  if (!cov_pre) {
-    cov_to_scale_rot(q, sv, scale_mod, cb.ocov, &o_sc[i3], &o_rot[4 * (size_t)i]);
-  } else {
-    for (int k = 0; k < 3; ++k) o_sc[i3 + k] = 0.f;
-    reinterpret_cast<float4*>(o_rot)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  if (!cov_pre) cov_to_scale_rot(q, sv, scale_mod, cb.ocov, &o_sc[i3], &o_rot[4 * (size_t)i]);
   o_m3d[i3] = dm.x; o_m3d[i3 + 1] = dm.y; o_m3d[i3 + 2] = dm.z;
   o_tau[i6 + 0] = tau_rho.x; o_tau[i6 + 1] = tau_rho.y; o_tau[i6 + 2] = tau_rho.z;
   o_tau[i6 + 3] = tau_theta.x; o_tau[i6 + 4] = tau_theta.y; o_tau[i6 + 5] = tau_theta.z;
 }
 
-// One wave of 64 Gaussians per workgroup.  The wave's SH slab (64 x 3M
-// floats, contiguous in HBM) moves through LDS in both directions, so SH
-// coefficients are read and dL/dsh written as coalesced 256-byte rows instead
-// of 3M-float strided per-thread runs; rows are padded to 3M + 1 floats so
-// each lane's row walk is bank-conflict free.
-//
-// kHalf: the slab moves through LDS 32 rows at a time (two passes, lanes
-// 0-31 then 32-63 run sh_backward), before the camera-side backward.  The
-// 64 x (3M+1) slab (12.5 KB at SH3) caps residency at 12 waves per CU; the
-// 32-row slab lets the VGPR limit (4 waves per SIMD) decide instead.
+// One wave of 64 Gaussians per workgroup (the view-sharded owner kernel below).
 constexpr int kGbWave = 64;
-//
-// kSparse: a Gaussian is live only if the render backward marked it in gflag
-// (wrote a partial record for it: bench scene 7.5 %); the others' outputs are
-// exactly zero, so their lanes skip every load (slot flags, parameters, SH
-// row) and only store zeros.  The stores stay the dense kernel's: every row
-// of the wave's span written by its own lane, the dL/dsh slab through LDS as
-// full coalesced rows -- scattered partial-line writes (a kernel that visits
-// only the marked rows) measured 20-40 % slower than these full lines.
-template <bool kHalf, bool kSparse>
-__global__ __launch_bounds__(kGbWave) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_gauss_bwd(
-    int P, int D, int M, const uint8_t* __restrict__ gflag, const int32_t* __restrict__ radii,
-    const uint32_t* __restrict__ slot_start,
-    const ListRec* __restrict__ lrec, const uint32_t* __restrict__ clamped, const float4* __restrict__ partial,
-    const uint8_t* __restrict__ pflag, const float* __restrict__ gsum,
-    const float* __restrict__ means, const float* __restrict__ scales, const float* __restrict__ rots,
-    const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
-    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
-    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau,
-    bool zeroed) {
-  extern __shared__ float s_sh[];  // kGbWave x (3M + 1) floats (dynamic)
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kGbWave, i = i0 + lane;
-  const int ng = min(kGbWave, P - i0);
-  const int S = 3 * M, SP = S + 1;
-  const bool sh = o_sh != nullptr;
-  // partial-record walk first: its loads are in flight before the SH staging
-  float g[10];
-  if (gsum && !kSparse) {  // summed by k_sum_partials
-#pragma unroll
-    for (int q = 0; q < 10; ++q) g[q] = i < P ? gsum[(size_t)q * P + i] : 0.f;
-  }
-  const bool live = i < P && (kSparse ? gflag[i] != 0 : radii[i] > 0);
-  if (kSparse) {  // summed by k_sum_active (live rows only)
-#pragma unroll
-    for (int q = 0; q < 10; ++q) g[q] = live ? gsum[(size_t)q * P + i] : 0.f;
-  } else if (!gsum) {
-    const uint32_t s0 = live ? slot_start[i] : 0u, s1 = live ? s0 + lrec[i].w.w : 0u;
-    sum_partials(s0, s1, pflag, partial, g);
-    scale_partial_sums(g, W, H);
-  }
-  if (kSparse && zeroed) {
-    // the render backward zero-filled every output: only the live rows are
-    // written, each by its own lane (dL/dsh straight to its 3M-float row)
-    if (!wave_any(live)) return;
-    if (!live) return;
-    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
-                  viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
-                  o_tau);
-    if (sh) {
-      const size_t i3 = 3 * (size_t)i;
-      const f3 dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[i3], means[i3 + 1], means[i3 + 2]),
-                                   mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
-                                   o_sh + (size_t)i * S);
-      o_m3d[i3] += dm_sh.x;  // (camera term) + (SH term), as in the other paths
-      o_m3d[i3 + 1] += dm_sh.y;
-      o_m3d[i3 + 2] += dm_sh.z;
-    }
-    return;
-  }
-  if (kHalf) {
-    // camera-side backward first (its registers are dead before the SH
-    // phase); the SH term of dL/dmean is added to the stored value after.
-    if (i < P)
-      gauss_bwd_one(i, D, M, live, clamped, g, means, scales, rots, cov_pre, nullptr, mk3(0.f, 0.f, 0.f), scale_mod,
-                    viewm, projm, praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot,
-                    o_tau);
-    if (sh) {
-      const f3 campos = mk3(campos_p[0], campos_p[1], campos_p[2]);
-      for (int h = 0; h < 2; ++h) {
-        const int h0 = i0 + 32 * h, nh = min(32, P - h0);
-        if (nh <= 0) break;  // uniform: P is the same for every lane
-        // sparse: the live rows are read by their own lanes below (few per
-        // wave), not staged as a whole slab
-        if (!kSparse) slab_to_lds(shs + (size_t)h0 * S, nh, S, s_sh, lane);
-        __syncthreads();
-        if ((lane >> 5) == h && i < P) {
-          float* row = &s_sh[(lane & 31) * SP];
-          if (live) {
-            const size_t i3 = 3 * (size_t)i;
-            const f3 dm_sh = sh_backward(D, M, kSparse ? shs + (size_t)i * S : row,
-                                         mk3(means[i3], means[i3 + 1], means[i3 + 2]), campos, clamped[i],
-                                         mk3(g[6], g[7], g[8]), row);
-            // same sum as the full-slab path: (camera term) + (SH term)
-            o_m3d[i3] += dm_sh.x;
-            o_m3d[i3 + 1] += dm_sh.y;
-            o_m3d[i3 + 2] += dm_sh.z;
-          } else {
-            for (int k = 0; k < S; ++k) row[k] = 0.f;
-          }
-        }
-        __syncthreads();
-        lds_to_slab(s_sh, nh, S, o_sh + (size_t)h0 * S, lane);
-        __syncthreads();
-      }
-    }
-    return;
-  }
-  if (sh) {
-    slab_to_lds(shs + (size_t)i0 * S, ng, S, s_sh, lane);
-    __syncthreads();
-  }
-  static_assert(kHalf || !kSparse, "the sparse variant reads SH rows per lane (32-row output slab)");
-  if (i < P)
-    gauss_bwd_one(i, D, M, live, clamped, g, means, scales, rots, cov_pre,
-                  sh ? &s_sh[lane * SP] : nullptr, mk3(0.f, 0.f, 0.f), scale_mod, viewm, projm, praw, campos_p, W, H,
-                  tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
-  if (sh) {
-    __syncthreads();
-    lds_to_slab(s_sh, ng, S, o_sh + (size_t)i0 * S, lane);
-  }
-}
 
-
-
-// Sparse per-Gaussian backward in one launch, on outputs the render backward
-// zero-filled: a workgroup of 256 threads owns 512 Gaussians and compacts the
-// ones that received gradient (gflag; ~8 % on the bench scene) into an LDS
-// list; the listed Gaussians' record slots are flattened into one list whose
-// flags and records every thread loads (512 slots at a time, coalesced, into
-// LDS), each listed Gaussian's thread sums its own slots in order, and then
-// runs the camera-side and SH backward, writing only its rows.  The
-// per-Gaussian VALU work runs on ~1/12 of the waves a one-lane-per-Gaussian
-// kernel would need.  (WGSR_GBC_FLAT=0: 16-lane groups per listed Gaussian
-// with a dependent slot-range load per group pass: 75 vs 65 us at 1M/1080p.)
+// Per-Gaussian backward in one launch, on outputs the render backward
+// zero-filled: a workgroup of 256 threads owns 256 kR Gaussians and compacts
+// the ones that received gradient (gflag; ~8 % on the bench scene) into an
+// LDS list; the listed Gaussians' record slots are flattened into one list
+// whose flags and records every thread loads (kRecChunk slots at a time,
+// coalesced, into LDS), each listed Gaussian's thread sums its own slots in
+// order (deterministic), and then runs the SH and camera-side backward,
+// writing only its rows.  The per-Gaussian VALU work runs on ~1/12 of the
+// waves a one-lane-per-Gaussian kernel would need.  (Measured alternatives,
+// removed in round 5: one lane per Gaussian over every row, 0.18 ms at
+// 1M / 1080p; the two-kernel sparse path k_sum_active + k_gauss_bwd, 89 us;
+// 16-lane groups per listed Gaussian with a dependent slot-range load per
+// group pass, 75 us; parameters loaded ahead of the record sums, 68-70 us.)
 constexpr int kGbcThreads = 256;
-// Gaussians per workgroup = kGbcThreads x kR, kR chosen per launch (below;
-// the two-kernel sparse path k_sum_active + k_gauss_bwd: 89 us at 1M)
-// WGSR_GBC_PREFETCH=1 (A/B): the listed Gaussians' parameters load before the
-// record sums instead of after them
-#ifndef WGSR_GBC_PREFETCH
-#define WGSR_GBC_PREFETCH 0
-#endif
-// WGSR_GBC_FLAT=0: one 16-lane group per listed Gaussian sums its records
-// (a dependent slot-range load per group pass)
-#ifndef WGSR_GBC_FLAT
-#define WGSR_GBC_FLAT 1
-#endif
-#if WGSR_GBC_FLAT
-#ifndef WGSR_GBC_PIPE  // the next record chunk's loads in flight during the current chunk's sums
-#define WGSR_GBC_PIPE 1
-#endif
-#ifndef WGSR_GBC_RECCHUNK
-#define WGSR_GBC_RECCHUNK 512
-#endif
-constexpr int kRecChunk = WGSR_GBC_RECCHUNK;  // flattened record slots staged in LDS at a time
-#endif
+constexpr int kRecChunk = 512;  // flattened record slots staged in LDS at a time
 template <int kR>
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
@@ -1692,13 +982,9 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
   constexpr int NW = kGbcThreads / 64;
   __shared__ uint32_t s_list[(kGbcThreads * kR)];
-#if WGSR_GBC_FLAT
   __shared__ uint32_t s_s0[(kGbcThreads * kR)], s_n[(kGbcThreads * kR)], s_off[(kGbcThreads * kR) + 1];
   __shared__ uint2 s_tmp4[4];
   __shared__ float s_rec[kRecChunk][10];
-#else
-  __shared__ float s_g[(kGbcThreads * kR)][11];
-#endif
   __shared__ uint32_t s_wc[kR][NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int i0 = blockIdx.x * (kGbcThreads * kR);
@@ -1731,28 +1017,6 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   if (nlive == 0) return;  // block-uniform
   __syncthreads();
-#if WGSR_GBC_PREFETCH
-  // every listed Gaussian's parameters (and a touch of its SH row's lines)
-  // loaded now, while the record sums below wait on their own round trips
-  GbPre pre[kR];
-  uint32_t pcl[kR];
-  float touch = 0.f;
-#pragma unroll
-  for (int r = 0; r < kR; ++r) {
-    const uint32_t c = r * kGbcThreads + t;
-    const int i = c < nlive ? (int)s_list[c] : 0;
-    const size_t i3 = 3 * (size_t)i;
-    pre[r].mean = mk3(means[i3], means[i3 + 1], means[i3 + 2]);
-    pre[r].sv = cov_pre ? mk3(0.f, 0.f, 0.f) : mk3(scales[i3], scales[i3 + 1], scales[i3 + 2]);
-    pre[r].q = cov_pre ? make_float4(1.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4*>(rots)[i];
-    pcl[r] = clamped[i];
-    if (o_sh) {
-      const float* row = shs + (size_t)i * (3 * M);
-      for (int k = 0; k < 3 * M; k += 32) touch += row[k];
-    }
-  }
-#endif
-#if WGSR_GBC_FLAT
   // record sums over the listed Gaussians' slots flattened into one list:
   // their slot ranges in one round trip, then kRecChunk slots at a time every
   // thread loads one slot's flag and record (coalesced within a range; the
@@ -1790,7 +1054,6 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   for (int r = 0; r < kR; ++r)
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[r][k] = 0.f;
-#if WGSR_GBC_PIPE
   // software pipeline: this thread's slots of the NEXT chunk are loaded into
   // registers while the current chunk is summed out of LDS (the loads' round
   // trip overlaps the sums and barriers instead of following them); same
@@ -1819,9 +1082,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     }
   };
   if (total > 0) fetch(0);
-#endif
   for (uint32_t base = 0; base < total; base += kRecChunk) {
-#if WGSR_GBC_PIPE
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t q = base + u * kGbcThreads + t;
@@ -1835,26 +1096,6 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
       }
     }
     if (base + kRecChunk < total) fetch(base + kRecChunk);
-#else
-#pragma unroll
-    for (int u = 0; u < kRecChunk / kGbcThreads; ++u) {
-      const uint32_t q = base + u * kGbcThreads + t;
-      if (q < total) {
-        uint32_t lo = 0, hi = nlive;  // s_off[lo] <= q < s_off[hi]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_off[mid] <= q) lo = mid; else hi = mid;
-        }
-        const size_t sl = (size_t)s_s0[lo] + (q - s_off[lo]);
-        const bool f = pflag[sl] != 0;
-        const float4 a0 = partial[3 * sl], a1 = partial[3 * sl + 1], a2 = partial[3 * sl + 2];
-        float* d = s_rec[q - base];
-        d[0] = f ? a0.x : 0.f; d[1] = f ? a0.y : 0.f; d[2] = f ? a0.z : 0.f; d[3] = f ? a0.w : 0.f;
-        d[4] = f ? a1.x : 0.f; d[5] = f ? a1.y : 0.f; d[6] = f ? a1.z : 0.f; d[7] = f ? a1.w : 0.f;
-        d[8] = f ? a2.x : 0.f; d[9] = f ? a2.y : 0.f;
-      }
-    }
-#endif
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
@@ -1876,78 +1117,20 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) g[k] = acc[r][k];
-#else
-  {  // record sums: one 16-lane group per listed Gaussian
-    const int grp = t >> 4, l = t & 15;
-    for (uint32_t c = grp; c < ((nlive + 15) & ~15u); c += kGbcThreads / 16) {
-      const bool have = c < nlive;  // (uniform in the group: the row reduction stays whole)
-      const uint32_t gi = have ? s_list[c] : 0u;
-      const uint32_t s0 = have ? slot_start[gi] : 0u, n = have ? lrec[gi].w.w : 0u;
-      float acc[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-      for (uint32_t b = 0; b < n; b += 64) {
-        bool f[4];
-        float4 r[4][3];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t k = b + 4 * l + u;
-          const bool ok = k < n;
-          const size_t sl = (size_t)s0 + (ok ? k : 0u);
-          f[u] = ok && pflag[sl] != 0;
-#pragma unroll
-          for (int h = 0; h < 3; ++h) r[u][h] = ok ? partial[3 * sl + h] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 a0 = r[u][0], a1 = r[u][1], a2 = r[u][2];
-          acc[0] += f[u] ? a0.x : 0.f; acc[1] += f[u] ? a0.y : 0.f;
-          acc[2] += f[u] ? a0.z : 0.f; acc[3] += f[u] ? a0.w : 0.f;
-          acc[4] += f[u] ? a1.x : 0.f; acc[5] += f[u] ? a1.y : 0.f;
-          acc[6] += f[u] ? a1.z : 0.f; acc[7] += f[u] ? a1.w : 0.f;
-          acc[8] += f[u] ? a2.x : 0.f; acc[9] += f[u] ? a2.y : 0.f;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 10; ++k) acc[k] = dpp_row_sum16(acc[k]);
-      if (l == 15 && have)
-#pragma unroll
-        for (int k = 0; k < 10; ++k) s_g[c][k] = acc[k];
-    }
-  }
-  __syncthreads();
-  for (uint32_t c = t; c < nlive; c += kGbcThreads) {
-    const int i = (int)s_list[c];
-    float g[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) g[k] = s_g[c][k];
-#endif
     scale_partial_sums(g, W, H);
     // SH backward first: its dL/dmean term goes into gauss_bwd_one's single
     // store of the row (no read-modify-write of o_m3d behind its stores)
     f3 dm_sh = mk3(0.f, 0.f, 0.f);
-#if WGSR_GBC_PREFETCH && WGSR_GBC_FLAT
-    const bool hp = cov_pre == nullptr;
-    const GbPre pp = pre[r];
-    const f3 pmean = pre[r].mean;
-    const uint32_t pcb = pcl[r];
-#else
-    const bool hp = false;
-    const GbPre pp{};
-    const f3 pmean = mk3(means[3 * (size_t)i], means[3 * (size_t)i + 1], means[3 * (size_t)i + 2]);
-    const uint32_t pcb = clamped[i];
-#endif
     if (o_sh) {
       const size_t S = 3 * (size_t)M;
-      dm_sh = sh_backward(D, M, shs + (size_t)i * S, pmean, mk3(campos_p[0], campos_p[1], campos_p[2]), pcb,
-                          mk3(g[6], g[7], g[8]), o_sh + (size_t)i * S);
+      dm_sh = sh_backward(D, M, shs + (size_t)i * S, mk3(means[3 * (size_t)i], means[3 * (size_t)i + 1],
+                                                        means[3 * (size_t)i + 2]),
+                          mk3(campos_p[0], campos_p[1], campos_p[2]), clamped[i], mk3(g[6], g[7], g[8]),
+                          o_sh + (size_t)i * S);
     }
-    gauss_bwd_one(i, D, M, true, clamped, g, means, scales, rots, cov_pre, nullptr, dm_sh, scale_mod, viewm, projm,
-                  praw, campos_p, W, H, tanx, tany, o_m2d, o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau, hp, pp);
+    gauss_bwd_one(i, g, means, scales, rots, cov_pre, dm_sh, scale_mod, viewm, projm, praw, W, H, tanx, tany, o_m2d,
+                  o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   }
-#if WGSR_GBC_PREFETCH
-  asm volatile("" ::"v"(touch));  // (the touch loads' only use: waited for here, at the end)
-#endif
 }
 
 // ---- view-sharded backward (wgsr/dp.py) ---------------------
@@ -2115,16 +1298,14 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   const char* env = getenv("WGSR_BWD_SPLIT_BELOW");  // read per launch: tests switch kernels
   const int split_below = env ? atoi(env) : kBwdSplitBelowTiles;
   if (nt < split_below) {
-    const char* segenv = getenv("WGSR_BWD_SEG");  // (read per launch: tests compare the two)
-    auto kern = (segenv ? atoi(segenv) != 0 : WGSR_BWD_SEG != 0) ? k_render_bwd_seg : k_render_bwd_split;
-    hipLaunchKernelGGL(kern, dim3(nt), dim3(256), 0, s, ranges, order, bwd_order_global(), meta,
+    hipLaunchKernelGGL(k_render_bwd_seg, dim3(nt), dim3(256), 0, s, ranges, order, false, meta,
                        lists_exact, lists_bins,
                        at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
                        at<uint32_t>(geom, L.slot_start), a.W, a.H, gx, nt, a.bg, final_T, n_contrib, dL_dcolor,
                        dL_ddepth, partial, pflag, at<uint8_t>(const_cast<void*>(geom), L.gflag), zero);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, bwd_order_global(), meta,
+  hipLaunchKernelGGL(k_render_bwd_quad, dim3(nt), dim3(64), 0, s, ranges, order, false, meta,
                      lists_exact, lists_bins,
                      at<float4>(geom, L.splat),
                      at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.slot_start), a.W,
@@ -2133,86 +1314,35 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
   return hipGetLastError();
 }
 
-GbMode gauss_bwd_mode() {
-  const char* e = getenv("WGSR_GB");  // read per call: tests switch modes
-  return (e && strcmp(e, "dense") == 0) ? kGbDense : kGbSparse;
-}
-
-hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
-                            const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
-                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                            float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau, GbMode mode,
-                            bool zeroed, hipStream_t s) {
+hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const void* geom, const float4* partial, const uint8_t* pflag,
+                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau,
+                            hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
-  static const bool split = [] {
-    const char* e = getenv("WGSR_GB_SPLIT");
-    return e && atoi(e) != 0;
+  // (no pair listed: gflag is all zero and nothing is written)
+  // the fewest Gaussians per workgroup (256, 512 or 1024) whose grid is ONE
+  // resident round at four workgroups per CU (LDS-limited): the chain of
+  // dependent loads per workgroup is the kernel's time, a second round
+  // doubles it (measured at 1M / 1080p: 1024 per workgroup 57-58 us, 512
+  // 63-64 us (two rounds), 768 68 us)
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
+    return n;
   }();
-  float* const gsum_buf = gsum;  // scratch [10][P]
-  if (split && mode == kGbDense) {
-    hipLaunchKernelGGL(k_sum_partials, dim3((a.P + 255) / 256), dim3(256), 0, s, a.P, radii,
-                       at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), pflag, partial, a.W, a.H, gsum);
-  } else {
-    gsum = nullptr;
-  }
-  static const bool full_slab = [] {  // WGSR_GB_FULLSLAB=1: the 64-row slab variant (A/B runs)
-    const char* e = getenv("WGSR_GB_FULLSLAB");
-    return e && atoi(e) != 0;
-  }();
-  const bool sparse = mode == kGbSparse;
-  const char* ce = getenv("WGSR_GB_COMPACT");  // read per call: tests compare the sparse kernels
-  if (sparse && zeroed && !(ce && strcmp(ce, "0") == 0)) {
-    // (no pair listed: gflag is all zero and nothing is written)
-    // (WGSR_GBC_R = 1..4 forces the rounds per workgroup: A/B)
-    static const int force_r = [] {
-      const char* e = getenv("WGSR_GBC_R");
-      const int v = e ? atoi(e) : 0;
-      return v >= 1 && v <= 4 ? v : 0;
-    }();
-    // the fewest Gaussians per workgroup (256, 512 or 1024) whose grid is ONE
-    // resident round at four workgroups per CU (LDS-limited): the chain of
-    // dependent loads per workgroup is the kernel's time, a second round
-    // doubles it (measured at 1M / 1080p: 1024 per workgroup 57-58 us, 512
-    // 63-64 us (two rounds), 768 68 us)
-    static const int ncu = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                  hipSuccess || n <= 0)
-        n = 256;
-      return n;
-    }();
-    int nr = 1;
-    while (nr < 4 && (a.P + kGbcThreads * nr - 1) / (kGbcThreads * nr) > 4 * ncu) nr *= 2;
-    if (force_r) nr = force_r;
-    const int span = kGbcThreads * nr;
-    hipLaunchKernelGGL(nr == 1 ? k_gauss_bwd_compact<1> : nr == 2 ? k_gauss_bwd_compact<2>
-                       : nr == 3 ? k_gauss_bwd_compact<3> : k_gauss_bwd_compact<4>,
-                       dim3((a.P + span - 1) / span), dim3(kGbcThreads), 0, s, a.P,
-                       a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
-                       at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
-                       a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,
-                       a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, dL_dmeans2D, dL_dcolors,
-                       dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr, dL_dscales, dL_drot, dL_dtau);
-    return hipGetLastError();
-  }
-  if (sparse) {
-    // (no pair listed: gflag is all zero and k_gauss_bwd never reads gsum)
-    gsum = gsum_buf;
-    if (partial)
-      hipLaunchKernelGGL(k_sum_active, dim3((a.P + 63) / 64), dim3(64), 0, s, a.P, at<uint8_t>(geom, L.gflag),
-                         at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), pflag, partial, a.W, a.H,
-                         gsum);
-  }
-  const size_t lds = a.shs ? sizeof(float) * (full_slab && !sparse ? kGbWave : 32) * (3 * (size_t)a.M + 1) : 0;
-  auto k = sparse ? k_gauss_bwd<true, true> : full_slab ? k_gauss_bwd<false, false> : k_gauss_bwd<true, false>;
-  hipLaunchKernelGGL(k, dim3((a.P + kGbWave - 1) / kGbWave), dim3(kGbWave), lds, s, a.P, a.D, a.M,
-                     at<uint8_t>(geom, L.gflag), radii,
-                     at<uint32_t>(geom, L.slot_start), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
-                     partial, pflag, gsum, a.means3D, a.scales, a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier,
-                     a.viewmatrix, a.projmatrix, a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy,
-                     dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr,
-                     dL_dscales, dL_drot, dL_dtau, sparse && zeroed);
+  int nr = 1;
+  while (nr < 4 && (a.P + kGbcThreads * nr - 1) / (kGbcThreads * nr) > 4 * ncu) nr *= 2;
+  const int span = kGbcThreads * nr;
+  hipLaunchKernelGGL(nr == 1 ? k_gauss_bwd_compact<1> : nr == 2 ? k_gauss_bwd_compact<2> : k_gauss_bwd_compact<4>,
+                     dim3((a.P + span - 1) / span), dim3(kGbcThreads), 0, s, a.P,
+                     a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
+                     at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
+                     a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,
+                     a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, dL_dmeans2D, dL_dcolors,
+                     dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr, dL_dscales, dL_drot, dL_dtau);
   return hipGetLastError();
 }
 

@@ -84,17 +84,11 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// One Gaussian of k_preprocess; returns (rect area, exact list length, bins
+// One Gaussian of k_preprocess2; returns (rect area, exact list length, bins
 // touched), 0 if culled.  The per-Gaussian words every Gaussian gets (radius,
 // list length, tb, depth key) are returned in `w` (radius, cnt, tb, key) and
 // stored once by the caller; the splat record, rect, row table and clamp bits
 // only for visible Gaussians.
-// records of a visible Gaussian kept in registers instead of stored
-// (k_preprocess2's deferred-store form: every store after the colour)
-struct PreDefer {
-  float4 A, B;
-  uint4 tab;
-};
 __device__ __forceinline__ uint3 preprocess_one(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
@@ -104,7 +98,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
     int i, const Cam& c, const f3 p, const f3 sc, const float4 q, const float o, const f3 sh_rgb,
-    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true, PreDefer* dfr = nullptr) {
+    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
   rcw = make_uint2(0u, 0u);
@@ -147,7 +141,7 @@ __device__ __forceinline__ uint3 preprocess_one(
   const int y1 = min(gy, max(0, (int)((py + r + kTile - 1) / kTile)));
   if ((x1 - x0) * (y1 - y0) == 0) return make_uint3(0u, 0u, 0u);
 
-  f3 rgb = sh_rgb;  // SH colour (k_preprocess evaluates it for every lane)
+  f3 rgb = sh_rgb;  // (colours given: read below; SH colours: k_preprocess2 evaluates them after the geometry)
   uint32_t cbits = sh_cbits;
   if (colors) {
     rgb = mk3(colors[3 * i], colors[3 * i + 1], colors[3 * i + 2]);
@@ -162,13 +156,8 @@ __device__ __forceinline__ uint3 preprocess_one(
   // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
   const float4 A = make_float4(px, py, kConicSq * (cc * det_inv), kConicSq * (a * det_inv));
   const float4 B = make_float4(kConicXY * (-b * det_inv), o, lim, 0.f);
-  if (dfr) {
-    dfr->A = A;
-    dfr->B = B;
-  } else {
-    splat[3 * (size_t)i + 0] = A;
-    splat[3 * (size_t)i + 1] = B;
-  }
+  splat[3 * (size_t)i + 0] = A;
+  splat[3 * (size_t)i + 1] = B;
   if (write_color) splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rcw = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
   // exact tile list length (row_span); upstream's num_rendered counts the rect
@@ -188,10 +177,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     }
     cnt += len;
   }
-  if (dfr)
-    dfr->tab = tab;
-  else
-    lrec[i].tab = tab;
+  lrec[i].tab = tab;
   if (write_color) clamped[i] = cbits;
   // bins of the rect (exact lists are per tile; a bin list holds every
   // Gaussian whose rect meets the bin, and the render waves cull the rest)
@@ -204,13 +190,6 @@ __device__ __forceinline__ uint3 preprocess_one(
   return make_uint3((uint32_t)((x1 - x0) * (y1 - y0)), cnt, nb);
 }
 
-// One wave of 64 Gaussians per workgroup.  With SH colours the wave's SH slab
-// (64 x 3M floats, contiguous in HBM) is staged through LDS with coalesced
-// loads (slab_to_lds), kPreRows rows at a time (lanes of those rows evaluate
-// their colour from LDS between two barriers), instead of each lane reading
-// its own 3M-float run.  (A smaller table lets more waves share a CU but
-// measured no faster at 1M/1080p: 8 rows 97 us, 16 rows 95, 32 rows 95, 64
-// rows 90.)
 // A preprocess wave's pair counts (upstream's num_rendered, exact pairs, bin
 // pairs) and visible depth-key range into the counter block: one atomic per
 // wave each, spread over kRectPairLanes words.  The wave sums / maxima are
@@ -251,106 +230,29 @@ __device__ __forceinline__ void wave_pair_counts(const uint3 ac, uint32_t khi, u
 }
 
 constexpr int kPreWave = 64;
-#ifndef WGSR_PRE_ROWS
-#define WGSR_PRE_ROWS 64
-#endif
-constexpr int kPreRows = WGSR_PRE_ROWS;
-__global__ __launch_bounds__(kPreWave) void k_preprocess(
-    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
-    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
-    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
-    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
-    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
-    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
-    uint32_t* __restrict__ meta) {
-
-  extern __shared__ float s_sh[];  // kPreRows x (3M + 1) floats when SH colours are used
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
-  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
-  // every input (camera, per-Gaussian parameters) is loaded up front, so its
-  // latency overlaps the SH slab's instead of following the colour evaluation
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
-  f3 sc = mk3(1.f, 1.f, 1.f);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  float o = 0.f;
-  if (i < P) {
-    if (!cov_pre) {
-      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-      q = reinterpret_cast<const float4*>(rots)[i];
-    }
-    o = opac[i];
-  }
-  f3 rgb = mk3(0.f, 0.f, 0.f);
-  uint32_t cbits = 0;
-  if (shs != nullptr && colors == nullptr) {
-#pragma clang fp contract(off)
-    f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
-    const float len = sqrtf(dot3(dir, dir));
-    dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-    const int S = 3 * M, ng = min(kPreWave, P - i0);
-    for (int r0 = 0; r0 < ng; r0 += kPreRows) {  // uniform
-      slab_to_lds(shs + (size_t)(i0 + r0) * S, min(kPreRows, ng - r0), S, s_sh, lane);
-      __syncthreads();
-      if (lane >= r0 && lane < r0 + kPreRows && i < P) rgb = sh_to_rgb(D, &s_sh[(lane - r0) * (S + 1)], dir, cbits);
-      __syncthreads();
-    }
-  }
-  uint3 ac = make_uint3(0u, 0u, 0u);
-  uint32_t khi = 0u, knlo = 0u;  // this lane's visible depth key and its complement (0: culled)
-  if (i < P) {
-    uint4 w;
-    uint2 rcw;
-    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
-                        sc, q, o, rgb, cbits, w, rcw);
-    // every Gaussian's words, one store each
-    radii[i] = (int32_t)w.x;
-    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);  // rect, tb, exact list length
-    if (bshift) tb[i] = w.z;
-    dkey[i] = w.w;
-    if (w.w != 0xFFFFFFFFu) {
-      khi = w.w;
-      knlo = ~w.w;
-    }
-    n_touched[i] = 0;
-    gflag[i] = 0;  // the backward's "received gradient" flag
-  }
-  // upstream num_rendered, the exact pair count and the bin pair count: one
-  // atomic per wave each, spread over kRectPairLanes words
-  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
-  // scratch the next kernels need zeroed (the depth sort's superblock sums)
-  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
-}
 
 // ---- k_preprocess2: the SH slab streams into LDS while the geometry runs ----
-// The same per-Gaussian work as k_preprocess, reordered so that the SH
-// fetch no longer sits in front of the geometry: the wave first queues its
-// 64 rows' evaluated coefficients as LDS-DMA loads (global_load_lds: no VGPR
+// One wave of 64 Gaussians per workgroup.  The wave first queues its 64
+// rows' evaluated SH coefficients as LDS-DMA loads (global_load_lds: no VGPR
 // holds them in flight), in a chunk-major layout [chunk][lane] (chunk = 4
 // floats when rows are 16-byte aligned, else 1) so that each lane later
 // reads its own row conflict-free; then it loads the parameters and runs the
 // projection / covariance / rectangle / row-table work and writes the
 // geometry records; only then does it wait for the slab and evaluate the
-// colour -- for visible Gaussians only (k_preprocess evaluates every lane).
-// Outputs are bit-identical to k_preprocess (same operation sequences).
-// kCh == 8: the row-major slab of k_preprocess2<8> (whole rows, 16-byte
-// chunks, row stride NCH chunks: only launched when every coefficient of the
-// row is evaluated, 3 (D + 1)^2 == 3 M)
+// colour -- for visible Gaussians only.  Measured alternatives (round 4,
+// removed in round 5; all bit-identical): the slab staged before the geometry
+// (k_preprocess, 90 us when this one was 86), SH coefficients in VGPRs (150
+// vs 103 us), the coalesced row-major slab (112 vs 102), one memory round
+// trip per wave (106.7 vs 103.4), records staged through LDS for contiguous
+// stores (115.8 vs 106.7).
 template <int kD, int kCh>
 __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lane, f3 dir, uint32_t& cbits) {
-  constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, kC = kCh == 8 ? 4 : kCh, NCH = (NF + kC - 1) / kC;
-  float sh[NCH * kC];
+  constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, NCH = (NF + kCh - 1) / kCh;
+  float sh[NCH * kCh];
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     if constexpr (kCh >= 4) {
-      const float4 v = reinterpret_cast<const float4*>(s_sh)[kCh == 8 ? lane * NCH + k : k * 64 + lane];
+      const float4 v = reinterpret_cast<const float4*>(s_sh)[k * 64 + lane];
       sh[4 * k] = v.x;
       sh[4 * k + 1] = v.y;
       sh[4 * k + 2] = v.z;
@@ -373,154 +275,6 @@ __device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_
   }
 }
 
-// k_preprocess2e (WGSR_PRE_EARLY=1, A/B; measured SLOWER at 1M / SH3: 106.7
-// vs 103.4 us -- the vector memory path, not the wait structure, bounds the
-// preprocess: TD busy 80 %, 74 % of it stalled on L2 data, tools/pmc_ta.py):
-// the same work with ONE memory round trip per wave.  k_preprocess2 as compiled
-// waits three times (vmcnt(0) after the means load -- slab included --, then
-// for scales / rotation, then for the opacity the compiler had sunk to its
-// use): here the slab and every parameter (unconditional, clamped row) are
-// issued together and waited for once, the SH degree is a template argument
-// (a fixed run of slab loads), and every store of the Gaussian is held back
-// to after the colour.
-// queue a wave's SH slab (64 rows' evaluated coefficients) into LDS:
-// chunk-major (kCh 4 / 1) or row-major (kCh 8), see k_preprocess2
-template <int kCh, int kD>
-__device__ __forceinline__ void queue_sh_slab(int P, int M, const float* __restrict__ shs, float* s_sh, int lane,
-                                              int i0, int i) {
-  constexpr int nf = 3 * (kD + 1) * (kD + 1), nch = (nf + (kCh == 8 ? 4 : kCh) - 1) / (kCh == 8 ? 4 : kCh);
-  const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
-  const size_t c_end = (size_t)P * (3 * M) / 4;  // chunks in the whole table
-#pragma unroll
-  for (int k = 0; k < nch; ++k) {
-    if constexpr (kCh == 8) {
-      const size_t c = min((size_t)i0 * (3 * M) / 4 + (size_t)(64 * k + lane), c_end - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(shs + 4 * c),
-                                       (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
-    } else if constexpr (kCh == 4)
-      __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
-                                       (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)(src + k),
-                                       (__attribute__((address_space(3))) void*)(s_sh + 64 * k), 4, 0, 0);
-  }
-}
-
-// kD < 0: no SH colour (colours given, or no SH table).  kStage (SH only;
-// WGSR_PRE_STAGE=1 with WGSR_PRE_EARLY=1, A/B: measured slower, 115.8 vs
-// 106.7 us at 1M / SH3):
-// the wave's 64 splat records (48 B each) and list records (32 B) leave as
-// whole contiguous runs -- staged in the slab's LDS, 1 KB per store
-// instruction -- instead of 16-byte stores strided by 48 / 32 bytes (rows
-// of culled Gaussians are written as zeros; nothing reads them)
-template <int kCh, int kD, bool kStage = false>
-__global__ __launch_bounds__(kPreWave) void k_preprocess2e(
-    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
-    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
-    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
-    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped, uint32_t* __restrict__ dkey,
-    int32_t* __restrict__ radii, int32_t* __restrict__ n_touched, uint32_t* __restrict__ err_flag,
-    unsigned long long* __restrict__ rect_pairs, unsigned long long* __restrict__ list_pairs,
-    unsigned long long* __restrict__ bin_pairs, int bshift, uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag,
-    uint32_t* __restrict__ drange, const ZeroJob zero, uint32_t* __restrict__ meta) {
-  extern __shared__ float s_sh[];  // nch x 64 x kCh floats (chunk-major), as k_preprocess2
-  constexpr bool sh_on = kD >= 0;
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
-  // every load of the Gaussian in flight at once: the slab, then the
-  // parameters (unconditional, clamped row: lanes past P compute nothing)
-  if constexpr (sh_on) queue_sh_slab<kCh, kD>(P, M, shs, s_sh, lane, i0, i);
-  const int ic = min(i, P - 1);
-  f3 p = mk3(means[3 * ic], means[3 * ic + 1], means[3 * ic + 2]);
-  f3 sc = mk3(1.f, 1.f, 1.f);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  if (!cov_pre) {  // (uniform)
-    sc = mk3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
-    q = reinterpret_cast<const float4*>(rots)[ic];
-  }
-  const float o = opac[ic];
-  // ONE wait for all of them, here: without this use the compiler sinks
-  // loads to their first use and waits at each (three round trips, each
-  // counting the slab too, since LDS-DMA loads are not counted past)
-  asm volatile("" ::"v"(p.x), "v"(p.y), "v"(p.z), "v"(sc.x), "v"(sc.y), "v"(sc.z), "v"(q.x), "v"(q.y), "v"(q.z),
-               "v"(q.w), "v"(o));
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
-  uint3 ac = make_uint3(0u, 0u, 0u);
-  uint32_t khi = 0u, knlo = 0u;
-  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
-  uint2 rcw = make_uint2(0u, 0u);
-  PreDefer dfr{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f), make_uint4(0u, 0u, 0u, 0u)};
-  if (i < P)
-    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p, sc,
-                        q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, !sh_on, &dfr);
-  float4 C = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t cbits = 0;
-  if constexpr (sh_on) {
-    __builtin_amdgcn_s_waitcnt(0);  // the slab has landed (no store issued since; one wave per workgroup)
-    __syncthreads();
-    if (i < P && w.x != 0u) {  // visible: the colour record
-#pragma clang fp contract(off)
-      f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
-      const float len = sqrtf(dot3(dir, dir));
-      dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-      const f3 rgb = sh_rgb_lds<(kD < 0 ? 0 : kD), kCh>(s_sh, lane, dir, cbits);
-      C = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
-    }
-  }
-  constexpr bool stage = kStage && sh_on;
-  if constexpr (stage) {
-    float4* sb = reinterpret_cast<float4*>(s_sh);  // 64 x 3 splat rows, then 64 x 2 list rows
-    __syncthreads();  // every lane's slab reads are done
-    const bool rec = i < P && ac.x != 0u;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    sb[3 * lane] = rec ? dfr.A : z4;
-    sb[3 * lane + 1] = rec ? dfr.B : z4;
-    sb[3 * lane + 2] = rec && w.x != 0u ? C : z4;
-    reinterpret_cast<uint4*>(sb)[192 + 2 * lane] = rec ? dfr.tab : make_uint4(0u, 0u, 0u, 0u);
-    reinterpret_cast<uint4*>(sb)[192 + 2 * lane + 1] = make_uint4(rcw.x, rcw.y, w.z, w.y);
-    __syncthreads();
-    const int nrow = min(kPreWave, P - i0);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int idx = 64 * k + lane;
-      if (idx < 3 * nrow) splat[3 * (size_t)i0 + idx] = sb[idx];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int idx = 64 * k + lane;
-      if (idx < 2 * nrow) reinterpret_cast<uint4*>(lrec + i0)[idx] = reinterpret_cast<const uint4*>(sb)[192 + idx];
-    }
-  }
-  if (i < P) {
-    if (!stage && ac.x != 0u) {  // preprocess_one reached its records (rect area > 0)
-      splat[3 * (size_t)i + 0] = dfr.A;
-      splat[3 * (size_t)i + 1] = dfr.B;
-      lrec[i].tab = dfr.tab;
-    }
-    if (sh_on && w.x != 0u) {  // (uniform sh_on)
-      if (!stage) splat[3 * (size_t)i + 2] = C;
-      clamped[i] = cbits;
-    }
-    radii[i] = (int32_t)w.x;
-    if (!stage) lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
-    if (bshift) tb[i] = w.z;
-    dkey[i] = w.w;
-    if (w.w != 0xFFFFFFFFu) {
-      khi = w.w;
-      knlo = ~w.w;
-    }
-    n_touched[i] = 0;
-    gflag[i] = 0;
-  }
-  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
-  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
-}
-
 template <int kCh>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
@@ -540,19 +294,10 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
   const bool sh_on = shs != nullptr && colors == nullptr;
   if (sh_on) {  // uniform: queue the slab first
-    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + (kCh == 8 ? 4 : kCh) - 1) / (kCh == 8 ? 4 : kCh);
+    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + kCh - 1) / kCh;
     const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
-    // kCh == 8: the wave's 64 rows as one contiguous run of 16-byte chunks,
-    // lane l of load k taking chunk 64 k + l (coalesced: each load covers
-    // 1 KB of HBM instead of 64 rows' 16 bytes each); the LDS copy is then
-    // row-major (a lane's reads stride 3M floats: 4-way bank conflicts, cheap)
-    const size_t c_end = (size_t)P * (3 * M) / 4;  // chunks in the whole table
     for (int k = 0; k < nch; ++k) {
-      if constexpr (kCh == 8) {
-        const size_t c = min((size_t)i0 * (3 * M) / 4 + (size_t)(64 * k + lane), c_end - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(shs + 4 * c),
-                                         (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
-      } else if constexpr (kCh == 4)
+      if constexpr (kCh == 4)
         __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
                                          (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
       else
@@ -602,94 +347,6 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       dir = mk3(dir.x / len, dir.y / len, dir.z / len);
       uint32_t cbits = 0;
       const f3 rgb = sh_rgb_lds_deg<kCh>(D, s_sh, lane, dir, cbits);
-      splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
-      clamped[i] = cbits;
-    }
-  }
-  wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
-  zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
-}
-
-// ---- k_preprocess3: the SH coefficients in VGPRs (WGSR_PRE=3, A/B) ----------
-// k_preprocess2 without LDS: each lane's evaluated coefficients (16-byte
-// loads of its own row, issued first) stay in registers across the geometry,
-// so the workgroup's occupancy is set by VGPRs instead of the 12 KB slab.
-// Needs 16-byte aligned rows (3M % 4 == 0); outputs bit-identical.
-template <int kD>
-__global__ __launch_bounds__(kPreWave) void k_preprocess3(
-    int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
-    const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
-    const float* __restrict__ colors, const float* __restrict__ cov_pre, float scale_mod,
-    const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ campos_p, int W,
-    int H, float tanx, float tany, int gx, int gy, int prefiltered, float4* __restrict__ splat,
-    ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
-    uint32_t* __restrict__ dkey, int32_t* __restrict__ radii, int32_t* __restrict__ n_touched,
-    uint32_t* __restrict__ err_flag, unsigned long long* __restrict__ rect_pairs,
-    unsigned long long* __restrict__ list_pairs, unsigned long long* __restrict__ bin_pairs, int bshift,
-    uint32_t* __restrict__ tb, uint8_t* __restrict__ gflag, uint32_t* __restrict__ drange, const ZeroJob zero,
-    uint32_t* __restrict__ meta) {
-  constexpr int NF = 3 * (kD + 1) * (kD + 1), NC = (NF + 3) / 4;
-  const int lane = threadIdx.x;
-  const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
-  // the parameters first, unconditionally (clamped row): the in-order load
-  // counter lets the geometry start while the 12 coefficient loads behind
-  // them are still in flight
-  const int ic = min(i, P - 1);
-  f3 p = mk3(means[3 * ic], means[3 * ic + 1], means[3 * ic + 2]);
-  f3 sc = mk3(1.f, 1.f, 1.f);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  if (!cov_pre) {  // (uniform)
-    sc = mk3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
-    q = reinterpret_cast<const float4*>(rots)[ic];
-  }
-  // (a volatile read keeps this load ahead of the coefficient loads: sunk to
-  // its use, its wait would also wait for the coefficients -- the load
-  // counter is in order)
-  float o = *reinterpret_cast<const volatile float*>(opac + ic);
-  float sh[4 * NC];
-  {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v* src = reinterpret_cast<const f4v*>(shs + (size_t)ic * (3 * M));
-    static_for<0, NC>([&](auto k) {
-      const f4v v = __builtin_nontemporal_load(src + k.value);
-      sh[4 * k.value] = v.x;
-      sh[4 * k.value + 1] = v.y;
-      sh[4 * k.value + 2] = v.z;
-      sh[4 * k.value + 3] = v.w;
-    });
-  }
-  if (i >= P) {
-    p = mk3(0.f, 0.f, 1.f);
-    o = 0.f;
-  }
-  Cam c;
-  load_cam(c, viewm, projm, W, H, tanx, tany);
-  uint3 ac = make_uint3(0u, 0u, 0u);
-  uint32_t khi = 0u, knlo = 0u;
-  uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
-  if (i < P) {
-    uint2 rcw;
-    ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
-                        W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
-                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, false);
-    radii[i] = (int32_t)w.x;
-    lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
-    if (bshift) tb[i] = w.z;
-    dkey[i] = w.w;
-    if (w.w != 0xFFFFFFFFu) {
-      khi = w.w;
-      knlo = ~w.w;
-    }
-    n_touched[i] = 0;
-    gflag[i] = 0;
-    if (w.x != 0u) {  // visible: the colour record
-#pragma clang fp contract(off)
-      f3 dir = sub3(p, mk3(campos_p[0], campos_p[1], campos_p[2]));
-      const float len = sqrtf(dot3(dir, dir));
-      dir = mk3(dir.x / len, dir.y / len, dir.z / len);
-      uint32_t cbits = 0;
-      const f3 rgb = sh_to_rgb(kD, sh, dir, cbits);
       splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
       clamped[i] = cbits;
     }
@@ -977,12 +634,6 @@ __global__ __launch_bounds__(256) void k_bin_bounds(const uint32_t* __restrict__
 // threads 44 us; one wave per row 73 us -- a bin's ~2000 entries then take
 // ~35 dependent steps; 512 threads 55 us -- fewer workgroups in flight.)
 constexpr int kExpThreads = 256;
-#ifndef WGSR_EXP_ITEMS  // entries per thread per compaction step (1 or 2; A/B)
-#define WGSR_EXP_ITEMS 1
-#endif
-#ifndef WGSR_EXP_PACK  // packed per-wave counts, one barrier per step (0: the plain loop; A/B)
-#define WGSR_EXP_PACK 1
-#endif
 __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __restrict__ skeys,
                                                              const uint32_t* __restrict__ sgid,
                                                              const uint2* __restrict__ bounds, int gx, int gy,
@@ -991,9 +642,6 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
                                                              uint32_t* __restrict__ tile_len,
                                                              uint32_t* __restrict__ meta) {
   constexpr int NW = kExpThreads / 64;
-#if WGSR_EXP_ITEMS == 2 || !WGSR_EXP_PACK
-  __shared__ uint32_t s_wc[NW][4];
-#endif
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (blockIdx.x == 0 && t == 0) meta[0] = 1u;  // the lists are the sort-bin region
   const int B = 1 << bshift;
@@ -1007,58 +655,15 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
   const size_t base0 = ((size_t)lo << (2 * bshift)) + (size_t)(r << bshift) * len;
   const uint32_t shift = 16u + ((uint32_t)r << bshift), rmask = (1u << B) - 1u;
   uint32_t count[4] = {0u, 0u, 0u, 0u};
-#if WGSR_EXP_ITEMS == 2
-  // two entries per thread per step (half the steps and barriers)
-  __shared__ uint32_t s_wc2[NW][4];
-  uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
-  uint32_t key2 = lo + 256 + t < hi ? skeys[lo + 256 + t] : 0u, gid2 = lo + 256 + t < hi ? sgid[lo + 256 + t] : 0u;
-  asm volatile("" ::"v"(key), "v"(gid), "v"(key2), "v"(gid2));
-  for (uint32_t e0 = lo; e0 < hi; e0 += 2 * kExpThreads) {
-    const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
-    const uint32_t bits2 = (key2 >> shift) & rmask, my_gid2 = gid2;
-    const uint32_t e1 = e0 + 2 * kExpThreads + t, e2 = e1 + kExpThreads;
-    key = e1 < hi ? skeys[e1] : 0u;
-    gid = e1 < hi ? sgid[e1] : 0u;
-    key2 = e2 < hi ? skeys[e2] : 0u;
-    gid2 = e2 < hi ? sgid[e2] : 0u;
-    uint64_t m[4], m2[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      m[c] = wave_ballot(c < B && ((bits >> c) & 1u));
-      m2[c] = wave_ballot(c < B && ((bits2 >> c) & 1u));
-      if (lane == 0 && c < B) {
-        s_wc[w][c] = (uint32_t)__popcll(m[c]);
-        s_wc2[w][c] = (uint32_t)__popcll(m2[c]);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c >= B) break;
-      uint32_t off = count[c], tot = 0, off2 = 0, tot2 = 0;
-#pragma unroll
-      for (int k = 0; k < NW; ++k) {
-        const uint32_t v = s_wc[k][c], v2 = s_wc2[k][c];
-        off += k < w ? v : 0u;
-        off2 += k < w ? v2 : 0u;
-        tot += v;
-        tot2 += v2;
-      }
-      if ((bits >> c) & 1u) lists[base0 + (size_t)c * len + off + lanes_below(m[c])] = my_gid;
-      if ((bits2 >> c) & 1u) lists[base0 + (size_t)c * len + count[c] + tot + off2 + lanes_below(m2[c])] = my_gid2;
-      count[c] += tot + tot2;
-    }
-    __syncthreads();
-    asm volatile("" ::"v"(key), "v"(gid), "v"(key2), "v"(gid2));
-  }
-#elif WGSR_EXP_PACK
   // the step's per-wave counts of each tile as four 16-bit fields of one
   // 64-bit LDS word (<= 4 x 64 entries per field): each wave's cross-wave
   // prefix is three conditional 64-bit adds instead of 16 LDS reads and 32
   // adds; the words are double-buffered by step parity, so a step needs one
   // barrier (a wave rewrites a buffer only after the next step's barrier,
   // which every wave passes after reading it); stores through a uniform base
-  // pointer with 32-bit offsets.  Same positions as the loop below.
+  // pointer with 32-bit offsets.  (Measured: 31.2 -> 28.5 us at 1M / 1080p
+  // against per-wave LDS counts with two barriers per step; two entries per
+  // thread per step: 35.5 us.)
   __shared__ unsigned long long s_wp[2][NW];
   uint32_t* const out0 = lists + base0;
   uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
@@ -1094,41 +699,6 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
     }
     asm volatile("" ::"v"(key), "v"(gid));
   }
-#else
-  uint32_t key = lo + t < hi ? skeys[lo + t] : 0u, gid = lo + t < hi ? sgid[lo + t] : 0u;
-  // the next step's entries load while this step runs: the empty asm uses
-  // below make the compiler wait for them at the END of a step (without
-  // them it waits at the top, right after issuing them)
-  asm volatile("" ::"v"(key), "v"(gid));
-  for (uint32_t e0 = lo; e0 < hi; e0 += kExpThreads) {
-    const uint32_t bits = (key >> shift) & rmask, my_gid = gid;
-    const uint32_t e1 = e0 + kExpThreads + t;
-    key = e1 < hi ? skeys[e1] : 0u;
-    gid = e1 < hi ? sgid[e1] : 0u;
-    uint64_t m[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      m[c] = wave_ballot(c < B && ((bits >> c) & 1u));
-      if (lane == 0 && c < B) s_wc[w][c] = (uint32_t)__popcll(m[c]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c >= B) break;
-      uint32_t off = count[c], tot = 0;
-#pragma unroll
-      for (int k = 0; k < NW; ++k) {
-        const uint32_t v = s_wc[k][c];
-        off += k < w ? v : 0u;
-        tot += v;
-      }
-      if ((bits >> c) & 1u) lists[base0 + (size_t)c * len + off + lanes_below(m[c])] = my_gid;
-      count[c] += tot;
-    }
-    __syncthreads();
-    asm volatile("" ::"v"(key), "v"(gid));
-  }
-#endif
   if (t < B) {
     const int tx = (bx << bshift) + t;
     if (tx < gx) {
@@ -1156,16 +726,9 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
 // spare key / payload buffers.  A bin of more than kBdsCap entries runs the
 // same passes chunk by chunk through global scratch (the sort-bin list
 // region, free until k_expand_bins writes it).
-#ifndef WGSR_BDS_ITEMS  // entries per lane of the LDS-resident sort
-#define WGSR_BDS_ITEMS 10
-#endif
-#ifndef WGSR_BDS_FINE  // entries per lane in steps of one (0: 1, 2, 4, 7 only)
-#define WGSR_BDS_FINE 1
-#endif
-#ifndef WGSR_BDS_THREADS  // workgroup size (512 or 1024)
-#define WGSR_BDS_THREADS 512
-#endif
-constexpr int kBdsThreads = WGSR_BDS_THREADS, kBdsWaves = kBdsThreads / 64, kBdsItems = WGSR_BDS_ITEMS;
+// (512 threads, up to 10 entries per lane in steps of one: 1024 threads with
+// 1, 2, 4, 7 entries per lane measured 42-46 vs 33 us at 1M / 1080p)
+constexpr int kBdsThreads = 512, kBdsWaves = kBdsThreads / 64, kBdsItems = 10;
 constexpr int kBdsCap = kBdsThreads * kBdsItems;  // entries sorted in LDS
 constexpr int kBdsMaxBits = 9, kBdsDigits = 1 << kBdsMaxBits;
 static_assert(kBdsDigits <= kBdsThreads, "threads t < kBdsDigits own digit t");
@@ -1176,28 +739,16 @@ __device__ __forceinline__ bool bds_owns_digit() { return (int)threadIdx.x < kBd
 // instead of one ballot and a 64-bit select per digit bit.  A wave's LDS
 // instructions complete in order, so every lane's OR lands before any lane's
 // read, and every read before the clear behind it.
-#ifndef WGSR_BDS_LDSMATCH
-#define WGSR_BDS_LDSMATCH 1
-#endif
-// WGSR_BDS_SHARE: the lane-mask table shares LDS with the staging buffer (a
-// pass ranks with the table, then scatters into the buffer; the table is
-// zeroed again before the next pass) -- 61 instead of 93 KB per 512-thread
-// workgroup, two workgroups per CU: the 1M frame's 510 bins in one round
-#ifndef WGSR_BDS_SHARE
-#define WGSR_BDS_SHARE 1
-#endif
+// The lane-mask table shares LDS with the staging buffer (a pass ranks with
+// the table, then scatters into the buffer; the table is zeroed again before
+// the next pass) -- 61 instead of 93 KB per 512-thread workgroup, two
+// workgroups per CU: the 1M frame's 510 bins in one round.  (Peer groups by
+// ballots: 73 vs 45.5 us at 1M, round 3.)
 struct BdsLds {
-#if WGSR_BDS_LDSMATCH && WGSR_BDS_SHARE
   union {
     uint2 buf[kBdsCap];                                // (depth key, position in the bin)
     unsigned long long match[kBdsWaves][kBdsDigits];  // lane masks per digit (zero between uses)
   };
-#else
-  uint2 buf[kBdsCap];                     // (depth key, position in the bin)
-#if WGSR_BDS_LDSMATCH
-  unsigned long long match[kBdsWaves][kBdsDigits];  // lane masks per digit (zero between uses)
-#endif
-#endif
   uint32_t wcnt[kBdsWaves][kBdsDigits];   // per wave digit counts, then their prefix over waves
   uint32_t base[kBdsDigits];              // per digit: first slot
   uint32_t tmp[kBdsWaves];
@@ -1321,14 +872,10 @@ __device__ __forceinline__ void bds_rank(BdsLds& L, uint32_t cn, uint32_t mn, in
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
     const bool valid = le < cn;
     const uint32_t d = ((k[j] - mn) >> shift) & mask;
-#if WGSR_BDS_LDSMATCH
     (void)bits;
     if (valid) atomicOr(&L.match[w][d], 1ull << lane);
     const uint64_t peers = valid ? L.match[w][d] : 0ull;
     if (valid) L.match[w][d] = 0ull;
-#else
-    const uint64_t peers = match_digit(d, bits, wave_ballot(valid));
-#endif
     const int leader = __ffsll((unsigned long long)peers) - 1;
     uint32_t old = 0;
     if (valid && lane == leader) old = atomicAdd(&L.wcnt[w][d], (uint32_t)__popcll(peers));
@@ -1389,9 +936,6 @@ __device__ __forceinline__ uint32_t bds_range(BdsLds& L, uint32_t mn, uint32_t m
 __device__ __forceinline__ void bds_plan(int R, int& passes, int& pbits) {
   passes = (R + kBdsMaxBits - 1) / kBdsMaxBits;
   pbits = passes ? (R + passes - 1) / passes : 0;
-#ifdef WGSR_BDS_DIAG_PASSES  // timing diagnostics only (wrong order)
-  passes = min(passes, WGSR_BDS_DIAG_PASSES);
-#endif
 }
 
 // a bin of n <= 64 JN x kBdsWaves entries: wave w owns slots [w JN 64,
@@ -1448,12 +992,10 @@ __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict_
 #pragma unroll
     for (int q = 0; q < kBdsWaves; ++q)
       if (bds_owns_digit()) L.wcnt[q][t] = 0u;
-#if WGSR_BDS_LDSMATCH && WGSR_BDS_SHARE
     if (p + 1 < npass) {  // the next pass ranks with the table the buffer overwrote
       __syncthreads();
       for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
     }
-#endif
     __syncthreads();
   }
   if (E) {  // the per-tile lists straight from the sorted bin
@@ -1641,36 +1183,28 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
 #pragma unroll
   for (int q = 0; q < kBdsWaves; ++q)
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
-#if WGSR_BDS_LDSMATCH
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
-#endif
   if (n <= 1u * kBdsThreads)
     bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 2u * kBdsThreads)
     bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#if WGSR_BDS_FINE
   // (every step of JN: a bin's time is its busiest wave's chain of JN entry
   // groups per pass, and a coarser JN leaves the last waves idle -- 4.7k
   // entries at JN = 7 keep 11 of 16 waves busy, at JN = 5 all 15 it needs)
   else if (n <= 3u * kBdsThreads)
     bds_small<3>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#endif
   else if (n <= 4u * kBdsThreads)
     bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#if WGSR_BDS_FINE
   else if (n <= 5u * kBdsThreads)
     bds_small<5>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 6u * kBdsThreads)
     bds_small<6>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#endif
   else if (n <= 7u * kBdsThreads)
     bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#if WGSR_BDS_FINE
   else if (kBdsItems > 8 && n <= 8u * kBdsThreads)
     bds_small<(kBdsItems > 8 ? 8 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 9 && n <= 9u * kBdsThreads)
     bds_small<(kBdsItems > 9 ? 9 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
-#endif
   else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
     bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
   else
@@ -1773,92 +1307,19 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict_
 // ahead).
 constexpr int kFwdBatch = 64;
 
-// One batch of staged list entries for one wave (8x8 quadrant): cull by the
-// exact ellipse test against the wave's pixel box, then blend the survivors
-// front to back.  Contributor number of entry j: cbase + j, or (bin lists)
-// sIdx[j] + 1, its position in the bin's list.  n_touched increments are
-// staged per entry in sTouch and leave as one atomic wave instruction.
-// WGSR_FWD_HALF: a batch whose wave has no pixel left with T > 0.5 runs the
-// entry loop without the n_touched bookkeeping (T only falls, so none of its
-// entries can touch a pixel): one compare, two VALU moves and one LDS store
-// fewer per entry, with no per-entry branch
-#ifndef WGSR_FWD_HALF
-#define WGSR_FWD_HALF 1
-#endif
-template <bool kIdx, bool kTouch>
-__device__ __forceinline__ void fwd_blend_loop(uint64_t todo, uint32_t cbase, const uint32_t* sIdx,
-                                               const float4* sA, const float4* sB, const float4* sC,
-                                               uint32_t* sTouch, v2f pxy, float& T, v2f& c01, v2f& c2d,
-                                               uint32_t& last, uint64_t& dm) {
-  while (todo != 0 && dm != ~0ull) {
-    const int j = __builtin_ctzll(todo);
-    todo &= ~(1ull << j);
-    const float4 A = sA[j];
-    const float2 B = *reinterpret_cast<const float2*>(&sB[j]);
-    const float4 Cc = sC[j];
-    const v2f d = v2f{A.x, A.y} - pxy;                     // (dx, dy) = mean - pixel
-    const float power = splat_power(v2f{A.z, A.w}, B.x, d);  // log2(e) x upstream's power
-    const float alpha = fminf(kMaxAlpha, B.y * __builtin_amdgcn_exp2f(power));
-    const float test_T = fmaf(-T, alpha, T);  // T (1 - alpha)
-    const uint64_t live = wave_ballot(power <= 0.0f) & wave_ballot(alpha >= kMinAlpha) & ~dm;
-    const uint64_t low = wave_ballot(test_T < kMinT);
-    const uint64_t blend = live & ~low;
-    const bool bl = __builtin_amdgcn_inverse_ballot_w64(blend);
-    const float wgt = bl ? alpha * T : 0.f;
-    c01 += wgt * v2f{Cc.x, Cc.y};
-    c2d += wgt * v2f{Cc.z, Cc.w};
-    // upstream n_touched: pixels whose T stays above 0.5 after this blend
-    uint32_t tot = 0;
-    if (kTouch) tot = (uint32_t)__popcll(blend & wave_ballot(test_T > 0.5f));
-    T = bl ? test_T : T;
-    last = bl ? (kIdx ? sIdx[j] + 1u : cbase + j) : last;
-    dm |= live & low;
-    if (kTouch) sTouch[j] = tot;  // (every lane stores the same value: no branch)
-  }
-}
-
-template <bool kIdx>
-__device__ __forceinline__ void fwd_blend_batch(int cnt, uint32_t cbase, const uint32_t* sIdx, const float4* sA,
-                                                const float4* sB, const float4* sC, const uint32_t* sG,
-                                                uint32_t* sTouch, int wx0, int wx1, int wy0, int wy1, v2f pxy,
-                                                int lane, int32_t* __restrict__ n_touched, float& T, v2f& c01,
-                                                v2f& c2d, uint32_t& last, uint64_t& dm) {
-  const uint64_t todo = wave_ballot(lane < cnt && ellipse_hits(sA[lane], sB[lane], wx0, wx1, wy0, wy1));
-#if WGSR_FWD_HALF
-  if ((wave_ballot(T > 0.5f) & ~dm) == 0) {  // (uniform)
-    fwd_blend_loop<kIdx, false>(todo, cbase, sIdx, sA, sB, sC, sTouch, pxy, T, c01, c2d, last, dm);
-    return;
-  }
-#endif
-  sTouch[lane] = 0;
-  fwd_blend_loop<kIdx, true>(todo, cbase, sIdx, sA, sB, sC, sTouch, pxy, T, c01, c2d, last, dm);
-  // one atomic per touched entry, all of the batch's in one wave instruction
-  const uint32_t tv = sTouch[lane];
-  if (tv != 0) atomicAdd(&n_touched[sG[lane]], (int)tv);
-}
-
-// Entry-pair blend (WGSR_FWD_EPAIR, the default): the batch's entries that
+// Entry-pair blend: the batch's entries that (one 8x8-quadrant wave's)
 // survive the wave's culling are first compacted into the wave's own LDS area
 // with two consecutive survivors interleaved per field (sQ: {x1, x2, y1, y2},
 // {A.z1, A.z2, A.w1, A.w2}, {B.x1, B.x2, o1, o2}), so that one ds_read_b128
 // hands two entries' operands to packed-FP32 math: the power, exp2 argument
 // and opacity product of BOTH entries cost one v_pk_* instruction each (the
 // forward's own operation sequence per lane, so alpha is bitwise that of
-// fwd_blend_loop and of the backward's recomputation).  Only the
+// the backward's recomputation).  Only the
 // transmittance recurrence, the compares and the colour accumulation stay
 // per entry.  n_touched increments are staged per compact slot.
-#ifndef WGSR_FWD_EPAIR
-#define WGSR_FWD_EPAIR 1
-#endif
 // wave 0 streams the next batch's records into a second LDS buffer with
 // global_load_lds instead of holding them in registers (every wave of the
 // kernel would allocate those VGPRs)
-#ifndef WGSR_FWD_LDSPF
-#define WGSR_FWD_LDSPF 1
-#endif
-#if WGSR_FWD_LDSPF && !WGSR_FWD_EPAIR
-#error "WGSR_FWD_LDSPF needs WGSR_FWD_EPAIR"
-#endif
 struct FwdPairRec {   // two consecutive survivors (one LDS address per pair)
   float4 q[3];       // {x, x', y, y'}, {A.z, A.z', A.w, A.w'}, {B.x, B.x', o, o'}
   float4 c[2];       // colour (c0, c1, c2, depth) of each
@@ -1927,7 +1388,10 @@ __device__ __forceinline__ void fwd_blend_batch_pairs(int cnt, uint32_t cbase, c
   const uint64_t todo = wave_ballot(mine);
   const int n = __popcll(todo);
   const uint32_t k = lanes_below(todo);
-  const bool touch = (wave_ballot(T > 0.5f) & ~dm) != 0;  // (uniform) see WGSR_FWD_HALF
+  // (uniform) a batch whose wave has no pixel left with T > 0.5 runs the entry
+  // loop without the n_touched bookkeeping: T only falls, so none of its
+  // entries can touch a pixel (one compare, two moves, one LDS store fewer)
+  const bool touch = (wave_ballot(T > 0.5f) & ~dm) != 0;
   if (mine) {
     FwdPairRec& R = L.p[k >> 1];
     float* q = &R.q[0].x + (k & 1);
@@ -1974,22 +1438,13 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     float* __restrict__ out_color, float* __restrict__ out_depth, float* __restrict__ out_opac,
     float* __restrict__ final_T, uint32_t* __restrict__ n_contrib, int32_t* __restrict__ n_touched,
     uint32_t* __restrict__ tile_m4) {
-#if WGSR_FWD_LDSPF
   // two batch buffers as separate objects, so that the compiler can tell the
   // LDS-DMA into one from the reads of the other (no vmcnt wait before them)
   __shared__ float4 sA_0[kFwdBatch], sB_0[kFwdBatch], sC_0[kFwdBatch];
   __shared__ float4 sA_1[kFwdBatch], sB_1[kFwdBatch], sC_1[kFwdBatch];
   __shared__ uint32_t sG_0[kFwdBatch], sG_1[kFwdBatch];
   __shared__ uint32_t sDone[2][4];  // per batch parity: wave w has no pixel left
-#else
-  __shared__ float4 sA[kFwdBatch], sB[kFwdBatch], sC[kFwdBatch];
-  __shared__ uint32_t sG[kFwdBatch];
-#endif
-#if WGSR_FWD_EPAIR
   __shared__ FwdPairLds sPair[4];  // per wave: the batch's surviving entries, compacted
-#else
-  __shared__ uint32_t sTouch[4][kFwdBatch];  // per wave: n_touched increments of the batch's entries
-#endif
   const uint32_t slot = xcd_remap(blockIdx.x, (uint32_t)ntiles);
   const uint32_t tile = order ? order[slot] : slot;  // null: xcd_remap's order as it is
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -2008,7 +1463,6 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
   v2f c01{0.f, 0.f}, c2d{0.f, 0.f};  // (colour 0, colour 1), (colour 2, depth)
   uint32_t last = 0;
 
-#if WGSR_FWD_LDSPF
   // prefetch pipeline (wave 0): batch b+1's records stream straight into the
   // other LDS buffer (global_load_lds_dwordx4, no VGPRs held), ids of b+2 in
   // registers.  ONE barrier per batch, which waits for LDS only: wave 0's
@@ -2083,49 +1537,6 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
     if (b0 + kFwdBatch >= range.y || !step(std::integral_constant<int, 1>{}, b0 + kFwdBatch)) break;
   }
   if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
-#else
-  // prefetch pipeline (wave 0): records of batch b+1 in registers, ids of b+2
-  uint32_t gcur = 0, gnext = 0;
-  float4 nA = make_float4(0, 0, 0, 0), nB = nA, nC = nA;
-  if (t < kFwdBatch) {
-    if (range.x + t < range.y) {
-      gcur = point_g[range.x + t];
-      nA = splat[3 * (size_t)gcur];
-      nB = splat[3 * (size_t)gcur + 1];
-      nC = splat[3 * (size_t)gcur + 2];
-    }
-    if (range.x + kFwdBatch + t < range.y) gnext = point_g[range.x + kFwdBatch + t];
-  }
-
-  for (uint32_t b0 = range.x; b0 < range.y; b0 += kFwdBatch) {
-    if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(dm)) == (int)blockDim.x) break;
-    if (t < kFwdBatch) {
-      sA[t] = nA;
-      sB[t] = nB;
-      sC[t] = nC;
-      sG[t] = gcur;
-    }
-    __syncthreads();
-    if (t < kFwdBatch) {
-      gcur = gnext;
-      if (b0 + kFwdBatch + t < range.y) {
-        nA = splat[3 * (size_t)gcur];
-        nB = splat[3 * (size_t)gcur + 1];
-        nC = splat[3 * (size_t)gcur + 2];
-      }
-      if (b0 + 2 * kFwdBatch + t < range.y) gnext = point_g[b0 + 2 * kFwdBatch + t];
-    }
-    if (dm == ~0ull) continue;  // this wave is finished; keep the barriers
-    const int cnt = (int)min((uint32_t)kFwdBatch, range.y - b0);
-#if WGSR_FWD_EPAIR
-    fwd_blend_batch_pairs(cnt, b0 - range.x + 1, sA, sB, sC, sG, sPair[w], wx0, wx1, wy0, wy1, pxy, lane, n_touched, T,
-                          c01, c2d, last, dm, nullptr, nullptr, nullptr, 0u, [] {});
-#else
-    fwd_blend_batch<false>(cnt, b0 - range.x + 1, nullptr, sA, sB, sC, sG, sTouch[w], wx0, wx1, wy0, wy1, pxy, lane,
-                           n_touched, T, c01, c2d, last, dm);
-#endif
-  }
-#endif
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w] (no barrier)
     uint32_t mx = last;
 #pragma unroll
@@ -2310,70 +1721,18 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
-  // k_preprocess2 (LDS-DMA slab behind the geometry) unless WGSR_PRE=1
-  // (read per call: tests compare the variants in one process)
-  const char* pre_env = getenv("WGSR_PRE");
-  const int pre_mode = pre_env ? atoi(pre_env) : 2;
-  if (pre_mode == 3 && a.shs && !a.colors && (a.M * 3) % 4 == 0 &&
-      (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) {
-    auto kern = a.D == 0 ? k_preprocess3<0> : a.D == 1 ? k_preprocess3<1> : a.D == 2 ? k_preprocess3<2>
-                                                                                    : k_preprocess3<3>;
-    hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), 0, s, a.P, a.D, a.M, a.means3D,
-                       a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
-                       a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
-                       at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
-                       at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs,
-                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
-    return hipGetLastError();
-  }
-  if (pre_mode != 1) {
-    const bool sh_on = a.shs && !a.colors;
-    const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
-    const int nf = 3 * (a.D + 1) * (a.D + 1);
-    const int kch = ch4 ? 4 : 1;
-    size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
-    // (WGSR_PRE=4, A/B, whole rows evaluated only: the coalesced row-major
-    // slab k_preprocess2<8> -- 112 vs 102 us at 1M / SH3: the strided
-    // chunk-major gather is not the limit)
-    const char* early_env = getenv("WGSR_PRE_EARLY");  // (read per call: tests compare the orders)
-    const bool early = early_env ? atoi(early_env) != 0 : false;  // (A/B: 106.7 vs 103.4 us at 1M)
-    auto kern = ch4 ? ((nf == 3 * a.M && pre_mode == 4) ? k_preprocess2<8> : k_preprocess2<4>) : k_preprocess2<1>;
-    if (early) {
-      // (the SH degree and slab layout as template arguments: the slab is a
-      // fixed run of loads, so the geometry's wait can count past it)
-      const int d = sh_on ? a.D : -1;
-      const char* st_env = getenv("WGSR_PRE_STAGE");  // (read per call: tests compare)
-      // (A/B: 115.8 vs 106.7 us without staging at 1M / SH3 -- rejected)
-      const bool stage = sh_on && ch4 && (st_env ? atoi(st_env) != 0 : false) && pre_mode != 4;
-      if (stage) {
-        kern = d == 0 ? k_preprocess2e<4, 0, true> : d == 1 ? k_preprocess2e<4, 1, true>
-             : d == 2 ? k_preprocess2e<4, 2, true> : k_preprocess2e<4, 3, true>;
-        lds2 = std::max(lds2, sizeof(float4) * 5 * 64);
-      } else if (pre_mode == 4 && ch4 && nf == 3 * a.M)
-        kern = d < 0 ? k_preprocess2e<8, -1> : d == 0 ? k_preprocess2e<8, 0> : d == 1 ? k_preprocess2e<8, 1>
-             : d == 2 ? k_preprocess2e<8, 2> : k_preprocess2e<8, 3>;
-      else if (ch4 || !sh_on)
-        kern = d < 0 ? k_preprocess2e<4, -1> : d == 0 ? k_preprocess2e<4, 0> : d == 1 ? k_preprocess2e<4, 1>
-             : d == 2 ? k_preprocess2e<4, 2> : k_preprocess2e<4, 3>;
-      else
-        kern = d == 0 ? k_preprocess2e<1, 0> : d == 1 ? k_preprocess2e<1, 1> : d == 2 ? k_preprocess2e<1, 2>
-                                                                          : k_preprocess2e<1, 3>;
-    }
-    hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds2, s, a.P, a.D, a.M, a.means3D,
-                       a.scales, a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier,
-                       a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
-                       at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
-                       at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs,
-                       bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
-    return hipGetLastError();
-  }
-  const size_t lds = (a.shs && !a.colors) ? sizeof(float) * kPreRows * (3 * (size_t)a.M + 1) : 0;
-  hipLaunchKernelGGL(k_preprocess, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave), lds, s, a.P, a.D, a.M, a.means3D, a.scales,
-                     a.rotations, a.opacities, a.shs, a.colors, a.cov3D_precomp, a.scale_modifier, a.viewmatrix,
-                     a.projmatrix, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, gx, gy, a.prefiltered,
-                     at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped),
-                     at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs, list_pairs, bin_pairs, bshift,
-                     at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero, meta);
+  const bool sh_on = a.shs && !a.colors;
+  const bool ch4 = sh_on && (a.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(a.shs) & 15) == 0;
+  const int nf = 3 * (a.D + 1) * (a.D + 1);
+  const int kch = ch4 ? 4 : 1;
+  const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
+  hipLaunchKernelGGL(ch4 ? k_preprocess2<4> : k_preprocess2<1>, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave),
+                     lds2, s, a.P, a.D, a.M, a.means3D, a.scales, a.rotations, a.opacities, a.shs, a.colors,
+                     a.cov3D_precomp, a.scale_modifier, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
+                     a.tan_fovy, gx, gy, a.prefiltered, at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
+                     at<uint32_t>(geom, L.clamped), at<uint32_t>(geom, L.dkey), radii, n_touched, err_flag, rect_pairs,
+                     list_pairs, bin_pairs, bshift, at<uint32_t>(geom, L.tb), at<uint8_t>(geom, L.gflag), drange, zero,
+                     meta);
   return hipGetLastError();
 }
 
@@ -2419,9 +1778,7 @@ __global__ __launch_bounds__(kBdsThreads) void k_argsort_small(const uint32_t* _
 #pragma unroll
   for (int q = 0; q < kBdsWaves; ++q)
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;
-#if WGSR_BDS_LDSMATCH
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
-#endif
   if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
     bds_small<1>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
   else if (n <= 2u * kBdsThreads)
@@ -2477,19 +1834,9 @@ hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, ui
   return hipGetLastError();
 }
 
-// WGSR_BWD_ORDER=global: one LPT list over all tiles instead of per XCD chunk
-bool bwd_order_global() {
-  static const bool v = [] {
-    const char* e = getenv("WGSR_BWD_ORDER");
-    return e && strcmp(e, "global") == 0;
-  }();
-  return v;
-}
-
 hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* order, hipStream_t s) {
-  const bool global = bwd_order_global();
-  hipLaunchKernelGGL(k_tile_order, dim3(global ? 1 : 8), dim3(1024), 0, s, work_quads, true, global, (uint32_t)ntiles,
-                     order);
+  // per-XCD chunks (one global LPT list measured 2 % slower)
+  hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, work_quads, true, false, (uint32_t)ntiles, order);
   return hipGetLastError();
 }
 

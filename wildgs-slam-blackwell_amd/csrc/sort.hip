@@ -3,13 +3,12 @@
 // Replaces the CUB primitives upstream's rasteriser and simple-knn lean on
 // (cub::DeviceRadixSort::SortPairs, cub::DeviceScan::InclusiveSum: SURVEY.md
 // 2 "Kernel inventory").  8-bit digits; a workgroup owns 4096 keys (2048 for
-// sorts of <= 2M keys, so a per-Gaussian pass still fills the chip).  Two
-// schedules share one scatter kernel:
-//  * reduce-then-scan (default): per pass, block histograms -> per-digit row
-//    scan over blocks -> stable scatter;
-//  * onesweep (WGSR_SORT=onesweep): one histogram kernel for all passes, then
-//    one scatter kernel per pass whose blocks find their offsets by decoupled
-//    look-back.
+// sorts of <= 2M keys, so a per-Gaussian pass still fills the chip).
+// Reduce-then-scan: per pass, block histograms (which also add into 16-block
+// superblock sums) -> stable scatter whose blocks derive their digit bases
+// from the superblock sums.  (A decoupled look-back "onesweep" schedule
+// measured 1.3-2x slower here -- look-back chains through ~700 resident
+// blocks -- and was removed in round 5.)
 // Block-local stable ranking uses 64-bit ballots to find the lanes that share
 // a digit; the scatter stages the block's keys in LDS in digit order so that
 // runs of one digit leave as contiguous (coalesced) stores.  Each wave of the
@@ -174,33 +173,8 @@ __global__ __launch_bounds__(256) void k_radix_rowscan(uint32_t* __restrict__ hi
   if (t == 0) totals[blockIdx.x] = tot;
 }
 
-// Onesweep mode: global digit histograms of every pass in one read of the keys.
-template <int I>
-__global__ __launch_bounds__(256) void k_onesweep_hist(const uint32_t* __restrict__ keys, uint32_t n, int begin_bit,
-                                                       int end_bit, uint32_t* __restrict__ ghist) {
-  __shared__ uint32_t s_h[kMaxSortPasses][256];
-  const int t = threadIdx.x;
-  const int passes = (end_bit - begin_bit + 7) / 8;
-#pragma unroll
-  for (int p = 0; p < kMaxSortPasses; ++p) s_h[p][t] = 0;
-  uint32_t k[I];
-  const int nv = load_run<I>(keys, n, (size_t)blockIdx.x * (256 * I) + (size_t)t * I, k);
-  __syncthreads();
-  const int per = (end_bit - begin_bit + passes - 1) / passes;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = begin_bit + per * p;
-    add_runs(s_h[p], k, nv, shift, (1u << min(per, end_bit - shift)) - 1u);
-  }
-  __syncthreads();
-  for (int p = 0; p < passes; ++p)
-    if (s_h[p][t]) atomicAdd(&ghist[p * 256 + t], s_h[p][t]);
-}
-
 // ---- scatter -----------------------------------------------------------------
-// Onesweep look-back status words: flag (bits 31..30: 0 not ready, 1 block
-// aggregate, 2 inclusive prefix) | count (bits 29..0).
-constexpr uint32_t kStAgg = 1u << 30, kStPre = 2u << 30, kStCount = (1u << 30) - 1u;
-constexpr int kLookback = 16;  // predecessor status words fetched per look-back round trip
+constexpr uint32_t kStCount = (1u << 30) - 1u;  // largest key count a sort takes
 
 // One stable digit pass over a block of 256 I keys.  Keys/payloads are loaded
 // up front (in flight while ranking); ranks come from LDS atomics-with-return
@@ -208,24 +182,19 @@ constexpr int kLookback = 16;  // predecessor status words fetched per look-back
 // issue order, so the returned counts are the sequential ones and the 16
 // atomics pipeline instead of forming a read-wait-write chain); keys and
 // payloads are staged as (key, value) pairs through one 32 KB LDS buffer in digit order so that each
-// digit's run leaves as contiguous stores.
-//   kOnesweep = false: the block's digit offsets come from the scanned
-//     per-block histogram (hist: [256][nb], totals: digit totals).
-//   kOnesweep = true: the block takes the next virtual id (so every block it
-//     waits on is already running), publishes its digit counts and looks back
-//     through its predecessors' status words (totals: this pass's global
-//     digit histogram).
-template <bool kOnesweep, int I>
+// digit's run leaves as contiguous stores.  The block's digit offsets come
+// from the superblock sums (sup) or, without them, from the row-scanned
+// per-block histogram (hist: [256][nb], totals: digit totals).
+template <int I>
 __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
-    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals,
-    uint32_t* __restrict__ vcounter, uint32_t* __restrict__ status, uint32_t* __restrict__ kout,
+    uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup, uint2* __restrict__ bounds,
     const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout, const uint32_t* __restrict__ ndev) {
   constexpr int kTile = 256 * I;
-  if (ndev) {  // capacity mode (reduce-then-scan only): blocks past the live keys have nothing to move
+  if (ndev) {  // capacity mode: blocks past the live keys have nothing to move
     n = min(n, *ndev);
-    if (!kOnesweep && (size_t)blockIdx.x * kTile >= n && !(blockIdx.x == 0 && bounds)) return;
+    if ((size_t)blockIdx.x * kTile >= n && !(blockIdx.x == 0 && bounds)) return;
   }
   __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16); then the
                                   // second payload (xin: the bin sort's depth keys) -- no extra LDS
@@ -233,14 +202,11 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
   __shared__ uint32_t s_tmp[4];
-  __shared__ uint32_t s_vid;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t mask = (1u << bits) - 1u;
-  if (kOnesweep && t == 0) s_vid = atomicAdd(vcounter, 1u);
 #pragma unroll
   for (int i = 0; i < 4; ++i) s_wcnt[i][t] = 0;
-  if (kOnesweep) __syncthreads();
-  const uint32_t bid = kOnesweep ? s_vid : blockIdx.x;
+  const uint32_t bid = blockIdx.x;
   const size_t blk0 = (size_t)bid * kTile;
   const size_t base = blk0 + (size_t)w * (64 * I);
   uint32_t key[I], val[I], rank[I], xv[I];
@@ -252,14 +218,12 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
     xv[j] = xin && valid ? xin[e] : 0u;
   }
-  uint32_t gdig = 0;  // reduce-then-scan: this block's global base of digit t
-  if (!kOnesweep) {  // (the scans' barriers publish s_wcnt = 0)
-    if (sup) {
-      gdig = sup_digit_base(hist, sup, nb, nsup, bid, t, s_tmp, bounds, mask);
-    } else {
-      const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);
-      gdig = ex + hist[(size_t)t * nb + bid];
-    }
+  uint32_t gdig = 0;  // this block's global base of digit t (the scans' barriers publish s_wcnt = 0)
+  if (sup) {
+    gdig = sup_digit_base(hist, sup, nb, nsup, bid, t, s_tmp, bounds, mask);
+  } else {
+    const uint32_t ex = block_excl_scan256(totals[t], s_tmp, nullptr);
+    gdig = ex + hist[(size_t)t * nb + bid];
   }
 #pragma unroll
   for (int j = 0; j < I; ++j) {
@@ -277,43 +241,12 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   {
     const uint32_t c0 = s_wcnt[0][t], c1 = s_wcnt[1][t], c2 = s_wcnt[2][t], c3 = s_wcnt[3][t];
     const uint32_t cnt_d = c0 + c1 + c2 + c3;
-    uint32_t* st = status + (size_t)bid * 256 + t;
-    if (kOnesweep)  // publish this block's count of digit t (block 0: already its prefix)
-      __hip_atomic_store(st, (bid == 0 ? kStPre : kStAgg) | cnt_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // per-digit: exclusive prefix over waves, then over digits (block-local)
     s_wcnt[0][t] = 0;
     s_wcnt[1][t] = c0;
     s_wcnt[2][t] = c0 + c1;
     s_wcnt[3][t] = c0 + c1 + c2;
     s_lbase[t] = block_excl_scan256(cnt_d, s_tmp, nullptr);
-    if (kOnesweep) {
-      gdig = block_excl_scan256(totals[t], s_tmp, nullptr);  // digit t's start in the output
-      // decoupled look-back: sum predecessors' counts of digit t until one
-      // carries its inclusive prefix
-      uint32_t excl = 0;
-      int64_t v = (int64_t)bid - 1;  // nearest predecessor not yet summed
-      while (v >= 0) {
-        uint32_t sv[kLookback];
-#pragma unroll
-        for (int k = 0; k < kLookback; ++k)
-          sv[k] = (v - k >= 0) ? __hip_atomic_load(status + (size_t)(v - k) * 256 + t, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : kStPre;
-        int k = 0;
-        bool done = false;
-        for (; k < kLookback; ++k) {
-          const uint32_t f = sv[k] & ~kStCount;
-          if (f == 0) break;  // not published yet: re-fetch from here
-          excl += sv[k] & kStCount;
-          if (f == kStPre) { done = true; break; }
-        }
-        if (done) break;
-        v -= k;
-        if (k < kLookback) __builtin_amdgcn_s_sleep(1);
-      }
-      if (bid > 0) __hip_atomic_store(st, kStPre | (excl + cnt_d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      gdig += excl;
-    }
     s_gbase[t] = gdig;
   }
   __syncthreads();
@@ -885,28 +818,8 @@ __global__ __launch_bounds__(1024) void k_scan2_bsum(uint2* __restrict__ bsum, u
 
 }  // namespace
 
-// WGSR_SORT=onesweep | onesweep_small (only sorts of <= kSmallSortN keys) |
-// rts (reduce-then-scan, the default)
-int sort_mode() {
-  static const int v = [] {
-    const char* e = getenv("WGSR_SORT");
-    if (e && strcmp(e, "onesweep") == 0) return 1;
-    if (e && strcmp(e, "onesweep_small") == 0) return 2;
-    return 0;
-  }();
-  return v;
-}
-
-// 9 or 10 key bits sort in one wide pass (WGSR_SORT_WIDE=0 keeps 8-bit passes)
-static bool wide_pass(int bits) {
-  const char* e = getenv("WGSR_SORT_WIDE");  // read per call: tests compare both
-  return bits > 8 && bits <= 10 && !(e && strcmp(e, "0") == 0) && sort_mode() == 0;
-}
-
-static bool sup_mode() {
-  const char* e = getenv("WGSR_SORT_SUP");  // read per call: tests compare both
-  return !(e && strcmp(e, "0") == 0);
-}
+// 9 or 10 key bits sort in one wide pass
+static bool wide_pass(int bits) { return bits > 8 && bits <= 10; }
 
 int radix_passes(int begin_bit, int end_bit) {
   const int bits = end_bit - begin_bit;
@@ -916,12 +829,12 @@ int radix_passes(int begin_bit, int end_bit) {
 
 // Superblock sums of a reduce-then-scan sort of n keys over [begin_bit,
 // end_bit): their place in `status` (words) and size (words); 0 words when the
-// sort does not use them (wide pass, onesweep, WGSR_SORT_SUP=0).  A caller
+// sort does not use them (wide pass).  A caller
 // that zeroes this range itself passes sup_zeroed to radix_sort_pairs.
 size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words) {
   const int bits = end_bit - begin_bit;
   if (offset_words) *offset_words = 0;
-  if (n == 0 || bits <= 0 || wide_pass(bits) || sort_mode() != 0 || !sup_mode()) return 0;
+  if (n == 0 || bits <= 0 || wide_pass(bits)) return 0;
   const uint32_t nb = sort_blocks(n);
   if (offset_words) *offset_words = 256 * (size_t)nb;
   return 256 * (size_t)((nb + kSupBlocks - 1) / kSupBlocks) * ((bits + 7) / 8);
@@ -959,28 +872,14 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
   }
   const int passes = (end_bit - begin_bit + 7) / 8;
   if (passes > kMaxSortPasses || n > (size_t)kStCount) return hipErrorInvalidValue;
-  // (the second payload rides the reduce-then-scan schedule only)
-  const bool onesweep = !xvals && !ndev && (sort_mode() == 1 || (sort_mode() == 2 && n <= kSmallSortN));
-  uint32_t* ghist = totals;                          // onesweep: [passes][256]; rts: digit totals
-  uint32_t* vcount = totals + kMaxSortPasses * 256;  // onesweep: virtual block counters [passes]
-  if (onesweep) {
-    hipError_t e = hipMemsetAsync(totals, 0, kSortTotalsBytes, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(status, 0, 4 * 256 * (size_t)nb * passes, stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_onesweep_hist<I>, dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit, end_bit,
-                       ghist);
-  }
-  // superblock mode (default for reduce-then-scan; WGSR_SORT_SUP=0 keeps the
-  // row-scan kernel): one memset of every pass's superblock sums replaces a
-  // row-scan launch per pass
+  uint32_t* ghist = totals;  // digit totals (row-scan path only)
+  // superblock sums: one memset of every pass's sums (or none: the caller
+  // zeroed them) replaces a row-scan launch per pass
   const uint32_t nsup = (nb + kSupBlocks - 1) / kSupBlocks;
-  uint32_t* sup = nullptr;
-  if (!onesweep && sup_mode()) {
-    sup = status + 256 * (size_t)nb;  // (sort_status_bytes reserves 256 nb + kMaxSortPasses x 256 nsup words)
-    if (!sup_zeroed) {
-      hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
-      if (e != hipSuccess) return e;
-    }
+  uint32_t* sup = status + 256 * (size_t)nb;  // (sort_status_bytes reserves 256 nb + kMaxSortPasses x 256 nsup words)
+  if (!sup_zeroed) {
+    hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
+    if (e != hipSuccess) return e;
   }
   uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt, *xi = xvals, *xo = xvals_alt;
   bool iota = vals_iota;
@@ -990,23 +889,16 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
   for (int p = 0; p < passes; ++p) {
     const int shift = begin_bit + per * p;
     const int bits = min(per, end_bit - shift);
-    if (onesweep) {
-      hipLaunchKernelGGL((k_radix_scatter<true, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, nullptr, ghist + 256 * p, vcount + p,
-                         status + 256 * (size_t)nb * p, ko, vo, nullptr, 0u, nullptr, nullptr, nullptr, nullptr);
-    } else {
-      // status doubles as the [256][nb] per-block histogram (and, in
-      // superblock mode, holds the passes' [256][nsup] superblock sums after it)
-      uint32_t* sp = sup ? sup + (size_t)p * 256 * nsup : nullptr;
-      hipLaunchKernelGGL(k_radix_hist<I>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status,
-                         sp, nsup, ndev);
-      if (!sp) hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(256), 0, stream, status, nb, ghist);
-      // a single superblock pass over bits [0, end_bit) also writes the digit bounds
-      uint2* db = (sp && passes == 1 && begin_bit == 0) ? digit_bounds : nullptr;
-      hipLaunchKernelGGL((k_radix_scatter<false, I>), dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0,
-                         (uint32_t)n, shift, bits, nb, status, ghist, nullptr, status, ko, vo, sp, nsup, db, xi, xo, ndev);
-      if (db && bounds_done) *bounds_done = true;
-    }
+    // status doubles as the [256][nb] per-block histogram, followed by the
+    // passes' [256][nsup] superblock sums
+    uint32_t* sp = sup + (size_t)p * 256 * nsup;
+    hipLaunchKernelGGL(k_radix_hist<I>, dim3(nb), dim3(256), 0, stream, ki, (uint32_t)n, shift, bits, nb, status,
+                       sp, nsup, ndev);
+    // a single pass over bits [0, end_bit) also writes the digit bounds
+    uint2* db = (passes == 1 && begin_bit == 0) ? digit_bounds : nullptr;
+    hipLaunchKernelGGL(k_radix_scatter<I>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
+                       bits, nb, status, ghist, ko, vo, sp, nsup, db, xi, xo, ndev);
+    if (db && bounds_done) *bounds_done = true;
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;
@@ -1072,13 +964,7 @@ hipError_t launch_depth_sort(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals,
                              const uint32_t* range, uint32_t* range2, uint32_t* scratch, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n > (size_t)kStCount) return hipErrorInvalidValue;
-  // WGSR_DEPTH_ITEMS=4|8|16 overrides the keys per thread (A/B runs)
-  static const int items = [] {
-    const char* e = getenv("WGSR_DEPTH_ITEMS");
-    const int v = e ? atoi(e) : 0;
-    return (v == kTinySortItems || v == kSmallSortItems || v == kSortItems) ? v : 0;
-  }();
-  switch (items ? items : sort_items(n)) {
+  switch (sort_items(n)) {
     case kTinySortItems:
       return depth_sort_tiled<kTinySortItems>(keys, keys_alt, vals, vals_alt, n, range, range2, scratch, s);
     case kSmallSortItems:

@@ -126,11 +126,7 @@ __device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
 // Packed butterfly for gfx950 (must be called with all 64 lanes active):
 //   v_permlane32_swap pairs values (lanes 0-31 keep value 2k, 32-63 value
 //   2k+1): 5 swaps + 5 adds; v_permlane16_swap pairs those by rows: 3 swaps
-//   + 3 adds; then 3 x 4 DPP row adds.  ~30 VALU ops instead of 60 shuffles.
-#ifndef WGSR_SUM10_V2
-#define WGSR_SUM10_V2 1
-#endif
-// WGSR_SUM10_V3 (default): the 8- and 4-lane stages are transposed too, with
+//   + 3 adds; then the 8- and 4-lane stages are transposed too, with
 // bank-masked DPP adds (a bank = 4 lanes of a row): 3 + 2 adds instead of
 // 3 x 2 row adds, then one quad butterfly on a single register, and each
 // sum leaves from its own lane by ONE store (23 VALU + 1 LDS store per call
@@ -142,10 +138,6 @@ __device__ __forceinline__ float2 permlane32_swap_add(float a, float b) {
 //   4-lane stage: S0's banks 0, 2 += banks 1, 3; bank 3 takes S2's banks 2 + 3;
 //   quad butterfly: lanes 0-3 of row r end with value m, lanes 8-11 with
 //   4 + m, lanes 12-15 (even rows) with 8 + m.
-#ifndef WGSR_SUM10_V3
-#define WGSR_SUM10_V3 1
-#endif
-#if WGSR_SUM10_V3
 // value index whose sum this lane stores (-1: none)
 __device__ __forceinline__ int sum10_value(int lane) {
   const int row = lane >> 4, pos = lane & 15, m = (row & 1) * 2 + (row >> 1);
@@ -163,14 +155,6 @@ __device__ __forceinline__ int sum10_slot(int lane) {
   const int v = sum10_value(lane);
   return v < 0 ? 0 : v;
 }
-#else
-// Lane 15 of row r holds, after wave_sum10, value m of S[0], 4 + m of S[1]
-// and (even rows only, where m = r / 2) 8 + m of S[2], m = sum10_slot(lane).
-__device__ __forceinline__ int sum10_slot(int lane) {
-  const int row = lane >> 4;
-  return (row & 1) * 2 + (row >> 1);
-}
-#endif
 __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) {
   float R[5];
   uint32_t R4b = 0u;
@@ -186,17 +170,11 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) 
     S[0] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v0 v2 v1 v3
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[2]), __float_as_uint(R[3]), false, false);
     S[1] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v4 v6 v5 v7
-#if WGSR_SUM10_V2 || WGSR_SUM10_V3
     // the partner register's rows only reach S[2]'s odd rows, which are never
     // stored: pass a dead register (no zero move)
     r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), R4b, false, false);
     S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 - v9 -
-#else
-    r = __builtin_amdgcn_permlane16_swap(__float_as_uint(R[4]), 0u, false, false);
-    S[2] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: v8 0 v9 0
-#endif
   }
-#if WGSR_SUM10_V3
   // bank-masked DPP adds write only the named banks; the rest of the tied
   // destination keeps its value.  Each asm opens with the 2 wait states a DPP
   // read of a just-written VGPR needs (the hazard check does not look inside
@@ -209,15 +187,6 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) 
   S[0] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(S[0]), 0xB1, 0xf, 0xf, true));
   S[0] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(S[0]), 0x4E, 0xf, 0xf, true));
   asm volatile("" ::"v"(S[0]));
-#else
-#pragma unroll
-  for (int i = 0; i < 3; ++i) S[i] = dpp_row_sum16(S[i]);
-#if WGSR_SUM10_V2
-  // materialise the sums before the store branch, so the last DPP step folds
-  // into one v_add_f32_dpp instead of a DPP move + an add inside the branch
-  asm volatile("" ::"v"(S[0]), "v"(S[1]), "v"(S[2]));
-#endif
-#endif
 }
 // dstm = the entry's 10 floats + sum10_slot(lane): the lane part of the
 // address computed once by the caller, one address register for all stores
@@ -225,16 +194,8 @@ __device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], float* 
   float S[3];
   wave_sum10(v, S);
   const int lane = __lane_id();
-#if WGSR_SUM10_V3
   (void)lane;
   if (__builtin_amdgcn_inverse_ballot_w64(kSum10StoreLanes)) dstm[0] = S[0];
-#else
-  if ((lane & 15) == 15) {
-    dstm[0] = S[0];
-    dstm[4] = S[1];
-    if (!((lane >> 4) & 1)) dstm[8] = S[2];
-  }
-#endif
 }
 __device__ __forceinline__ void wave_sum10_store(const float (&v)[10], float* dst) {
   wave_sum10_store_m(v, dst + sum10_slot(__lane_id()));
@@ -623,20 +584,10 @@ __device__ __forceinline__ v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elem
 // evaluated as dx (A.z dx + B.x dy) + A.w dy^2 -- one packed multiply and
 // three scalar ops.  The forward and both backwards call this one helper, so
 // the backward recomputes exactly the forward's alpha.
-#ifndef WGSR_POWER_FMA
-#define WGSR_POWER_FMA 1
-#endif
 __device__ __forceinline__ float splat_power(v2f cd, float cxy, v2f d) {
-#if WGSR_POWER_FMA
   const v2f t = cd * d;
   return fmaf(d.x, fmaf(cxy, d.y, t.x), t.y * d.y);
-#else
-  const v2f q2 = cd * d * d;
-  return q2.x + q2.y + (cxy * d.x) * d.y;
-#endif
 }
-
-// Runtime knob for the render kernels' pixels per lane (1, 2 or 4).
 
 // ---------------------------------------------------------------------------
 // Small fp32 math (upstream operation order where it matters).  The geometry

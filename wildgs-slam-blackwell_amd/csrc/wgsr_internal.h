@@ -112,7 +112,6 @@ hipError_t launch_ranges(const uint32_t* sorted_keys, uint32_t N, int ntiles, ui
                          uint32_t* meta, hipStream_t s);
 // the backward's launch order (tiles by deepest contributor, per XCD chunk)
 hipError_t launch_tile_order(const uint32_t* work_quads, int ntiles, uint32_t* order, hipStream_t s);
-bool bwd_order_global();
 hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, const uint32_t* point_g,
                              const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
@@ -127,19 +126,12 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
                              const void* geom, const float* final_T,
                              const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_ddepth,
                              float4* partial, uint8_t* pflag, const ZeroJob& zero, hipStream_t s);
-// Per-Gaussian backward.  GbMode:
-//   kGbDense   k_gauss_bwd over every Gaussian (each lane walks its records);
-//   kGbSparse  k_sum_active (record sums of the Gaussians the render
-//              backward marked in gflag) + k_gauss_bwd<kSparse>: the same
-//              lanes and stores, loads and arithmetic only for marked lanes.
-enum GbMode { kGbDense = 0, kGbSparse = 1 };
-GbMode gauss_bwd_mode();  // WGSR_GB=dense|sparse (default: sparse)
-hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const int32_t* radii, const void* geom,
-                            const float4* partial, const uint8_t* pflag, float* gsum, float* dL_dmeans2D,
-                            float* dL_dcolors, float* dL_dopacity,
-                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
-                            float* dL_drot, float* dL_dtau, GbMode mode,
-                            bool zeroed, hipStream_t s);
+// Per-Gaussian backward (k_gauss_bwd_compact): the rows of the Gaussians the
+// render backward marked in gflag; the render backward zero-filled the outputs.
+hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const void* geom, const float4* partial, const uint8_t* pflag,
+                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau,
+                            hipStream_t s);
 // view-sharded backward (raster_bwd.hip, wgsr/dp.py)
 hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, const void* geom, const float4* partial,
                                const uint8_t* pflag, int P_pad, float* records, hipStream_t s);
