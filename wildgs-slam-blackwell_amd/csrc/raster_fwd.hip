@@ -467,6 +467,29 @@ __device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0,
   return mask;
 }
 
+// Exact tile mask inside bin (bx, by) of a splat whose rect rows all sit in
+// its row table (not `tall`): the bin's 2^S rows' spans come out of the
+// table as one byte run (rows above the rect shift in zeros, rows below it
+// are zero in the table), each row a bit field of the mask.
+template <int S>
+__device__ __forceinline__ uint32_t bin_mask_tab(int bx, int by, int x0, int y0, const uint4& tab) {
+  constexpr int B = 1 << S;
+  const int kr0 = (by << S) - y0;  // in [-(B - 1), kRowTab - 1]
+  const uint64_t L64 = ((uint64_t)tab.y << 32) | tab.x, X64 = ((uint64_t)tab.w << 32) | tab.z;
+  const uint32_t lens = kr0 >= 0 ? (uint32_t)(L64 >> (8 * kr0)) : (uint32_t)(L64 << (-8 * kr0));
+  const uint32_t xs = kr0 >= 0 ? (uint32_t)(X64 >> (8 * kr0)) : (uint32_t)(X64 << (-8 * kr0));
+  const int c0 = bx << S;
+  uint32_t mask = 0;
+#pragma unroll
+  for (int rr = 0; rr < B; ++rr) {
+    const int len = (int)((lens >> (8 * rr)) & 0xFFu);
+    const int xa = x0 + (int)((xs >> (8 * rr)) & 0xFFu);
+    const int cl = max(xa, c0), w = max(min(xa + len, c0 + B) - cl, 0);
+    mask |= ((1u << w) - 1u) << (rr * B + cl - c0);
+  }
+  return mask;
+}
+
 // Sort bins, after the dual scan's block sums (packed_scan_blocks: bsum[b]
 // = exclusive prefix of (exact list length, bins touched) over the 256-rank
 // blocks in depth order): each 256-thread workgroup finishes the scan for its
@@ -478,9 +501,17 @@ __device__ __forceinline__ uint32_t bin_mask(int bx, int by, int bshift, int x0,
 // 2^s x 2^s tile mask (bin_mask; high 16 bits, carried through the sort).  A
 // Gaussian's pairs in row-major bin order (the stable sort by bin keeps the
 // depth order inside each bin).
+// A pair's owner (the rank whose rectangle it belongs to) is found without a
+// search: each rank with bins writes its lane id at its first pair's place
+// in a 64-entry LDS row, and an inclusive max-scan over the row (DPP) hands
+// every pair its owner -- the last rank starting at or before it; the
+// owner's record (rect, first pair, Gaussian, depth key, row table) is read
+// from LDS where every rank staged it (three LDS reads per pair instead of a
+// six-step shuffle search and ten shuffles).
 constexpr int kDupScanThreads = kPackedScanTile;  // one rank per thread
+template <int S>
 __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
-    uint32_t P, int bshift, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
+    uint32_t P, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
     uint32_t* __restrict__ vals, const ZeroJob zero, const uint32_t* __restrict__ dkey,
@@ -488,7 +519,12 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   // (cap_slots / cap_pairs: the capacity-mode forward's buffer sizes -- writes
   // past them are dropped and the forward flags the overflow; ~0 otherwise)
   constexpr int NW = kDupScanThreads / 64;
+  constexpr int bshift = S;
   __shared__ uint2 s_w[NW], s_p[NW];
+  __shared__ uint4 s_ra[NW][64];    // per rank: rect lo | hi, first bin pair, Gaussian
+  __shared__ uint4 s_rt[NW][64];    // per rank: row table
+  __shared__ uint32_t s_rd[NW][64]; // per rank: depth key
+  __shared__ uint32_t s_own[NW][64];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
@@ -558,9 +594,16 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   }
   const uint2 wt = s_w[w];  // the wave's totals
   if (in) slot_start[g] = wb.x + ic - cnt;
-  // the wave's slots are contiguous: one byte store per lane per 64 slots
-  for (uint32_t k = lane; k < wt.x; k += 64)
-    if (wb.x + k < cap_slots) pflag[wb.x + k] = 0;
+  // the wave's slots are contiguous: dword stores for the aligned interior,
+  // byte stores for the (< 4-byte) head and tail
+  {
+    const uint32_t f0 = wb.x, f1 = min(wb.x + wt.x, cap_slots);
+    const uint32_t a0 = min((f0 + 3u) & ~3u, max(f1, f0)), a1 = max(f1 & ~3u, a0);
+    if (lane < (int)(a0 - f0)) pflag[f0 + lane] = 0;
+    if (lane < (int)(f1 - a1)) pflag[a1 + lane] = 0;
+    uint32_t* pw = reinterpret_cast<uint32_t*>(pflag);
+    for (uint32_t k = (a0 >> 2) + lane; k < (a1 >> 2); k += 64) pw[k] = 0u;
+  }
   // scratch the bin sort needs zeroed (its superblock sums)
   zero_share(zero, blockIdx.x, gridDim.x, t, kDupScanThreads);
   if (wt.y == 0) return;  // wave-uniform; no barrier below
@@ -569,32 +612,27 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const bool any_tall = wave_any(tall);
   Reach rr{};
   if (any_tall && tall) rr = reach_of(splat[3 * (size_t)g], splat[3 * (size_t)g + 1]);
+  // every rank's record, for its pairs' lanes
+  s_ra[w][lane] = make_uint4(rlo, rhi, my_off, g);
+  s_rt[w][lane] = tab;
+  s_rd[w][lane] = dk;
+  uint32_t carry = 0;  // owner of the chunk's first pair (the first chunk: a rank starts there)
   for (uint32_t base = start; base < end; base += 64) {
     const uint32_t k = base + lane;
     const uint32_t kk = min(k, end - 1);
-    // owner lane of pair kk: the highest lane whose first pair is <= kk
-    // (lanes without pairs share their successor's offset and lose the tie)
-    int lo = 0, hi = 64;
-#pragma unroll
-    for (int it = 0; it < 6; ++it) {
-      const int mid = (lo + hi) >> 1;
-      const uint32_t x = __shfl(my_off, mid, 64);
-      if (x <= kk) lo = mid; else hi = mid;
-    }
-    const uint32_t local = kk - __shfl(my_off, lo, 64);
-    const uint32_t gg = __shfl(g, lo, 64);
-    const uint32_t a = __shfl(rlo, lo, 64), b = __shfl(rhi, lo, 64);
-    const int x0 = (int)(a & 0xFFFFu), y0 = (int)(a >> 16), x1 = (int)(b & 0xFFFFu), y1 = (int)(b >> 16);
-    const uint4 tq = make_uint4(__shfl(tab.x, lo, 64), __shfl(tab.y, lo, 64), __shfl(tab.z, lo, 64),
-                                __shfl(tab.w, lo, 64));
-    const bool tl = __shfl((int)tall, lo, 64) != 0;
-    Reach rg{};
-    if (any_tall) {  // wave-uniform: the shuffles need every lane
-      rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
-      rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
-      rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
-      rg.ok = __shfl(rr.ok, lo, 64);
-    }
+    // owner of pair kk: the highest lane with bins whose first pair is <= kk
+    // (lanes without bins share their successor's offset: they do not write)
+    s_own[w][lane] = lane == 0 ? carry : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (nb && my_off >= base && my_off < base + 64) s_own[w][my_off - base] = (uint32_t)lane;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t lo = wave_incl_max(s_own[w][lane]);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+    const uint4 ra = s_ra[w][lo];
+    const uint32_t local = kk - ra.z;
+    const uint32_t gg = ra.w;
+    const int x0 = (int)(ra.x & 0xFFFFu), y0 = (int)(ra.x >> 16), x1 = (int)(ra.y & 0xFFFFu), y1 = (int)(ra.y >> 16);
+    const uint4 tq = s_rt[w][lo];
     const int bx0 = x0 >> bshift, bw = ((x1 - 1) >> bshift) - bx0 + 1;
     // local / bw without the integer-division sequence: local < 2^16 (a
     // Gaussian's bins), so the float estimate is within one of the quotient
@@ -602,12 +640,24 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     int col = (int)local - row * bw;
     if (col < 0) { --row; col += bw; } else if (col >= bw) { ++row; col -= bw; }
     const int bx = bx0 + col, by = (y0 >> bshift) + row;
-    const uint32_t pd = pair_depth ? (uint32_t)__shfl((int)dk, lo, 64) : 0u;
-    if (k < end && k < cap_pairs) {
-      keys[k] = (uint32_t)(by * gbx + bx) | (bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, tl, rg) << 16);
-      vals[k] = gg;
-      if (pair_depth) pair_depth[k] = pd;
+    uint32_t mask;
+    if (!any_tall) {  // (wave-uniform) every owner's rows sit in its row table
+      mask = bin_mask_tab<S>(bx, by, x0, y0, tq);
+    } else {
+      const bool tl = __shfl((int)tall, (int)lo, 64) != 0;
+      Reach rg;  // (the shuffles need every lane)
+      rg.mx = __shfl(rr.mx, lo, 64); rg.my = __shfl(rr.my, lo, 64); rg.ca = __shfl(rr.ca, lo, 64);
+      rg.cb = __shfl(rr.cb, lo, 64); rg.L = __shfl(rr.L, lo, 64); rg.det = __shfl(rr.det, lo, 64);
+      rg.ey = __shfl(rr.ey, lo, 64); rg.dya = __shfl(rr.dya, lo, 64); rg.ica = __shfl(rr.ica, lo, 64);
+      rg.ok = __shfl(rr.ok, lo, 64);
+      mask = tl ? bin_mask(bx, by, bshift, x0, y0, x1, y1, tq, true, rg) : bin_mask_tab<S>(bx, by, x0, y0, tq);
     }
+    if (k < end && k < cap_pairs) {
+      keys[k] = (uint32_t)(by * gbx + bx) | (mask << 16);
+      vals[k] = gg;
+      if (pair_depth) pair_depth[k] = s_rd[w][lo];
+    }
+    __builtin_amdgcn_wave_barrier();  // (the next chunk's owner row is rewritten)
   }
 }
 
@@ -1742,8 +1792,10 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
-  hipLaunchKernelGGL(k_duplicate_bins, dim3((a.P + kDupScanThreads - 1) / kDupScanThreads), dim3(kDupScanThreads), 0,
-                     s, (uint32_t)a.P, bshift, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
+  if (bshift < 1 || bshift > kMaxBinShift) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bshift == 1 ? k_duplicate_bins<1> : k_duplicate_bins<2>,
+                     dim3((a.P + kDupScanThreads - 1) / kDupScanThreads), dim3(kDupScanThreads), 0,
+                     s, (uint32_t)a.P, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
                      at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, at<uint32_t>(geom, L.dkey),

@@ -252,14 +252,27 @@ __device__ __forceinline__ int sum20_z_value(int lane) {
 constexpr uint64_t kSum20StoreY = 0x1111111111111111ull;
 constexpr uint64_t kSum20StoreZ = (1ull << 12) | (1ull << 28) | (1ull << 44) | (1ull << 60);
 
-// inclusive prefix sum across the wave
+// inclusive prefix sum across the wave: four DPP row shifts (lanes shifted in
+// from outside the row read 0), then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3 -- six VALU ops, no LDS round trips (the
+// __shfl_up form was six ds_bpermute + twelve VALU)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    uint32_t o = __shfl_up(v, off, kWave);
-    if (lane >= off) v += o;
-  }
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+// inclusive prefix maximum across the wave (the same DPP pattern)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
   return v;
 }
 
