@@ -1,0 +1,202 @@
+// Micro-benchmark: the HBM access shape of k_preprocess2 at 1M Gaussians /
+// SH3 without its arithmetic (VERDICT r4 "Next round" item 3: turn the
+// "memory-path bound" claim into a measured ceiling).
+//
+// Every kernel moves exactly what k_preprocess2 moves per Gaussian:
+//   reads   means 12 B, scales 12 B, rotations 16 B, opacity 4 B, SH row 192 B
+//           (48 floats: 12 x 16-byte chunks)                      = 236 B
+//   writes  splat record 48 B, list record 32 B, clamp bits / depth key /
+//           radius / tb / n_touched 4 B each, gflag 1 B           = 101 B
+// and differ only in HOW:
+//   shape      k_preprocess2's own pattern: one wave of 64 Gaussians per
+//              workgroup, the SH slab as 12 chunk-major global_load_lds per
+//              lane (lane l: chunk k of row l), parameters strided per lane,
+//              records AoS (three 16-byte stores at a 48-byte stride, two at
+//              32), the 4-byte words per lane
+//   soa        the same reads, records SoA: splat as three float4 arrays and
+//              the list record as two uint4 arrays (every record store one
+//              coalesced 1 KB wave store)
+//   rowmajor   soa with the SH slab loaded row-major (chunk 64 k + l of the
+//              wave's contiguous 12 KB run: coalesced 1 KB loads)
+//   reads      shape's reads only (one 4-byte store per Gaussian)
+//   writes     shape's writes only (no loads but a 4-byte id)
+//   copy       a plain float4 stream copy of the same 236 B in / 101 B out
+//              per Gaussian (the ceiling for this byte count)
+// Each kernel's checksum of what it read goes to a 4-byte word so nothing is
+// optimised away.  Timed with HIP events over 50 launches after 5 warm-ups.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/ubench/pre_copy.hip -o tools/ubench/ub_pre_copy
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#define CHK(x)                                                                   \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__);                  \
+      return 1;                                                                  \
+    }                                                                            \
+  } while (0)
+
+struct Bufs {
+  const float *means, *scales, *rots, *opac, *shs;
+  float4 *splat, *sA, *sB, *sC;
+  uint4 *lrec, *lA, *lB;
+  uint32_t *clamped, *dkey, *radii, *tb, *ntouch;
+  uint8_t* gflag;
+  uint32_t* sink;
+};
+
+constexpr int kNF = 48;             // SH3: 16 coefficients x 3
+constexpr int kNCH = kNF / 4;       // 16-byte chunks per row
+
+template <int kMode>  // 0 shape, 1 soa, 2 rowmajor, 3 reads
+__global__ __launch_bounds__(64) void k_shape(int P, Bufs b) {
+  __shared__ float s_sh[64 * kNF];
+  const int lane = threadIdx.x, i0 = blockIdx.x * 64, i = i0 + lane;
+  const int ic = min(i, P - 1);
+  for (int k = 0; k < kNCH; ++k) {
+    if (kMode == 2) {
+      const size_t c = min((size_t)i0 * kNCH + (size_t)(64 * k + lane), (size_t)P * kNCH - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(b.shs + 4 * c), (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds((const void*)(b.shs + (size_t)ic * kNF + 4 * k),
+                                       (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+    }
+  }
+  const float m0 = b.means[3 * ic], m1 = b.means[3 * ic + 1], m2 = b.means[3 * ic + 2];
+  const float s0 = b.scales[3 * ic], s1 = b.scales[3 * ic + 1], s2 = b.scales[3 * ic + 2];
+  const float4 q = reinterpret_cast<const float4*>(b.rots)[ic];
+  const float o = b.opac[ic];
+  const float geo = m0 + m1 + m2 + s0 + s1 + s2 + q.x + q.y + q.z + q.w + o;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  float col = 0.f;
+  for (int k = 0; k < kNCH; ++k) {
+    const float4 v = reinterpret_cast<const float4*>(s_sh)[k * 64 + lane];
+    col += v.x + v.y + v.z + v.w;
+  }
+  if (i >= P) return;
+  const uint32_t u = __float_as_uint(geo + col);
+  if (kMode == 3) {
+    b.sink[i] = u;
+    return;
+  }
+  const float4 A = make_float4(geo, col, 1.f, 2.f), B = make_float4(col, geo, 3.f, 0.f), C = make_float4(o, q.x, col, m2);
+  const uint4 T = make_uint4(u, u + 1, u + 2, u + 3), W = make_uint4(u ^ 5u, u, 7u, u & 255u);
+  if (kMode == 0) {
+    b.splat[3 * (size_t)i] = A;
+    b.splat[3 * (size_t)i + 1] = B;
+    b.splat[3 * (size_t)i + 2] = C;
+    b.lrec[2 * (size_t)i] = T;
+    b.lrec[2 * (size_t)i + 1] = W;
+  } else {
+    b.sA[i] = A;
+    b.sB[i] = B;
+    b.sC[i] = C;
+    b.lA[i] = T;
+    b.lB[i] = W;
+  }
+  b.clamped[i] = u & 7u;
+  b.dkey[i] = u;
+  b.radii[i] = u >> 20;
+  b.tb[i] = u >> 3;
+  b.ntouch[i] = 0u;
+  b.gflag[i] = 0;
+}
+
+__global__ __launch_bounds__(64) void k_writes(int P, Bufs b) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= P) return;
+  const uint32_t u = (uint32_t)i * 2654435761u;
+  const float f = __uint_as_float(u & 0x3FFFFFFFu);
+  b.splat[3 * (size_t)i] = make_float4(f, f, f, f);
+  b.splat[3 * (size_t)i + 1] = make_float4(f, f, 1.f, 0.f);
+  b.splat[3 * (size_t)i + 2] = make_float4(f, 2.f, f, f);
+  b.lrec[2 * (size_t)i] = make_uint4(u, u, u, u);
+  b.lrec[2 * (size_t)i + 1] = make_uint4(u, 1u, u, 2u);
+  b.clamped[i] = u & 7u;
+  b.dkey[i] = u;
+  b.radii[i] = u >> 20;
+  b.tb[i] = u >> 3;
+  b.ntouch[i] = 0u;
+  b.gflag[i] = 0;
+}
+
+// plain stream copy: n_in float4 read, n_out float4 written (grid-stride)
+__global__ __launch_bounds__(256) void k_copy(const float4* __restrict__ in, size_t n_in, float4* __restrict__ out,
+                                              size_t n_out) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_in; k += stride) {
+    const float4 v = in[k];
+    if (k < n_out) out[k] = v;
+    else if (v.x == 12345.f) out[0] = v;  // (keeps the load)
+  }
+}
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 1000000;
+  const int iters = 50;
+  float *means, *scales, *rots, *opac, *shs;
+  CHK(hipMalloc(&means, 12 * (size_t)P));
+  CHK(hipMalloc(&scales, 12 * (size_t)P));
+  CHK(hipMalloc(&rots, 16 * (size_t)P));
+  CHK(hipMalloc(&opac, 4 * (size_t)P));
+  CHK(hipMalloc(&shs, 4 * kNF * (size_t)P));
+  Bufs b{};
+  b.means = means; b.scales = scales; b.rots = rots; b.opac = opac; b.shs = shs;
+  CHK(hipMalloc(&b.splat, 48 * (size_t)P));
+  CHK(hipMalloc(&b.sA, 16 * (size_t)P));
+  CHK(hipMalloc(&b.sB, 16 * (size_t)P));
+  CHK(hipMalloc(&b.sC, 16 * (size_t)P));
+  CHK(hipMalloc(&b.lrec, 32 * (size_t)P));
+  CHK(hipMalloc(&b.lA, 16 * (size_t)P));
+  CHK(hipMalloc(&b.lB, 16 * (size_t)P));
+  for (uint32_t** p : {&b.clamped, &b.dkey, &b.radii, &b.tb, &b.ntouch, &b.sink}) CHK(hipMalloc(p, 4 * (size_t)P));
+  CHK(hipMalloc(&b.gflag, (size_t)P));
+  CHK(hipMemset(means, 0, 12 * (size_t)P));
+  CHK(hipMemset(scales, 0, 12 * (size_t)P));
+  CHK(hipMemset(rots, 0, 16 * (size_t)P));
+  CHK(hipMemset(opac, 0, 4 * (size_t)P));
+  CHK(hipMemset(shs, 0, 4 * kNF * (size_t)P));
+  const size_t in_bytes = 236 * (size_t)P, out_bytes = 101 * (size_t)P;
+  float4 *cin, *cout;
+  CHK(hipMalloc(&cin, in_bytes + 16));
+  CHK(hipMalloc(&cout, out_bytes + 16));
+  CHK(hipMemset(cin, 0, in_bytes + 16));
+  const dim3 g((P + 63) / 64), blk(64);
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  const char* names[] = {"shape", "soa", "rowmajor", "reads", "writes", "copy"};
+  const double bytes[] = {(double)(in_bytes + out_bytes), (double)(in_bytes + out_bytes),
+                          (double)(in_bytes + out_bytes), (double)(in_bytes + 4 * (size_t)P), (double)out_bytes,
+                          (double)(in_bytes + out_bytes)};
+  printf("{\"P\": %d, \"iters\": %d, \"kernels\": {", P, iters);
+  for (int m = 0; m < 6; ++m) {
+    auto launch = [&]() {
+      switch (m) {
+        case 0: hipLaunchKernelGGL(k_shape<0>, g, blk, 0, 0, P, b); break;
+        case 1: hipLaunchKernelGGL(k_shape<1>, g, blk, 0, 0, P, b); break;
+        case 2: hipLaunchKernelGGL(k_shape<2>, g, blk, 0, 0, P, b); break;
+        case 3: hipLaunchKernelGGL(k_shape<3>, g, blk, 0, 0, P, b); break;
+        case 4: hipLaunchKernelGGL(k_writes, g, blk, 0, 0, P, b); break;
+        default:
+          hipLaunchKernelGGL(k_copy, dim3(256 * 16), dim3(256), 0, 0, cin, in_bytes / 16, cout, out_bytes / 16);
+      }
+    };
+    for (int w = 0; w < 5; ++w) launch();
+    CHK(hipDeviceSynchronize());
+    CHK(hipEventRecord(e0, 0));
+    for (int it = 0; it < iters; ++it) launch();
+    CHK(hipEventRecord(e1, 0));
+    CHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CHK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / iters;
+    printf("%s\"%s\": {\"us\": %.2f, \"GBps\": %.0f}", m ? ", " : "", names[m], us, bytes[m] / (us * 1e3));
+  }
+  printf("}}\n");
+  return 0;
+}
