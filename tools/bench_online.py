@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--refine-iters", type=int, default=300, help="final_refine iterations after the last keyframe")
     ap.add_argument("--no-deform", action="store_true", help="skip the per-keyframe pose updates / map deformation")
+    ap.add_argument("--phases", action="store_true", help="time the insertion / deformation phases (synchronised)")
     a = ap.parse_args()
     from diff_gaussian_rasterization import _C
     from wgsr.camera import PinholeCamera
@@ -120,6 +121,8 @@ def main():
     m.initialize(kfs[:a.init_keyframes], iters=a.init_iters)
     torch.cuda.synchronize()
     t_init = time.perf_counter() - t0
+    if a.phases:
+        m.phase_ms = {}
     ins_ms, it_ms, its = [], 0.0, 0
     deform_ms, deform_kfs = [], 0
 
@@ -146,11 +149,7 @@ def main():
             deform_ms.append(1e3 * (time.perf_counter() - t0))
             deform_kfs += moved
         t0 = time.perf_counter()
-        vis = m.visibility(kf)
-        m.keyframes[kf.uid] = kf
-        m.window = m._add_to_window(kf.uid, vis, m.window)
-        m._add_points(kf, init=False)
-        m._new_exposure_optimizer()
+        m.prepare_keyframe(kf)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         split = m.map_opt_online(m.window, a.iters)
@@ -188,6 +187,7 @@ def main():
         "keyframes_deformed_per_call": (deform_kfs / len(deform_ms)) if deform_ms else None,
         "final_refine_iterations": a.refine_iters, "ms_per_final_refine_iteration": refine_ms,
         "init_seconds": t_init, "gaussians_final": m.ms.P,
+        "phase_ms_mean": ({k: sum(v) / len(v) for k, v in m.phase_ms.items()} if m.phase_ms is not None else None),
         "events": [(i, k, v) for i, k, v in m.events][:40],
         "psnr_db_mean": sum(ps) / len(ps), "psnr_db_per_keyframe": ps,
         "graph": (dict(m.graphs.stats, cap=m.graphs.cap, disabled=m.graphs.disabled) if m.graphs is not None

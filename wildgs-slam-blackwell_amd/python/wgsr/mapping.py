@@ -219,6 +219,19 @@ class MappingStep:
         self._skip = getattr(self, "_skip", set()) | {"opacity"}
 
     # -----------------------------------------------------------------------
+    def activated(self) -> dict:
+        """The activated opacity / scales / rotations (get_opacity, get_scaling,
+        get_rotation; the activation kernel the render path uses) -> self.act."""
+        L = _lib.load()
+        dev = self.xyz.device
+        p = _lib.ptr
+        a = self.act
+        with torch.cuda.device(dev):
+            _lib.check(L.wgsr_gaussian_activate(self.P, p(self.opacity), p(self.scaling), p(self.rotation),
+                                                p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
+                                                p(self.iso_part), _lib.stream_handle(dev)))
+        return a
+
     def _render(self, cam: dict, H: int, W: int, bg, cap: int | None = None, counts=None):
         """Activations (+ isotropic partial sums) and the rasteriser forward
         (``cap``: the capacity-mode forward, its counts into ``counts``)."""
@@ -240,13 +253,16 @@ class MappingStep:
             cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
             self.D, cam["campos"], False, False)
 
-    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True, skip=None):
+    def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True, skip=None,
+                  stats: bool = True):
         """Rasteriser backward straight into the gradient storage, activation
         backward (isotropic term folded in), densification statistics.
         ``skip``: a capacity-mode forward's overflow word (counts[3:4]); when
         set on the device the statistics stay unchanged (that iteration has no
-        gradient).  -> (dL/dmeans2D, dL/dtau summed over P, or None without
-        need_tau)."""
+        gradient).  ``stats=False``: no densification statistics at all (the
+        reference's final_refine, mapper.py:1346-1362, never calls
+        add_densification_stats).  -> (dL/dmeans2D, dL/dtau summed over P, or
+        None without need_tau)."""
         from diff_gaussian_rasterization import _C
         L = _lib.load()
         dev = self.xyz.device
@@ -263,11 +279,17 @@ class MappingStep:
             cam["campos"], geom, nr, binning, img, False, out=out)
         dL_dmeans2D, dL_dtau = g[0], g[8]
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_gaussian_activate_backward_stats(
-                self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
-                p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
-                p(self.grad["scaling"]), p(self.grad["rotation"]), p(radii), p(dL_dmeans2D), p(self.max_radii2D),
-                p(self.xyz_gradient_accum), p(self.denom), p(skip) if skip is not None else None, st))
+            if stats:
+                _lib.check(L.wgsr_gaussian_activate_backward_stats(
+                    self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
+                    p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
+                    p(self.grad["scaling"]), p(self.grad["rotation"]), p(radii), p(dL_dmeans2D), p(self.max_radii2D),
+                    p(self.xyz_gradient_accum), p(self.denom), p(skip) if skip is not None else None, st))
+            else:
+                _lib.check(L.wgsr_gaussian_activate_backward(
+                    self.P, p(self.opacity), p(self.scaling), p(self.rotation), p(self.act_grad["opacity"]),
+                    p(self.act_grad["scales"]), p(self.act_grad["rotations"]), float(w_iso), p(self.grad["opacity"]),
+                    p(self.grad["scaling"]), p(self.grad["rotation"]), st))
         return dL_dmeans2D, (dL_dtau.sum(0) if need_tau else None)
 
     def forward_backward(self, cam: dict, gt_image, gt_depth, exposure_a, exposure_b, bg,
@@ -331,7 +353,7 @@ class MappingStep:
                                      initialization: bool = False, freeze_uncertainty_loss: bool = False,
                                      median_depth=None, iso_weight: float = 10.0, pre_exposed: bool = True,
                                      cap: int | None = None, counts=None, need_tau: bool = True,
-                                     exposure_partials: bool = False):
+                                     exposure_partials: bool = False, stats: bool = True):
         """The reference's DEFAULT mapping iteration (uncertainty_params.activate):
         get_loss_mapping_uncertainty (slam_utils.py:146-258) + 10 * isotropic
         loss, and their backward.
@@ -361,7 +383,8 @@ class MappingStep:
         ``counts``: the capacity-mode forward (no host wait; graph capture,
         wgsr.online).  ``exposure_partials``: the exposure gradient as the loss
         backward's per-block (a, b) partial sums (``dexposure_partials``
-        [n, 2], for wgsr_exposure_step) instead of its sum.  Returns the dict of
+        [n, 2], for wgsr_exposure_step) instead of its sum.  ``stats=False``:
+        no densification statistics (final_refine).  Returns the dict of
         ``forward_backward`` plus ``uncertainty_grad`` and ``uncertainty_loss``."""
         from . import uncertainty as U
         cfg = U.flatten_config(config)
@@ -375,7 +398,7 @@ class MappingStep:
                                      median_depth, extra=(self.iso_part, w_iso), pre_exposed=pre_exposed)
         d_image, d_depth, d_a, d_b, d_unc = U.loss_backward(state, exposure_partials=exposure_partials)
         _, tau = self._backward(cam, bg, fwd, d_image, d_depth, w_iso, need_tau,
-                                skip=counts[3:4] if cap is not None else None)
+                                skip=counts[3:4] if cap is not None else None, stats=stats)
         if uncertainty.requires_grad and not freeze_uncertainty_loss:
             uncertainty.backward(d_unc.to(uncertainty.dtype))
         if exposure_partials:

@@ -76,7 +76,8 @@ DEFAULT_CONFIG = {
     "position_lr_max_steps": 30000, "feature_lr": 0.0025, "opacity_lr": 0.05, "scaling_lr": 0.001,
     "rotation_lr": 0.001, "percent_dense": 0.01, "densify_grad_threshold": 0.0002, "spatial_lr_scale": 6.0,
     "train_frac_fix": 0.3, "reg_stride": 2, "reg_mult": 0.5, "uncer_lr": 0.0004, "uncer_weight_decay": 0.00001,
-    "exposure_lr": 0.01,
+    "exposure_lr": 0.01, "edge_threshold": 4.0, "lr_cam_rot_delta": 0.003, "lr_cam_trans_delta": 0.001,
+    "tracking_itr_num": 100,
 }
 
 
@@ -178,6 +179,8 @@ class OnlineMapper:
         self.iterations_after_densify_or_reset = 0
         self.bg = torch.zeros(3, device=self.dev)
         self.events = []  # (iteration, "densify" | "reset", details)
+        self.last_removed = None  # keyframe the last window update dropped
+        self.phase_ms = None      # {phase: [ms, ...]} when prepare_keyframe / update_keyframes are timed
 
     # ---- Gaussians from a keyframe (gaussian_model.py:108-226) ---------------
     @staticmethod
@@ -243,8 +246,8 @@ class OnlineMapper:
         opac = torch.log(torch.full((xyz.shape[0], 1), 0.5, device=self.dev) / (1 - 0.5))  # inverse_sigmoid(0.5)
         return xyz, feats, scales, rots, opac
 
-    def _add_points(self, kf: Keyframe, init: bool):
-        xyz, feats, scales, rots, opac = self.keyframe_points(kf, init)
+    def _add_points(self, kf: Keyframe, init: bool, keep=None):
+        xyz, feats, scales, rots, opac = self.keyframe_points(kf, init, keep=keep)
         if self.ms is None:
             e = lambda *s: torch.empty(*s, device=self.dev)  # noqa: E731
             self.ms = MappingStep(e(0, 3), e(0, 1, 3), e(0, self.M - 1, 3), e(0, 1), e(0, 3), e(0, 4), self.D,
@@ -270,27 +273,36 @@ class OnlineMapper:
         self.occ_vis = {k: self.visibility(self.keyframes[k]) for k in window}
 
     def _add_to_window(self, cur, cur_vis, window):
-        """MonoGS window update (mapper.py:648-706)."""
+        """MonoGS window update (mapper.py:648-706) -> (window, removed uid or
+        None).  The overlap ratios (Szymkiewicz-Simpson: |cur & k| / min(|cur|,
+        |k|), fp32 as torch's int / int division) of every candidate come from
+        one device pass with one read-back; the inverse-distance eviction uses
+        fp32 getWorld2View2 poses and fp32 4x4 inverses, as the reference.  A
+        window keyframe without an occlusion-aware visibility of the current
+        length is an error, as in the reference (a shape mismatch raises)."""
         N_dont_touch = 2
         window = [cur] + window
-        to_remove = []
-        for i in range(N_dont_touch, len(window)):
-            k = window[i]
-            other = self.occ_vis.get(k)
-            if other is None or other.numel() != cur_vis.numel():
-                continue
-            inter = torch.logical_and(cur_vis, other).count_nonzero()
-            denom = min(cur_vis.count_nonzero(), other.count_nonzero())
-            ratio = inter / denom
-            if ratio <= self.cfg["kf_cutoff"]:
-                to_remove.append(k)
-        if to_remove:
-            window.remove(to_remove[-1])
+        removed = None
+        cand = window[N_dont_touch:]
+        if cand:
+            for k in cand:
+                o = self.occ_vis.get(k)
+                if o is None or o.numel() != cur_vis.numel():
+                    raise RuntimeError(f"_add_to_window: keyframe {k} has no occlusion-aware visibility of "
+                                       f"{cur_vis.numel()} Gaussians")
+            occ = torch.stack([self.occ_vis[k].reshape(-1) for k in cand]).bool()
+            cv = cur_vis.reshape(-1).bool()
+            counts = torch.cat([(occ & cv).sum(1), occ.sum(1), cv.sum().reshape(1)]).cpu().numpy()
+            n = len(cand)
+            inter, nk, nc = counts[:n], counts[n:2 * n], counts[2 * n]
+            ratio = inter.astype(np.float32) / np.minimum(nc, nk).astype(np.float32)
+            to_remove = [k for k, r in zip(cand, ratio) if r <= np.float32(self.cfg["kf_cutoff"])]
+            if to_remove:
+                window.remove(to_remove[-1])
+                removed = to_remove[-1]
 
         def w2c(kf):
-            m = torch.eye(4, dtype=torch.float64)
-            m[:3, :3], m[:3, 3] = kf.R.double().cpu(), kf.T.double().cpu()
-            return m
+            return get_world2view2(kf.R.float().cpu(), kf.T.float().cpu())
         kf0_wc = torch.linalg.inv(w2c(self.keyframes[cur]))
         if len(window) > self.cfg["window_size"]:
             inv_dist = []
@@ -302,10 +314,11 @@ class OnlineMapper:
                         continue
                     t = ki_cw @ torch.linalg.inv(w2c(self.keyframes[window[j]]))
                     d.append(1.0 / (torch.norm(t[0:3, 3]) + 1e-6).item())
-                k = math.sqrt(torch.norm((ki_cw @ kf0_wc)[0:3, 3]).item())
+                k = torch.sqrt(torch.norm((ki_cw @ kf0_wc)[0:3, 3])).item()
                 inv_dist.append(k * sum(d))
-            window.remove(window[N_dont_touch + int(np.argmax(inv_dist))])
-        return window
+            removed = window[N_dont_touch + int(np.argmax(inv_dist))]
+            window.remove(removed)
+        return window, removed
 
     def _perm(self, n: int, k: int | None = None) -> torch.Tensor:
         """The DINO term's feature sampling draw (the reference's
@@ -440,7 +453,8 @@ class OnlineMapper:
         ms.optimizer_step()
         ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
                                  lr_delay_mult=c["position_lr_delay_mult"], max_steps=c["position_lr_max_steps"])
-        self._exposure_step(kf, out)
+        if not initialization:  # (the initialisation loss has no exposure term: torch's Adam skips it)
+            self._exposure_step(kf, out)
         self.uopt.step()
         self.uopt.zero_grad()
         return out
@@ -498,32 +512,75 @@ class OnlineMapper:
 
     # ---- the reference's entry points ----------------------------------------
     def initialize(self, keyframes, iters: int | None = None):
-        """initialize_mapper + initialize_map_opt (mapper.py:732-1047)."""
-        c = self.cfg
+        """initialize_mapper + initialize_map_opt (mapper.py:732-1047): the
+        keyframes' points (pcd_downsample_init), the window in insertion order,
+        the exposure optimiser over every keyframe but 0, the initial
+        optimisation, then the window cut to its last window_size keyframes
+        (mapper.py:804-805)."""
         self.iteration_count = 0
         self.iterations_after_densify_or_reset = 0
         for kf in keyframes:
             self.keyframes[kf.uid] = kf
             self._add_points(kf, init=True)
-            self.window = [kf.uid] + self.window
+            self.window = self.window + [kf.uid]
         self._new_exposure_optimizer()
+        self.initialize_map_opt(iters)
+        self.window = self.window[-self.cfg["window_size"]:]
+
+    def initialize_map_opt(self, iters: int | None = None):
+        """Mapper.initialize_map_opt (mapper.py:922-1047) over the current
+        window: per iteration a uniformly drawn keyframe, the initialisation
+        loss (no exposure) + the strided DINO term + the isotropic term,
+        statistics, densify_and_prune (init_gaussian_th, init_gaussian_extent,
+        no size limit) every init_gaussian_update iterations from the first,
+        reset_opacity at iteration_count == init_gaussian_reset, the Adams,
+        and the keyframe's occlusion-aware visibility (n_touched > 0)."""
+        c = self.cfg
         stack = list(self.window)
         self.bank.sync(self.keyframes)
         for it in range(c["init_itr_num"] if iters is None else iters):
-            kf = self.keyframes[stack[int(self.rng.integers(len(stack)))]]
+            kf = self.keyframes[stack[int(self.rng.choice(len(stack)))]]
             update = it % c["init_gaussian_update"] == 0
             reset = "all" if self.iteration_count + 1 == c["init_gaussian_reset"] else None
             out = self._iteration(kf, [kf.uid], True, update, reset)
-            self.occ_vis[kf.uid] = (out["radii"] > 0).long()  # (n_touched > 0 in the reference)
+            self.occ_vis[kf.uid] = (out["n_touched"] > 0).long()
+        self._settle_replays()
 
-    def insert_keyframe(self, kf: Keyframe, iters: int | None = None):
-        """The Mapper's per-keyframe work (mapper.py:153-266)."""
+    def prepare_keyframe(self, kf: Keyframe, keep=None):
+        """The per-keyframe work before the mapping iterations
+        (mapper.py:198-241): the visibility render, the window update, the
+        keyframe's points, a fresh exposure optimiser -> the number of
+        Gaussians added.  With ``self.phase_ms`` a dict, each phase is timed
+        (device-synchronised) into it."""
+        import time
+        tm = self.phase_ms
+
+        def mark(name, t0):
+            if tm is None:
+                return 0.0
+            torch.cuda.synchronize(self.dev)
+            t1 = time.perf_counter()
+            if name:
+                tm.setdefault(name, []).append(1e3 * (t1 - t0))
+            return t1
+        t = mark(None, 0.0)
         vis = self.visibility(kf)
+        t = mark("visibility", t)
         self.keyframes[kf.uid] = kf
         self.bank.sync(self.keyframes)
-        self.window = self._add_to_window(kf.uid, vis, self.window)
-        added = self._add_points(kf, init=False)
+        t = mark("bank_sync", t)
+        self.window, self.last_removed = self._add_to_window(kf.uid, vis, self.window)
+        t = mark("add_to_window", t)
+        added = self._add_points(kf, init=False, keep=keep)
+        t = mark("add_points", t)
         self._new_exposure_optimizer()
+        mark("exposure_optimizer", t)
+        return added
+
+    def insert_keyframe(self, kf: Keyframe, iters: int | None = None, keep=None):
+        """The Mapper's per-keyframe work (mapper.py:184-266) -> the number of
+        Gaussians added.  ``keep``: the point subset (keyframe_points)."""
+        added = self.prepare_keyframe(kf, keep=keep)
         split = self.map_opt_online(self.window, self.cfg["mapping_itr_num"] if iters is None else iters)
         if split:
             self.map_opt_online(self.window, 1)
@@ -545,6 +602,11 @@ class OnlineMapper:
         is handed the keyframe's depth AFTER it was replaced by the new one
         (mapper.py:399-401 then 423-429), so its rescale factor is 1.
         Returns the number of keyframes moved."""
+        import time
+        tm = self.phase_ms
+        if tm is not None:
+            torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
         frames = []
         for k, upd in updates.items():
             w2c, depth = upd[0], upd[1]
@@ -564,11 +626,72 @@ class OnlineMapper:
             else:
                 fr["method"] = "rigid"
             frames.append(fr)
+        if tm is not None:
+            torch.cuda.synchronize(self.dev)
+            t1 = time.perf_counter()
+            tm.setdefault("uk_keyframes", []).append(1e3 * (t1 - t0))
         if deform and frames and self.ms is not None:
             K = self.keyframes[frames[0]["kf_id"]].K
             self.ms.store.update_mapping_points(frames, K)
+        if tm is not None:
+            torch.cuda.synchronize(self.dev)
+            t2 = time.perf_counter()
+            tm.setdefault("uk_deform", []).append(1e3 * (t2 - t1))
         self.bank.sync(self.keyframes)  # (the new cameras / depths into the banks)
+        if tm is not None:
+            torch.cuda.synchronize(self.dev)
+            tm.setdefault("uk_bank_sync", []).append(1e3 * (time.perf_counter() - t2))
         return len(frames)
+
+    def refine_pose_non_key_frame(self, w2c_init, image, fx: float, fy: float, cx: float, cy: float,
+                                  features=None, uncertainty_aware: bool = True, iters: int | None = None):
+        """Mapper.refine_pose_non_key_frame (mapper.py:810-917): a frame's pose
+        refined against the map -> (w2c [4, 4] fp32 on the CPU, iterations run).
+
+        As the reference: with uncertainty-aware tracking, the uncertainty MLP
+        on the frame's features (no gradient; its dropout on), clipped at 0.1
+        (+1e-3), bilinearly resized to the image, rescaled by 1 +
+        bias_factor(train_frac_fix, 0.8) about 0.1; the frame's grad mask
+        (Camera.compute_grad_mask); then up to tracking_itr_num iterations of
+        render -> get_loss_tracking -> Adam over (cam_rot_delta 0.003,
+        cam_trans_delta 0.001, exposure a / b 0.01, from zero) ->
+        update_pose, stopping once |tau| < 1e-4 (wgsr.tracking.PoseRefine: the
+        Adam step, SE3_exp update and next camera in one launch)."""
+        from .camera import get_projection_matrix2
+        from .tracking import PoseRefine, compute_grad_mask
+        c = self.cfg
+        dev = self.dev
+        img = image.to(dev, torch.float32).reshape(3, *image.shape[-2:]).contiguous()
+        H, W = int(img.shape[-2]), int(img.shape[-1])
+        uncer = self.tracking_uncertainty(features, H, W) if uncertainty_aware and features is not None else None
+        gm = compute_grad_mask(img, float(c["edge_threshold"]))
+        ms = self.ms
+        act = ms.activated()
+        praw = get_projection_matrix2(0.01, 100.0, cx, cy, fx, fy, W, H).T.contiguous().to(dev)
+        pr = PoseRefine(ms.xyz, act["opacity"], act["scales"], act["rotations"], ms.features, self.D, self.bg, praw,
+                        H, W, focal2fov(fx, W), focal2fov(fy, H), lr_rot=c["lr_cam_rot_delta"],
+                        lr_trans=c["lr_cam_trans_delta"], lr_exposure=0.01)
+        w2c = torch.as_tensor(w2c_init, dtype=torch.float32).cpu()
+        zero = torch.zeros(1, device=dev)
+        R, T, _, _, n = pr.refine(w2c[:3, :3], w2c[:3, 3], zero, zero, img, gm, uncer,
+                                  iters=c["tracking_itr_num"] if iters is None else iters)
+        out = torch.eye(4)
+        out[:3, :3], out[:3, 3] = R.cpu(), T.cpu()
+        return out, n
+
+    @torch.no_grad()
+    def tracking_uncertainty(self, features, H: int, W: int):
+        """The frame's uncertainty for pose refinement (mapper.py:837-849): the
+        MLP (dropout on, no gradient), clip(min=0.1) + 1e-3, bilinear resize
+        to H x W, (u - 0.1) (1 + bias_factor(train_frac_fix, 0.8)) + 0.1."""
+        import torch.nn.functional as F
+
+        from .uncertainty import bias_factor
+        u = self.net(features.to(self.dev))
+        u = torch.clip(u, min=0.1) + 1e-3
+        u = F.interpolate(u.unsqueeze(0).unsqueeze(0), size=(H, W), mode="bilinear").squeeze()
+        rate = 1 + 1 * bias_factor(self.cfg["train_frac_fix"], 0.8)
+        return ((u - 0.1) * rate + 0.1).contiguous()
 
     def final_refine(self, iters: int = 26000):
         """Mapper.final_refine (mapper.py:1234-1372): uniform random
@@ -576,7 +699,8 @@ class OnlineMapper:
         applied once), the uncertainty loss frozen for 200 iterations after
         the last densify / reset and the DINO term after them, the isotropic
         term; Adam for the Gaussians (no densification), the last window's
-        exposure optimizer and the MLP.  (The reference's preceding
+        exposure optimizer and the MLP; no densification statistics (the
+        reference never adds them here).  (The reference's preceding
         _update_keyframes_from_frontend is ``update_keyframes``.)"""
         c = self.cfg
         ms = self.ms
@@ -601,7 +725,7 @@ class OnlineMapper:
                 out = self._mlp_pair_loss(kf, nbrs, lambda unc: ms.forward_backward_uncertainty(
                     kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, self.bg, unc, c["train_frac_fix"],
                     c["train_frac_fix"], freeze_uncertainty_loss=False, median_depth=kf.median_depth,
-                    pre_exposed=False, need_tau=False, exposure_partials=True))
+                    pre_exposed=False, need_tau=False, exposure_partials=True, stats=False))
                 self._max_nr = max(self._max_nr, int(out["num_rendered"]))
             else:
                 unc = self.net(kf.features)
@@ -609,7 +733,8 @@ class OnlineMapper:
                 out = ms.forward_backward_uncertainty(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b,
                                                       self.bg, unc, c["train_frac_fix"], c["train_frac_fix"],
                                                       freeze_uncertainty_loss=freeze, median_depth=kf.median_depth,
-                                                      pre_exposed=False, need_tau=False, exposure_partials=True)
+                                                      pre_exposed=False, need_tau=False, exposure_partials=True,
+                                                      stats=False)
                 self._max_nr = max(self._max_nr, int(out["num_rendered"]))
                 if self.iterations_after_densify_or_reset >= 200:
                     self._dino_term(nbrs, kf)

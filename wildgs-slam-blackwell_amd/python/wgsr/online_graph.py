@@ -355,7 +355,7 @@ class IterationGraphs:
                                               u.view(h, w), c["train_frac_fix"], c["train_frac_fix"],
                                               freeze_uncertainty_loss=False, median_depth=S.med,
                                               pre_exposed=not refine, cap=self.cap, counts=self.counts,
-                                              need_tau=False, exposure_partials=True)
+                                              need_tau=False, exposure_partials=True, stats=not refine)
         du = out["uncertainty_grad"].reshape(-1).contiguous()
         if ns > 0:
             _, gu = dino_reg_raw(u2, sf, want_loss=False)
