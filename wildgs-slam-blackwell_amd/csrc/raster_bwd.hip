@@ -69,6 +69,11 @@ __device__ __forceinline__ void record_sums(const float4& A, const float4& B, fl
 // the quadrants the splat can reach (wave-uniform branches) -- the culling of
 // the 4-wave layout -- but sums all of them with ONE wave reduction and writes
 // the record without a cross-wave combine.
+// Measured (round 5, 1M/1080p, rocprof): reducing two hit entries' sums
+// together with wave_sum20 (42 instead of 2 x 23 VALU) costs 10 more VGPRs
+// held across the walk -- 326 us with 5 spilled VGPRs at 4 waves/SIMD, 350 us
+// at 3 waves/SIMD, vs 311 us for one wave_sum10 per entry (3 waves/SIMD with
+// this code: 313 us).
 // kBg = false: a black background (the mapper's default), whose term
 // -T_final (bg . dL/dpixel) / (1 - alpha) of dL/dalpha is zero -- one packed
 // multiply and a register move fewer per evaluation

@@ -50,16 +50,31 @@ def get_projection_matrix2(znear, zfar, cx, cy, fx, fy, W, H) -> torch.Tensor:
     right = znear / fx * right
     top = znear / fy * top
     bottom = znear / fy * bottom
-    P = torch.zeros(4, 4)
     z_sign = 1.0
-    P[0, 0] = 2.0 * znear / (right - left)
-    P[1, 1] = 2.0 * znear / (top - bottom)
-    P[0, 2] = (right + left) / (right - left)
-    P[1, 2] = (top + bottom) / (top - bottom)
-    P[3, 2] = z_sign
-    P[2, 2] = z_sign * zfar / (zfar - znear)
-    P[2, 3] = -(zfar * znear) / (zfar - znear)
-    return P
+    # (the entries in double, each rounded to fp32 once: as the reference's
+    # element assignments into a zero fp32 tensor; one tensor construction)
+    return torch.tensor([[2.0 * znear / (right - left), 0.0, (right + left) / (right - left), 0.0],
+                         [0.0, 2.0 * znear / (top - bottom), (top + bottom) / (top - bottom), 0.0],
+                         [0.0, 0.0, z_sign * zfar / (zfar - znear), -(zfar * znear) / (zfar - znear)],
+                         [0.0, 0.0, z_sign, 0.0]], dtype=torch.float32)
+
+
+def raster_fields_batched(R: torch.Tensor, T: torch.Tensor, fx, fy, cx, cy, W: int, H: int, znear: float = 0.01,
+                          zfar: float = 100.0) -> dict:
+    """PinholeCamera.raster_fields of n cameras sharing intrinsics in one
+    pass: R [n, 3, 3], T [n, 3] -> viewmatrix / projmatrix [n, 4, 4],
+    projmatrix_raw [4, 4], campos [n, 3].  The same operations batched
+    (torch's batched 4x4 inverses and products on the CPU give the
+    per-camera results bit for bit; tests/test_camera_host.py)."""
+    n = R.shape[0]
+    Rt = torch.zeros((n, 4, 4), dtype=torch.float32)
+    Rt[:, :3, :3] = R
+    Rt[:, :3, 3] = T
+    Rt[:, 3, 3] = 1.0
+    wv = torch.linalg.inv(torch.linalg.inv(Rt)).transpose(1, 2)
+    proj = get_projection_matrix2(znear, zfar, cx, cy, fx, fy, W, H).transpose(0, 1)
+    return dict(viewmatrix=wv, projmatrix=wv.bmm(proj.unsqueeze(0).expand(n, 4, 4)), projmatrix_raw=proj,
+                campos=wv.inverse()[:, 3, :3])
 
 
 def skew(x: torch.Tensor) -> torch.Tensor:
@@ -139,16 +154,19 @@ class PinholeCamera:
 
     def raster_fields(self) -> dict:
         """The camera-derived ``GaussianRasterizationSettings`` fields
-        (gaussian_renderer/__init__.py:55-72)."""
+        (gaussian_renderer/__init__.py:55-72); the properties' operations,
+        each matrix formed once."""
+        wv = self.world_view_transform
+        proj = self.projection_matrix
         return dict(
             image_height=int(self.H),
             image_width=int(self.W),
             tanfovx=math.tan(self.FoVx * 0.5),
             tanfovy=math.tan(self.FoVy * 0.5),
-            viewmatrix=self.world_view_transform,
-            projmatrix=self.full_proj_transform,
-            projmatrix_raw=self.projection_matrix,
-            campos=self.camera_center,
+            viewmatrix=wv,
+            projmatrix=wv.unsqueeze(0).bmm(proj.unsqueeze(0)).squeeze(0),
+            projmatrix_raw=proj,
+            campos=wv.inverse()[3, :3],
         )
 
 

@@ -197,9 +197,7 @@ class MappingStep:
     # densification (GaussianModel, gaussian_model.py:231-269, 389-402, 646-743)
     def extend(self, xyz, features, scaling, rotation, opacity, kf_id=None):
         """extend_from_pcd (gaussian_model.py:231-259): features [n, M, 3]."""
-        n = xyz.shape[0]
-        kf = None if kf_id is None else torch.full((n,), int(kf_id), dtype=torch.int32)
-        self.store.append(xyz, features, opacity, scaling, rotation, kf_id=kf)
+        self.store.append(xyz, features, opacity, scaling, rotation, kf_id=None if kf_id is None else int(kf_id))
 
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, percent_dense=0.01, z=None,
                           generator=None):

@@ -128,15 +128,20 @@ class Keyframe:
 
     def w2c(self) -> torch.Tensor:
         """[4, 4] fp32 world->camera (mapper.py:387-389)."""
-        m = torch.eye(4)
-        m[:3, :3], m[:3, 3] = self.R.float().cpu(), self.T.float().cpu()
-        return m
+        m = np.eye(4, dtype=np.float32)
+        m[:3, :3], m[:3, 3] = self.R.float().cpu().numpy(), self.T.float().cpu().numpy()
+        return torch.from_numpy(m)
 
-    def update_RT(self, R, T):
-        """Camera.update_RT (camera_utils.py:153-155) + the raster fields."""
+    def update_RT(self, R, T, upload: bool = True):
+        """Camera.update_RT (camera_utils.py:153-155) + the raster fields.
+        ``upload=False``: only the pose; the caller forms and uploads the
+        raster fields of several keyframes at once
+        (OnlineMapper._upload_cameras)."""
         self.R, self.T = torch.as_tensor(R).float().cpu(), torch.as_tensor(T).float().cpu()
-        dev = self.image.device
+        if not upload:
+            return
         pc = PinholeCamera(R=self.R, T=self.T, fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy, W=self.W, H=self.H)
+        dev = self.image.device
         self.cam = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in pc.raster_fields().items()}
 
     @property
@@ -214,22 +219,45 @@ class OnlineMapper:
         this mapper's generator."""
         from simple_knn._C import distCUDA2
         c = self.cfg
+        mark = self._phase("kp_start")
         ds = c["pcd_downsample_init"] if init else c["pcd_downsample"]
         image_ab = torch.clamp(torch.exp(kf.exposure_a) * kf.image + kf.exposure_b, 0.0, 1.0)
         u8 = (image_ab * 255).byte()
         depth = kf.depth[0]
         point_size = c["point_size"]
-        if c["adaptive_pointsize"]:
-            point_size = min(0.05, point_size * self.np_median(depth))
         valid = (depth > 0) & (depth < 100.0)                          # depth_trunc = 100
-        v, u = torch.nonzero(valid, as_tuple=True)
-        n = v.numel()
+        # the median and the valid-pixel count in ONE read-back (np_median's
+        # arithmetic; the count sizes the nonzero below without another sync)
+        head = [valid.sum().double()]
+        if c["adaptive_pointsize"]:
+            sv = torch.sort(depth.reshape(-1).float()).values
+            N = sv.numel()
+            lo = sv[(N - 1) // 2]
+            hi = sv[N // 2] if N % 2 == 0 else lo
+            head.append(((lo + hi) / 2).double())
+        head = torch.stack(head).tolist()
+        n = int(head[0])
+        if c["adaptive_pointsize"]:
+            point_size = min(0.05, point_size * head[1])
+        mark("kp_median_count")
         if keep is None:
-            keep = torch.randperm(n, device=self.dev, generator=self.gen)[: int((1.0 / ds) * n)]
-            keep = torch.sort(keep).values
+            # a uniform int(n / ds)-subset of the valid pixels in pixel order
+            # (Open3D's random_down_sample keeps its shuffled prefix sorted):
+            # the k smallest of one random key per pixel, invalid pixels keyed
+            # above every valid one -- fixed-size device ops, no nonzero and
+            # no randperm of the n valid pixels
+            k = int((1.0 / ds) * n)
+            Wd = depth.shape[1]
+            key = torch.rand(depth.numel(), device=self.dev, generator=self.gen)
+            key = torch.where(valid.reshape(-1), key, 2.0)
+            pix = torch.sort(torch.topk(key, k, largest=False, sorted=False).indices).values
+            v, u = pix // Wd, pix % Wd
         else:
+            # the caller's subset: indices into the valid pixels (row-major)
+            v, u = torch.nonzero(valid, as_tuple=True)
             keep = torch.as_tensor(keep, device=self.dev, dtype=torch.long)
-        v, u = v[keep], u[keep]
+            v, u = v[keep], u[keep]
+        mark("kp_subset")
         z = depth[v, u].double()
         pc = torch.stack([(u.double() - kf.cx) * z / kf.fx, (v.double() - kf.cy) * z / kf.fy, z,
                           torch.ones_like(z)], 0)
@@ -239,12 +267,33 @@ class OnlineMapper:
         col = (u8[:, v, u].T.double() / 255.0).float()
         feats = torch.zeros(xyz.shape[0], self.M, 3, device=self.dev)
         feats[:, 0] = (col - 0.5) / SH_C0                               # RGB2SH
-        dist2 = torch.clamp_min(distCUDA2(xyz), 0.0000001) * point_size
+        mark("kp_points")
+        d2 = distCUDA2(xyz)
+        mark("kp_knn")
+        dist2 = torch.clamp_min(d2, 0.0000001) * point_size
         scales = torch.log(torch.sqrt(dist2))[..., None].repeat(1, 3)
         rots = torch.zeros(xyz.shape[0], 4, device=self.dev)
         rots[:, 0] = 1
         opac = torch.log(torch.full((xyz.shape[0], 1), 0.5, device=self.dev) / (1 - 0.5))  # inverse_sigmoid(0.5)
+        mark("kp_rest")
         return xyz, feats, scales, rots, opac
+
+    def _phase(self, first: str):
+        """A phase timer for ``self.phase_ms`` (device-synchronised marks);
+        a no-op unless phase timing is on."""
+        if self.phase_ms is None:
+            return lambda name: None
+        import time
+        tm = self.phase_ms
+        torch.cuda.synchronize(self.dev)
+        t = [time.perf_counter()]
+
+        def mark(name):
+            torch.cuda.synchronize(self.dev)
+            t1 = time.perf_counter()
+            tm.setdefault(name, []).append(1e3 * (t1 - t[0]))
+            t[0] = t1
+        return mark
 
     def _add_points(self, kf: Keyframe, init: bool, keep=None):
         xyz, feats, scales, rots, opac = self.keyframe_points(kf, init, keep=keep)
@@ -252,7 +301,9 @@ class OnlineMapper:
             e = lambda *s: torch.empty(*s, device=self.dev)  # noqa: E731
             self.ms = MappingStep(e(0, 3), e(0, 1, 3), e(0, self.M - 1, 3), e(0, 1), e(0, 3), e(0, 4), self.D,
                                   lr=self.lr, capacity=1 << 16)
+        mark = self._phase("extend")
         self.ms.extend(xyz, feats, scales, rots, opac, kf_id=kf.uid)
+        mark("extend")
         return xyz.shape[0]
 
     # ---- rendering helpers ---------------------------------------------------
@@ -301,21 +352,19 @@ class OnlineMapper:
                 window.remove(to_remove[-1])
                 removed = to_remove[-1]
 
-        def w2c(kf):
-            return get_world2view2(kf.R.float().cpu(), kf.T.float().cpu())
-        kf0_wc = torch.linalg.inv(w2c(self.keyframes[cur]))
         if len(window) > self.cfg["window_size"]:
-            inv_dist = []
-            for i in range(N_dont_touch, len(window)):
-                ki_cw = w2c(self.keyframes[window[i]])
-                d = []
-                for j in range(N_dont_touch, len(window)):
-                    if i == j:
-                        continue
-                    t = ki_cw @ torch.linalg.inv(w2c(self.keyframes[window[j]]))
-                    d.append(1.0 / (torch.norm(t[0:3, 3]) + 1e-6).item())
-                k = torch.sqrt(torch.norm((ki_cw @ kf0_wc)[0:3, 3])).item()
-                inv_dist.append(k * sum(d))
+            # every candidate's getWorld2View2 and its inverse once, the pair
+            # products batched (fp32, as the reference's per-pair 4x4 ops;
+            # the sums over j in the reference's order, in double)
+            ks = [cur] + window[N_dont_touch:]
+            cw = torch.stack([get_world2view2(self.keyframes[k].R.float().cpu(), self.keyframes[k].T.float().cpu())
+                              for k in ks])
+            wc = torch.linalg.inv(cw)
+            n = len(ks) - 1
+            t_ij = torch.matmul(cw[1:, None], wc[None, 1:])[:, :, 0:3, 3]          # [n, n, 3]: T_CiCj
+            inv_ij = (1.0 / (torch.linalg.vector_norm(t_ij, dim=-1) + 1e-6)).tolist()
+            k_i = torch.sqrt(torch.linalg.vector_norm(torch.matmul(cw[1:], wc[0])[:, 0:3, 3], dim=-1)).tolist()
+            inv_dist = [k_i[i] * sum(inv_ij[i][j] for j in range(n) if j != i) for i in range(n)]
             removed = window[N_dont_touch + int(np.argmax(inv_dist))]
             window.remove(removed)
         return window, removed
@@ -607,17 +656,21 @@ class OnlineMapper:
         if tm is not None:
             torch.cuda.synchronize(self.dev)
             t0 = time.perf_counter()
-        frames = []
+        frames, moved, new_depth = [], [], False
         for k, upd in updates.items():
             w2c, depth = upd[0], upd[1]
             invalid = bool(upd[2]) if len(upd) > 2 else False
             kf = self.keyframes[k]
             w2c = torch.as_tensor(w2c, dtype=torch.float32).cpu()
             w2c_old = kf.w2c()
-            if torch.allclose(w2c_old, w2c, atol=1e-6) and depth is None:
+            # torch.allclose(w2c_old, w2c, atol=1e-6) (|a - b| <= atol + rtol |b|,
+            # rtol 1e-5), evaluated in numpy: ~15x cheaper on the host
+            if depth is None and np.allclose(w2c_old.numpy(), w2c.numpy(), rtol=1e-5, atol=1e-6):
                 continue
-            kf.update_RT(w2c[:3, :3], w2c[:3, 3])
+            kf.update_RT(w2c[:3, :3], w2c[:3, 3], upload=False)
+            moved.append(kf)
             if depth is not None:
+                new_depth = True
                 kf.depth = depth.to(kf.image.device, torch.float32).reshape(1, kf.H, kf.W).contiguous()
                 kf.median_depth = kf.depth.median()
             fr = {"kf_id": k, "w2c": w2c, "w2c_old": w2c_old}
@@ -626,6 +679,7 @@ class OnlineMapper:
             else:
                 fr["method"] = "rigid"
             frames.append(fr)
+        in_bank = self._upload_cameras(moved)
         if tm is not None:
             torch.cuda.synchronize(self.dev)
             t1 = time.perf_counter()
@@ -637,11 +691,49 @@ class OnlineMapper:
             torch.cuda.synchronize(self.dev)
             t2 = time.perf_counter()
             tm.setdefault("uk_deform", []).append(1e3 * (t2 - t1))
-        self.bank.sync(self.keyframes)  # (the new cameras / depths into the banks)
+        if new_depth or not in_bank:
+            self.bank.sync(self.keyframes)  # (new depths, or cameras outside the banks)
         if tm is not None:
             torch.cuda.synchronize(self.dev)
             tm.setdefault("uk_bank_sync", []).append(1e3 * (time.perf_counter() - t2))
         return len(frames)
+
+    def _upload_cameras(self, kfs) -> bool:
+        """The new raster fields (Keyframe.update_RT(upload=False)) of several
+        keyframes in ONE host->device copy, written straight into their rows
+        of the keyframe bank when it holds cameras (the Keyframes' fields
+        rebound to them); else the Keyframes keep views of the staging copy.
+        -> whether every camera went into the bank."""
+        from .camera import raster_fields_batched
+        from .online_graph import CAM_FLOATS
+        if not kfs:
+            return True
+        host = torch.zeros(len(kfs), CAM_FLOATS)
+        groups: dict = {}   # keyframes sharing intrinsics: one batched formation each
+        for i, kf in enumerate(kfs):
+            groups.setdefault((kf.fx, kf.fy, kf.cx, kf.cy, kf.W, kf.H), []).append(i)
+        for (fx, fy, cx, cy, W, H), idx in groups.items():
+            f = raster_fields_batched(torch.stack([kfs[i].R for i in idx]), torch.stack([kfs[i].T for i in idx]),
+                                      fx, fy, cx, cy, W, H)
+            rows = torch.tensor(idx)
+            host[rows, 0:16] = f["viewmatrix"].reshape(-1, 16)
+            host[rows, 16:32] = f["projmatrix"].reshape(-1, 16)
+            host[rows, 32:48] = f["projmatrix_raw"].reshape(1, 16)
+            host[rows, 48:51] = f["campos"]
+        dev = host.to(self.dev)
+        for i, kf in enumerate(kfs):
+            c = dev[i]
+            kf.cam = dict(kf.cam, viewmatrix=c[0:16].view(4, 4), projmatrix=c[16:32].view(4, 4),
+                          projmatrix_raw=c[32:48].view(4, 4), campos=c[48:51])
+        b = self.bank
+        if not (b.uniform and b.cam is not None and all(b.kfs.get(kf.uid) is kf for kf in kfs)):
+            return False
+        rows = torch.tensor([b.slots[kf.uid] for kf in kfs]).to(self.dev)
+        with torch.no_grad():
+            b.cam.index_copy_(0, rows, dev)
+        for kf in kfs:
+            b._bind(kf.uid, kf)
+        return True
 
     def refine_pose_non_key_frame(self, w2c_init, image, fx: float, fy: float, cx: float, cy: float,
                                   features=None, uncertainty_aware: bool = True, iters: int | None = None):

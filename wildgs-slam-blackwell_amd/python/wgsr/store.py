@@ -25,6 +25,7 @@ from __future__ import annotations
 import ctypes
 import math
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -41,21 +42,32 @@ def rotation_matrix_to_quaternion(R: torch.Tensor) -> torch.Tensor:
     """general_utils.rotation_matrix_to_quaternion (general_utils.py:138-162),
     op for op in fp32: [B, >=3, >=3] -> [B, 4] (w, x, y, z), including its sign
     rule q_i *= sign(q_i (R_kj - R_jk)) (a zero difference zeroes q_i)."""
-    z = torch.tensor(0.0, dtype=R.dtype)
-    q = torch.zeros((R.size(0), 4), dtype=R.dtype)
-    q[:, 0] = torch.sqrt(torch.max(z, 1 + R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2])) / 2
-    q[:, 1] = torch.sqrt(torch.max(z, 1 + R[:, 0, 0] - R[:, 1, 1] - R[:, 2, 2])) / 2
-    q[:, 2] = torch.sqrt(torch.max(z, 1 - R[:, 0, 0] + R[:, 1, 1] - R[:, 2, 2])) / 2
-    q[:, 3] = torch.sqrt(torch.max(z, 1 - R[:, 0, 0] - R[:, 1, 1] + R[:, 2, 2])) / 2
-    q[:, 1] *= torch.sign(q[:, 1] * (R[:, 2, 1] - R[:, 1, 2]))
-    q[:, 2] *= torch.sign(q[:, 2] * (R[:, 0, 2] - R[:, 2, 0]))
-    q[:, 3] *= torch.sign(q[:, 3] * (R[:, 1, 0] - R[:, 0, 1]))
-    return q
+    # (the sums, maxima, halvings and signs in numpy on the host tensor's
+    # dtype -- the same IEEE operations in the same order -- and each square
+    # root by torch on its [n] vector as the reference takes it (torch's CPU
+    # sqrt is not always numpy's): bit-identical to the ~20 small torch ops,
+    # in a tenth of the host time; tests/test_online_host.py)
+    r = R.detach().cpu().numpy()
+    one = r.dtype.type(1)
+    zero = r.dtype.type(0)
+    r00, r11, r22 = r[:, 0, 0], r[:, 1, 1], r[:, 2, 2]
+    q = np.empty((r.shape[0], 4), dtype=r.dtype)
+    for i, v in enumerate((one + r00 + r11 + r22, one + r00 - r11 - r22, one - r00 + r11 - r22,
+                           one - r00 - r11 + r22)):
+        q[:, i] = torch.sqrt(torch.from_numpy(np.maximum(zero, v))).numpy() / 2
+    q[:, 1] *= np.sign(q[:, 1] * (r[:, 2, 1] - r[:, 1, 2]))
+    q[:, 2] *= np.sign(q[:, 2] * (r[:, 0, 2] - r[:, 2, 0]))
+    q[:, 3] *= np.sign(q[:, 3] * (r[:, 1, 0] - r[:, 0, 1]))
+    return torch.from_numpy(q)
 
 
 def deform_transform(w2c: torch.Tensor, w2c_old: torch.Tensor):
     """(T, q) of mapper.py:449-460 / 530-545: T = inv(inv(w2c_old) @ w2c),
-    q = rotation_matrix_to_quaternion(T), fp32 on the host."""
+    q = rotation_matrix_to_quaternion(T), fp32 on the host.  Batched: [n, 4,
+    4] poses give [n, 4, 4] / [n, 4]."""
+    if w2c.dim() == 3:
+        T = torch.linalg.inv(torch.linalg.inv(w2c_old) @ w2c)
+        return T, rotation_matrix_to_quaternion(T)
     T = torch.linalg.inv(torch.linalg.inv(w2c_old) @ w2c)
     return T, rotation_matrix_to_quaternion(T.unsqueeze(0))[0]
 
@@ -182,8 +194,14 @@ class GaussianStore:
             b[name][P:P + n].copy_(t.detach().reshape(self._shape(name, n)))
             b["m_" + name][P:P + n].zero_()
             b["v_" + name][P:P + n].zero_()
-        b["kf_id"][P:P + n].copy_(kf_id if kf_id is not None else torch.full((n,), -1, dtype=torch.int32))
-        b["n_obs"][P:P + n].copy_(n_obs if n_obs is not None else torch.zeros(n, dtype=torch.int32))
+        if kf_id is None or isinstance(kf_id, int):   # (one id for every new row: filled on the device)
+            b["kf_id"][P:P + n].fill_(-1 if kf_id is None else kf_id)
+        else:
+            b["kf_id"][P:P + n].copy_(kf_id)
+        if n_obs is None:
+            b["n_obs"][P:P + n].zero_()
+        else:
+            b["n_obs"][P:P + n].copy_(n_obs)
         self.P = P + n
         self.zero_stats()
 
@@ -280,19 +298,22 @@ class GaussianStore:
         seen = set()
         keep = []
         Kc = None if K is None else torch.as_tensor(K, dtype=torch.float32).cpu().reshape(3, 3)
+        # every frame's transformation and quaternion in one batched host pass
+        W = torch.stack([torch.as_tensor(fr["w2c"], dtype=torch.float32).cpu().reshape(4, 4) for fr in frames])
+        Wo = torch.stack([torch.as_tensor(fr["w2c_old"], dtype=torch.float32).cpu().reshape(4, 4) for fr in frames])
+        Ts, qs = deform_transform(W, Wo)
+        Ts, qs = Ts.reshape(len(frames), 16).tolist(), qs.tolist()
         for j, fr in enumerate(frames):
             k = int(fr["kf_id"])
             if k in seen:
                 raise ValueError(f"update_mapping_points: keyframe {k} given twice")
             seen.add(k)
             method = fr.get("method") or ("rigid" if fr.get("depth") is None else "depth")
-            w2c = torch.as_tensor(fr["w2c"], dtype=torch.float32).cpu().reshape(4, 4)
-            w2c_old = torch.as_tensor(fr["w2c_old"], dtype=torch.float32).cpu().reshape(4, 4)
-            T, q = deform_transform(w2c, w2c_old)
+            w2c_old = Wo[j]
             f = arr[j]
             f.kf_id, f.method = k, (0 if method == "rigid" else 1)
-            f.T[:] = T.flatten().tolist()
-            f.q[:] = q.tolist()
+            f.T[:] = Ts[j]
+            f.q[:] = qs[j]
             if method != "rigid":
                 if Kc is None:
                     raise ValueError("update_mapping_points: the depth branch needs the intrinsics K")
