@@ -188,6 +188,10 @@ def main():
         "final_refine_iterations": a.refine_iters, "ms_per_final_refine_iteration": refine_ms,
         "init_seconds": t_init, "gaussians_final": m.ms.P,
         "phase_ms_mean": ({k: sum(v) / len(v) for k, v in m.phase_ms.items()} if m.phase_ms is not None else None),
+        "phase_ms": ({k: [round(x, 3) for x in v] for k, v in m.phase_ms.items()} if m.phase_ms is not None
+                     else None),
+        "ms_keyframe_insertion_each": [round(x, 3) for x in ins_ms],
+        "ms_deformation_call_each": [round(x, 3) for x in deform_ms],
         "events": [(i, k, v) for i, k, v in m.events][:40],
         "psnr_db_mean": sum(ps) / len(ps), "psnr_db_per_keyframe": ps,
         "graph": (dict(m.graphs.stats, cap=m.graphs.cap, disabled=m.graphs.disabled) if m.graphs is not None

@@ -537,6 +537,25 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   // list length: one cache line)
   uint4 lw = lrec[g0].w, tab = lrec[g0].tab;
   const uint32_t dk0 = pair_depth ? dkey[g0] : 0u;
+  // the block prefix's inputs, issued behind the record loads (the scans
+  // below wait for the records only; vmcnt counts in order): the earlier
+  // superblocks' sums plus the earlier blocks of its own superblock
+  uint2 pre = make_uint2(0u, 0u);
+  if (bsup) {
+    const uint32_t b = blockIdx.x, sb = b / kScanSupBlocks;
+    for (uint32_t q = (uint32_t)t; q < sb; q += kDupScanThreads) {
+      const uint2 x = bsup[(size_t)q * kScanSupStride];
+      pre.x += x.x;
+      pre.y += x.y;
+    }
+    if ((uint32_t)t < kScanSupBlocks && sb * kScanSupBlocks + t < b) {
+      const uint2 x = bsum[sb * kScanSupBlocks + t];
+      pre.x += x.x;
+      pre.y += x.y;
+    }
+  } else {
+    pre = bsum[blockIdx.x];
+  }
   const uint32_t g = in ? g0 : 0u;
   if (!in) {
     lw = make_uint4(0u, 0u, 0u, 0u);
@@ -559,23 +578,9 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   if (lane == 63) s_w[w] = make_uint2(ic, ib);
   uint2 wb;  // this block's first slot / first bin pair
   if (bsup) {
-    // exclusive prefix of the blocks before this one: the earlier
-    // superblocks' sums plus the earlier blocks of its own superblock
-    const uint32_t b = blockIdx.x, sb = b / kScanSupBlocks;
-    uint2 v = make_uint2(0u, 0u);
-    for (uint32_t q = (uint32_t)t; q < sb; q += kDupScanThreads) {
-      const uint2 x = bsup[(size_t)q * kScanSupStride];
-      v.x += x.x;
-      v.y += x.y;
-    }
-    if ((uint32_t)t < kScanSupBlocks && sb * kScanSupBlocks + t < b) {
-      const uint2 x = bsum[sb * kScanSupBlocks + t];
-      v.x += x.x;
-      v.y += x.y;
-    }
-    v.x = wave_sum_u32(v.x);
-    v.y = wave_sum_u32(v.y);
-    if (lane == 0) s_p[w] = v;
+    pre.x = wave_sum_u32(pre.x);
+    pre.y = wave_sum_u32(pre.y);
+    if (lane == 0) s_p[w] = pre;
     __syncthreads();
     wb = make_uint2(0u, 0u);
 #pragma unroll
@@ -585,7 +590,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     }
   } else {
     __syncthreads();
-    wb = bsum[blockIdx.x];
+    wb = pre;
   }
 #pragma unroll
   for (int k = 0; k < NW; ++k) {
