@@ -476,16 +476,20 @@ __device__ __forceinline__ uint32_t bin_mask_tab(int bx, int by, int x0, int y0,
   constexpr int B = 1 << S;
   const int kr0 = (by << S) - y0;  // in [-(B - 1), kRowTab - 1]
   const uint64_t L64 = ((uint64_t)tab.y << 32) | tab.x, X64 = ((uint64_t)tab.w << 32) | tab.z;
-  const uint32_t lens = kr0 >= 0 ? (uint32_t)(L64 >> (8 * kr0)) : (uint32_t)(L64 << (-8 * kr0));
-  const uint32_t xs = kr0 >= 0 ? (uint32_t)(X64 >> (8 * kr0)) : (uint32_t)(X64 << (-8 * kr0));
-  const int c0 = bx << S;
+  // branch-free: one of the two shifts is by zero
+  const uint32_t sr = 8u * (uint32_t)max(kr0, 0), sl = 8u * (uint32_t)max(-kr0, 0);
+  const uint32_t lens = (uint32_t)((L64 >> sr) << sl);
+  const uint32_t xs = (uint32_t)((X64 >> sr) << sl);
+  const int d0 = x0 - (bx << S);  // the rect's left edge relative to the bin's
   uint32_t mask = 0;
 #pragma unroll
   for (int rr = 0; rr < B; ++rr) {
-    const int len = (int)((lens >> (8 * rr)) & 0xFFu);
-    const int xa = x0 + (int)((xs >> (8 * rr)) & 0xFFu);
-    const int cl = max(xa, c0), w = max(min(xa + len, c0 + B) - cl, 0);
-    mask |= ((1u << w) - 1u) << (rr * B + cl - c0);
+    // row rr covers bin columns [lo, hi) (clamped to the bin; len >= 0 so
+    // hi >= lo, and an empty or outside row gives lo == hi)
+    const int xa = d0 + (int)((xs >> (8 * rr)) & 0xFFu);
+    const int xe = xa + (int)((lens >> (8 * rr)) & 0xFFu);
+    const int lo = min(max(xa, 0), B), hi = min(max(xe, 0), B);  // (v_med3_i32)
+    mask |= (((1u << hi) - 1u) ^ ((1u << lo) - 1u)) << (rr * B);
   }
   return mask;
 }
@@ -524,6 +528,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   __shared__ uint4 s_ra[NW][64];    // per rank: rect lo | hi, first bin pair, Gaussian
   __shared__ uint4 s_rt[NW][64];    // per rank: row table
   __shared__ uint32_t s_rd[NW][64]; // per rank: depth key
+  __shared__ uint2 s_rw[NW][64];    // per rank: bin columns of the rect, their reciprocal (float bits)
   __shared__ uint32_t s_own[NW][64];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
@@ -621,6 +626,10 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   s_ra[w][lane] = make_uint4(rlo, rhi, my_off, g);
   s_rt[w][lane] = tab;
   s_rd[w][lane] = dk;
+  {  // the rect's bin-column count and its reciprocal, once per rank
+    const int bw = (((int)(rhi & 0xFFFFu) - 1) >> bshift) - ((int)(rlo & 0xFFFFu) >> bshift) + 1;
+    s_rw[w][lane] = make_uint2((uint32_t)bw, __float_as_uint(__builtin_amdgcn_rcpf((float)bw)));
+  }
   uint32_t carry = 0;  // owner of the chunk's first pair (the first chunk: a rank starts there)
   for (uint32_t base = start; base < end; base += 64) {
     const uint32_t k = base + lane;
@@ -638,12 +647,17 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     const uint32_t gg = ra.w;
     const int x0 = (int)(ra.x & 0xFFFFu), y0 = (int)(ra.x >> 16), x1 = (int)(ra.y & 0xFFFFu), y1 = (int)(ra.y >> 16);
     const uint4 tq = s_rt[w][lo];
-    const int bx0 = x0 >> bshift, bw = ((x1 - 1) >> bshift) - bx0 + 1;
+    const uint2 rw = s_rw[w][lo];
+    const int bx0 = x0 >> bshift, bw = (int)rw.x;
     // local / bw without the integer-division sequence: local < 2^16 (a
     // Gaussian's bins), so the float estimate is within one of the quotient
-    int row = (int)((float)local * __builtin_amdgcn_rcpf((float)bw));
+    int row = (int)((float)local * __uint_as_float(rw.y));
     int col = (int)local - row * bw;
-    if (col < 0) { --row; col += bw; } else if (col >= bw) { ++row; col -= bw; }
+    {  // (selects, not branches)
+      const int dn = col < 0 ? 1 : 0, up = col >= bw ? 1 : 0;
+      row += up - dn;
+      col += (dn - up) * bw;
+    }
     const int bx = bx0 + col, by = (y0 >> bshift) + row;
     uint32_t mask;
     if (!any_tall) {  // (wave-uniform) every owner's rows sit in its row table
