@@ -143,8 +143,10 @@ def main():
         if not a.no_deform:
             # _update_keyframes_from_frontend before the insertion (mapper.py:194):
             # every existing keyframe's pose moved a little, its Gaussians deformed
+            # (the tracker's new poses, formed outside the timed call)
+            upd = {k: (nudge(k, 1.0 + 0.1 * n_kf), None) for k in list(m.keyframes)}
             t0 = time.perf_counter()
-            moved = m.update_keyframes({k: (nudge(k, 1.0 + 0.1 * n_kf), None) for k in list(m.keyframes)})
+            moved = m.update_keyframes(upd)
             torch.cuda.synchronize()
             deform_ms.append(1e3 * (time.perf_counter() - t0))
             deform_kfs += moved
@@ -190,6 +192,8 @@ def main():
         "phase_ms_mean": ({k: sum(v) / len(v) for k, v in m.phase_ms.items()} if m.phase_ms is not None else None),
         "phase_ms": ({k: [round(x, 3) for x in v] for k, v in m.phase_ms.items()} if m.phase_ms is not None
                      else None),
+        "ms_keyframe_insertion_median": (sorted(ins_ms)[len(ins_ms) // 2] if ins_ms else None),
+        "ms_deformation_call_median": (sorted(deform_ms)[len(deform_ms) // 2] if deform_ms else None),
         "ms_keyframe_insertion_each": [round(x, 3) for x in ins_ms],
         "ms_deformation_call_each": [round(x, 3) for x in deform_ms],
         "events": [(i, k, v) for i, k, v in m.events][:40],

@@ -18,6 +18,9 @@
 //              coalesced 1 KB wave store)
 //   rowmajor   soa with the SH slab loaded row-major (chunk 64 k + l of the
 //              wave's contiguous 12 KB run: coalesced 1 KB loads)
+//   rowread    rowmajor's loads with the kernel's own LDS read of a row-major
+//              slab (lane l reads chunk 12 l + k: 4-way ds_read_b128
+//              conflicts) and AoS records as in shape
 //   reads      shape's reads only (one 4-byte store per Gaussian)
 //   writes     shape's writes only (no loads but a 4-byte id)
 //   copy       a plain float4 stream copy of the same 236 B in / 101 B out
@@ -51,13 +54,13 @@ struct Bufs {
 constexpr int kNF = 48;             // SH3: 16 coefficients x 3
 constexpr int kNCH = kNF / 4;       // 16-byte chunks per row
 
-template <int kMode>  // 0 shape, 1 soa, 2 rowmajor, 3 reads
+template <int kMode>  // 0 shape, 1 soa, 2 rowmajor, 3 reads, 4 rowread
 __global__ __launch_bounds__(64) void k_shape(int P, Bufs b) {
   __shared__ float s_sh[64 * kNF];
   const int lane = threadIdx.x, i0 = blockIdx.x * 64, i = i0 + lane;
   const int ic = min(i, P - 1);
   for (int k = 0; k < kNCH; ++k) {
-    if (kMode == 2) {
+    if (kMode == 2 || kMode == 4) {
       const size_t c = min((size_t)i0 * kNCH + (size_t)(64 * k + lane), (size_t)P * kNCH - 1);
       __builtin_amdgcn_global_load_lds((const void*)(b.shs + 4 * c), (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
     } else {
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(64) void k_shape(int P, Bufs b) {
   __syncthreads();
   float col = 0.f;
   for (int k = 0; k < kNCH; ++k) {
-    const float4 v = reinterpret_cast<const float4*>(s_sh)[k * 64 + lane];
+    const float4 v = reinterpret_cast<const float4*>(s_sh)[kMode == 4 ? lane * kNCH + k : k * 64 + lane];
     col += v.x + v.y + v.z + v.w;
   }
   if (i >= P) return;
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(64) void k_shape(int P, Bufs b) {
   }
   const float4 A = make_float4(geo, col, 1.f, 2.f), B = make_float4(col, geo, 3.f, 0.f), C = make_float4(o, q.x, col, m2);
   const uint4 T = make_uint4(u, u + 1, u + 2, u + 3), W = make_uint4(u ^ 5u, u, 7u, u & 255u);
-  if (kMode == 0) {
+  if (kMode == 0 || kMode == 4) {
     b.splat[3 * (size_t)i] = A;
     b.splat[3 * (size_t)i + 1] = B;
     b.splat[3 * (size_t)i + 2] = C;
@@ -169,12 +172,12 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
-  const char* names[] = {"shape", "soa", "rowmajor", "reads", "writes", "copy"};
+  const char* names[] = {"shape", "soa", "rowmajor", "reads", "writes", "copy", "rowread"};
   const double bytes[] = {(double)(in_bytes + out_bytes), (double)(in_bytes + out_bytes),
                           (double)(in_bytes + out_bytes), (double)(in_bytes + 4 * (size_t)P), (double)out_bytes,
-                          (double)(in_bytes + out_bytes)};
+                          (double)(in_bytes + out_bytes), (double)(in_bytes + out_bytes)};
   printf("{\"P\": %d, \"iters\": %d, \"kernels\": {", P, iters);
-  for (int m = 0; m < 6; ++m) {
+  for (int m = 0; m < 7; ++m) {
     auto launch = [&]() {
       switch (m) {
         case 0: hipLaunchKernelGGL(k_shape<0>, g, blk, 0, 0, P, b); break;
@@ -182,6 +185,7 @@ int main(int argc, char** argv) {
         case 2: hipLaunchKernelGGL(k_shape<2>, g, blk, 0, 0, P, b); break;
         case 3: hipLaunchKernelGGL(k_shape<3>, g, blk, 0, 0, P, b); break;
         case 4: hipLaunchKernelGGL(k_writes, g, blk, 0, 0, P, b); break;
+        case 6: hipLaunchKernelGGL(k_shape<4>, g, blk, 0, 0, P, b); break;
         default:
           hipLaunchKernelGGL(k_copy, dim3(256 * 16), dim3(256), 0, 0, cin, in_bytes / 16, cout, out_bytes / 16);
       }

@@ -33,6 +33,23 @@ constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 #if WGSR_BWD_STATS
 __device__ unsigned long long g_bwd_stats[32];
 #endif
+// diagnostic build: per-workgroup phase clocks of k_gauss_bwd_compact summed
+// over workgroups (s_memtime; wgsr_debug_gbc_times)
+#ifndef WGSR_GBC_TIMES
+#define WGSR_GBC_TIMES 0
+#endif
+#if WGSR_GBC_TIMES
+__device__ unsigned long long g_gbc_times[16];
+#define GBC_MARK(k)                                                                    \
+  do {                                                                                 \
+    if (t == 0) {                                                                      \
+      const unsigned long long now = __builtin_amdgcn_s_memtime();                    \
+      atomicAdd(&g_gbc_times[k], now - gbc_t0);                                         \
+    }                                                                                  \
+  } while (0)
+#else
+#define GBC_MARK(k) do {} while (0)
+#endif
 // below this many tiles the backward runs k_render_bwd_seg (four waves per
 // tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
 constexpr int kBwdSplitBelowTiles = 3072;
@@ -993,6 +1010,10 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   __shared__ uint32_t s_wc[kR][NW];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int i0 = blockIdx.x * (kGbcThreads * kR);
+#if WGSR_GBC_TIMES
+  const unsigned long long gbc_t0 = __builtin_amdgcn_s_memtime();
+  if (t == 0) atomicAdd(&g_gbc_times[15], 1ull);
+#endif
   // compaction of the live Gaussians (list order = index order)
   bool live[kR];
   uint64_t bal[kR];
@@ -1022,17 +1043,30 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   if (nlive == 0) return;  // block-uniform
   __syncthreads();
+  GBC_MARK(0);  // flags loaded, list built
+#if WGSR_GBC_TIMES
+  if (t == 0) { atomicAdd(&g_gbc_times[8], 1ull); atomicAdd(&g_gbc_times[9], (unsigned long long)nlive); }
+#endif
   // record sums over the listed Gaussians' slots flattened into one list:
   // their slot ranges in one round trip, then kRecChunk slots at a time every
   // thread loads one slot's flag and record (coalesced within a range; the
   // slot's Gaussian by binary search over the range offsets) into LDS, and
   // each Gaussian's own thread sums its slots in slot order (deterministic)
+  // (measured, round 5: each live row's slot range loaded by its own thread
+  // during the compaction instead of this gather: the mean workgroup's clocks
+  // -8 % (WGSR_GBC_TIMES) but the kernel 58.3 vs 57.8 us -- its time is the
+  // slowest workgroups', the ones with the most record slots; loading every
+  // row's range instead reads all of the 32-byte list records: 62 us)
   for (uint32_t c = t; c < nlive; c += kGbcThreads) {
     const uint32_t gi = s_list[c];
     s_s0[c] = slot_start[gi];
     s_n[c] = lrec[gi].w.w;
+#if WGSR_GBC_TIMES
+    atomicMax(&g_gbc_times[14], (unsigned long long)s_n[c]);
+#endif
   }
   __syncthreads();
+  GBC_MARK(1);  // slot ranges loaded
   {
     uint32_t v[kR], loc = 0;
 #pragma unroll
@@ -1054,6 +1088,10 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   }
   __syncthreads();
   const uint32_t total = s_off[nlive];
+  GBC_MARK(2);  // scanned
+#if WGSR_GBC_TIMES
+  if (t == 0) atomicAdd(&g_gbc_times[10], (unsigned long long)total);
+#endif
   float acc[kR][10];
 #pragma unroll
   for (int r = 0; r < kR; ++r)
@@ -1114,6 +1152,13 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     }
     __syncthreads();
   }
+  GBC_MARK(3);  // records summed
+#if WGSR_GBC_TIMES
+  if (t == 0) {
+    atomicMax(&g_gbc_times[11], __builtin_amdgcn_s_memtime() - gbc_t0);   // slowest to here
+    atomicMax(&g_gbc_times[12], (unsigned long long)total);               // most slots
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < kR; ++r) {
     const uint32_t c = r * kGbcThreads + t;
@@ -1136,6 +1181,11 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     gauss_bwd_one(i, g, means, scales, rots, cov_pre, dm_sh, scale_mod, viewm, projm, praw, W, H, tanx, tany, o_m2d,
                   o_col, o_opac, o_m3d, o_cov, o_sc, o_rot, o_tau);
   }
+#if WGSR_GBC_TIMES
+  __syncthreads();
+  GBC_MARK(4);  // every listed Gaussian's backward done
+  if (t == 0) atomicMax(&g_gbc_times[13], __builtin_amdgcn_s_memtime() - gbc_t0);
+#endif
 }
 
 // ---- view-sharded backward (wgsr/dp.py) ---------------------
@@ -1385,6 +1435,20 @@ hipError_t launch_gauss_bwd_views(const wgsr_raster_args& a, int lo, int hi, int
 
 }  // namespace wgsr
 
+#if WGSR_GBC_TIMES
+// diagnostic build only: read and clear k_gauss_bwd_compact's phase clocks
+// [0..4] cumulative s_memtime since the workgroup's start at each phase end,
+// summed over workgroups with work; [8] such workgroups, [9] listed
+// Gaussians, [10] record slots, [11] / [13] the slowest workgroup's clocks
+// to the record sums' end / its end, [12] the most slots in one workgroup,
+// [14] the largest slot range of one Gaussian, [15] workgroups launched
+extern "C" int wgsr_debug_gbc_times(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_gbc_times), sizeof(unsigned long long) * 16) != hipSuccess)
+    return 1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_gbc_times), z, sizeof(z)) != hipSuccess;
+}
+#endif
 #if WGSR_BWD_STATS
 // diagnostic build only: read and clear the quad backward's entry histogram
 extern "C" int wgsr_debug_bwd_stats(unsigned long long* out) {

@@ -242,9 +242,12 @@ constexpr int kPreWave = 64;
 // colour -- for visible Gaussians only.  Measured alternatives (round 4,
 // removed in round 5; all bit-identical): the slab staged before the geometry
 // (k_preprocess, 90 us when this one was 86), SH coefficients in VGPRs (150
-// vs 103 us), the coalesced row-major slab (112 vs 102), one memory round
-// trip per wave (106.7 vs 103.4), records staged through LDS for contiguous
-// stores (115.8 vs 106.7).
+// vs 103 us), the coalesced row-major slab (112 vs 102; round 5 again with
+// the twelve 1 KB loads unrolled at compile time for SH3 rows: 109.3 vs
+// 102.5 us, although tools/ubench/pre_copy.hip's copy of this access shape
+// runs 62 us row-major -- LDS read conflicts included -- vs 92 chunk-major),
+// one memory round trip per wave (106.7 vs 103.4), records staged through
+// LDS for contiguous stores (115.8 vs 106.7).
 template <int kD, int kCh>
 __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lane, f3 dir, uint32_t& cbits) {
   constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, NCH = (NF + kCh - 1) / kCh;

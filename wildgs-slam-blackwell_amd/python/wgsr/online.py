@@ -243,14 +243,19 @@ class OnlineMapper:
         if keep is None:
             # a uniform int(n / ds)-subset of the valid pixels in pixel order
             # (Open3D's random_down_sample keeps its shuffled prefix sorted):
-            # the k smallest of one random key per pixel, invalid pixels keyed
-            # above every valid one -- fixed-size device ops, no nonzero and
-            # no randperm of the n valid pixels
+            # the k smallest of one random key per pixel (invalid pixels keyed
+            # above every valid one), marked in a pixel mask and read back in
+            # pixel order.  Every kernel's input has the frame's size whatever
+            # k is, so the initial keyframes load them all (a top-k / sort of k
+            # elements loaded new kernels at the first insertion: 45 ms)
             k = int((1.0 / ds) * n)
             Wd = depth.shape[1]
-            key = torch.rand(depth.numel(), device=self.dev, generator=self.gen)
+            HW = depth.numel()
+            key = torch.rand(HW, device=self.dev, generator=self.gen)
             key = torch.where(valid.reshape(-1), key, 2.0)
-            pix = torch.sort(torch.topk(key, k, largest=False, sorted=False).indices).values
+            sel = torch.zeros(HW, dtype=torch.bool, device=self.dev)
+            sel[torch.sort(key).indices[:k]] = True
+            pix = torch.nonzero_static(sel, size=k).reshape(-1)
             v, u = pix // Wd, pix % Wd
         else:
             # the caller's subset: indices into the valid pixels (row-major)
@@ -575,6 +580,18 @@ class OnlineMapper:
         self._new_exposure_optimizer()
         self.initialize_map_opt(iters)
         self.window = self.window[-self.cfg["window_size"]:]
+        self._warm_deformation()
+
+    def _warm_deformation(self):
+        """One no-op pass of the map deformation (a keyframe id no Gaussian
+        carries, identity poses) while the mapper initialises: its kernels and
+        host ops are loaded here instead of in the first pose update of the
+        live loop (~1 ms once)."""
+        if self.ms is None or self.ms.P == 0 or not self.keyframes:
+            return
+        ghost = max(self.keyframes) + 1
+        self.ms.store.update_mapping_points([{"kf_id": ghost, "w2c": torch.eye(4), "w2c_old": torch.eye(4),
+                                              "method": "rigid"}], self.keyframes[self.window[-1]].K)
 
     def initialize_map_opt(self, iters: int | None = None):
         """Mapper.initialize_map_opt (mapper.py:922-1047) over the current
@@ -663,10 +680,12 @@ class OnlineMapper:
             kf = self.keyframes[k]
             w2c = torch.as_tensor(w2c, dtype=torch.float32).cpu()
             w2c_old = kf.w2c()
-            # torch.allclose(w2c_old, w2c, atol=1e-6) (|a - b| <= atol + rtol |b|,
-            # rtol 1e-5), evaluated in numpy: ~15x cheaper on the host
-            if depth is None and np.allclose(w2c_old.numpy(), w2c.numpy(), rtol=1e-5, atol=1e-6):
-                continue
+            # torch.allclose(w2c_old, w2c, atol=1e-6): |a - b| <= atol + rtol |b|
+            # (rtol 1e-5), on the host arrays (a tenth of torch.allclose's time)
+            if depth is None:
+                a_, b_ = w2c_old.numpy(), w2c.numpy()
+                if (np.abs(a_ - b_) <= 1e-6 + 1e-5 * np.abs(b_)).all():
+                    continue
             kf.update_RT(w2c[:3, :3], w2c[:3, 3], upload=False)
             moved.append(kf)
             if depth is not None:
@@ -708,32 +727,37 @@ class OnlineMapper:
         from .online_graph import CAM_FLOATS
         if not kfs:
             return True
-        host = torch.zeros(len(kfs), CAM_FLOATS)
         groups: dict = {}   # keyframes sharing intrinsics: one batched formation each
         for i, kf in enumerate(kfs):
             groups.setdefault((kf.fx, kf.fy, kf.cx, kf.cy, kf.W, kf.H), []).append(i)
+        parts, order = [], []
         for (fx, fy, cx, cy, W, H), idx in groups.items():
             f = raster_fields_batched(torch.stack([kfs[i].R for i in idx]), torch.stack([kfs[i].T for i in idx]),
                                       fx, fy, cx, cy, W, H)
-            rows = torch.tensor(idx)
-            host[rows, 0:16] = f["viewmatrix"].reshape(-1, 16)
-            host[rows, 16:32] = f["projmatrix"].reshape(-1, 16)
-            host[rows, 32:48] = f["projmatrix_raw"].reshape(1, 16)
-            host[rows, 48:51] = f["campos"]
+            n = len(idx)
+            parts.append(torch.cat([f["viewmatrix"].reshape(n, 16), f["projmatrix"].reshape(n, 16),
+                                    f["projmatrix_raw"].reshape(1, 16).expand(n, 16), f["campos"],
+                                    torch.zeros(n, CAM_FLOATS - 51)], 1))
+            order += idx
+        kfs = [kfs[i] for i in order]
+        host = parts[0] if len(parts) == 1 else torch.cat(parts)
+        b = self.bank
+        in_bank = b.uniform and b.cam is not None and all(b.kfs.get(kf.uid) is kf for kf in kfs)
+        if in_bank:
+            # the keyframes' camera fields are views of their bank rows
+            # (KeyframeBank._bind): the new values land under them in place.
+            # The bank rows ride in the pad word of the same upload (one copy)
+            host[:, CAM_FLOATS - 1] = torch.tensor([float(b.slots[kf.uid]) for kf in kfs])
+            dev = host.to(self.dev)
+            with torch.no_grad():
+                b.cam.index_copy_(0, dev[:, CAM_FLOATS - 1].long(), dev)
+            return True
         dev = host.to(self.dev)
-        for i, kf in enumerate(kfs):
+        for i, kf in enumerate(kfs):  # (views of the staging copy)
             c = dev[i]
             kf.cam = dict(kf.cam, viewmatrix=c[0:16].view(4, 4), projmatrix=c[16:32].view(4, 4),
                           projmatrix_raw=c[32:48].view(4, 4), campos=c[48:51])
-        b = self.bank
-        if not (b.uniform and b.cam is not None and all(b.kfs.get(kf.uid) is kf for kf in kfs)):
-            return False
-        rows = torch.tensor([b.slots[kf.uid] for kf in kfs]).to(self.dev)
-        with torch.no_grad():
-            b.cam.index_copy_(0, rows, dev)
-        for kf in kfs:
-            b._bind(kf.uid, kf)
-        return True
+        return False
 
     def refine_pose_non_key_frame(self, w2c_init, image, fx: float, fy: float, cx: float, cy: float,
                                   features=None, uncertainty_aware: bool = True, iters: int | None = None):

@@ -327,21 +327,26 @@ class GaussianStore:
                 f.K[:] = Kc.flatten().tolist()
                 f.H, f.W = int(d.shape[0]), int(d.shape[1])
                 f.depth, f.depth_old = d.data_ptr(), d_old.data_ptr()
-        lut_h = torch.full((max(seen) + 1 if max(seen) >= 0 else 1,), -1, dtype=torch.int32)
+        nlut = max(seen) + 1 if max(seen) >= 0 else 1
+        lut_h = np.full(nlut, -1, dtype=np.int32)
         for j, fr in enumerate(frames):
             if int(fr["kf_id"]) >= 0:
                 lut_h[int(fr["kf_id"])] = j
         dev = self.device
-        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-        frames_d = raw.to(dev)
-        lut = lut_h.to(dev)
+        # the frame table and the keyframe -> frame lookup in ONE upload
+        fb = bytes(arr)
+        off = (len(fb) + 255) & ~255
+        blob = np.zeros(off + 4 * nlut, dtype=np.uint8)
+        blob[:len(fb)] = np.frombuffer(fb, dtype=np.uint8)
+        blob[off:] = lut_h.view(np.uint8)
+        blob_d = torch.from_numpy(blob).to(dev)
         flags = torch.empty(2, dtype=torch.int32, device=dev)
         bank = self._bank_struct(self.cur)
         with torch.cuda.device(dev):
-            _lib.check(L.wgsr_deform_points(self.P, ctypes.byref(bank), frames_d.data_ptr(), len(frames),
-                                            lut.data_ptr(), int(lut.numel()), flags.data_ptr(),
+            _lib.check(L.wgsr_deform_points(self.P, ctypes.byref(bank), blob_d.data_ptr(), len(frames),
+                                            blob_d.data_ptr() + off, nlut, flags.data_ptr(),
                                             _lib.stream_handle(dev)))
-        self._deform_keep = (keep, frames_d, lut, flags)  # alive until the next call (stream order)
+        self._deform_keep = (keep, blob_d, flags)  # alive until the next call (stream order)
         return len(frames)
 
     def _reset_opacity(self, vis, value):
