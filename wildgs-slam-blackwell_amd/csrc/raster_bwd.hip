@@ -1145,7 +1145,22 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
       const uint32_t c = r * kGbcThreads + t;
       if (c < nlive) {
         const uint32_t qa = max(s_off[c], base), qb = min(s_off[c + 1], base + kRecChunk);
-        for (uint32_t q = qa; q < qb; ++q)
+        // four slots' rows read before their adds (one LDS round trip per
+        // four slots on the long ranges the slowest workgroups wait for);
+        // the adds keep the slot order, so the sums are bit-identical
+        uint32_t q = qa;
+        for (; q + 4 <= qb; q += 4) {
+          float v[4][10];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v[j][k] = s_rec[q + j - base][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) acc[r][k] += v[j][k];
+        }
+        for (; q < qb; ++q)
 #pragma unroll
           for (int k = 0; k < 10; ++k) acc[r][k] += s_rec[q - base][k];
       }
