@@ -39,7 +39,12 @@ extern "C" {
 #define WGSR_EALLOC 3   /* an allocation callback returned NULL             */
 
 /* Returns a device pointer to at least `bytes` bytes, 256-byte aligned, that
- * stays valid until the caller releases it.  `bytes` may be 0. */
+ * stays valid until the caller releases it.  `bytes` may be 0.  Within one
+ * library call a callback may be called twice for the same buffer (the
+ * forward's binning buffer: a predicted size before its host wait, then the
+ * exact size): the library uses the pointer of the last call and has written
+ * nothing through the first, so a callback may narrow its first allocation
+ * when that is large enough (as wgsr's own wrappers do) or allocate anew. */
 typedef void* (*wgsr_alloc_fn)(void* ctx, size_t bytes);
 
 /* The rasterisation inputs shared by forward and backward: the tensors and

@@ -35,6 +35,24 @@ struct HostCounters {
 // one pinned block + event per (host thread, device): an event recorded on a
 // stream must belong to that stream's device
 constexpr int kMaxDevices = 64;
+// The binning buffer's size is known only after the forward's one host wait;
+// allocating it there put the allocation (~10 us of the caller's allocator)
+// on the GPU's critical path.  The previous forward of the same shape on this
+// thread predicts it: a buffer of that size (+1/16) is allocated BEFORE the
+// wait, while k_preprocess runs, and only a forward that needs more allocates
+// again after it.  (The binning layout is sized by num_rendered as always; a
+// larger buffer just leaves its tail unused.)
+struct BinningGuess {
+  int P = -1, W = 0, H = 0, bshift = -1;
+  size_t bytes = 0;
+};
+BinningGuess& binning_guess() {
+  thread_local BinningGuess g[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+  return g[dev];
+}
+
 HostCounters& host_counters() {
   thread_local HostCounters per_dev[kMaxDevices];
   int dev = 0;
@@ -420,6 +438,15 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     return WGSR_OK;
   };
   if (int e = queue_scan()) return e;
+  // the predicted binning buffer, allocated while the GPU works
+  BinningGuess& bg = binning_guess();
+  void* binning = nullptr;
+  size_t binning_have = 0;
+  if (bg.P == a.P && bg.W == a.W && bg.H == a.H && bg.bshift == bshift && bg.bytes > 0) {
+    binning_have = bg.bytes + bg.bytes / 16;
+    binning = call_alloc(binning_alloc, ctx, binning_have);
+    if (!binning) binning_have = 0;
+  }
   HIPCHK(hipEventSynchronize(hc.ev));
   sync_on_error.armed = false;
   const uint32_t* host_counter = hc.buf;
@@ -492,8 +519,14 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // ping-pong arrays; not the list region, which the same kernel now writes)
   const size_t bds_bytes = bin_depth ? align256(16 * (size_t)N_bin) : 0;
   const size_t binning_bytes = BL.total + lists_bytes + 8 * pdep_words + bds_bytes;
-  void* binning = call_alloc(binning_alloc, ctx, binning_bytes);
-  if (!binning && binning_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  bg.P = a.P; bg.W = a.W; bg.H = a.H; bg.bshift = bshift; bg.bytes = binning_bytes;
+  // the exact size: allocated now without (or beyond) a prediction, else the
+  // caller's callback narrows the predicted buffer (ours do; any other gets a
+  // new buffer of the exact size -- nothing was written to the first)
+  if (binning_bytes > binning_have || binning_bytes < binning_have) {
+    binning = call_alloc(binning_alloc, ctx, binning_bytes);
+    if (!binning && binning_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
+  }
   uint32_t* lists = bshift ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
   uint32_t* pdep = bin_depth ? at<uint32_t>(binning, BL.total + lists_bytes) : nullptr;
   uint32_t* pdep_alt = bin_depth ? pdep + pdep_words : nullptr;

@@ -104,14 +104,20 @@ const float* fp(const at::Tensor& t) { return t.defined() ? t.data_ptr<float>() 
 // allocation (e.g. torch's OutOfMemoryError) is kept and NULL returned, the
 // library reports WGSR_EALLOC through its own error path, and check() then
 // rethrows the original exception.
+// A second call for the same buffer within one library call (the forward's
+// predicted binning buffer, then its exact size) narrows the first
+// allocation when it is large enough (wgsr.h: the library uses the pointer of
+// the last call).
 struct Alloc {
   at::Device dev;
   at::Tensor geom, binning, image, scratch;
+  at::Tensor geom_b, binning_b, image_b, scratch_b;  // the allocations the slots view
   std::exception_ptr failure;
   explicit Alloc(const at::Device& d) : dev(d) {}
-  void* take(at::Tensor& slot, size_t n) noexcept {
+  void* take(at::Tensor& slot, at::Tensor& base, size_t n) noexcept {
     try {
-      at::Tensor base = at::empty({(int64_t)(n > 0 ? n : 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
+      if (!base.defined() || base.numel() < (int64_t)(n > 0 ? n : 1))
+        base = at::empty({(int64_t)(n > 0 ? n : 1)}, at::TensorOptions().dtype(at::kByte).device(dev));
       slot = base.narrow(0, 0, (int64_t)n);
       return base.data_ptr();
     } catch (...) {
@@ -120,10 +126,16 @@ struct Alloc {
     }
   }
 };
-void* alloc_geom(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->geom, n); }
-void* alloc_binning(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->binning, n); }
-void* alloc_image(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->image, n); }
-void* alloc_scratch(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->scratch, n); }
+void* alloc_geom(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->geom, a->geom_b, n); }
+void* alloc_binning(void* ctx, size_t n) {
+  auto* a = static_cast<Alloc*>(ctx);
+  return a->take(a->binning, a->binning_b, n);
+}
+void* alloc_image(void* ctx, size_t n) { auto* a = static_cast<Alloc*>(ctx); return a->take(a->image, a->image_b, n); }
+void* alloc_scratch(void* ctx, size_t n) {
+  auto* a = static_cast<Alloc*>(ctx);
+  return a->take(a->scratch, a->scratch_b, n);
+}
 
 wgsr_raster_args make_args(int P, int D, int M, int W, int H, const at::Tensor& bg, const at::Tensor& means3D,
                            const at::Tensor& colors, const at::Tensor& opacity, const at::Tensor& scales,

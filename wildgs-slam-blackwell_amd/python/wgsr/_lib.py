@@ -404,10 +404,16 @@ class AllocRequest:
 
 
 def _make_alloc(slot: str):
+    # (a second call for the same buffer within one library call -- the
+    # forward's predicted binning buffer, then its exact size -- narrows the
+    # first allocation when it is large enough; the library uses the pointer
+    # of the last call)
     def _alloc(_ctx, nbytes):
         req = _tls.req
         n = int(nbytes)
-        base = torch.empty(max(n, 1), dtype=torch.uint8, device=req.device)
+        base = req.buffers.get(slot + "_base")
+        if base is None or base.numel() < max(n, 1):
+            base = torch.empty(max(n, 1), dtype=torch.uint8, device=req.device)
         req.buffers[slot] = base[:n]
         req.buffers[slot + "_base"] = base
         return base.data_ptr()
