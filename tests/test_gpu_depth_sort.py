@@ -8,7 +8,8 @@
   k_bin_depth_sort: pairs duplicated in index order, every sort bin ordered by
   depth key, ties by index), which has no Gaussian-level order: every raster
   output bit-identical to the global schedules, incl. bins larger than one
-  LDS tile (the chunked pass through global scratch).
+  LDS tile (the chunked pass through global scratch; its keys gathered from
+  the Gaussians' depth keys through each bin's ids).
 
 Both are stable sorts of the same keys, so the depth order (rank -> Gaussian,
 read from the geometry buffer at wgsr_depth_order_offset()) and every raster

@@ -28,7 +28,7 @@ def run(P, W, H, deg):
     e = torch.empty(0, device=dev)
     bg = torch.zeros(3, device=dev)
     lib = ctypes.CDLL(_lib.LIB_PATH)
-    out = (ctypes.c_ulonglong * 32)()
+    out = (ctypes.c_ulonglong * 64)()
     nr, color, radii, geom, binning, img, depth, opac, nt = _C.rasterize_gaussians(
         bg, sc.means3D, e, sc.opacities, sc.scales, sc.rotations, 1.0, e, d["viewmatrix"], d["projmatrix"],
         d["projmatrix_raw"], d["tanfovx"], d["tanfovy"], H, W, sc.shs, deg, d["campos"], False, False)
@@ -58,7 +58,10 @@ def run(P, W, H, deg):
             "p2_by_mask": p2, "reach_popcount": pop(reach), "p2_popcount": pop(p2),
             "quadrant_evals_p1": sum(c * bin(m).count("1") for m, c in enumerate(reach)),
             "quadrant_evals_p2": sum(c * bin(m).count("1") for m, c in enumerate(p2)),
-            "hit_entries": n - p2[0], "reach_rows": rows(reach), "p2_rows": rows(p2)}
+            "hit_entries": n - p2[0], "reach_rows": rows(reach), "p2_rows": rows(p2),
+            # log2 bins: [1], [2, 3], [4, 7], ... [128, 256]
+            "pixels_per_hit_entry_log2": list(out[32:40]), "lanes_per_p2_eval_log2": list(out[40:48]),
+            "p2_lanes": out[48], "p1_evals_without_p2": out[49]}
 
 
 if __name__ == "__main__":

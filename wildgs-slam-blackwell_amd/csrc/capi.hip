@@ -88,6 +88,7 @@ struct DevCounters {
 // sort costs more than k_expand_bins' 4x wider grid (140.8 vs 131.3 us).
 bool bds_emit(int bshift) { return bshift <= 1; }
 
+
 DevCounters* dev_counters(hipStream_t s) {
   thread_local DevCounters per_dev[kMaxDevices];
   int dev = 0;
@@ -512,13 +513,10 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // sort bins the per-tile lists follow it (2^2s entries per bin pair)
   const BinLayout BL(N_rect);
   const size_t lists_bytes = bshift ? align256(4 * ((size_t)N_bin << (2 * bshift))) : 0;
-  // per-bin depth sort: the pairs' depth keys ride the bin sort as a second
-  // payload, in two arrays after the lists
-  const size_t pdep_words = bin_depth ? align256(4 * N_bin) / 4 : 0;
   // per-bin depth sort: scratch of the bins beyond one LDS tile (two uint2
   // ping-pong arrays; not the list region, which the same kernel now writes)
   const size_t bds_bytes = bin_depth ? align256(16 * (size_t)N_bin) : 0;
-  const size_t binning_bytes = BL.total + lists_bytes + 8 * pdep_words + bds_bytes;
+  const size_t binning_bytes = BL.total + lists_bytes + bds_bytes;
   bg.P = a.P; bg.W = a.W; bg.H = a.H; bg.bshift = bshift; bg.bytes = binning_bytes;
   // the exact size: allocated now without (or beyond) a prediction, else the
   // caller's callback narrows the predicted buffer (ours do; any other gets a
@@ -528,9 +526,9 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (!binning && binning_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   }
   uint32_t* lists = bshift ? at<uint32_t>(binning, BL.total) : at<uint32_t>(binning, BL.point_g);
-  uint32_t* pdep = bin_depth ? at<uint32_t>(binning, BL.total + lists_bytes) : nullptr;
-  uint32_t* pdep_alt = bin_depth ? pdep + pdep_words : nullptr;
-  void* bds_scratch = bin_depth ? static_cast<void*>(at<char>(binning, BL.total + lists_bytes + 8 * pdep_words)) : nullptr;
+  // (the per-bin depth sort gathers its keys from the Gaussians' depth keys)
+  const uint32_t* gdep = bin_depth ? at<uint32_t>(geom, GeomLayout((size_t)a.P).dkey) : nullptr;
+  void* bds_scratch = bin_depth ? static_cast<void*>(at<char>(binning, BL.total + lists_bytes)) : nullptr;
   uint2* ranges = at<uint2>(image, IL.ranges);
   // sorted pairs: (Gaussian, bin) pairs, or with bin shift 0 the exact
   // (Gaussian, tile) pairs themselves
@@ -555,7 +553,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bshift) {
       // (the backward's record flags live on the exact slots: zeroed here too)
       STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
-                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, odd ? pdep_alt : pdep));
+                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
@@ -567,8 +565,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     { StageTimer T(4, s);
     STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false,
                                  NL, 0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s,
-                                 &talt, bin_bounds, &bounds_done, bs_words != 0, odd ? pdep_alt : pdep,
-                                 odd ? pdep : pdep_alt)); }
+                                 &talt, bin_bounds, &bounds_done, bs_words != 0)); }
     // the Gaussian ids are the payload; the backward recomputes each pair's
     // record slot from (Gaussian, tile) instead of carrying it through the sort
     if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
@@ -583,7 +580,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
       const bool emit = bds_emit(bshift);
       STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)NL, bshift, at<uint2>(image, IL.tile_m),
-                                        bounds_done, pdep, okeys, ogid, bds_scratch, s, emit ? lists : nullptr,
+                                        bounds_done, gdep, okeys, ogid, bds_scratch, s, emit ? lists : nullptr,
                                         ranges, at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta)));
       bounds_done = true;
       if (!emit) {
@@ -620,7 +617,7 @@ size_t wgsr_binning_bytes_cap(const wgsr_raster_args* args, int64_t cap) {
   if (!args || cap < 0) return 0;
   const int bshift = bin_shift(*args);
   const size_t C = (size_t)cap;
-  return BinLayout(C).total + align256(4 * (C << (2 * bshift))) + 8 * (align256(4 * C) / 4) + align256(16 * C);
+  return BinLayout(C).total + align256(4 * (C << (2 * bshift))) + align256(16 * C);
 }
 
 // Capacity mode (wgsr.h): the forward above without its one host wait.  The
@@ -674,14 +671,12 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   const size_t C = (size_t)cap;
   const BinLayout BL(C);
   const size_t lists_bytes = align256(4 * (C << (2 * bshift)));
-  const size_t pdep_words = align256(4 * C) / 4;
-  const size_t binning_bytes = BL.total + lists_bytes + 8 * pdep_words + align256(16 * C);
+  const size_t binning_bytes = BL.total + lists_bytes + align256(16 * C);
   void* binning = call_alloc(binning_alloc, ctx, binning_bytes);
   if (!binning) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   uint32_t* lists = at<uint32_t>(binning, BL.total);
-  uint32_t* pdep = at<uint32_t>(binning, BL.total + lists_bytes);
-  uint32_t* pdep_alt = pdep + pdep_words;
-  void* bds_scratch = at<char>(binning, BL.total + lists_bytes + 8 * pdep_words);
+  const uint32_t* gdep = at<uint32_t>(geom, GL.dkey);
+  void* bds_scratch = at<char>(binning, BL.total + lists_bytes);
   uint32_t* counter = at<uint32_t>(geom, GL.counter);
   uint32_t* meta = at<uint32_t>(image, IL.meta);
   HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
@@ -712,15 +707,13 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   }
   { StageTimer T(3, s);  // (pairs past the capacity are not written; exact-slot flags likewise)
   STAGE(a, s, launch_duplicate_bins(a, geom, nullptr, bshift, at<uint8_t>(binning, BL.flag),
-                                    at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, odd ? pdep_alt : pdep,
-                                    (uint32_t)C, (uint32_t)C)); }
+                                    at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, (uint32_t)C, (uint32_t)C)); }
   bool talt = false, bounds_done = false;
   uint2* bin_bounds = at<uint2>(image, IL.tile_m);
   { StageTimer T(4, s);
   STAGE(a, s, radix_sort_pairs(at<uint32_t>(binning, BL.key), at<uint32_t>(binning, BL.key_alt), vin, valt, false, C,
                                0, bits, at<uint32_t>(binning, BL.hist), at<uint32_t>(binning, BL.totals), s, &talt,
-                               bin_bounds, &bounds_done, bs_words != 0, odd ? pdep_alt : pdep, odd ? pdep : pdep_alt,
-                               counts + 4)); }
+                               bin_bounds, &bounds_done, bs_words != 0, counts + 4)); }
   if (talt != odd) return set_error(WGSR_EHIP, "internal: list sort parity");
   if (!bounds_done) return set_error(WGSR_EHIP, "internal: capacity mode without the sort's bin bounds");
   const uint32_t* sorted_keys = at<uint32_t>(binning, talt ? BL.key_alt : BL.key);
@@ -730,7 +723,7 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   uint32_t* okeys = at<uint32_t>(binning, talt ? BL.key : BL.key_alt);
   uint32_t* ogid = at<uint32_t>(binning, BL.slot_g);
   { StageTimer T(4, s);
-  STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)C, bshift, bin_bounds, true, pdep, okeys,
+  STAGE(a, s, launch_bin_depth_sort(a, sorted_keys, sorted_gid, (uint32_t)C, bshift, bin_bounds, true, gdep, okeys,
                                     ogid, bds_scratch, s, emit ? lists : nullptr, ranges,
                                     at<uint32_t>(image, IL.tile_len), meta)); }
   if (!emit) { StageTimer T(5, s);

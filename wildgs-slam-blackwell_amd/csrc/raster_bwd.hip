@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
 
@@ -31,7 +33,7 @@ constexpr int kBatch = 64;  // entries staged per LDS batch in the backward
 #define WGSR_BWD_STATS 0
 #endif
 #if WGSR_BWD_STATS
-__device__ unsigned long long g_bwd_stats[32];
+__device__ unsigned long long g_bwd_stats[64];
 #endif
 // diagnostic build: per-workgroup phase clocks of k_gauss_bwd_compact summed
 // over workgroups (s_memtime; wgsr_debug_gbc_times)
@@ -49,6 +51,15 @@ __device__ unsigned long long g_gbc_times[16];
   } while (0)
 #else
 #define GBC_MARK(k) do {} while (0)
+#endif
+// diagnostic build: each k_render_bwd_quad workgroup's start / end
+// (s_memrealtime, 100 MHz) and hardware id (wgsr_debug_bwd_wgtime)
+#ifndef WGSR_BWD_WGTIME
+#define WGSR_BWD_WGTIME 0
+#endif
+#if WGSR_BWD_WGTIME
+constexpr int kWgtMax = 32768;
+__device__ unsigned long long g_bwd_wgt[3 * kWgtMax];
 #endif
 // below this many tiles the backward runs k_render_bwd_seg (four waves per
 // tile) instead of k_render_bwd_quad (one); WGSR_BWD_SPLIT_BELOW overrides
@@ -108,8 +119,9 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   const size_t HW = (size_t)H * W;
   const uint2 range = ranges[tile];
 #if WGSR_BWD_STATS
-  uint32_t* const sStat = sHit;
-  if (lane < 32) sStat[lane] = 0;
+  uint32_t* const sStat = sHit;  // [0, 16) reach masks, [16, 32) phase-2 masks, [32, 40) pixels per hit
+  sStat[lane] = 0;                // entry (log2 bins), [40, 48) lanes per phase-2 evaluation, [48] phase-2
+                                  // lanes, [49] phase-1 evaluations without a phase 2
   __syncthreads();
 #endif
 
@@ -273,11 +285,12 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       // pixel sums of u = G dL/dalpha (dx, dy) and of its moments; the
       // entry's constants (opacity, conic) multiply the sums afterwards
       // (record_sums)
-      // (five zero pairs: one 64-bit move each per entry)
-      v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g45{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
+      // (zero pairs: one 64-bit move each per entry)
+      v2f g01{0.f, 0.f}, g23{0.f, 0.f}, g67{0.f, 0.f}, g89{0.f, 0.f};
+      float g4 = 0.f, g5 = 0.f;  // (scalars: one FMA + one add, no pair to build)
       bool hit = false;
 #if WGSR_BWD_STATS
-      uint32_t st_reach = 0, st_p2 = 0;
+      uint32_t st_reach = 0, st_p2 = 0, st_pix = 0;
 #endif
 #pragma unroll
       for (int p = 0; p < Q; ++p) {
@@ -291,9 +304,18 @@ __device__ __forceinline__ void render_bwd_quad_tile(
         const float G = __builtin_amdgcn_exp2f(power);
         const float av = fminf(kMaxAlpha, op * G);
         const bool v = cidx < last[p] && power <= 0.0f && av >= kMinAlpha;
+#if WGSR_BWD_STATS
+        const uint32_t nv = (uint32_t)__builtin_popcountll(wave_ballot(v));
+        if (lane == 0 && nv == 0) atomicAdd(&sStat[49], 1u);
+#endif
         if (!wave_any(v)) continue;
 #if WGSR_BWD_STATS
         st_p2 |= 1u << p;
+        st_pix += nv;
+        if (lane == 0) {
+          atomicAdd(&sStat[40 + min(7u, 31u - (uint32_t)__builtin_clz(nv))], 1u);
+          atomicAdd(&sStat[48], nv);
+        }
 #endif
         // phase 2 on the lanes whose pixel the entry reaches (exec mask): the
         // others keep T, the accumulated colour and their sums as they are.
@@ -317,8 +339,8 @@ __device__ __forceinline__ void render_bwd_quad_tile(
           const v2f u = gl * d;        // (G dx, G dy) dL/dG / opacity
           g01 += u;
           g23 += u.x * d;  // (G dx dx, G dx dy) dL/dG / opacity
-          g45.x += u.y * d.y;
-          g45.y += gl;
+          g4 = fmaf(u.y, d.y, g4);
+          g5 += gl;
           g67 += dch * dp01[p];
           g89 += dch * dp2d[p];
         }
@@ -327,10 +349,11 @@ __device__ __forceinline__ void render_bwd_quad_tile(
       if (lane == 0) {
         atomicAdd(&sStat[st_reach], 1u);
         atomicAdd(&sStat[16 + st_p2], 1u);
+        if (st_pix) atomicAdd(&sStat[32 + min(7u, 31u - (uint32_t)__builtin_clz(st_pix))], 1u);
       }
 #endif
       if (!hit) continue;  // no pixel of the tile: no partial
-      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g45.x, g45.y, g67.x, g67.y, g89.x, g89.y};
+      const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
       wave_sum10_store_m(gv, sPm + 11 * j);
       hitm |= 1ull << j;
     }
@@ -339,7 +362,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   write_records();  // the last batch's
 #if WGSR_BWD_STATS
   __syncthreads();
-  if (lane < 32) atomicAdd(&g_bwd_stats[lane], (unsigned long long)sStat[lane]);
+  atomicAdd(&g_bwd_stats[lane], (unsigned long long)sStat[lane]);
 #endif
 }
 
@@ -363,6 +386,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
     return;
   }
+#if WGSR_BWD_WGTIME
+  const unsigned long long wgt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // where the forward left the tile lists (ImageLayout::meta)
   const uint32_t* __restrict__ point_g = meta[0] ? lists_bins : lists_exact;
   const uint32_t tile = order[global_order ? blockIdx.x : xcd_remap(blockIdx.x, (uint32_t)ntiles)];
@@ -377,6 +403,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   // here; measured at 1M/1080p: render_bwd +2 % with the fill after the walk,
   // +4.5 % before it, while k_gauss_bwd drops from 86 to 49 us)
   zero_share(zero, blockIdx.x, gridDim.x, threadIdx.x, 64);
+#if WGSR_BWD_WGTIME
+  const unsigned long long wgt1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && blockIdx.x < (unsigned)kWgtMax) {
+    g_bwd_wgt[3 * blockIdx.x] = wgt0;
+    g_bwd_wgt[3 * blockIdx.x + 1] = wgt1;
+    // HW_ID (wave, SIMD, CU, SH, SE), XCC_ID and the tile
+    g_bwd_wgt[3 * blockIdx.x + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (31 << 11)) |
+                                    ((unsigned long long)(__builtin_amdgcn_s_getreg((20 << 0) | (15 << 11)) & 15) << 32) |
+                                    ((unsigned long long)tile << 40);
+  }
+#endif
 }
 
 // Entry pairs in the four-wave backward (k_render_bwd_seg): a wave owns one
@@ -1464,12 +1501,23 @@ extern "C" int wgsr_debug_gbc_times(unsigned long long* out) {
   return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_gbc_times), z, sizeof(z)) != hipSuccess;
 }
 #endif
+#if WGSR_BWD_WGTIME
+// diagnostic build only: read (and clear) the quad backward's workgroup times
+extern "C" int wgsr_debug_bwd_wgtime(unsigned long long* out, int n) {
+  n = n < wgsr::kWgtMax ? n : wgsr::kWgtMax;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_bwd_wgt), sizeof(unsigned long long) * 3 * n) != hipSuccess)
+    return 1;
+  std::vector<unsigned long long> z(3 * (size_t)wgsr::kWgtMax, 0ull);
+  return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_bwd_wgt), z.data(), sizeof(unsigned long long) * z.size()) !=
+         hipSuccess;
+}
+#endif
 #if WGSR_BWD_STATS
 // diagnostic build only: read and clear the quad backward's entry histogram
 extern "C" int wgsr_debug_bwd_stats(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_bwd_stats), sizeof(unsigned long long) * 32) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_bwd_stats), sizeof(unsigned long long) * 64) != hipSuccess)
     return 1;
-  unsigned long long z[32] = {};
+  unsigned long long z[64] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_bwd_stats), z, sizeof(z)) != hipSuccess;
 }
 #endif

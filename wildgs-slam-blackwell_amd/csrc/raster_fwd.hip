@@ -267,18 +267,12 @@ __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lan
   return sh_to_rgb(kD, sh, dir, cbits);
 }
 
-template <int kCh>
-__device__ __forceinline__ f3 sh_rgb_lds_deg(int D, const float* __restrict__ s_sh, int lane, f3 dir,
-                                             uint32_t& cbits) {
-  switch (D) {
-    case 0: return sh_rgb_lds<0, kCh>(s_sh, lane, dir, cbits);
-    case 1: return sh_rgb_lds<1, kCh>(s_sh, lane, dir, cbits);
-    case 2: return sh_rgb_lds<2, kCh>(s_sh, lane, dir, cbits);
-    default: return sh_rgb_lds<3, kCh>(s_sh, lane, dir, cbits);
-  }
-}
-
-template <int kCh>
+// kD: the evaluated SH degree (-1: no slab -- colours given, or no SH).  The
+// degree is a template parameter so that the slab is a compile-time number of
+// loads queued AFTER the parameter loads: vmcnt retires in issue order, and
+// with the slab queued first (or a run-time trip count) the first parameter
+// use waited for the whole slab, so nothing overlapped it.
+template <int kCh, int kD>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ opac, const float* __restrict__ shs,
@@ -294,33 +288,39 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   extern __shared__ float s_sh[];  // nch x 64 x kCh floats (chunk-major)
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * kPreWave, i = i0 + lane;
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
-  const bool sh_on = shs != nullptr && colors == nullptr;
-  if (sh_on) {  // uniform: queue the slab first
-    const int nf = 3 * (D + 1) * (D + 1), nch = (nf + kCh - 1) / kCh;
-    const float* src = shs + (size_t)min(i, P - 1) * (3 * M);
-    for (int k = 0; k < nch; ++k) {
+  constexpr bool sh_on = kD >= 0;
+  // the parameters first, in one basic block (clamped rows; with cov_pre the
+  // scale / rotation loads read its first words and are discarded)
+  const int ic = min(i, P - 1);
+  const int ir = cov_pre ? 0 : ic;
+  const float* __restrict__ sp = cov_pre ? cov_pre : scales;
+  const float* __restrict__ rp = cov_pre ? cov_pre : rots;
+  const f3 pl = mk3(means[3 * ic], means[3 * ic + 1], means[3 * ic + 2]);
+  const f3 sl = mk3(sp[3 * ir], sp[3 * ir + 1], sp[3 * ir + 2]);
+  const float4 ql = make_float4(rp[4 * ir], rp[4 * ir + 1], rp[4 * ir + 2], rp[4 * ir + 3]);
+  const float ol = opac[ic];
+  // an opaque use of every parameter: the four loads share one round trip
+  // (none sinks into the branch below), completed before the slab is queued
+  asm volatile("" ::"v"(pl.x), "v"(pl.y), "v"(pl.z), "v"(sl.x), "v"(sl.y), "v"(sl.z), "v"(ql.x), "v"(ql.y),
+               "v"(ql.z), "v"(ql.w), "v"(ol));
+  if constexpr (sh_on) {  // then the slab, in flight while the geometry runs
+    using lds_t = __attribute__((address_space(3))) void*;
+    constexpr int kNch = (3 * (kD + 1) * (kD + 1) + kCh - 1) / kCh;
+    const float* src = shs + (size_t)ic * (3 * M);
+#pragma unroll
+    for (int k = 0; k < kNch; ++k) {
       if constexpr (kCh == 4)
-        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k),
-                                         (__attribute__((address_space(3))) void*)(s_sh + 256 * k), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(src + 4 * k), (lds_t)(s_sh + 256 * k), 16, 0, 0);
       else
-        __builtin_amdgcn_global_load_lds((const void*)(src + k),
-                                         (__attribute__((address_space(3))) void*)(s_sh + 64 * k), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(src + k), (lds_t)(s_sh + 64 * k), 4, 0, 0);
     }
   }
-  const f3 p = i < P ? mk3(means[3 * i], means[3 * i + 1], means[3 * i + 2]) : mk3(0.f, 0.f, 1.f);
+  const f3 p = i < P ? pl : mk3(0.f, 0.f, 1.f);
+  const float o = i < P ? ol : 0.f;
+  const f3 sc = cov_pre ? mk3(1.f, 1.f, 1.f) : sl;
+  const float4 q = cov_pre ? make_float4(1.f, 0.f, 0.f, 0.f) : ql;
   Cam c;
   load_cam(c, viewm, projm, W, H, tanx, tany);
-  f3 sc = mk3(1.f, 1.f, 1.f);
-  float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-  float o = 0.f;
-  if (i < P) {
-    if (!cov_pre) {
-      sc = mk3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-      q = reinterpret_cast<const float4*>(rots)[i];
-    }
-    o = opac[i];
-  }
   uint3 ac = make_uint3(0u, 0u, 0u);
   uint32_t khi = 0u, knlo = 0u;
   uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     n_touched[i] = 0;
     gflag[i] = 0;
   }
-  if (sh_on) {
+  if constexpr (sh_on) {
     __builtin_amdgcn_s_waitcnt(0);  // the slab has landed (one wave per workgroup)
     __syncthreads();
     if (i < P && w.x != 0u) {  // visible: the colour record
@@ -349,13 +349,14 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       const float len = sqrtf(dot3(dir, dir));
       dir = mk3(dir.x / len, dir.y / len, dir.z / len);
       uint32_t cbits = 0;
-      const f3 rgb = sh_rgb_lds_deg<kCh>(D, s_sh, lane, dir, cbits);
+      const f3 rgb = sh_rgb_lds<(kD < 0 ? 0 : kD), kCh>(s_sh, lane, dir, cbits);
       splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
       clamped[i] = cbits;
     }
   }
   wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
+  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
 }
 
 // Expand the exact tile lists (row_span) of depth ranks [r0, r0 + 64) (one
@@ -512,7 +513,7 @@ __device__ __forceinline__ uint32_t bin_mask_tab(int bx, int by, int x0, int y0,
 // search: each rank with bins writes its lane id at its first pair's place
 // in a 64-entry LDS row, and an inclusive max-scan over the row (DPP) hands
 // every pair its owner -- the last rank starting at or before it; the
-// owner's record (rect, first pair, Gaussian, depth key, row table) is read
+// owner's record (rect, first pair, Gaussian, row table) is read
 // from LDS where every rank staged it (three LDS reads per pair instead of a
 // six-step shuffle search and ten shuffles).
 constexpr int kDupScanThreads = kPackedScanTile;  // one rank per thread
@@ -521,8 +522,7 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     uint32_t P, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
-    uint32_t* __restrict__ vals, const ZeroJob zero, const uint32_t* __restrict__ dkey,
-    uint32_t* __restrict__ pair_depth, uint32_t cap_slots, uint32_t cap_pairs) {
+    uint32_t* __restrict__ vals, const ZeroJob zero, uint32_t cap_slots, uint32_t cap_pairs) {
   // (cap_slots / cap_pairs: the capacity-mode forward's buffer sizes -- writes
   // past them are dropped and the forward flags the overflow; ~0 otherwise)
   constexpr int NW = kDupScanThreads / 64;
@@ -530,21 +530,18 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   __shared__ uint2 s_w[NW], s_p[NW];
   __shared__ uint4 s_ra[NW][64];    // per rank: rect lo | hi, first bin pair, Gaussian
   __shared__ uint4 s_rt[NW][64];    // per rank: row table
-  __shared__ uint32_t s_rd[NW][64]; // per rank: depth key
   __shared__ uint2 s_rw[NW][64];    // per rank: bin columns of the rect, their reciprocal (float bits)
   __shared__ uint32_t s_own[NW][64];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
   // (unconditional loads of a clamped rank, the selects after: a load under
-  // `in` would be waited for at its join.  The depth key rides in the same
-  // round trip as the list record.)
+  // `in` would be waited for at its join.)
   const uint32_t rc = min(r, P - 1u);
   const uint32_t g0 = sorted_g ? sorted_g[rc] : rc;  // (null: index order)
   // the whole 32-byte list record in one round trip (row table + rect, tb,
   // list length: one cache line)
   uint4 lw = lrec[g0].w, tab = lrec[g0].tab;
-  const uint32_t dk0 = pair_depth ? dkey[g0] : 0u;
   // the block prefix's inputs, issued behind the record loads (the scans
   // below wait for the records only; vmcnt counts in order): the earlier
   // superblocks' sums plus the earlier blocks of its own superblock
@@ -571,7 +568,6 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   }
   const uint32_t v = lw.z;
   const uint32_t cnt = v & 0xFFFFu, nb = v >> 16;
-  const uint32_t dk = in && nb ? dk0 : 0u;  // (per-bin depth sort input)
   uint32_t rlo = 0, rhi = 0;
   bool tall = false;
   if (nb) {
@@ -628,7 +624,6 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   // every rank's record, for its pairs' lanes
   s_ra[w][lane] = make_uint4(rlo, rhi, my_off, g);
   s_rt[w][lane] = tab;
-  s_rd[w][lane] = dk;
   {  // the rect's bin-column count and its reciprocal, once per rank
     const int bw = (((int)(rhi & 0xFFFFu) - 1) >> bshift) - ((int)(rlo & 0xFFFFu) >> bshift) + 1;
     s_rw[w][lane] = make_uint2((uint32_t)bw, __float_as_uint(__builtin_amdgcn_rcpf((float)bw)));
@@ -677,7 +672,6 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     if (k < end && k < cap_pairs) {
       keys[k] = (uint32_t)(by * gbx + bx) | (mask << 16);
       vals[k] = gg;
-      if (pair_depth) pair_depth[k] = s_rd[w][lo];
     }
     __builtin_amdgcn_wave_barrier();  // (the next chunk's owner row is rewritten)
   }
@@ -1015,16 +1009,24 @@ __device__ __forceinline__ void bds_plan(int R, int& passes, int& pbits) {
 template <int JN>
 __device__ __forceinline__ void bds_small(BdsLds& L, const uint32_t* __restrict__ skeys,
                                           const uint32_t* __restrict__ sgid, const uint32_t* __restrict__ sdep,
-                                          uint32_t lo, uint32_t n, uint32_t* __restrict__ okeys,
-                                          uint32_t* __restrict__ ogid, bool E, const BdsEmit& EM) {
+                                          const uint32_t* __restrict__ gdep, uint32_t lo, uint32_t n,
+                                          uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, bool E,
+                                          const BdsEmit& EM) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   constexpr uint32_t kPosMask = (1u << kBdsPosBits) - 1u;
   uint32_t k[JN], pk[JN];
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
   // (loads of clamped positions, all issued before any is used: a load under
   // `le < n` is waited for at its join, one round trip per j)
+  if (gdep) {  // (uniform) the Gaussians' depth keys through the bin's ids: two round trips
 #pragma unroll
-  for (int j = 0; j < JN; ++j) k[j] = sdep[lo + min((uint32_t)(w * JN + j) * 64u + (uint32_t)lane, n - 1u)];
+    for (int j = 0; j < JN; ++j) k[j] = sgid[lo + min((uint32_t)(w * JN + j) * 64u + (uint32_t)lane, n - 1u)];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) k[j] = gdep[k[j]];
+  } else {
+#pragma unroll
+    for (int j = 0; j < JN; ++j) k[j] = sdep[lo + min((uint32_t)(w * JN + j) * 64u + (uint32_t)lane, n - 1u)];
+  }
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
     const uint32_t le = (uint32_t)(w * JN + j) * 64u + (uint32_t)lane;
@@ -1146,13 +1148,14 @@ __device__ __forceinline__ void bds_emit_big(BdsLds& L, const uint32_t* __restri
 // then ranks kBdsCap-entry chunks in order with running digit bases, the
 // (key, position) pairs ping-ponging through global scratch
 __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid,
-                                     const uint32_t* __restrict__ sdep, uint32_t lo, uint32_t n, uint32_t NL,
+                                     const uint32_t* __restrict__ gdep, uint32_t lo, uint32_t n, uint32_t NL,
                                      uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch,
                                      bool E, const BdsEmit& EM) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  auto dep = [&](uint32_t e) { return gdep[sgid[lo + e]]; };
   for (uint32_t e = (uint32_t)t; e < n; e += kBdsThreads) {
-    const uint32_t x = sdep[lo + e];
+    const uint32_t x = dep(e);
     mn = min(mn, x);
     mx = max(mx, x);
   }
@@ -1180,7 +1183,7 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
     const uint2* src = (p & 1) ? bufA : bufB;  // pass p - 1's output
     uint2* dst = (p & 1) ? bufB : bufA;
     auto load = [&](uint32_t e) -> uint2 {
-      return p == 0 ? make_uint2(sdep[lo + e], e) : bds_load_scratch(src + e);
+      return p == 0 ? make_uint2(dep(e), e) : bds_load_scratch(src + e);
     };
     if (bds_owns_digit()) L.base[t] = 0u;
     __syncthreads();
@@ -1240,8 +1243,8 @@ __device__ __forceinline__ void bds_big(BdsLds& L, const uint32_t* __restrict__ 
 
 __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sgid, const uint2* __restrict__ bounds,
-    const uint32_t* __restrict__ sdep, uint32_t NL, uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid,
-    uint2* scratch, BdsEmit emit) {
+    const uint32_t* __restrict__ gdep, uint32_t NL,
+    uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch, BdsEmit emit) {
   __shared__ BdsLds L;
   const int t = threadIdx.x;
   const uint2 bb = bounds[blockIdx.x];
@@ -1257,30 +1260,30 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;  // (published by bds_range's barrier)
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
   if (n <= 1u * kBdsThreads)
-    bds_small<1>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<1>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 2u * kBdsThreads)
-    bds_small<2>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<2>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   // (every step of JN: a bin's time is its busiest wave's chain of JN entry
   // groups per pass, and a coarser JN leaves the last waves idle -- 4.7k
   // entries at JN = 7 keep 11 of 16 waves busy, at JN = 5 all 15 it needs)
   else if (n <= 3u * kBdsThreads)
-    bds_small<3>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<3>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 4u * kBdsThreads)
-    bds_small<4>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<4>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 5u * kBdsThreads)
-    bds_small<5>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<5>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 6u * kBdsThreads)
-    bds_small<6>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<6>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (n <= 7u * kBdsThreads)
-    bds_small<7>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<7>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 8 && n <= 8u * kBdsThreads)
-    bds_small<(kBdsItems > 8 ? 8 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<(kBdsItems > 8 ? 8 : 7)>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 9 && n <= 9u * kBdsThreads)
-    bds_small<(kBdsItems > 9 ? 9 : 7)>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<(kBdsItems > 9 ? 9 : 7)>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else if (kBdsItems > 7 && n <= (uint32_t)kBdsCap)
-    bds_small<kBdsItems>(L, skeys, sgid, sdep, lo, n, okeys, ogid, E, emit);
+    bds_small<kBdsItems>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else
-    bds_big(L, skeys, sgid, sdep, lo, n, NL, okeys, ogid, scratch, E, emit);
+    bds_big(L, skeys, sgid, gdep, lo, n, NL, okeys, ogid, scratch, E, emit);
   if (E) bds_emit_ranges(L, emit, blockIdx.x, lo, n);
 }
 
@@ -1798,7 +1801,13 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
   const int nf = 3 * (a.D + 1) * (a.D + 1);
   const int kch = ch4 ? 4 : 1;
   const size_t lds2 = sh_on ? sizeof(float) * 64 * (size_t)(((nf + kch - 1) / kch) * kch) : 0;
-  hipLaunchKernelGGL(ch4 ? k_preprocess2<4> : k_preprocess2<1>, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave),
+  using PreKernel = decltype(&k_preprocess2<1, -1>);
+  static constexpr PreKernel kPre[2][4] = {{k_preprocess2<1, 0>, k_preprocess2<1, 1>, k_preprocess2<1, 2>,
+                                            k_preprocess2<1, 3>},
+                                           {k_preprocess2<4, 0>, k_preprocess2<4, 1>, k_preprocess2<4, 2>,
+                                            k_preprocess2<4, 3>}};
+  const PreKernel kern = sh_on ? kPre[ch4 ? 1 : 0][std::min(std::max(a.D, 0), 3)] : k_preprocess2<1, -1>;
+  hipLaunchKernelGGL(kern, dim3((a.P + kPreWave - 1) / kPreWave), dim3(kPreWave),
                      lds2, s, a.P, a.D, a.M, a.means3D, a.scales, a.rotations, a.opacities, a.shs, a.colors,
                      a.cov3D_precomp, a.scale_modifier, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
                      a.tan_fovy, gx, gy, a.prefiltered, at<float4>(geom, L.splat), at<ListRec>(geom, L.lrec),
@@ -1810,7 +1819,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t* pair_depth, uint32_t cap_slots, uint32_t cap_pairs) {
+                                 hipStream_t s, uint32_t cap_slots, uint32_t cap_pairs) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
@@ -1820,8 +1829,7 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
                      s, (uint32_t)a.P, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
-                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, at<uint32_t>(geom, L.dkey),
-                     pair_depth, cap_slots, cap_pairs);
+                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, cap_slots, cap_pairs);
   return hipGetLastError();
 }
 
@@ -1854,13 +1862,13 @@ __global__ __launch_bounds__(kBdsThreads) void k_argsort_small(const uint32_t* _
     if (bds_owns_digit()) L.wcnt[q][t] = 0u;
   for (int i = t; i < kBdsWaves * kBdsDigits; i += kBdsThreads) (&L.match[0][0])[i] = 0ull;
   if (kBdsThreads >= 1024 && n <= 1u * kBdsThreads)
-    bds_small<1>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+    bds_small<1>(L, nullptr, nullptr, keys, nullptr, 0u, n, nullptr, perm, false, none);
   else if (n <= 2u * kBdsThreads)
-    bds_small<2>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+    bds_small<2>(L, nullptr, nullptr, keys, nullptr, 0u, n, nullptr, perm, false, none);
   else if (n <= 4u * kBdsThreads)
-    bds_small<4>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+    bds_small<4>(L, nullptr, nullptr, keys, nullptr, 0u, n, nullptr, perm, false, none);
   else
-    bds_small<kBdsItems>(L, nullptr, nullptr, keys, 0u, n, nullptr, perm, false, none);
+    bds_small<kBdsItems>(L, nullptr, nullptr, keys, nullptr, 0u, n, nullptr, perm, false, none);
 }
 }  // namespace
 
@@ -1873,7 +1881,7 @@ hipError_t launch_argsort_small(const uint32_t* keys, uint32_t n, uint32_t* perm
 }
 
 hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
-                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
+                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* gdepth,
                                  uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s, uint32_t* lists,
                                  uint2* ranges, uint32_t* tile_len, uint32_t* meta) {
   const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
@@ -1887,7 +1895,7 @@ hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sort
   // k_expand_bins); else the sorted bins go to okeys / ogid
   const BdsEmit emit{lists, ranges, tile_len, meta, gx, gy, bshift, B.bx};
   hipLaunchKernelGGL(k_bin_depth_sort, dim3((uint32_t)B.n), dim3(kBdsThreads), 0, s, sorted_keys, sorted_g, bounds,
-                     sdepth, NB, okeys, ogid, static_cast<uint2*>(scratch), emit);
+                     gdepth, NB, okeys, ogid, static_cast<uint2*>(scratch), emit);
   return hipGetLastError();
 }
 

@@ -190,14 +190,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, const uint32_t* __restrict__ sup, uint32_t nsup, uint2* __restrict__ bounds,
-    const uint32_t* __restrict__ xin, uint32_t* __restrict__ xout, const uint32_t* __restrict__ ndev) {
+    const uint32_t* __restrict__ ndev) {
   constexpr int kTile = 256 * I;
   if (ndev) {  // capacity mode: blocks past the live keys have nothing to move
     n = min(n, *ndev);
     if ((size_t)blockIdx.x * kTile >= n && !(blockIdx.x == 0 && bounds)) return;
   }
-  __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16); then the
-                                  // second payload (xin: the bin sort's depth keys) -- no extra LDS
+  __shared__ uint2 s_buf[kTile];  // (key, value) pairs in digit order (32 KB at I = 16)
   __shared__ uint32_t s_wcnt[4][256];
   __shared__ uint32_t s_lbase[256];
   __shared__ uint32_t s_gbase[256];
@@ -209,14 +208,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
   const uint32_t bid = blockIdx.x;
   const size_t blk0 = (size_t)bid * kTile;
   const size_t base = blk0 + (size_t)w * (64 * I);
-  uint32_t key[I], val[I], rank[I], xv[I];
+  uint32_t key[I], val[I], rank[I];
 #pragma unroll
   for (int j = 0; j < I; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     key[j] = valid ? kin[e] : 0u;
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
-    xv[j] = xin && valid ? xin[e] : 0u;
   }
   uint32_t gdig = 0;  // this block's global base of digit t (the scans' barriers publish s_wcnt = 0)
   if (sup) {
@@ -270,25 +268,6 @@ __global__ __launch_bounds__(256) void k_radix_scatter(
       vout[dst] = kv.y;
     }
   }
-  if (xin) {  // the second payload replaces the values in the staging buffer (keys kept)
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < I; ++j) {
-      const size_t e = base + (size_t)j * 64 + lane;
-      const uint32_t d = (key[j] >> shift) & mask;
-      if (e < n) s_buf[s_lbase[d] + s_wcnt[w][d] + rank[j]].y = xv[j];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < I; ++r) {
-      const uint32_t i = (uint32_t)t + 256u * r;
-      if (i < cnt) {
-        const uint2 kx = s_buf[i];
-        const uint32_t d = (kx.x >> shift) & mask;
-        xout[s_gbase[d] + (i - s_lbase[d])] = kx.y;
-      }
-    }
-  }
 }
 
 // ---- wide single pass (9-10 bit digits) ------------------------------------
@@ -318,14 +297,13 @@ template <int DIG, int I>
 __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, int iota, uint32_t n, int shift, int bits,
     uint32_t nb, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout, uint2* __restrict__ digit_bounds, const uint32_t* __restrict__ xin,
-    uint32_t* __restrict__ xout, const uint32_t* __restrict__ ndev) {
+    uint32_t* __restrict__ vout, uint2* __restrict__ digit_bounds, const uint32_t* __restrict__ ndev) {
   constexpr int kT = 256 * I, DPT = DIG / 256;
   if (ndev) {
     n = min(n, *ndev);
     if ((size_t)blockIdx.x * kT >= n && !(blockIdx.x == 0 && digit_bounds)) return;
   }
-  __shared__ uint2 s_buf[kT];  // (key, value) in digit order, then the second payload (xin)
+  __shared__ uint2 s_buf[kT];  // (key, value) in digit order
   __shared__ uint32_t s_wcnt[4][DIG];
   __shared__ uint32_t s_lbase[DIG];
   __shared__ uint32_t s_gbase[DIG];
@@ -337,14 +315,13 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
   const uint32_t bid = blockIdx.x;
   const size_t blk0 = (size_t)bid * kT;
   const size_t base = blk0 + (size_t)w * (64 * I);
-  uint32_t key[I], val[I], rank[I], xv[I];
+  uint32_t key[I], val[I], rank[I];
 #pragma unroll
   for (int j = 0; j < I; ++j) {
     const size_t e = base + (size_t)j * 64 + lane;
     const bool valid = e < n;
     key[j] = valid ? kin[e] : 0u;
     val[j] = iota ? (uint32_t)e : (valid ? vin[e] : 0u);
-    xv[j] = xin && valid ? xin[e] : 0u;
   }
   {  // global base of this block's digits: digit start (scan of totals) + block offset
     uint32_t tot[DPT], s = 0;
@@ -401,38 +378,19 @@ __global__ __launch_bounds__(256) void k_radix_scatter_wide(
     const uint32_t d = (key[j] >> shift) & mask;
     const uint32_t slot = s_lbase[d] + s_wcnt[w][d] + rank[j];
     if (e < n) s_buf[slot] = make_uint2(key[j], val[j]);
-    rank[j] = slot;  // (kept for the second payload)
   }
   __syncthreads();
   const uint32_t cnt = (size_t)n > blk0 ? (uint32_t)min((size_t)kT, (size_t)n - blk0) : 0u;
-  uint32_t dsts[I];
 #pragma unroll
   for (int r = 0; r < I; ++r) {
     const uint32_t i = (uint32_t)t + 256u * r;
-    dsts[r] = 0u;
     if (i < cnt) {
       const uint2 kv = s_buf[i];
       const uint32_t d = (kv.x >> shift) & mask;
       const uint32_t dst = s_gbase[d] + (i - s_lbase[d]);
       kout[dst] = kv.x;
       vout[dst] = kv.y;
-      dsts[r] = dst;
     }
-  }
-  if (!xin) return;  // block-uniform
-  // the second payload through the same LDS (no extra LDS: occupancy kept)
-  uint32_t* s_x = reinterpret_cast<uint32_t*>(s_buf);
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < I; ++j) {
-    const size_t e = base + (size_t)j * 64 + lane;
-    if (e < n) s_x[rank[j]] = xv[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < I; ++r) {
-    const uint32_t i = (uint32_t)t + 256u * r;
-    if (i < cnt) xout[dsts[r]] = s_x[i];
   }
 }
 
@@ -845,8 +803,7 @@ template <int I>
 static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt,
                                    bool vals_iota, size_t n, int begin_bit, int end_bit, uint32_t* status,
                                    uint32_t* totals, hipStream_t stream, bool* result_in_alt, uint2* digit_bounds,
-                                   bool* bounds_done, bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt,
-                                   const uint32_t* ndev) {
+                                   bool* bounds_done, bool sup_zeroed, const uint32_t* ndev) {
   const uint32_t nb = sort_blocks(n);
   if (wide_pass(end_bit - begin_bit) && n <= (size_t)kStCount) {
     const int bits = end_bit - begin_bit;
@@ -857,14 +814,14 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
       hipLaunchKernelGGL(k_radix_rowscan, dim3(512), dim3(256), 0, stream, status, nb, totals);
       hipLaunchKernelGGL((k_radix_scatter_wide<512, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
                          vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt, ndev);
+                         begin_bit == 0 ? digit_bounds : nullptr, ndev);
     } else {
       hipLaunchKernelGGL((k_radix_hist_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, (uint32_t)n, begin_bit,
                          bits, nb, status, ndev);
       hipLaunchKernelGGL(k_radix_rowscan, dim3(1024), dim3(256), 0, stream, status, nb, totals);
       hipLaunchKernelGGL((k_radix_scatter_wide<1024, I>), dim3(nb), dim3(256), 0, stream, keys, vals,
                          vals_iota ? 1 : 0, (uint32_t)n, begin_bit, bits, nb, status, totals, keys_alt, vals_alt,
-                         begin_bit == 0 ? digit_bounds : nullptr, xvals, xvals_alt, ndev);
+                         begin_bit == 0 ? digit_bounds : nullptr, ndev);
     }
     *result_in_alt = true;
     if (bounds_done) *bounds_done = digit_bounds && begin_bit == 0;
@@ -881,7 +838,7 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
     hipError_t e = hipMemsetAsync(sup, 0, 4 * 256 * (size_t)nsup * passes, stream);
     if (e != hipSuccess) return e;
   }
-  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt, *xi = xvals, *xo = xvals_alt;
+  uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
   bool iota = vals_iota;
   // balanced digits (13 tile-id bits -> 7 + 6, not 8 + 5): wider per-block
   // digit runs leave as longer contiguous stores in every pass
@@ -897,12 +854,11 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
     // a single pass over bits [0, end_bit) also writes the digit bounds
     uint2* db = (passes == 1 && begin_bit == 0) ? digit_bounds : nullptr;
     hipLaunchKernelGGL(k_radix_scatter<I>, dim3(nb), dim3(256), 0, stream, ki, vi, iota ? 1 : 0, (uint32_t)n, shift,
-                       bits, nb, status, ghist, ko, vo, sp, nsup, db, xi, xo, ndev);
+                       bits, nb, status, ghist, ko, vo, sp, nsup, db, ndev);
     if (db && bounds_done) *bounds_done = true;
     iota = false;
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;
-    uint32_t* tx = xi; xi = xo; xo = tx;
     *result_in_alt = !*result_in_alt;
   }
   return hipGetLastError();
@@ -911,9 +867,8 @@ static hipError_t radix_sort_tiled(uint32_t* keys, uint32_t* keys_alt, uint32_t*
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, bool vals_iota,
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt, uint2* digit_bounds, bool* bounds_done,
-                            bool sup_zeroed, uint32_t* xvals, uint32_t* xvals_alt, const uint32_t* ndev) {
+                            bool sup_zeroed, const uint32_t* ndev) {
   *result_in_alt = false;
-  if (!xvals != !xvals_alt) return hipErrorInvalidValue;
   if (bounds_done) *bounds_done = false;
   if (n == 0 || end_bit <= begin_bit) {
     if (vals_iota && n > 0) {
@@ -926,15 +881,15 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
     case kTinySortItems:
       return radix_sort_tiled<kTinySortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
                                               totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed,
-                                              xvals, xvals_alt, ndev);
+                                              ndev);
     case kSmallSortItems:
       return radix_sort_tiled<kSmallSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit,
                                                status, totals, stream, result_in_alt, digit_bounds, bounds_done,
-                                               sup_zeroed, xvals, xvals_alt, ndev);
+                                               sup_zeroed, ndev);
     default:
       return radix_sort_tiled<kSortItems>(keys, keys_alt, vals, vals_alt, vals_iota, n, begin_bit, end_bit, status,
                                           totals, stream, result_in_alt, digit_bounds, bounds_done, sup_zeroed,
-                                              xvals, xvals_alt, ndev);
+                                          ndev);
   }
 }
 

@@ -21,12 +21,9 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, 
                             size_t n, int begin_bit, int end_bit, uint32_t* status, uint32_t* totals,
                             hipStream_t stream, bool* result_in_alt,
                             uint2* digit_bounds = nullptr, bool* bounds_done = nullptr, bool sup_zeroed = false,
-                            uint32_t* xvals = nullptr, uint32_t* xvals_alt = nullptr,
                             const uint32_t* ndev = nullptr);
 // (ndev: capacity mode -- n is the capacity the grid is sized for, *ndev the
 // live key count, read on the device; reduce-then-scan / wide schedules only)
-// (xvals / xvals_alt: an optional second payload, moved like vals and ending
-// in the same buffer parity; reduce-then-scan schedule)
 // words of `status` a reduce-then-scan sort accumulates superblock sums in
 // (zero before the sort; 0 = none), at *offset_words
 size_t sort_sup_words(size_t n, int begin_bit, int end_bit, size_t* offset_words);
@@ -83,13 +80,13 @@ hipError_t launch_cap_counts(const unsigned long long* partial, uint64_t cap_rec
 // Gaussian) pair expansion.
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t* pair_depth = nullptr,
-                                 uint32_t cap_slots = 0xFFFFFFFFu, uint32_t cap_pairs = 0xFFFFFFFFu);
-// (pair_depth: each pair's depth key too -- the per-bin depth sort's input)
+                                 hipStream_t s, uint32_t cap_slots = 0xFFFFFFFFu,
+                                 uint32_t cap_pairs = 0xFFFFFFFFu);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
 // per-bin depth sort (pairs duplicated in index order): every bin's entries
-// stably by depth key (sdepth: the pairs' depth keys in bin-sorted order)
+// stably by depth key (gdepth: the Gaussians' depth keys, gathered through
+// each bin's Gaussian ids)
 // (bounds written first unless bounds_done); scratch: >= 2 NB uint2 (bins
 // beyond one LDS tile).  With lists: the per-tile exact lists, ranges,
 // tile_len and meta emitted straight from each sorted bin (what
@@ -98,7 +95,7 @@ hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const u
 uint32_t argsort_small_max();
 hipError_t launch_argsort_small(const uint32_t* keys, uint32_t n, uint32_t* perm, hipStream_t s);
 hipError_t launch_bin_depth_sort(const wgsr_raster_args& a, const uint32_t* sorted_keys, const uint32_t* sorted_g,
-                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* sdepth,
+                                 uint32_t NB, int bshift, uint2* bounds, bool bounds_done, const uint32_t* gdepth,
                                  uint32_t* okeys, uint32_t* ogid, void* scratch, hipStream_t s,
                                  uint32_t* lists = nullptr, uint2* ranges = nullptr, uint32_t* tile_len = nullptr,
                                  uint32_t* meta = nullptr);
