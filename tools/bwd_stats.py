@@ -61,7 +61,7 @@ def run(P, W, H, deg):
             "hit_entries": n - p2[0], "reach_rows": rows(reach), "p2_rows": rows(p2),
             # log2 bins: [1], [2, 3], [4, 7], ... [128, 256]
             "pixels_per_hit_entry_log2": list(out[32:40]), "lanes_per_p2_eval_log2": list(out[40:48]),
-            "p2_lanes": out[48], "p1_evals_without_p2": out[49]}
+            "p2_lanes": out[48], "p1_evals_without_p2": out[49], "p1_evals_in_all_live_batches": out[50]}
 
 
 if __name__ == "__main__":

@@ -121,7 +121,8 @@ __device__ __forceinline__ void render_bwd_quad_tile(
 #if WGSR_BWD_STATS
   uint32_t* const sStat = sHit;  // [0, 16) reach masks, [16, 32) phase-2 masks, [32, 40) pixels per hit
   sStat[lane] = 0;                // entry (log2 bins), [40, 48) lanes per phase-2 evaluation, [48] phase-2
-                                  // lanes, [49] phase-1 evaluations without a phase 2
+                                  // lanes, [49] phase-1 evaluations without a phase 2, [50] phase-1
+                                  // evaluations in batches live at every pixel of the quadrant
   __syncthreads();
 #endif
 
@@ -138,6 +139,9 @@ __device__ __forceinline__ void render_bwd_quad_tile(
   v2f na[Q];
   float T[Q], tb[Q];
   uint32_t last[Q], mq[Q];
+#if WGSR_BWD_STATS
+  uint32_t minq[Q];  // every pixel of quadrant p takes entries below minq[p]
+#endif
   uint32_t m = 0;
   // every quadrant's pixel loads first (one round trip; pixels outside the
   // image read pixel 0 and are zeroed after), then the sums
@@ -167,12 +171,20 @@ __device__ __forceinline__ void render_bwd_quad_tile(
     for (int off = 32; off >= 1; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
     mq[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)x);  // wave-uniform: an SGPR
     m = max(m, mq[p]);
+#if WGSR_BWD_STATS
+    uint32_t y = last[p];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) y = min(y, (uint32_t)__shfl_xor((int)y, off, 64));
+    minq[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)y);
+#endif
   }
   // entries behind every pixel's last contributor get no record: their slot
   // flags stay 0 (zeroed before the launch), and so does every entry no pixel
   // of the tile receives gradient from -- typically > 90 % of all pairs
   const uint32_t end = range.x + m;
-  float* const sPm = &sP[0][0] + sum10_slot(lane);  // this lane's store slot in an entry's row
+  // this lane's store slot in an entry's row (an LDS-space pointer: 32-bit address math)
+  using lds_f = __attribute__((address_space(3))) float;
+  const uint32_t sPm = (uint32_t)(size_t)((lds_f*)(&sP[0][0]) + sum10_slot(lane));  // (LDS byte address)
 
   // prefetch pipeline (back to front): records of the next batch in
   // registers, ids one batch further.  A batch's partial records are written
@@ -307,6 +319,7 @@ __device__ __forceinline__ void render_bwd_quad_tile(
 #if WGSR_BWD_STATS
         const uint32_t nv = (uint32_t)__builtin_popcountll(wave_ballot(v));
         if (lane == 0 && nv == 0) atomicAdd(&sStat[49], 1u);
+        if (lane == 0 && cfirst < minq[p]) atomicAdd(&sStat[50], 1u);  // the batch is live at every pixel
 #endif
         if (!wave_any(v)) continue;
 #if WGSR_BWD_STATS
@@ -354,7 +367,10 @@ __device__ __forceinline__ void render_bwd_quad_tile(
 #endif
       if (!hit) continue;  // no pixel of the tile: no partial
       const float gv[10] = {g01.x, g01.y, g23.x, g23.y, g4, g5, g67.x, g67.y, g89.x, g89.y};
-      wave_sum10_store_m(gv, sPm + 11 * j);
+      // (the entry's row offset on the scalar unit: one VALU add per entry)
+      uint32_t joff;
+      asm("s_mul_i32 %0, %1, 44" : "=s"(joff) : "s"(j));  // (else a 64-bit VALU multiply-add)
+      wave_sum10_store_m(gv, (lds_f*)(size_t)(sPm + joff));
       hitm |= 1ull << j;
     }
     hit_prev = hitm & (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull));

@@ -190,7 +190,10 @@ __device__ __forceinline__ void wave_sum10(const float (&v)[10], float (&S)[3]) 
 }
 // dstm = the entry's 10 floats + sum10_slot(lane): the lane part of the
 // address computed once by the caller, one address register for all stores
-__device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], float* dstm) {
+// (P: float* or an LDS-space float*, whose 32-bit address math per entry is
+// one VALU add instead of a 64-bit multiply-add)
+template <class P>
+__device__ __forceinline__ void wave_sum10_store_m(const float (&v)[10], P dstm) {
   float S[3];
   wave_sum10(v, S);
   const int lane = __lane_id();
