@@ -1640,6 +1640,16 @@ __global__ __launch_bounds__(256) void k_render_fwd1(
 #ifndef WGSR_FWD_DEC
 #define WGSR_FWD_DEC 1
 #endif
+// diagnostic build: per quadrant wave of k_render_fwd_dec -- [0] waves, [1]
+// batches, [2] entries in them, [3] survivors of the culling, [4] pair
+// iterations (survivor pairs), [5] batches with the n_touched bookkeeping,
+// [6] waves that stopped with every pixel done (wgsr_debug_fwd_stats)
+#ifndef WGSR_FWD_STATS
+#define WGSR_FWD_STATS 0
+#endif
+#if WGSR_FWD_STATS
+__device__ unsigned long long g_fwd_stats[8];
+#endif
 __global__ __launch_bounds__(256) void k_render_fwd_dec(
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ order, const uint32_t* __restrict__ point_g,
     const float4* __restrict__ splat, int W, int H, int gx, int ntiles, const float* __restrict__ bg,
@@ -1674,6 +1684,9 @@ __global__ __launch_bounds__(256) void k_render_fwd_dec(
     if (range.x + kFwdBatch < range.y) gnext = point_g[min(range.x + kFwdBatch + lane, last_i)];
   }
   uint32_t fl_gid = 0, fl_tv = 0;  // this lane's n_touched increment of the previous batch
+#if WGSR_FWD_STATS
+  uint32_t st_b = 0, st_e = 0, st_s = 0, st_p = 0, st_t = 0;
+#endif
   for (uint32_t b0 = range.x; b0 < range.y && dm != ~0ull; b0 += kFwdBatch) {  // (wave-uniform)
     const float4 pre[3] = {nA, nB, nC};
     const uint32_t gme = gcur;
@@ -1707,6 +1720,13 @@ __global__ __launch_bounds__(256) void k_render_fwd_dec(
       q[0] = 0.f; q[2] = 0.f; q[4] = 0.f; q[6] = 0.f; q[8] = 0.f; q[10] = 0.f;
       R.c[1] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+#if WGSR_FWD_STATS
+    ++st_b;
+    st_e += (uint32_t)cnt;
+    st_s += (uint32_t)n;
+    st_p += (uint32_t)((n + 1) / 2);
+    st_t += touch ? 1u : 0u;
+#endif
     // cross-lane LDS traffic of one wave: ordered by the hardware, and kept in
     // program order by the (instruction-free) wave barriers here and below
     __builtin_amdgcn_wave_barrier();
@@ -1722,6 +1742,17 @@ __global__ __launch_bounds__(256) void k_render_fwd_dec(
     __builtin_amdgcn_wave_barrier();
   }
   if (fl_tv != 0) atomicAdd(&n_touched[fl_gid], (int)fl_tv);
+#if WGSR_FWD_STATS
+  if (lane == 0) {
+    atomicAdd(&g_fwd_stats[0], 1ull);
+    atomicAdd(&g_fwd_stats[1], (unsigned long long)st_b);
+    atomicAdd(&g_fwd_stats[2], (unsigned long long)st_e);
+    atomicAdd(&g_fwd_stats[3], (unsigned long long)st_s);
+    atomicAdd(&g_fwd_stats[4], (unsigned long long)st_p);
+    atomicAdd(&g_fwd_stats[5], (unsigned long long)st_t);
+    atomicAdd(&g_fwd_stats[6], dm == ~0ull ? 1ull : 0ull);
+  }
+#endif
   {  // this quadrant's deepest contributor: tile_m4[4 tile + w]
     uint32_t mx = last;
 #pragma unroll
@@ -1945,3 +1976,13 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, c
 }
 
 }  // namespace wgsr
+
+#if WGSR_FWD_STATS
+// diagnostic build only: read and clear the forward's per-wave census
+extern "C" int wgsr_debug_fwd_stats(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wgsr::g_fwd_stats), sizeof(unsigned long long) * 8) != hipSuccess)
+    return 1;
+  unsigned long long z[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(wgsr::g_fwd_stats), z, sizeof(z)) != hipSuccess;
+}
+#endif
