@@ -232,22 +232,24 @@ __device__ __forceinline__ void wave_pair_counts(const uint3 ac, uint32_t khi, u
 constexpr int kPreWave = 64;
 
 // ---- k_preprocess2: the SH slab streams into LDS while the geometry runs ----
-// One wave of 64 Gaussians per workgroup.  The wave first queues its 64
-// rows' evaluated SH coefficients as LDS-DMA loads (global_load_lds: no VGPR
-// holds them in flight), in a chunk-major layout [chunk][lane] (chunk = 4
-// floats when rows are 16-byte aligned, else 1) so that each lane later
-// reads its own row conflict-free; then it loads the parameters and runs the
-// projection / covariance / rectangle / row-table work and writes the
-// geometry records; only then does it wait for the slab and evaluate the
-// colour -- for visible Gaussians only.  Measured alternatives (round 4,
-// removed in round 5; all bit-identical): the slab staged before the geometry
-// (k_preprocess, 90 us when this one was 86), SH coefficients in VGPRs (150
-// vs 103 us), the coalesced row-major slab (112 vs 102; round 5 again with
-// the twelve 1 KB loads unrolled at compile time for SH3 rows: 109.3 vs
-// 102.5 us, although tools/ubench/pre_copy.hip's copy of this access shape
-// runs 62 us row-major -- LDS read conflicts included -- vs 92 chunk-major),
-// one memory round trip per wave (106.7 vs 103.4), records staged through
-// LDS for contiguous stores (115.8 vs 106.7).
+// One wave of 64 Gaussians per workgroup.  The wave loads its parameters
+// (one round trip for all four arrays), then queues its 64 rows' evaluated
+// SH coefficients as LDS-DMA loads (global_load_lds: no VGPR holds them in
+// flight), in a chunk-major layout [chunk][lane] (chunk = 4 floats when rows
+// are 16-byte aligned, else 1) so that each lane later reads its own row
+// conflict-free; runs the projection / covariance / rectangle / row-table
+// work and writes the geometry records while the slab is in flight; only
+// then does it wait for the slab and evaluate the colour -- for visible
+// Gaussians only.  (The order matters: vmcnt retires in issue order, so with
+// the slab queued first every parameter use waited for the whole slab.)
+// Measured alternatives (all bit-identical): the slab staged before the
+// geometry (k_preprocess, 90 us when this one was 86), SH coefficients in
+// VGPRs (150 vs 103 us), the coalesced row-major slab (112 vs 102; round 5:
+// 109.3 vs 102.5 us, and again 107.2 vs 101.1 with the parameters first and
+// XOR-swizzled conflict-free LDS rows, although tools/ubench/pre_copy.hip's
+// copy of this access shape runs 62 us row-major vs 92 chunk-major), one
+// memory round trip per wave (106.7 vs 103.4), records staged through LDS
+// for contiguous stores (115.8 vs 106.7).
 template <int kD, int kCh>
 __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lane, f3 dir, uint32_t& cbits) {
   constexpr int K = (kD + 1) * (kD + 1), NF = 3 * K, NCH = (NF + kCh - 1) / kCh;
