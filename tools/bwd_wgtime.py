@@ -3,7 +3,8 @@ kernel's span is the tail, where fewer waves run than the GPU holds.
   VFLAGS=-DWGSR_BWD_WGTIME=1 bash tools/build_variant.sh wgtime /tmp/empty
   WGSR_LIB=wildgs-slam-blackwell_amd/lib/variants/wgtime.so python tools/bwd_wgtime.py
 Each workgroup (one wave, one tile) stores its s_memrealtime start / end
-(100 MHz) and hardware id.  Prints the span, the summed wave time, the
+(100 MHz) and hardware id (WGTIME_DUMP=file.npz: the first measured call's
+per-workgroup arrays).  Prints the span, the summed wave time, the
 resident-wave profile over the span (in tenths), the time from the last
 workgroup start to the end, and the LPT bound max(sum / slots, longest)."""
 import ctypes
@@ -69,6 +70,8 @@ def main():
         peak = max(prof)
         total = int(dur.sum())
         per_xcc_end = [int(t1[xcc == x].max()) for x in range(8) if (xcc == x).any()]
+        if rep == 1 and os.environ.get("WGTIME_DUMP"):
+            np.savez(os.environ["WGTIME_DUMP"], t0=t0, t1=t1, hw=hw.astype(np.int64))
         res.append({
             "span_us": span / 1e3, "sum_wave_us": total / 1e3, "mean_resident": total / span,
             "peak_resident": peak, "resident_profile_tenths": prof,
