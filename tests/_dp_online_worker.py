@@ -1,0 +1,95 @@
+"""One rank of tests/test_gpu_dp_online.py (launched by torch.distributed.run,
+two ranks sharing the box's GPU over gloo).
+
+1. The whole online loop data-parallel (wgsr.dp_online.DPOnlineMapper):
+   initialisation with densify / reset_opacity, keyframe insertions with
+   densify_and_prune and reset_opacity_nonvisible -> every rank's replica
+   digest, the events, the final PSNR.
+2. One data-parallel mapping step against its definition:
+   from the same state, rank r's view fwd+bwd, the flat gradient
+   all-reduce and Adam, versus one process summing the two views'
+   gradients before the same Adam step.
+Rank 0 writes the results as JSON to argv[1]."""
+import json
+import math
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (os.path.join(ROOT, "wildgs-slam-blackwell_amd", "python"), ROOT, HERE):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def main(out_path):
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    from test_gpu_online import _keyframes, _psnr
+    from wgsr.dp_online import DPOnlineMapper, allreduce_flat
+    kfs = _keyframes(4)
+    cfg = {"init_itr_num": 24, "init_gaussian_update": 10, "init_gaussian_reset": 15, "mapping_itr_num": 24,
+           "gaussian_th": 0.05, "gaussian_update_every": 12, "gaussian_update_offset": 5, "gaussian_reset": 19,
+           "window_size": 3}
+    m = DPOnlineMapper(sh_degree=0, device=DEV, config=cfg, seed=1)
+    m.initialize(kfs[:2])
+    for kf in kfs[2:]:
+        m.insert_keyframe(kf)
+    torch.cuda.synchronize()
+    digest = m.replica_digest().cpu()
+    kinds = [k for _, k, _ in m.events]
+    psnr = _psnr(m, kfs)
+
+    # 2. one step from the current state: DP versus the summed single-view gradients
+    ms = m.ms
+    st = ms.store
+    names = ms.GROUPS
+    snap = {n: (st.param(n).clone(), st.exp_avg(n).clone(), st.exp_avg_sq(n).clone()) for n in names}
+    steps0, skip0 = dict(ms.steps), set(getattr(ms, "_skip", set()))
+
+    def restore():
+        for n in names:
+            for dst, src in zip((st.param(n), st.exp_avg(n), st.exp_avg_sq(n)), snap[n]):
+                dst.copy_(src)
+        ms.steps = dict(steps0)
+        ms._skip = set(skip0)
+
+    def view_grad(kf):
+        ms.forward_backward(kf.cam, kf.image, kf.depth, kf.exposure_a, kf.exposure_b, m.bg)
+
+    views = kfs[:world]
+    view_grad(views[rank])
+    allreduce_flat([st.grad(n) for n in names])
+    ms.optimizer_step()
+    dp = {n: st.param(n).clone() for n in names}
+    restore()
+    acc = {n: torch.zeros_like(st.grad(n)) for n in names}
+    for kf in views:
+        view_grad(kf)
+        for n in names:
+            acc[n] += st.grad(n)
+    for n in names:
+        st.grad(n).copy_(acc[n])
+    ms.optimizer_step()
+    rel = {}
+    for n in names:
+        ref = st.param(n)
+        moved = (ref - snap[n][0]).abs().sum().item()
+        rel[n] = {"max_abs": float((dp[n] - ref).abs().max()), "moved_l1": moved,
+                  "rel_l1_of_update": float((dp[n] - ref).abs().sum()) / max(moved, 1e-30)}
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"world": world, "digest": digest.tolist(), "events": kinds, "psnr": psnr, "P": int(ms.P),
+                       "finite": all(bool(torch.isfinite(st.param(n)).all()) for n in names),
+                       "step_vs_summed_views": rel, "psnr_finite": math.isfinite(psnr)}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -484,7 +484,7 @@ class OnlineMapper:
             if self.iterations_after_densify_or_reset >= 20:
                 self._dino_term(neighbours, kf)
         self._max_nr = max(self._max_nr, int(out["num_rendered"]))
-        vis = out["radii"] > 0
+        vis = self._after_backward(out, update, reset == "nonvisible")
         if occ_window is not None:  # last iteration of a map_opt_online call (mapper.py:1174-1175)
             self._update_occ_aware_visibility(occ_window)
         if update:
@@ -528,15 +528,7 @@ class OnlineMapper:
         L = _lib.load()
         p = _lib.ptr
         if "dexposure_partials" in out:  # the loss backward's per-block partials, summed in the step (as replays do)
-            g = out["dexposure_partials"]
-            hs = np.zeros(6, dtype=np.float32)
-            hs[0], hs[1] = lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)
-            hs[2:4].view(np.int64)[0] = self.bank.slots[kf.uid]
-            dv = torch.from_numpy(hs).to(self.dev, non_blocking=True)
-            with torch.cuda.device(self.dev):
-                _lib.check(L.wgsr_exposure_step(p(self.bank.ex), p(dv[2:4]), p(g), int(g.shape[0]), p(dv[0:2]),
-                                                p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None, None,
-                                                _lib.stream_handle(self.dev)))
+            self._exposure_apply(kf.uid, out["dexposure_partials"], n, lr)
             return
         da, db = out["dexposure_a"], out["dexposure_b"]
         g = da if db.data_ptr() == da.data_ptr() + 4 else torch.cat([da.reshape(1), db.reshape(1)])
@@ -544,6 +536,39 @@ class OnlineMapper:
         t = _lib.AdamTensor(prm, g.data_ptr(), m, v, 2, lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n))
         with torch.cuda.device(self.dev):
             _lib.check(L.wgsr_adam_step((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, _lib.stream_handle(self.dev)))
+
+    def _exposure_apply(self, uid, g, n, lr):
+        """Adam step n of keyframe ``uid``'s exposure row from the loss
+        backward's per-block (a, b) partials ``g`` [rows, 2] (summed in the
+        step kernel)."""
+        from . import _lib
+        L = _lib.load()
+        p = _lib.ptr
+        hs = np.zeros(6, dtype=np.float32)
+        hs[0], hs[1] = lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)
+        hs[2:4].view(np.int64)[0] = self.bank.slots[uid]
+        dv = torch.from_numpy(hs).to(self.dev, non_blocking=True)
+        with torch.cuda.device(self.dev):
+            _lib.check(L.wgsr_exposure_step(p(self.bank.ex), p(dv[2:4]), p(g), int(g.shape[0]), p(dv[0:2]),
+                                            p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None, None,
+                                            _lib.stream_handle(self.dev)))
+
+    # ---- hooks of the keyframe-view data-parallel mapper (wgsr.dp_online) ----
+    def _pick(self, draw):
+        """This process's keyframe draw of one iteration (one draw here;
+        DPOnlineMapper draws one per rank and keeps its own)."""
+        return draw()
+
+    def _after_backward(self, out, update: bool, need_vis: bool):
+        """Between the iteration's backward and its densify / opacity reset /
+        optimiser steps: -> the visibility filter of reset_opacity_nonvisible
+        (DPOnlineMapper reduces gradients and statistics over the ranks here)."""
+        return out["radii"] > 0
+
+    def _record_occ(self, kf, out):
+        """initialize_map_opt's occlusion-aware visibility of the rendered
+        keyframe (mapper.py:1025-1027)."""
+        self.occ_vis[kf.uid] = (out["n_touched"] > 0).long()
 
     def _settle_replays(self):
         """The graph replays' overflow bookkeeping (IterationGraphs.account)
@@ -605,11 +630,11 @@ class OnlineMapper:
         stack = list(self.window)
         self.bank.sync(self.keyframes)
         for it in range(c["init_itr_num"] if iters is None else iters):
-            kf = self.keyframes[stack[int(self.rng.choice(len(stack)))]]
+            kf = self.keyframes[stack[self._pick(lambda: int(self.rng.choice(len(stack))))]]
             update = it % c["init_gaussian_update"] == 0
             reset = "all" if self.iteration_count + 1 == c["init_gaussian_reset"] else None
             out = self._iteration(kf, [kf.uid], True, update, reset)
-            self.occ_vis[kf.uid] = (out["n_touched"] > 0).long()
+            self._record_occ(kf, out)
         self._settle_replays()
 
     def prepare_keyframe(self, kf: Keyframe, keep=None):
@@ -823,7 +848,7 @@ class OnlineMapper:
         stack = [k for k in self.keyframes]
         self.bank.sync(self.keyframes)
         for _ in range(iters):
-            ci = int(self.rng.choice(len(stack)))
+            ci = self._pick(lambda: int(self.rng.choice(len(stack))))
             kf = self.keyframes[stack[ci]]
             if (self.graphs is not None and self.iterations_after_densify_or_reset + 1 >= 200
                     and self.graphs.step(kf, [stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))],
@@ -854,6 +879,7 @@ class OnlineMapper:
                 self._max_nr = max(self._max_nr, int(out["num_rendered"]))
                 if self.iterations_after_densify_or_reset >= 200:
                     self._dino_term(nbrs, kf)
+            self._after_backward(out, False, False)
             ms.optimizer_step()
             ms.lr["xyz"] = lr_helper(self.iteration_count, self.lr_xyz[0], self.lr_xyz[1],
                                      lr_delay_mult=c["position_lr_delay_mult"], max_steps=c["position_lr_max_steps"])
@@ -887,8 +913,8 @@ class OnlineMapper:
         self.bank.sync(self.keyframes)
         ms = self.ms
         for it in range(iters):
-            ci = (int(cdf.searchsorted(self.rng.random(), side="right")) if fast
-                  else int(self.rng.choice(len(stack), p=prob)))
+            ci = self._pick(lambda: int(cdf.searchsorted(self.rng.random(), side="right")) if fast
+                            else int(self.rng.choice(len(stack), p=prob)))
             kf = self.keyframes[stack[ci]]
             nb = [stack[j] for j in range(max(0, ci - 2), min(len(stack), ci + 3))]
             nxt = self.iteration_count + 1
