@@ -247,7 +247,9 @@ constexpr int kPreWave = 64;
 // VGPRs (150 vs 103 us), the coalesced row-major slab (112 vs 102; round 5:
 // 109.3 vs 102.5 us, and again 107.2 vs 101.1 with the parameters first and
 // XOR-swizzled conflict-free LDS rows, although tools/ubench/pre_copy.hip's
-// copy of this access shape runs 62 us row-major vs 92 chunk-major), one
+// copy of this access shape runs 62 us row-major vs 92 chunk-major; a
+// 16-row-group slab -- each load 16 rows x 64 contiguous bytes, rotated for
+// conflict-free reads -- 103.7-108.0 vs 101.1-102.0 over three A/B pairs), one
 // memory round trip per wave (106.7 vs 103.4), records staged through LDS
 // for contiguous stores (115.8 vs 106.7).
 template <int kD, int kCh>
