@@ -87,3 +87,31 @@ def test_single_row_and_batched_shapes():
         u = net(x)
         assert u.shape == x.shape[:-1]
         torch.testing.assert_close(u, _torch_mlp(net, x), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,C,p", [(1275, 384, 0.2), (972, 384, 0.0), (300, 128, 0.2), (17, 64, 0.5)])
+def test_matrix_core_forward_is_bitwise_the_valu_forward(N, C, p):
+    """k_mlp_fwd_small (layers 1-2 on v_mfma_f32_16x16x4_f32) against the
+    VALU kernel k_mlp_fwd (taken when X is not 16-byte aligned): every output
+    -- both dropout-masked hidden layers, the pre-activation and the
+    softplus -- bit for bit (the matrix-core step is a k-ordered fmaf chain)."""
+    from wgsr import _lib
+    L = _lib.load()
+    torch.manual_seed(7)
+    f = dict(device=DEV, dtype=torch.float32)
+    W1, b1 = torch.randn(64, C, **f) * 0.1, torch.randn(64, **f) * 0.1
+    W2, b2 = torch.randn(64, 64, **f) * 0.1, torch.randn(64, **f) * 0.1
+    W3, b3 = torch.randn(1, 64, **f) * 0.1, torch.randn(1, **f) * 0.1
+    x = torch.randn(N, C, **f)
+    xm = torch.empty(N * C + 1, **f)[1:]          # the same rows at a 4-byte offset
+    xm.copy_(x.reshape(-1))
+    outs = []
+    for X in (x, xm):
+        o = [torch.full((N, 64), float("nan"), **f), torch.full((N, 64), float("nan"), **f),
+             torch.full((N,), float("nan"), **f), torch.full((N,), float("nan"), **f)]
+        p_ = _lib.ptr
+        _lib.check(L.wgsr_mlp_forward(N, C, p_(X), p_(W1), p_(b1), p_(W2), p_(b2), p_(W3), p_(b3), float(p), 12345,
+                                      p_(o[0]), p_(o[1]), p_(o[2]), p_(o[3]), _lib.stream_handle(DEV)))
+        outs.append(o)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -141,12 +141,13 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int N, int C, const float* __re
 // features and W2 streamed into LDS in ONE round of LDS-DMA loads
 // (global_load_lds, 16 B per lane: no staging registers, every load in
 // flight at once -- instead of a K-slab loop of dependent load -> barrier ->
-// multiply-add steps), then layer 1 as C/4 steps of four k with b128 LDS
-// reads (each wave's four rows broadcast; lane c reads row c of W1, whose
-// float4 chunks are XOR-swizzled by c mod 16 so the 16 lanes of every b128
-// pass hit distinct banks), layers 2 and 3 from LDS.  Same sums in the same
-// k order as k_mlp_fwd: bit-identical outputs.
+// multiply-add steps), then layers 1 and 2 on the f32 matrix cores (one
+// 16 x 16 output tile per wave, one b32 LDS read per operand and step) and
+// layer 3 from LDS.  Same sums in the same k order as k_mlp_fwd: bit-identical
+// outputs.  (The VALU form -- b128 LDS reads, each wave's four rows
+// broadcast, 16 FMAs per five reads -- ran 18.9 us on the mapper's 1275 rows.)
 constexpr int kSmallRows = 16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __host__ __device__ inline size_t mlp_small_lds(int C) {
   return sizeof(float) * ((size_t)(kHid + kSmallRows) * C + (size_t)kHid * kHid + (size_t)kSmallRows * 68);
 }
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
   float* const sH = reinterpret_cast<float*>(sW2 + kHid * 16);  // [16][68] layer inputs
   if (seed_dev) seed = *seed_dev;
   const uint32_t seed2 = sg.seed2_dev ? *sg.seed2_dev : sg.seed2;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, col = t & 63, rq = t >> 6;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int r0 = blockIdx.x * kSmallRows;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   {
@@ -204,7 +205,8 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
       const int sl = (w * NX + q) * 64 + lane, r = sl / C4, k4 = sl - r * C4;
       const int rr = min(r0 + r, N - 1);
       const float4* src = rr < sg.N1 ? Xv + (size_t)rr * C4 : reinterpret_cast<const float4*>(sg.X2) + (size_t)(rr - sg.N1) * C4;
-      __builtin_amdgcn_global_load_lds((const void*)(src + k4), (lds_ptr)(sX + (w * NX + q) * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(src + (k4 ^ (r & 15))), (lds_ptr)(sX + (w * NX + q) * 64), 16, 0,
+                                       0);
     }
 #pragma unroll
     for (int q = 0; q < NW2; ++q) {
@@ -215,50 +217,50 @@ __global__ __launch_bounds__(256) void k_mlp_fwd_small(int N, const float* __res
     __builtin_amdgcn_s_waitcnt(0);  // (this wave's DMA has landed; the barrier covers the others)
   }
   __syncthreads();
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int sw = col & 15;
-#pragma unroll 4
-  for (int k4 = 0; k4 < C4; ++k4) {
-    const float4 b = sW[col * C4 + (k4 ^ sw)];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 a = sX[(4 * rq + i) * C4 + k4];
-      acc[i] = fmaf(a.x, b.x, acc[i]);
-      acc[i] = fmaf(a.y, b.y, acc[i]);
-      acc[i] = fmaf(a.z, b.z, acc[i]);
-      acc[i] = fmaf(a.w, b.w, acc[i]);
-    }
+  // layer 1 on the matrix cores: wave w owns output columns 16 w .. 16 w + 15
+  // of the 16 rows; v_mfma_f32_16x16x4_f32 step m sums k = 4 m + (lane >> 4)
+  // (A: row lane & 15 of X, B: column 16 w + (lane & 15) of W1), and its
+  // result is the k-ordered fmaf chain -- the same sums in the same order as
+  // the VALU kernels (k_mlp_fwd): bit-identical.  X and W1 rows sit in LDS
+  // with their float4 chunks XOR-swizzled by row & 15, so the 64 lanes' b32
+  // reads of a step hit 64 distinct banks.
+  const int ar = lane & 15, kh = lane >> 4, wc = 16 * w + ar;
+  const float* const sXf = reinterpret_cast<const float*>(sX);
+  const float* const sWf = reinterpret_cast<const float*>(sW);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int m = 0; m < C4; ++m) {
+    const float a = sXf[4 * (ar * C4 + (m ^ ar)) + kh];
+    const float b = sWf[4 * (wc * C4 + (m ^ (wc & 15))) + kh];
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
   }
+  // D: column wc, rows 4 kh + i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = 4 * rq + i;
-    float v = fmaxf(acc[i] + b1[col], 0.f);
-    v = seg2_keep(seed, sg, seed2, 0, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
-    sH[r * 68 + col] = v;
-    if (r0 + r < N) h1d[(size_t)(r0 + r) * kHid + col] = v;
-    acc[i] = 0.f;
+    const int r = 4 * kh + i;
+    float v = fmaxf(acc[i] + b1[wc], 0.f);
+    v = seg2_keep(seed, sg, seed2, 0, (uint32_t)(r0 + r), wc, p) ? v * scale : 0.f;
+    sH[r * 68 + wc] = v;
+    if (r0 + r < N) h1d[(size_t)(r0 + r) * kHid + wc] = v;
   }
   __syncthreads();
-#pragma unroll 4
-  for (int k4 = 0; k4 < 16; ++k4) {
-    const float4 b = sW2[col * 16 + (k4 ^ sw)];
+  // layer 2 likewise (sH rows of 68 floats: conflict-free without a swizzle)
+  const float* const sW2f = reinterpret_cast<const float*>(sW2);
+  acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 a = *reinterpret_cast<const float4*>(&sH[(4 * rq + i) * 68 + 4 * k4]);
-      acc[i] = fmaf(a.x, b.x, acc[i]);
-      acc[i] = fmaf(a.y, b.y, acc[i]);
-      acc[i] = fmaf(a.z, b.z, acc[i]);
-      acc[i] = fmaf(a.w, b.w, acc[i]);
-    }
+  for (int m = 0; m < 16; ++m) {
+    const float a = sH[ar * 68 + 4 * m + kh];
+    const float b = sW2f[4 * (wc * 16 + (m ^ (wc & 15))) + kh];
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = 4 * rq + i;
-    float v = fmaxf(acc[i] + b2[col], 0.f);
-    v = seg2_keep(seed, sg, seed2, 1, (uint32_t)(r0 + r), col, p) ? v * scale : 0.f;
-    sH[r * 68 + col] = v;  // layer-3 input
-    if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + col] = v;
+    const int r = 4 * kh + i;
+    float v = fmaxf(acc[i] + b2[wc], 0.f);
+    v = seg2_keep(seed, sg, seed2, 1, (uint32_t)(r0 + r), wc, p) ? v * scale : 0.f;
+    sH[r * 68 + wc] = v;  // layer-3 input
+    if (r0 + r < N) h2d[(size_t)(r0 + r) * kHid + wc] = v;
   }
   __syncthreads();
   if (t < kSmallRows && r0 + t < N) {
