@@ -115,3 +115,35 @@ def test_matrix_core_forward_is_bitwise_the_valu_forward(N, C, p):
         outs.append(o)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,C,p", [(1275, 384, 0.2), (130, 128, 0.0), (17, 64, 0.5)])
+def test_matrix_core_backward_is_bitwise_the_valu_backward(N, C, p):
+    """k_mlp_bwd2 (its three 64 x 64 x 64 products on v_mfma_f32_16x16x4_f32)
+    against the VALU kernel k_mlp_bwd (taken when X is not 16-byte aligned):
+    the summed parameter gradient bit for bit."""
+    from wgsr import _lib
+    L = _lib.load()
+    torch.manual_seed(8)
+    f = dict(device=DEV, dtype=torch.float32)
+    W1, b1 = torch.randn(64, C, **f) * 0.1, torch.randn(64, **f) * 0.1
+    W2, b2 = torch.randn(64, 64, **f) * 0.1, torch.randn(64, **f) * 0.1
+    W3, b3 = torch.randn(1, 64, **f) * 0.1, torch.randn(1, **f) * 0.1
+    x = torch.randn(N, C, **f)
+    xm = torch.empty(N * C + 1, **f)[1:]
+    xm.copy_(x.reshape(-1))
+    du = torch.randn(N, **f)
+    p_ = _lib.ptr
+    st = _lib.stream_handle(DEV)
+    h1, h2, o, u = (torch.empty(N, 64, **f), torch.empty(N, 64, **f), torch.empty(N, **f), torch.empty(N, **f))
+    _lib.check(L.wgsr_mlp_forward(N, C, p_(x), p_(W1), p_(b1), p_(W2), p_(b2), p_(W3), p_(b3), float(p), 99,
+                                  p_(h1), p_(h2), p_(o), p_(u), st))
+    nscr = int(L.wgsr_mlp_scratch_bytes(N, C)) // 4
+    G = []
+    for X in (x, xm):
+        scr = torch.empty(max(nscr, 1), **f)
+        g = torch.full((int(L.wgsr_mlp_grad_floats(C)),), float("nan"), **f)
+        _lib.check(L.wgsr_mlp_backward(N, C, p_(X), p_(W2), p_(W3), float(p), p_(h1), p_(h2), p_(o), p_(du), p_(scr),
+                                       p_(g), st))
+        G.append(g)
+    assert torch.isfinite(G[0]).all() and torch.equal(G[0], G[1])

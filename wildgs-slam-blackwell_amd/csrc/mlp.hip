@@ -393,28 +393,13 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int N, int C, const float* __re
 }
 
 // k_mlp_bwd with every global load issued up front: the kept activations,
-// W2 and the X slab stream into LDS in their natural row-major layouts by
-// LDS-DMA (no staging registers, one round trip instead of three), and the
-// products read those operands as [k][column] (one b128 read per k, lanes
-// on consecutive columns).  Rows past N re-read row N - 1 (finite) and get a
+// W2 and the X slab stream into LDS by LDS-DMA (no staging registers, one
+// round trip instead of three), and the three products run on the matrix
+// cores (tile_mac_mfma).  Rows past N re-read row N - 1 (finite) and get a
 // zero upstream gradient, so they add nothing.  Same products summed in the
-// same order as k_mlp_bwd: bit-identical partials.
-__device__ __forceinline__ void tile_mac_kc(const float (*A)[kLd], const float* __restrict__ Bt, int ty, int tx,
-                                            float (&acc)[4][4]) {
-#pragma unroll 8
-  for (int k = 0; k < 64; ++k) {
-    float a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = A[ty * 4 + i][k];
-    const float4 b4 = *reinterpret_cast<const float4*>(&Bt[k * 64 + tx * 4]);
-    const float b[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-  }
-}
-
+// same order as k_mlp_bwd: bit-identical partials.  (Its VALU form -- one
+// b128 LDS read per k, 16 FMAs per five reads -- ran 14.9 us on the mapper's
+// 1275 rows.)
 // (two row segments as k_mlp_fwd_small's: rows >= N1 take X2's rows and the
 // upstream gradient du2 x du_scale2)
 struct MlpBwdSeg2 {
@@ -423,19 +408,46 @@ struct MlpBwdSeg2 {
   const float* du2;
   float du_scale2;
 };
+
+// The three 64 x 64 x 64 products of k_mlp_bwd2 on the f32 matrix cores.
+// A operands: [64][kLdM] LDS rows (16 rows x 4 k of one step hit 64 distinct
+// banks); B operands: [64][64] images whose element (k, c) sits at bsw(k, c),
+// the float4 chunks of row k XOR-moved by 16 (k & 3) floats, so the four k of
+// a step (lanes 16 apart, same column) hit distinct banks.
+constexpr int kLdM = 68;
+__device__ __forceinline__ int bsw(int k, int c) { return k * 64 + (c ^ ((k & 3) << 4)); }
+
+// acc[j]: this wave's 16 x 16 tile j of sum_k A[row][k] Bt[k][col] -- rows
+// 16 w + 4 (lane >> 4) + i (i: the register), columns 16 j + (lane & 15) --
+// as v_mfma_f32_16x16x4_f32 steps over k = 0 .. 63 in order: the k-ordered
+// fmaf chain of k_mlp_bwd's tile_mac_cw, bit for bit.
+__device__ __forceinline__ void tile_mac_mfma(const float (*A)[kLdM], const float* __restrict__ Bt, int w, int lane,
+                                              f32x4 (&acc)[4]) {
+  const int ar = 16 * w + (lane & 15), kh = lane >> 4, bc = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int m = 0; m < 16; ++m) {
+    const int k = 4 * m + kh;
+    const float a = A[ar][k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bt[bsw(k, 16 * j + bc)], acc[j], 0, 0, 0);
+  }
+}
 __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __restrict__ X,
                                                   const float* __restrict__ W2, const float* __restrict__ W3, float p,
                                                   const float* __restrict__ h1d, const float* __restrict__ h2d,
                                                   const float* __restrict__ o_pre, const float* __restrict__ du,
                                                   float* __restrict__ part, float du_scale, const MlpBwdSeg2 sg) {
-  __shared__ float4 sH1v[1024], sH2v[1024], sW2v[1024], sXv[1024];  // [64][64] each, natural layouts
-  __shared__ float sA[64][kLd], sB[64][kLd];
+  __shared__ float4 sH1v[1024], sH2v[1024], sW2v[1024], sXv[1024];  // [64][64] each (sH1, sW2, sX: bsw layout)
+  __shared__ float sA[64][kLdM], sB[64][kLdM];
   __shared__ float sDo[kRows];
   const float* const sH1 = reinterpret_cast<const float*>(sH1v);
   const float* const sH2 = reinterpret_cast<const float*>(sH2v);
   const float* const sW2 = reinterpret_cast<const float*>(sW2v);
   const float* const sX = reinterpret_cast<const float*>(sXv);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, ty = t >> 4, tx = t & 15;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int r0 = blockIdx.x * kRows, c0 = 64 * (int)blockIdx.y;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   float o = 0.f, g = 0.f;
@@ -449,15 +461,16 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // wave w fills float4 slots [(4 w + q) 64, +64): row sl / 16, chunk sl % 16
       const int sl = (4 * w + q) * 64 + lane, row = min(r0 + (sl >> 4), N - 1), c4 = sl & 15;
-      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(h1d) + (size_t)row * 16 + c4),
+      const int cs = c4 ^ (((sl >> 4) & 3) << 2);  // the bsw image's source chunk
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(h1d) + (size_t)row * 16 + cs),
                                        (lds_ptr)(sH1v + (4 * w + q) * 64), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(h2d) + (size_t)row * 16 + c4),
                                        (lds_ptr)(sH2v + (4 * w + q) * 64), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(W2) + sl),
+      __builtin_amdgcn_global_load_lds((const void*)(reinterpret_cast<const float4*>(W2) + (sl >> 4) * 16 + cs),
                                        (lds_ptr)(sW2v + (4 * w + q) * 64), 16, 0, 0);
       const float4* xr = row < sg.N1 ? reinterpret_cast<const float4*>(X) + (size_t)row * C4
                                      : reinterpret_cast<const float4*>(sg.X2) + (size_t)(row - sg.N1) * C4;
-      __builtin_amdgcn_global_load_lds((const void*)(xr + (c0 >> 2) + c4), (lds_ptr)(sXv + (4 * w + q) * 64), 16, 0,
+      __builtin_amdgcn_global_load_lds((const void*)(xr + (c0 >> 2) + cs), (lds_ptr)(sXv + (4 * w + q) * 64), 16, 0,
                                        0);
     }
   }
@@ -496,13 +509,14 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
     sB[c][r] = v;
   }
   __syncthreads();
+  const int orow = 16 * w + 4 * (lane >> 4), ocol = lane & 15;  // this lane's rows orow + i, columns 16 j + ocol
   if (head) {  // dW2[o][i] = sum_r dA2[r][o] h1[r][i]
-    float acc[4][4] = {};
-    tile_mac_kc(sB, sH1, ty, tx, acc);
+    f32x4 acc[4];
+    tile_mac_mfma(sB, sH1, w, lane, acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) gW2[(ty * 4 + i) * kHid + tx * 4 + j] = acc[i][j];
+      for (int j = 0; j < 4; ++j) gW2[(orow + i) * kHid + 16 * j + ocol] = acc[j][i];
   }
   if (head && t < kHid) {
     float s = 0.f;
@@ -510,15 +524,15 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
     gb2[t] = s;
   }
   // dA1[r][i] = sum_o dA2[r][o] W2[o][i] through ReLU / dropout, into sB as [i][r]
-  float acc1[4][4] = {};
-  tile_mac_kc(sA, sW2, ty, tx, acc1);
+  f32x4 acc1[4];
+  tile_mac_mfma(sA, sW2, w, lane, acc1);
   __syncthreads();  // (every wave is done reading sB as dA2 transposed)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int r = ty * 4 + i, c = tx * 4 + j;
-      sB[c][r] = sH1[r * 64 + c] > 0.f ? acc1[i][j] * scale : 0.f;
+      const int r = orow + i, c = 16 * j + ocol;
+      sB[c][r] = sH1[bsw(r, c)] > 0.f ? acc1[j][i] * scale : 0.f;
     }
   __syncthreads();
   if (head && t < kHid) {
@@ -527,12 +541,12 @@ __global__ __launch_bounds__(256) void k_mlp_bwd2(int N, int C, const float* __r
     gb1[t] = s;
   }
   // this workgroup's 64-column chunk of dW1[o][c] = sum_r dA1[r][o] X[r][c]
-  float acc[4][4] = {};
-  tile_mac_kc(sB, sX, ty, tx, acc);
+  f32x4 acc[4];
+  tile_mac_mfma(sB, sX, w, lane, acc);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) gW1[(size_t)(ty * 4 + i) * C + c0 + tx * 4 + j] = acc[i][j];
+    for (int j = 0; j < 4; ++j) gW1[(size_t)(orow + i) * C + c0 + 16 * j + ocol] = acc[j][i];
 }
 
 // two-stage fixed-order sum over the row blocks' partials: grid.y segments of
@@ -547,7 +561,8 @@ __global__ __launch_bounds__(256) void k_mlp_reduce_seg(int nblocks, int total, 
   if (e >= total) return;
   const int b0 = blockIdx.y * seglen, b1 = min(nblocks, b0 + seglen);
   float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += part[(size_t)b * total + e];
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) s += part[(size_t)b * total + e];  // (unrolled: the loads in flight together)
   float* d = &seg[(size_t)blockIdx.y * total + e];
   *d = acc ? *d + s : s;
 }
