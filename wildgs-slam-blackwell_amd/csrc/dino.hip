@@ -82,18 +82,21 @@ __global__ __launch_bounds__(256) void k_dino_similarity(const float* __restrict
 
 // The same tiles with both 32-row operand blocks streamed into LDS ONCE, over
 // the whole feature dimension (LDS-DMA, 16 B per lane, every load in flight
-// at once) instead of 12 dependent chunk rounds; float4 chunk k4 of row r
-// sits at k4 ^ ((r >> 1) & 15) so that the 16 column rows 2 tx a wave reads
-// at one k land on distinct banks.  Same products in the same k order:
-// bit-identical to k_dino_similarity.  C % 64 == 0, C <= 384 (96 KB of LDS).
+// at once) instead of 12 dependent chunk rounds, and the products on the f32
+// matrix cores: wave w owns the 16 x 16 quarter (w >> 1, w & 1) of the tile,
+// v_mfma_f32_16x16x4_f32 step m summing k = 4 m + (lane >> 4) -- a k-ordered
+// fmaf chain, so the same products in the same k order as k_dino_similarity:
+// bit-identical.  Float4 chunk k4 of row r sits at k4 ^ (r & 15), so the 16
+// rows x 4 k of a step's b32 reads land on 64 distinct banks.  C % 64 == 0,
+// C <= 384 (96 KB of LDS).  (The VALU form, 2 x 2 outputs per thread from
+// b128 reads, ran 13.4 us on the mapper's 303-row sample.)
 constexpr int kSim2MaxC = 384;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_dino_similarity2(const float* __restrict__ fn, int N, int C,
-                                                          float* __restrict__ S) {
+                                                         float* __restrict__ S) {
   extern __shared__ float4 s_sim[];  // [2][32][C / 4]
-  const int t = threadIdx.x, tx = t & 15, ty = t >> 4, w = t >> 6, lane = t & 63;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int i0 = blockIdx.y * kSimTile, j0 = blockIdx.x * kSimTile, C4 = C >> 2;
-  float4* const sa = s_sim;
-  float4* const sb = s_sim + kSimTile * C4;
   {
     typedef __attribute__((address_space(3))) void* lds_ptr;
     const float4* src = reinterpret_cast<const float4*>(fn);
@@ -102,35 +105,27 @@ __global__ __launch_bounds__(256) void k_dino_similarity2(const float* __restric
       const int sl = b + lane;
       const int op = sl >= per_op, s2 = sl - op * per_op, r = s2 / C4, k4 = s2 - r * C4;
       const int row = min((op ? j0 : i0) + r, N - 1);  // rows past N: a valid row, never stored
-      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)row * C4 + (k4 ^ ((r >> 1) & 15))),
+      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)row * C4 + (k4 ^ (r & 15))),
                                        (lds_ptr)(s_sim + b), 16, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(0);
   }
   __syncthreads();
-  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  const int ra = 2 * ty, rb = 2 * tx;
-  const int za = ty & 15, zb = tx & 15;  // (r >> 1) & 15 of rows 2 ty (+1) and 2 tx (+1)
-  for (int k4 = 0; k4 < C4; ++k4) {
-    const float4 a0 = sa[ra * C4 + (k4 ^ za)], a1 = sa[(ra + 1) * C4 + (k4 ^ za)];
-    const float4 b0 = sb[rb * C4 + (k4 ^ zb)], b1 = sb[(rb + 1) * C4 + (k4 ^ zb)];
-    const float av0[4] = {a0.x, a0.y, a0.z, a0.w}, av1[4] = {a1.x, a1.y, a1.z, a1.w};
-    const float bv0[4] = {b0.x, b0.y, b0.z, b0.w}, bv1[4] = {b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      acc[0][0] = fmaf(av0[q], bv0[q], acc[0][0]);
-      acc[0][1] = fmaf(av0[q], bv1[q], acc[0][1]);
-      acc[1][0] = fmaf(av1[q], bv0[q], acc[1][0]);
-      acc[1][1] = fmaf(av1[q], bv1[q], acc[1][1]);
-    }
+  const int lr = lane & 15, kh = lane >> 4;
+  const int ra = 16 * (w >> 1) + lr, rb = 16 * (w & 1) + lr;  // this lane's A row, B row (= output column)
+  const float* const fa = reinterpret_cast<const float*>(s_sim) + (size_t)4 * ra * C4;
+  const float* const fb = reinterpret_cast<const float*>(s_sim) + (size_t)4 * (kSimTile + rb) * C4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < C4; ++m) {
+    const int o = 4 * (m ^ lr) + kh;  // (ra & 15 == rb & 15 == lr)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[o], fb[o], acc, 0, 0, 0);
   }
+  const int j = j0 + rb;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int i = i0 + 2 * ty + a, j = j0 + 2 * tx + b;
-      if (i < N && j < N) S[(size_t)i * N + j] = acc[a][b];
-    }
+  for (int q = 0; q < 4; ++q) {
+    const int i = i0 + 16 * (w >> 1) + 4 * kh + q;
+    if (i < N && j < N) S[(size_t)i * N + j] = acc[q];
+  }
 }
 
 // one wave per sample i: the selection, its mean / variance and the
