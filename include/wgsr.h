@@ -42,9 +42,10 @@ extern "C" {
  * stays valid until the caller releases it.  `bytes` may be 0.  Within one
  * library call a callback may be called twice for the same buffer (the
  * forward's binning buffer: a predicted size before its host wait, then the
- * exact size): the library uses the pointer of the last call and has written
- * nothing through the first, so a callback may narrow its first allocation
- * when that is large enough (as wgsr's own wrappers do) or allocate anew. */
+ * exact size) only when the predicted size was too small: the library then
+ * uses the pointer of the second call and has written nothing through the
+ * first, which the callback may release or grow.  A large-enough prediction
+ * is used as it is (no second call). */
 typedef void* (*wgsr_alloc_fn)(void* ctx, size_t bytes);
 
 /* The rasterisation inputs shared by forward and backward: the tensors and
@@ -107,6 +108,17 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap,
                                void* stream);
 /* Bytes of the binning buffer wgsr_rasterize_forward_cap requests for `cap`. */
 size_t wgsr_binning_bytes_cap(const wgsr_raster_args* args, int64_t cap);
+
+/* Consistency check of a forward's tile lists (test and debug aid, no
+ * upstream counterpart): for every tile, its [start, end) lies inside the
+ * list region the forward sized from num_rendered (the capacity in capacity
+ * mode) and matches its list length, every listed Gaussian id is < P, and no
+ * pixel's last contributor lies beyond its tile's list.  Adds the number of
+ * bad tiles, bad ids and bad pixels to bad[0..2] (device uint32 words, not
+ * zeroed here).  Stream-ordered with no host wait, so it can sit inside a
+ * captured graph between the forward and the backward. */
+int wgsr_check_tile_lists(const wgsr_raster_args* args, int64_t num_rendered, const void* binning,
+                          const void* image, uint32_t* bad, void* stream);
 
 /* Replaces _C.rasterize_gaussians_backward.
  * Inputs: the forward's radii, state buffers and num_rendered; upstream

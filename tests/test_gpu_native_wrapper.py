@@ -48,8 +48,12 @@ def test_native_wrapper_matches_ctypes_bodies():
     finally:
         _C.use_native(True)
     assert rn[0] == rp[0]
-    for a, b in zip(rn[1:], rp[1:]):
-        assert a.dtype == b.dtype and a.shape == b.shape
+    for i, (a, b) in enumerate(zip(rn[1:], rp[1:])):
+        assert a.dtype == b.dtype
+        if i == 3:  # binningBuffer: the previous forward's predicted size when that was large enough
+            assert a.numel() > 0 and b.numel() > 0
+            continue
+        assert a.shape == b.shape
         if a.dtype != torch.uint8:  # (state buffers: same sizes; their scratch bytes may differ)
             np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
     for a, b in zip(gn, gp):

@@ -76,6 +76,18 @@ def test_capacity_forward_matches_and_overflow_zeroes_gradients():
     small = rasterize_forward_cap(bg, xyz, opac, scales, rots, shs, 0, cam, H, W, N // 3, counts)
     c = counts.cpu().tolist()
     assert c[0] == N and c[3] == 1 and c[4] == min(c[2], N // 3)
+    # the truncated forward's tile lists stay inside the capacity-sized region
+    from wgsr.mapping import check_tile_lists
+    bad = torch.zeros(3, dtype=torch.int32, device=DEV)
+    for f in (ref, out, small):
+        check_tile_lists(f, xyz, cam, H, W, 0, shs, bad)
+    assert bad.tolist() == [0, 0, 0]
+    # (and it sees a broken one: tile 0's range -- the image buffer's first
+    # word pair -- pointed past the region)
+    img = out[5].clone()
+    img[:8].view(torch.int32).copy_(torch.tensor([0, 1 << 30], dtype=torch.int32))
+    check_tile_lists(out[:5] + (img,) + out[6:], xyz, cam, H, W, 0, shs, bad)
+    assert bad.tolist()[0] == 1
     go = _backward(args, cam, small, W, H, dcol, ddep)
     for t in go:
         assert not t.any()
@@ -185,6 +197,9 @@ def _run(graphs: bool, cap=None, refine=0):
     if not graphs:
         m.graphs = None
     m.initialize(kfs[:2])
+    # every forward's tile lists checked on the device (inside the captured
+    # graphs too): ranges inside the capacity-sized list region, ids < P
+    m.ms.list_check = torch.zeros(3, dtype=torch.int32, device=DEV)
     if graphs and cap is not None:  # capacities far below the pair counts: every map state overflows
         m.graphs.cap, m.graphs.min_cap, m.graphs.cap_scale, m.graphs.cap_margin = cap, cap, 0.25, 0
     for kf in kfs[2:]:
@@ -206,6 +221,7 @@ def _state(m):
 def test_graph_replayed_loop_matches_eager():
     a = _state(_run(False, refine=40))
     mg = _run(True, refine=40)
+    assert mg.ms.list_check.tolist() == [0, 0, 0]
     b = _state(mg)
     st = mg.graphs.stats
     assert st["replays"] > 100 and st["captures"] >= 2 and st["overflows"] == 0, st
@@ -220,6 +236,8 @@ def test_graph_capacity_overflow_recovers():
     m = _run(True, cap=512)
     st = m.graphs.stats
     assert st["overflows"] >= 1 and st["skipped_iterations"] >= 1, st
+    # the overflowed (truncated) forwards left consistent tile lists
+    assert m.ms.list_check.tolist() == [0, 0, 0]
     assert any(k == "capacity_overflow" for _, k, _ in m.events)
     assert int(m.graphs.sticky_np[0]) == 0 or st["overflows"] >= 2
     for n in m.ms.GROUPS:

@@ -24,6 +24,23 @@ def test_np_median_semantics(shape):
     assert OnlineMapper.np_median(x) == pytest.approx(want, rel=1e-7, abs=0)
 
 
+def test_np_median_nan_and_zero_maps():
+    """Degenerate depth maps: np.median is NaN as soon as one value is NaN
+    (torch.sort puts NaN last, so the middle values alone would not say so),
+    and an all-zero map gives 0."""
+    from wgsr.online import OnlineMapper
+    g = torch.Generator().manual_seed(7)
+    for shape, nan_at in (((6, 8), [(0, 0)]), ((5, 7), [(4, 6), (2, 3)]), ((1, 1), [(0, 0)])):
+        x = torch.rand(shape, generator=g) * 3
+        x[0, :] = 0.0
+        for ij in nan_at:
+            x[ij] = float("nan")
+        assert np.isnan(np.median(x.numpy()))
+        assert np.isnan(OnlineMapper.np_median(x))
+    z = torch.zeros(4, 6)
+    assert OnlineMapper.np_median(z) == float(np.median(z.numpy())) == 0.0
+
+
 def test_np_median_of_the_pcd_fixtures():
     from wgsr.online import OnlineMapper
     F = np.load(os.path.join(GOLD, "ref_pcd.npz"))

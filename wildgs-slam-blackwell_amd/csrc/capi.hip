@@ -518,10 +518,11 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   const size_t bds_bytes = bin_depth ? align256(16 * (size_t)N_bin) : 0;
   const size_t binning_bytes = BL.total + lists_bytes + bds_bytes;
   bg.P = a.P; bg.W = a.W; bg.H = a.H; bg.bshift = bshift; bg.bytes = binning_bytes;
-  // the exact size: allocated now without (or beyond) a prediction, else the
-  // caller's callback narrows the predicted buffer (ours do; any other gets a
-  // new buffer of the exact size -- nothing was written to the first)
-  if (binning_bytes > binning_have || binning_bytes < binning_have) {
+  // the exact size is allocated only without (or beyond) a prediction; a
+  // predicted buffer that is large enough is used as it is (the layout only
+  // needs binning_bytes of it), so a callback is never asked twice for a
+  // buffer it has to keep
+  if (binning_bytes > binning_have) {
     binning = call_alloc(binning_alloc, ctx, binning_bytes);
     if (!binning && binning_bytes) return set_error(WGSR_EALLOC, "binning buffer allocation failed");
   }
@@ -610,6 +611,18 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
                                 out_color, out_depth, out_opacity, at<float>(image, IL.final_T),
                                 at<uint32_t>(image, IL.n_contrib), n_touched, at<uint32_t>(image, IL.tile_m), s)); }
   *num_rendered = (int64_t)N_rect;
+  return WGSR_OK;
+}
+
+int wgsr_check_tile_lists(const wgsr_raster_args* args, int64_t num_rendered, const void* binning, const void* image,
+                          uint32_t* bad, void* stream) {
+  g_err[0] = 0;
+  if (int e = validate(args)) return e;
+  if (!bad || !image || num_rendered < 0 || (num_rendered > 0 && !binning))
+    return set_error(WGSR_EINVAL, "wgsr_check_tile_lists: missing buffers");
+  if (args->P == 0 || num_rendered == 0) return WGSR_OK;
+  HIPCHK(launch_check_tile_lists(*args, bin_shift(*args), (uint64_t)num_rendered, binning, image, bad,
+                                 (hipStream_t)stream));
   return WGSR_OK;
 }
 

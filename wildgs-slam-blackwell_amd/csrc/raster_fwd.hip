@@ -1971,6 +1971,54 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
   return hipGetLastError();
 }
 
+// Consistency check of a forward's tile lists (wgsr_check_tile_lists): one
+// wave per tile.  bad[0] += tiles whose [start, end) leaves the list region
+// or disagrees with tile_len; bad[1] += listed ids >= P; bad[2] += pixels
+// whose last contributor lies beyond their tile's list.  The entries of a
+// tile with a bad range are not read.
+__global__ __launch_bounds__(64) void k_check_tile_lists(const uint2* __restrict__ ranges,
+                                                         const uint32_t* __restrict__ tile_len,
+                                                         const uint32_t* __restrict__ meta,
+                                                         const uint32_t* __restrict__ lists_exact,
+                                                         const uint32_t* __restrict__ lists_bins, uint64_t n_exact,
+                                                         uint64_t n_bins, uint32_t P, int W, int H, int gx,
+                                                         const uint32_t* __restrict__ n_contrib,
+                                                         uint32_t* __restrict__ bad) {
+  const uint32_t tile = blockIdx.x;
+  const int lane = threadIdx.x;
+  const bool bins = meta[0] != 0u;
+  const uint32_t* __restrict__ lists = bins ? lists_bins : lists_exact;
+  const uint64_t region = bins ? n_bins : n_exact;
+  const uint2 r = ranges[tile];
+  const bool ok = r.x <= r.y && (uint64_t)r.y <= region && tile_len[tile] == r.y - r.x;
+  if (!ok) {
+    if (lane == 0) atomicAdd(&bad[0], 1u);
+    return;
+  }
+  uint32_t nb = 0;
+  for (uint32_t e = r.x + (uint32_t)lane; e < r.y; e += 64) nb += lists[e] >= P ? 1u : 0u;
+  const int tx0 = (int)(tile % (uint32_t)gx) * kTile, ty0 = (int)(tile / (uint32_t)gx) * kTile;
+  uint32_t np = 0;
+  for (int q = lane; q < kTile * kTile; q += 64) {
+    const int px = tx0 + (q % kTile), py = ty0 + (q / kTile);
+    if (px < W && py < H) np += n_contrib[(size_t)py * W + px] > r.y - r.x ? 1u : 0u;
+  }
+  if (nb) atomicAdd(&bad[1], nb);
+  if (np) atomicAdd(&bad[2], np);
+}
+
+hipError_t launch_check_tile_lists(const wgsr_raster_args& a, int bshift, uint64_t num_rendered, const void* binning,
+                                   const void* image, uint32_t* bad, hipStream_t s) {
+  const int gx = (a.W + kTile - 1) / kTile, gy = (a.H + kTile - 1) / kTile;
+  const ImageLayout IL(a.W, a.H);
+  const BinLayout BL((size_t)num_rendered);
+  hipLaunchKernelGGL(k_check_tile_lists, dim3((uint32_t)(gx * gy)), dim3(64), 0, s, at<uint2>(image, IL.ranges),
+                     at<uint32_t>(image, IL.tile_len), at<uint32_t>(image, IL.meta), at<uint32_t>(binning, BL.point_g),
+                     at<uint32_t>(binning, BL.total), num_rendered, num_rendered << (2 * bshift), (uint32_t)a.P, a.W,
+                     a.H, gx, at<uint32_t>(image, IL.n_contrib), bad);
+  return hipGetLastError();
+}
+
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present,
                                hipStream_t s) {
   (void)proj;

@@ -279,6 +279,8 @@ def load():
                                                  _fp, _fp, _fp, _fp, _fp, _fp, _fp]
         L.wgsr_binning_bytes_cap.restype = c_sz
         L.wgsr_binning_bytes_cap.argtypes = [P_ARGS, c_i64]
+        L.wgsr_check_tile_lists.restype = c_int
+        L.wgsr_check_tile_lists.argtypes = [P_ARGS, c_i64, _fp, _fp, _fp, _fp]
         L.wgsr_compact_rows.restype = c_int
         L.wgsr_compact_rows.argtypes = [_fp, c_i64, ctypes.POINTER(RowTensor), c_int, ALLOC_FN,
                                         ctypes.c_void_p, _fp]
@@ -316,7 +318,7 @@ EXPORTED_SYMBOLS = (
     "wgsr_geometry_bytes", "wgsr_binning_bytes", "wgsr_image_bytes", "wgsr_last_error",
     "wgsr_version", "wgsr_depth_order_offset", "wgsr_profile_enable", "wgsr_profile_read", "wgsr_profile_stage_name",
     "wgsr_adam_step", "wgsr_adam_step_dev", "wgsr_compact_rows",
-    "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
+    "wgsr_rasterize_forward_cap", "wgsr_binning_bytes_cap", "wgsr_check_tile_lists", "wgsr_mlp_forward_dev_seed", "wgsr_random_keys",
     "wgsr_random_perm_max", "wgsr_random_perm", "wgsr_random_perm_prefix_max_n", "wgsr_random_perm_prefix_max_k",
     "wgsr_random_perm_prefix", "wgsr_mlp_forward_seg2", "wgsr_mlp_backward_seg2",
     "wgsr_gaussian_activate_backward_stats", "wgsr_ssim_forward_partials", "wgsr_ssim_tiles",
@@ -405,9 +407,9 @@ class AllocRequest:
 
 def _make_alloc(slot: str):
     # (a second call for the same buffer within one library call -- the
-    # forward's predicted binning buffer, then its exact size -- narrows the
-    # first allocation when it is large enough; the library uses the pointer
-    # of the last call)
+    # forward's predicted binning buffer was too small for the exact size --
+    # replaces the first allocation; the library uses the pointer of the last
+    # call and wrote nothing through the first)
     def _alloc(_ctx, nbytes):
         req = _tls.req
         n = int(nbytes)

@@ -75,6 +75,25 @@ def rasterize_forward_cap(bg, means3D, opacity, scales, rotations, sh, degree: i
             opac, n_touched)
 
 
+def check_tile_lists(fwd, means3D, cam: dict, H: int, W: int, degree: int, sh, bad):
+    """wgsr_check_tile_lists on a forward's state buffers (``fwd``: the
+    rasteriser forward's 9-tuple; its num_rendered -- the capacity in
+    capacity mode -- sizes the list region): bad tiles, bad ids and bad
+    pixels are added to ``bad`` (int32 [3] device tensor).  No host wait."""
+    L = _lib.load()
+    dev = means3D.device
+    p = _lib.ptr
+    a = _lib.RasterArgs(P=int(means3D.shape[0]), D=int(degree), M=int(sh.shape[1]), W=int(W), H=int(H),
+                        bg=p(means3D), means3D=p(means3D), colors=None, opacities=p(means3D), scales=p(means3D),
+                        rotations=p(means3D), cov3D_precomp=None, shs=p(sh), viewmatrix=p(cam["viewmatrix"]),
+                        projmatrix=p(cam["projmatrix"]), projmatrix_raw=p(cam["projmatrix_raw"]),
+                        campos=p(cam["campos"]), scale_modifier=1.0, tan_fovx=float(cam["tanfovx"]),
+                        tan_fovy=float(cam["tanfovy"]), prefiltered=0, debug=0)
+    with torch.cuda.device(dev):
+        _lib.check(L.wgsr_check_tile_lists(ctypes.byref(a), int(fwd[0]), p(fwd[4]), p(fwd[5]), p(bad),
+                                           _lib.stream_handle(dev)))
+
+
 class MappingStep:
     """GaussianModel state in the fused layout + one-call mapping iterations.
 
@@ -104,6 +123,7 @@ class MappingStep:
         # skips its update and its count (f_dc and f_rest always move together)
         self.steps = {g: 0 for g in self.GROUPS}
         self._iso = None
+        self.list_check = None  # int32 [3] device tensor: every forward's tile lists checked into it (tests)
 
     # storage views (current bank, [:P]) --------------------------------------
     @property
@@ -244,12 +264,16 @@ class MappingStep:
                                                 p(a["opacity"]), p(a["scales"]), p(a["rotations"]),
                                                 p(self.iso_part), _lib.stream_handle(dev)))
         if cap is not None:
-            return rasterize_forward_cap(bg, self.xyz, a["opacity"], a["scales"], a["rotations"], self.features,
-                                         self.D, cam, H, W, cap, counts)
-        return _C.rasterize_gaussians(
-            bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
-            cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
-            self.D, cam["campos"], False, False)
+            fwd = rasterize_forward_cap(bg, self.xyz, a["opacity"], a["scales"], a["rotations"], self.features,
+                                        self.D, cam, H, W, cap, counts)
+        else:
+            fwd = _C.rasterize_gaussians(
+                bg, self.xyz, e, a["opacity"], a["scales"], a["rotations"], 1.0, e, cam["viewmatrix"],
+                cam["projmatrix"], cam["projmatrix_raw"], cam["tanfovx"], cam["tanfovy"], H, W, self.features,
+                self.D, cam["campos"], False, False)
+        if self.list_check is not None:  # (tests: the forward's tile lists checked on the device)
+            check_tile_lists(fwd, self.xyz, cam, H, W, self.D, self.features, self.list_check)
+        return fwd
 
     def _backward(self, cam: dict, bg, fwd, d_image, d_depth, w_iso: float, need_tau: bool = True, skip=None,
                   stats: bool = True):

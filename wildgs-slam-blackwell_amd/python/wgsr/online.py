@@ -200,7 +200,8 @@ class OnlineMapper:
         sv = torch.sort(v).values
         lo = sv[(n - 1) // 2]
         hi = sv[n // 2] if n % 2 == 0 else lo
-        return float(((lo + hi) / 2).item())
+        # np.median is NaN when any value is (torch sorts NaN last)
+        return float(torch.where(torch.isnan(sv[-1]), sv[-1], (lo + hi) / 2).item())
 
     @torch.no_grad()
     def keyframe_points(self, kf: Keyframe, init: bool, keep=None):
@@ -234,7 +235,8 @@ class OnlineMapper:
             N = sv.numel()
             lo = sv[(N - 1) // 2]
             hi = sv[N // 2] if N % 2 == 0 else lo
-            head.append(((lo + hi) / 2).double())
+            # (np.median's NaN when any depth is NaN: torch sorts NaN last)
+            head.append(torch.where(torch.isnan(sv[-1]), sv[-1], (lo + hi) / 2).double())
         head = torch.stack(head).tolist()
         n = int(head[0])
         if c["adaptive_pointsize"]:

@@ -260,6 +260,10 @@ class IterationGraphs:
         return (st.P, st.cur, id(st.banks), self.m.bank.version)
 
     def invalidate(self):
+        if self.graphs and self.replays_since_account:
+            # (a replay may still be running: its graph, kernel arguments and
+            # pool must outlive it)
+            torch.cuda.synchronize(self.dev)
         self.graphs = {}
         self.pool = None
         self.S = None
@@ -507,6 +511,10 @@ class IterationGraphs:
         key = self._map_key()
         fresh = key != self.key
         if fresh:
+            # settle the replays of the old map state first: account() waits
+            # for them (no graph or pool is dropped under an in-flight replay)
+            # and rolls the MLP step counts back while S still holds them
+            self.account()
             self.invalidate()
             self.key = key
         self._check_capacity(fresh)
