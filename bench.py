@@ -307,7 +307,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "Gaussians/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic",
+        "data": "synthetic", "build": _lib.load().wgsr_version().decode(),
         "config": {
             "workload": (f"{label}: {P} Gaussians, {W}x{H}, SH{deg}, single-view fwd+bwd, pose grad on"
                          if world == 1 else
@@ -361,6 +361,11 @@ def main():
             out["roofline"]["frac_incl_zero_fill"] = zb / (ms_avg * 1e-3) / 1e9 / HBM_PEAK_GBPS
         if traffic is not None:
             out["roofline"]["traffic_source"] = pmc.get("source")
+        if pmc:
+            # the counters are quoted only with the build they were taken on named
+            # (the "src:" digest of wgsr_version())
+            src = out["build"].split("src:")[-1]
+            out["roofline"]["counters_from_this_build"] = src in str(pmc.get("source", ""))
         # whole fwd+bwd pass against HBM (the north-star roofline) over the
         # timed step; the render kernels' pair arithmetic against the fp32 VALU peak
         total_bytes = sum(model.values())

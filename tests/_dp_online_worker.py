@@ -82,13 +82,55 @@ def main(out_path):
         moved = (ref - snap[n][0]).abs().sum().item()
         rel[n] = {"max_abs": float((dp[n] - ref).abs().max()), "moved_l1": moved,
                   "rel_l1_of_update": float((dp[n] - ref).abs().sum()) / max(moved, 1e-30)}
+    graphs = graph_phase(kfs, rank)
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump({"world": world, "digest": digest.tolist(), "events": kinds, "psnr": psnr, "P": int(ms.P),
                        "finite": all(bool(torch.isfinite(st.param(n)).all()) for n in names),
-                       "step_vs_summed_views": rel, "psnr_finite": math.isfinite(psnr)}, f)
+                       "step_vs_summed_views": rel, "psnr_finite": math.isfinite(psnr), "graphs": graphs}, f)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def graph_phase(kfs, rank):
+    """3. The steady state as graph replays (wgsr.dp_online.DPIterationGraphs:
+    graph A, the two all-reduces, graph B, the exposure steps) against the
+    eager data-parallel loop from the same seeds: the replicas' digests, the
+    replay counts and the state's distance to the eager run (the MLP
+    gradient's sum order differs, as on one GPU)."""
+    from wgsr.dp_online import DPOnlineMapper
+    cfg = {"init_itr_num": 30, "init_gaussian_update": 100, "init_gaussian_reset": 10_000, "mapping_itr_num": 60,
+           "gaussian_update_every": 100_000, "gaussian_update_offset": 99_999, "gaussian_reset": 100_001,
+           "window_size": 4}
+
+    def run(graphs):
+        m = DPOnlineMapper(sh_degree=0, device=DEV, config=cfg, seed=3)
+        if not graphs:
+            m.graphs = None
+        m.initialize(kfs[:2])
+        for kf in kfs[2:]:
+            m.insert_keyframe(kf, iters=60)
+        m.iterations_after_densify_or_reset = 1000
+        m.final_refine(40)
+        torch.cuda.synchronize()
+        return m
+
+    def state(m):
+        out = {n: m.ms.store.param(n).clone() for n in m.ms.GROUPS}
+        out.update({f"mlp{i}": p.detach().clone() for i, p in enumerate(m.net.parameters())})
+        out["exposure"] = m.bank.ex[:, 0].clone()
+        return out
+    eager = run(False)
+    a = state(eager)
+    mg = run(True)
+    b = state(mg)
+    rel = {k: float((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-12)) if a[k].shape == b[k].shape else None
+           for k in a}
+    st = mg.graphs.stats
+    return {"digest_graphs": mg.replica_digest().cpu().tolist(), "digest_eager": eager.replica_digest().cpu().tolist(),
+            "replays": st["replays"], "captures": st["captures"], "overflows": st["overflows"],
+            "allreduce_ms_per_replay": 1e3 * st["allreduce_s"] / max(1, st["replays"]),
+            "rel_vs_eager": rel, "disabled": mg.graphs.disabled}
 
 
 if __name__ == "__main__":

@@ -28,13 +28,21 @@ def _free_port():
 class _Store:
     def __init__(self, rank):
         g = torch.Generator().manual_seed(10 + rank)
-        self.t = {n: torch.randn(5, k, generator=g) for n, k in (("xyz", 3), ("features", 3), ("opacity", 1),
-                                                                 ("scaling", 3), ("rotation", 4))}
+        # the gradients as views of one flat buffer (GaussianStore.grad_flat)
+        widths = (("xyz", 3), ("features", 3), ("opacity", 1), ("scaling", 3), ("rotation", 4))
+        self.flat = torch.randn(5 * sum(k for _, k in widths), generator=g)
+        self.t, off = {}, 0
+        for n, k in widths:
+            self.t[n] = self.flat[off:off + 5 * k].view(5, k)
+            off += 5 * k
         self.s = {"xyz_gradient_accum": torch.rand(5, 1, generator=g), "denom": torch.randint(0, 3, (5, 1)).float(),
                   "max_radii2D": torch.rand(5, generator=g) * 10}
 
     def grad(self, n):
         return self.t[n]
+
+    def grad_flat(self):
+        return self.flat
 
     def stat(self, n):
         return self.s[n]

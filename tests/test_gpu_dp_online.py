@@ -10,6 +10,9 @@ definition.
 * one data-parallel step equals the Adam step on the SUM of the two views'
   single-process gradients (8(e)'s parity bar: rel L1 <= 1e-5 of the update;
   the two-operand sum is exact, so it is bit-identical in practice);
+* the steady state as graph replays (DPIterationGraphs) keeps the replicas
+  identical and stays within the MLP sum order of the eager data-parallel
+  loop (the single-GPU bar of test_gpu_online_graph);
 * every branch ran and the map is usable (finite, PSNR as in
   test_gpu_online)."""
 import json
@@ -38,7 +41,7 @@ def test_dp_online_mapper_two_ranks(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "_dp_online_worker.py"), str(out)]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads(out.read_text())
     assert res["world"] == 2
@@ -50,3 +53,12 @@ def test_dp_online_mapper_two_ranks(tmp_path):
     for name, v in res["step_vs_summed_views"].items():
         assert v["moved_l1"] > 0, name
         assert v["rel_l1_of_update"] <= 1e-5, (name, v)
+    # the graph-replayed data-parallel steady state: replicas identical, most
+    # iterations replayed, the state within the MLP sum order of the eager loop
+    g = res["graphs"]
+    assert g["disabled"] is None
+    assert g["digest_graphs"][0] == g["digest_graphs"][1], g["digest_graphs"]
+    assert g["digest_eager"][0] == g["digest_eager"][1], g["digest_eager"]
+    assert g["replays"] > 100 and g["captures"] >= 2 and g["overflows"] == 0, g
+    for k, r in g["rel_vs_eager"].items():
+        assert r is not None and r <= 2e-3, (k, r)

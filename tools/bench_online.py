@@ -90,12 +90,28 @@ def main():
     ap.add_argument("--refine-iters", type=int, default=300, help="final_refine iterations after the last keyframe")
     ap.add_argument("--no-deform", action="store_true", help="skip the per-keyframe pose updates / map deformation")
     ap.add_argument("--phases", action="store_true", help="time the insertion / deformation phases (synchronised)")
+    ap.add_argument("--dp", action="store_true",
+                    help="data-parallel over keyframe views (wgsr.dp_online.DPOnlineMapper): launch with "
+                         "torch.distributed.run, one rank per GPU (RCCL); WGSR_BENCH_BACKEND=gloo and "
+                         "WGSR_BENCH_SHARE_GPU=1 rehearse it with every rank on cuda:0")
     a = ap.parse_args()
     from diff_gaussian_rasterization import _C
     from wgsr.camera import PinholeCamera
     from wgsr.online import Keyframe, OnlineMapper
 
-    dev = torch.device("cuda:0")
+    world, rank, local_rank = (int(os.environ.get(k, d)) for k, d in (("WORLD_SIZE", "1"), ("RANK", "0"),
+                                                                       ("LOCAL_RANK", "0")))
+    if os.environ.get("WGSR_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
+    if a.dp:
+        import torch.distributed as dist
+        backend = os.environ.get("WGSR_BENCH_BACKEND", "nccl")
+        torch.cuda.set_device(local_rank)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local_rank)
     W, H = a.width, a.height
     fx = fy = 517.3 * W / 512.0
     cx, cy = W / 2.0, H / 2.0
@@ -116,7 +132,11 @@ def main():
         kfs.append(Keyframe(k, R, T, fx, fy, cx, cy, img.clamp(0, 1).contiguous(), dep.contiguous(), feats))
     torch.cuda.synchronize()
 
-    m = OnlineMapper(sh_degree=0, device=dev, seed=a.seed)
+    if a.dp:
+        from wgsr.dp_online import DPOnlineMapper
+        m = DPOnlineMapper(sh_degree=0, device=dev, seed=a.seed)
+    else:
+        m = OnlineMapper(sh_degree=0, device=dev, seed=a.seed)
     t0 = time.perf_counter()
     m.initialize(kfs[:a.init_keyframes], iters=a.init_iters)
     torch.cuda.synchronize()
@@ -174,13 +194,35 @@ def main():
         m.final_refine(a.refine_iters)
         torch.cuda.synchronize()
         refine_ms = 1e3 * (time.perf_counter() - t0) / a.refine_iters
+    dp = None
+    if a.dp:
+        # the slowest rank's loop time; views per second over all ranks
+        t = torch.tensor([it_ms], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        it_ms = float(t.item())
+        gst = m.graphs.stats if m.graphs is not None else {}
+        dp = {"world": world, "backend": dist.get_backend(), "shared_gpu": os.environ.get("WGSR_BENCH_SHARE_GPU") == "1",
+              "views_per_s": world * its / max(it_ms * 1e-3, 1e-12),
+              "allreduce_ms_per_replay": 1e3 * gst.get("allreduce_s", 0.0) / max(1, gst.get("replays", 0)),
+              "allreduce_bytes_per_iteration": 4 * (m.ms.store.grad_flat().numel()
+                                                    + (m.graphs.tail.numel() if m.graphs is not None
+                                                       and m.graphs.tail is not None else 0)),
+              "replica_digest_equal": None}
+        dg = m.replica_digest().cpu()
+        dp["replica_digest_equal"] = bool((dg == dg[0]).all())
     # PSNR of the final map against every keyframe's ground truth
     ps = []
     for kf in kfs:
         img, _ = m.render_image(kf)
         mse = float(((img.clamp(0, 1) - kf.image) ** 2).mean())
         ps.append(10 * math.log10(1.0 / max(mse, 1e-12)))
+    if rank != 0:
+        if a.dp:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     print(json.dumps({
+        "dp": dp,
         "workload": f"configs[4]-shaped online mapping: synthetic room, {W}x{H}, SH0, {a.keyframes} keyframes "
                     f"({a.init_keyframes} init x {a.init_iters} its, then {a.iters} its per keyframe)",
         "ms_per_mapping_iteration": it_ms / max(its, 1), "mapping_iterations": its,
@@ -204,6 +246,9 @@ def main():
                 "Adam (Gaussians, exposures, MLP); before every insertion each existing keyframe's pose is "
                 "nudged and its Gaussians deformed (update_keyframes, one device pass); final_refine at the "
                 "end; wall clock with a device sync per keyframe"}))
+    if a.dp:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -302,7 +302,11 @@ int wgsr_profile_read(double* ms, int64_t* counts, int n, int reset) {
 }
 
 const char* wgsr_profile_stage_name(int i) { return (i >= 0 && i < WGSR_NUM_STAGES) ? kStageNames[i] : ""; }
-const char* wgsr_version(void) { return "wgsr 0.1 gfx950"; }
+#ifndef WGSR_SRC_ID
+#define WGSR_SRC_ID "unversioned"
+#endif
+// (src: digest of csrc/ + include/wgsr.h at build time, Makefile SRC_ID)
+const char* wgsr_version(void) { return "wgsr 0.1 gfx950 src:" WGSR_SRC_ID; }
 int64_t wgsr_depth_order_offset(void) { return g_depth_order_off; }
 
 size_t wgsr_geometry_bytes(int P) { return GeomLayout((size_t)(P > 0 ? P : 0)).total; }

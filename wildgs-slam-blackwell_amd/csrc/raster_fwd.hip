@@ -276,6 +276,11 @@ __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lan
 // loads queued AFTER the parameter loads: vmcnt retires in issue order, and
 // with the slab queued first (or a run-time trip count) the first parameter
 // use waited for the whole slab, so nothing overlapped it.
+// WGSR_PRE_LATE_SH: the SH slab loaded after the geometry, by the visible
+// rows only (A/B build switch)
+#ifndef WGSR_PRE_LATE_SH
+#define WGSR_PRE_LATE_SH 0
+#endif
 template <int kCh, int kD>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
@@ -307,9 +312,9 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   // (none sinks into the branch below), completed before the slab is queued
   asm volatile("" ::"v"(pl.x), "v"(pl.y), "v"(pl.z), "v"(sl.x), "v"(sl.y), "v"(sl.z), "v"(ql.x), "v"(ql.y),
                "v"(ql.z), "v"(ql.w), "v"(ol));
-  if constexpr (sh_on) {  // then the slab, in flight while the geometry runs
+  auto load_slab = [&]() {
     using lds_t = __attribute__((address_space(3))) void*;
-    constexpr int kNch = (3 * (kD + 1) * (kD + 1) + kCh - 1) / kCh;
+    constexpr int kNch = (3 * ((kD < 0 ? 0 : kD) + 1) * ((kD < 0 ? 0 : kD) + 1) + kCh - 1) / kCh;
     const float* src = shs + (size_t)ic * (3 * M);
 #pragma unroll
     for (int k = 0; k < kNch; ++k) {
@@ -318,7 +323,8 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       else
         __builtin_amdgcn_global_load_lds((const void*)(src + k), (lds_t)(s_sh + 64 * k), 4, 0, 0);
     }
-  }
+  };
+  if constexpr (sh_on && !WGSR_PRE_LATE_SH) load_slab();  // then the slab, in flight while the geometry runs
   const f3 p = i < P ? pl : mk3(0.f, 0.f, 1.f);
   const float o = i < P ? ol : 0.f;
   const f3 sc = cov_pre ? mk3(1.f, 1.f, 1.f) : sl;
@@ -343,6 +349,9 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     }
     n_touched[i] = 0;
     gflag[i] = 0;
+  }
+  if constexpr (sh_on && WGSR_PRE_LATE_SH) {
+    if (i < P && w.x != 0u) load_slab();  // (visible rows only: culled rows read no SH)
   }
   if constexpr (sh_on) {
     __builtin_amdgcn_s_waitcnt(0);  // the slab has landed (one wave per workgroup)
@@ -715,8 +724,12 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (blockIdx.x == 0 && t == 0) meta[0] = 1u;  // the lists are the sort-bin region
   const int B = 1 << bshift;
-  const uint32_t bin = blockIdx.x >> bshift;
-  const int r = (int)(blockIdx.x & (uint32_t)(B - 1));
+  // (work item = xcd_remap(block): the 2^s row workgroups of a bin run on one
+  // XCD, so the bin's entries come from HBM once and from that XCD's L2 for
+  // the other rows -- round-robin dispatch would put every row on another XCD)
+  const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t bin = wi >> bshift;
+  const int r = (int)(wi & (uint32_t)(B - 1));
   const int bx = (int)(bin % (uint32_t)gbx), by = (int)(bin / (uint32_t)gbx);
   const int ty = (by << bshift) + r;
   if (ty >= gy) return;  // block-uniform
@@ -1251,12 +1264,15 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch, BdsEmit emit) {
   __shared__ BdsLds L;
   const int t = threadIdx.x;
-  const uint2 bb = bounds[blockIdx.x];
+  // (bins in contiguous chunks per XCD, as k_expand_bins takes them: a bin's
+  // sorted entries are read back from the L2 they were written through)
+  const uint32_t bin = xcd_remap(blockIdx.x, gridDim.x);
+  const uint2 bb = bounds[bin];
   const uint32_t lo = bb.x, n = bb.y - bb.x;
   // (a flag, not a pointer to the by-value argument: that would put it in scratch)
   const bool E = emit.lists != nullptr;
   if (n == 0) {  // block-uniform
-    if (E) bds_emit_ranges(L, emit, blockIdx.x, lo, 0u);
+    if (E) bds_emit_ranges(L, emit, bin, lo, 0u);
     return;
   }
 #pragma unroll
@@ -1288,7 +1304,7 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     bds_small<kBdsItems>(L, skeys, sgid, nullptr, gdep, lo, n, okeys, ogid, E, emit);
   else
     bds_big(L, skeys, sgid, gdep, lo, n, NL, okeys, ogid, scratch, E, emit);
-  if (E) bds_emit_ranges(L, emit, blockIdx.x, lo, n);
+  if (E) bds_emit_ranges(L, emit, bin, lo, n);
 }
 
 // ---- tile ranges and the tiles' launch order ---------------------------------

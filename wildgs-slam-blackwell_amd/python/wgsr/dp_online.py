@@ -26,6 +26,16 @@ keyframe exposures:
 * initialize_map_opt's occlusion-aware visibility of each drawn keyframe is
   gathered the same way (``gather_rows``).
 
+The steady-state iterations replay captured graphs here too
+(``DPIterationGraphs``): the iteration is captured as TWO graphs around the
+exchange -- (A) this rank's view up to its gradients, which also packs the MLP
+gradient, the overflow word and this rank's exposure partials into one flat
+"tail" buffer, then the eager collectives (a SUM all-reduce of the store's
+packed gradient rows, ``GaussianStore.grad_flat``, and one of the tail: two
+collectives, no copies), then (B) the Adam steps with the all-reduced
+overflow word as their skip word; the exposure steps of the step's distinct
+keyframes follow eagerly from the summed tail.
+
 Densify's random split samples come from the replicated generator and its
 decisions from reduced statistics, Adam is deterministic: the replicas stay
 bit-identical (tests/test_gpu_dp_online.py checks it after a run through every
@@ -39,10 +49,14 @@ collective here is an all-reduce (RCCL, and gloo on CPU or CUDA tensors).
 """
 from __future__ import annotations
 
+import math
+
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from .online import OnlineMapper
+from .online_graph import IterationGraphs
 
 
 def _all_reduce(t: torch.Tensor, op, group=None):
@@ -54,6 +68,14 @@ def _all_reduce(t: torch.Tensor, op, group=None):
         t.copy_(h)
         return
     dist.all_reduce(t, op=op, group=group)
+
+
+def allreduce_grads(store, mlp_params, group=None):
+    """SUM-all-reduce the step's gradients: the store's packed gradient rows
+    in place (``grad_flat``: one contiguous range, no copy) and the MLP's
+    (a few thousand floats, through one small flat buffer)."""
+    _all_reduce(store.grad_flat(), dist.ReduceOp.SUM, group)
+    allreduce_flat([p.grad for p in mlp_params], group)
 
 
 def allreduce_flat(tensors, group=None):
@@ -107,17 +129,18 @@ class DPOnlineMapper(OnlineMapper):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.graphs = None
+        self.graphs = DPIterationGraphs(self) if self.dev.type == "cuda" else None
+        self.picks = []
 
     def _pick(self, draw):
         picks = [draw() for _ in range(self.world)]
+        self.picks = picks
         return picks[self.rank]
 
     def _after_backward(self, out, update: bool, need_vis: bool):
         ms = self.ms
         st = ms.store
-        grads = [st.grad(n) for n in ms.GROUPS] + [p.grad for p in self.net.parameters()]
-        allreduce_flat(grads, self.group)
+        allreduce_grads(st, list(self.net.parameters()), self.group)
         if update:  # the statistics densify_and_prune is about to read
             allreduce_flat([st.stat("xyz_gradient_accum"), st.stat("denom")], self.group)
             _all_reduce(st.stat("max_radii2D"), dist.ReduceOp.MAX, self.group)
@@ -156,3 +179,99 @@ class DPOnlineMapper(OnlineMapper):
         d = torch.stack([x.sum(), (x * x).sum(), (x * w).sum(), torch.tensor(float(self.ms.P), dtype=torch.float64,
                                                                              device=x.device)])
         return gather_rows(d, self.group)
+
+
+class DPIterationGraphs(IterationGraphs):
+    """IterationGraphs for DPOnlineMapper (module docstring): graph A (this
+    rank's view -> gradients + the tail), the two SUM all-reduces, graph B
+    (Adam on the summed gradients, skipped when any rank overflowed), then
+    the exposure steps of the step's keyframes from the summed partials.
+
+    Every rank takes the same path: whether an iteration replays depends only
+    on replicated state, and a capture failure raises instead of falling back
+    (an eager iteration on one rank would issue other collectives).  Host
+    step counts are not rolled back after an overflow (``rollback`` False):
+    the rollback would depend on when each rank's host sees its overflow, and
+    the replicas' bias corrections must agree."""
+
+    def __init__(self, mapper):
+        super().__init__(mapper)
+        self.rollback = False
+        self.tail = None
+        self.skip_dp = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.stats.update(allreduce_s=0.0)
+
+    def _capture_body(self, nbc: int, refine: bool):
+        m = self.m
+        world, rank = m.world, m.rank
+        nG = sum(p.numel() for p in self.S.mlp_params)
+        self.nG = nG
+
+        def body_a():
+            G, gex, skip = self._body_grads(nbc, refine)
+            self.nparts = int(gex.shape[0])
+            # the tail: MLP gradient | overflow (float) | [world, nparts, 2]
+            # exposure partials, this rank's row filled (a gather by SUM)
+            ex = torch.zeros(world, self.nparts * 2, device=self.dev)
+            ex[rank].copy_(gex.reshape(-1))
+            self.tail = torch.cat([G.reshape(-1), skip.to(torch.float32), ex.reshape(-1)])
+            # this rank's overflow bookkeeping (the capacity is per rank)
+            self.sticky[0:1].add_(self.counts[3:4].to(torch.int64))
+            torch.maximum(self.sticky[1:2], self.counts[0:1].to(torch.int64), out=self.sticky[1:2])
+            self.sticky_host.copy_(self.sticky, non_blocking=True)
+
+        def body_b():
+            self.skip_dp.copy_((self.tail[nG:nG + 1] > 0).to(torch.int32))
+            self._body_adam(self.tail[:nG], self.skip_dp)
+
+        ga = self._capture_one(body_a)
+        gb = self._capture_one(body_b)
+        return ga, gb
+
+    def _capture(self, nbc: int, refine: bool):
+        g = super()._capture(nbc, refine)
+        if g is None and self.disabled is not None:
+            raise RuntimeError(f"DPIterationGraphs: capture failed on rank {self.m.rank}: {self.disabled}")
+        return g
+
+    def _fill_exposure(self, kf, f, u):
+        pass  # (the exposure steps run after the exchange, _replay)
+
+    def _replay(self, g, kf):
+        m = self.m
+        ga, gb = g
+        ga.replay()
+        t0 = _time()
+        _all_reduce(m.ms.store.grad_flat(), dist.ReduceOp.SUM, m.group)
+        _all_reduce(self.tail, dist.ReduceOp.SUM, m.group)
+        self.stats["allreduce_s"] += _time() - t0
+        gb.replay()
+        # the exposure steps: every keyframe the ranks drew (every rank knows
+        # the draws), one step on the sum of its ranks' partials
+        uids = [m.stack[c] for c in m.picks]
+        ex = self.tail[self.nG + 1:].view(m.world, self.nparts, 2)
+        L = _lib.load()
+        p = _lib.ptr
+        lr = m.cfg["exposure_lr"]
+        done = set()
+        for r, uid in enumerate(uids):
+            if uid in done or uid not in m.kopt_uids:
+                continue
+            done.add(uid)
+            rows = [q for q, v in enumerate(uids) if v == uid]
+            g_ex = ex[r] if len(rows) == 1 else ex[rows].reshape(-1, 2)
+            m.kopt_steps[uid] += 1
+            n = m.kopt_steps[uid]
+            hs = torch.tensor([lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)], dtype=torch.float32)
+            idx = torch.tensor([m.bank.slots[uid]], dtype=torch.int64)
+            dv = torch.cat([hs, idx.view(torch.float32), torch.zeros(2)]).to(self.dev, non_blocking=True)
+            zero = dv[4:5].view(torch.int32)
+            with torch.cuda.device(self.dev):
+                _lib.check(L.wgsr_exposure_step(p(m.bank.ex), p(dv[2:4].view(torch.int64)), p(g_ex),
+                                                int(g_ex.shape[0]), p(dv[0:2]), p(self.skip_dp), p(zero), 0.9,
+                                                0.999, 1e-8, None, None, None, _lib.stream_handle(self.dev)))
+
+
+def _time():
+    import time
+    return time.perf_counter()

@@ -848,6 +848,7 @@ class OnlineMapper:
         c = self.cfg
         ms = self.ms
         stack = [k for k in self.keyframes]
+        self.stack = stack  # (the draws' keyframe list, for the data-parallel graphs)
         self.bank.sync(self.keyframes)
         for _ in range(iters):
             ci = self._pick(lambda: int(self.rng.choice(len(stack))))
@@ -912,6 +913,7 @@ class OnlineMapper:
         cdf /= cdf[-1]
         fast = isinstance(self.rng, np.random.Generator)
         split = False
+        self.stack = stack
         self.bank.sync(self.keyframes)
         ms = self.ms
         for it in range(iters):

@@ -243,6 +243,9 @@ class IterationGraphs:
                       "replay_call_s": 0.0, "step_host_s": 0.0}
         # capacity = max(min_cap, cap_scale x the largest recent pair count + cap_margin)
         self.min_cap, self.cap_scale, self.cap_margin = 1 << 16, 2.0, 4096
+        # account() rolls the host step counts of overflowed (skipped) replays
+        # back; the data-parallel graphs keep them (wgsr.dp_online)
+        self.rollback = True
 
     # -- eligibility -----------------------------------------------------------
     def usable(self) -> bool:
@@ -321,6 +324,17 @@ class IterationGraphs:
 
     def _body(self, nbc: int, refine: bool):
         """One mapping iteration's device work (captured; see the module doc)."""
+        G, gex, skip = self._body_grads(nbc, refine)
+        self._body_exposure(gex, skip)
+        self._body_adam(G, skip)
+        # the overflow bookkeeping, seen by the host through pinned memory
+        self.sticky_host.copy_(self.sticky, non_blocking=True)
+
+    def _body_grads(self, nbc: int, refine: bool):
+        """The iteration up to its gradients: the keyframe's rows gathered, the
+        DINO draw, the MLP forwards, the loss and rasteriser forward/backward
+        (capacity mode; the Gaussians' gradients into the store) and the MLP
+        backward -> (MLP gradient G, exposure partials, overflow word)."""
         m, S = self.m, self.S
         ms, B, c = m.ms, m.bank, m.cfg
         L = _lib.load()
@@ -366,16 +380,29 @@ class IterationGraphs:
             G = backward_raw2(sv, du, gu, 1.0, float(c["reg_mult"]))
         else:
             G = backward_raw(sv, du)
-        skip = self.counts[3:4]
-        # Adam: the Gaussians, the keyframe's exposure on its bank row (skipped
-        # unless the window optimiser holds it; also the overflow bookkeeping),
-        # the MLP (L2 weight decay)
-        gex = out["dexposure_partials"]  # (summed inside the exposure step)
-        with torch.cuda.device(dev):
-            _lib.check(L.wgsr_exposure_step(p(B.ex), p(self.i64), p(gex), int(gex.shape[0]),
+        return G, out["dexposure_partials"], self.counts[3:4]
+
+    def _body_exposure(self, gex, skip):
+        """The keyframe's exposure Adam step on its bank row (skipped unless the
+        window optimiser holds it; also the overflow bookkeeping)."""
+        L = _lib.load()
+        p = _lib.ptr
+        with torch.cuda.device(self.dev):
+            _lib.check(L.wgsr_exposure_step(p(self.m.bank.ex), p(self.i64), p(gex), int(gex.shape[0]),
                                             p(self.f32[self.F_EXPO:self.F_EXPO + 2]),
                                             p(skip), p(self.i32[self.F_EXSKIP:self.F_EXSKIP + 1]), 0.9, 0.999, 1e-8,
-                                            p(self.sticky), p(self.counts), p(self.slot_skips), st))
+                                            p(self.sticky), p(self.counts), p(self.slot_skips),
+                                            _lib.stream_handle(self.dev)))
+
+    def _body_adam(self, G, skip):
+        """The Gaussians' and the MLP's Adam (L2 weight decay for the MLP), one
+        launch when their betas agree; nothing moves when the skip word is set."""
+        m, S = self.m, self.S
+        ms = m.ms
+        L = _lib.load()
+        dev = self.dev
+        st = _lib.stream_handle(dev)
+        p = _lib.ptr
         ts, off = [], 0
         opt = m.uopt
         for prm in S.mlp_params:
@@ -398,8 +425,22 @@ class IterationGraphs:
                 _lib.check(L.wgsr_adam_step_dev((_lib.AdamTensor * len(ts))(*ts), len(ts), S.mlp_betas[0],
                                                 S.mlp_betas[1], S.mlp_eps, S.mlp_wd,
                                                 p(self.f32[self.F_MLP:self.F_MLP + 18]), p(skip), st))
-        # the overflow bookkeeping, seen by the host through pinned memory
-        self.sticky_host.copy_(self.sticky, non_blocking=True)
+
+    def _capture_one(self, fn):
+        """One graph of ``fn``'s device work on the capture stream, in the
+        shared pool."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(self.stream):
+            g.capture_begin(pool=self.pool)
+            try:
+                fn()
+            finally:
+                g.capture_end()
+        return g
+
+    def _capture_body(self, nbc: int, refine: bool):
+        """-> what ``_replay`` launches: the whole iteration as one graph."""
+        return self._capture_one(lambda: self._body(nbc, refine))
 
     def _capture(self, nbc: int, refine: bool):
         t0 = time.perf_counter()
@@ -419,14 +460,8 @@ class IterationGraphs:
             self.stream = torch.cuda.Stream(self.dev)
         cur = torch.cuda.current_stream(self.dev)
         self.stream.wait_stream(cur)
-        g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.stream(self.stream):
-                g.capture_begin(pool=self.pool)
-                try:
-                    self._body(nbc, refine)
-                finally:
-                    g.capture_end()
+            g = self._capture_body(nbc, refine)
         except Exception as e:  # e.g. a configuration the capacity-mode forward does not cover
             self.disabled = f"{type(e).__name__}: {e}"
             self.invalidate()
@@ -437,6 +472,24 @@ class IterationGraphs:
         return g
 
     # -- the step ----------------------------------------------------------------
+    def _fill_exposure(self, kf, f, u):
+        """The per-step block's exposure fields: keyframe ``kf``'s Adam step
+        size and bias correction when the window optimiser holds it (its host
+        step count advanced), else the skip flag."""
+        m = self.m
+        if kf.uid in m.kopt_uids:
+            m.kopt_steps[kf.uid] += 1
+            ne = m.kopt_steps[kf.uid]
+            lr = m.cfg["exposure_lr"]
+            f[self.F_EXPO:self.F_EXPO + 3] = (lr / (1.0 - 0.9 ** ne), math.sqrt(1.0 - 0.999 ** ne), 0.0)
+            u[self.F_EXSKIP] = 0
+        else:
+            u[self.F_EXSKIP] = 1
+
+    def _replay(self, g, kf):
+        """Launch the captured iteration (its per-step block already queued)."""
+        g.replay()
+
     def account(self, consume: bool = False):
         """Settle the overflow bookkeeping of the replays so far: wait for them
         (so no in-flight replay is missed), roll back the step counts of the
@@ -455,7 +508,11 @@ class IterationGraphs:
         torch.cuda.synchronize(self.dev)
         self.replays_since_account = 0
         ovf, mx = int(self.sticky_np[0]), max(int(self.sticky_np[1]), self.pending_mx)
-        if ovf:
+        if ovf and not self.rollback:
+            self.stats["overflows"] += 1
+            self.stats["skipped_iterations"] += ovf
+            self.m.events.append((self.m.iteration_count, "capacity_overflow", {"cap": self.cap, "skipped": ovf}))
+        elif ovf:
             self.stats["overflows"] += 1
             self.stats["skipped_iterations"] += ovf
             # the skipped steps advanced no moments on the device: undo their counts
@@ -539,14 +596,7 @@ class IterationGraphs:
         bc1 = 1.0 - b1 ** n
         bc2s = math.sqrt(1.0 - b2 ** n)
         f[self.F_MLP:self.F_MLP + 18] = np.tile(np.array([S.mlp_lr / bc1, bc2s, S.mlp_lr / bc1], np.float32), 6)
-        if kf.uid in m.kopt_uids:
-            m.kopt_steps[kf.uid] += 1
-            ne = m.kopt_steps[kf.uid]
-            lr = m.cfg["exposure_lr"]
-            f[self.F_EXPO:self.F_EXPO + 3] = (lr / (1.0 - 0.9 ** ne), math.sqrt(1.0 - 0.999 ** ne), 0.0)
-            u[self.F_EXSKIP] = 0
-        else:
-            u[self.F_EXSKIP] = 1
+        self._fill_exposure(kf, f, u)
         ix[0] = m.bank.slots[kf.uid]
         for j, k in enumerate(neighbours):
             ix[1 + j] = m.bank.slots[k]
@@ -555,7 +605,7 @@ class IterationGraphs:
             ev = self.ring_ev[i] = torch.cuda.Event()
         ev.record()
         t_rep = time.perf_counter()
-        g.replay()
+        self._replay(g, kf)
         t_end = time.perf_counter()
         torch._foreach_add_(S.mlp_steps, 1.0)
         self.stats["replays"] += 1

@@ -109,9 +109,16 @@ class GaussianStore:
         b["n_obs"] = torch.empty(cap, dtype=torch.int32, device=self.device)
         return b
 
+    def _grad_widths(self):
+        return {"xyz": 3, "features": 3 * self.M, "opacity": 1, "scaling": 3, "rotation": 4}
+
     def _new_single(self, cap):
         f32 = dict(dtype=torch.float32, device=self.device)
-        s = {"grad_" + n: torch.zeros(self._shape(n, cap), **f32) for n in PARAMS}
+        # the five parameter gradients in ONE flat buffer, packed by the
+        # current row count (grad(): group g at P x (widths before g)): per-
+        # iteration scratch, so a data-parallel step all-reduces the P rows of
+        # every group as one contiguous range (grad_flat())
+        s = {"grad_flat": torch.zeros(cap * sum(self._grad_widths().values()) + 64 * len(PARAMS), **f32)}
         s["xyz_gradient_accum"] = torch.zeros(cap, 1, **f32)
         s["denom"] = torch.zeros(cap, 1, **f32)
         s["max_radii2D"] = torch.zeros(cap, **f32)
@@ -134,7 +141,8 @@ class GaussianStore:
             nb[0][k][:P].copy_(t[:P])
         ns = self._new_single(cap)
         for k, t in self.single.items():
-            ns[k][:P].copy_(t[:P])
+            if k != "grad_flat":  # (scratch: rewritten by every backward)
+                ns[k][:P].copy_(t[:P])
         self.banks, self.single, self.cur, self.capacity = nb, ns, 0, cap
 
     # ---- views [:P] ---------------------------------------------------------
@@ -147,8 +155,25 @@ class GaussianStore:
     def exp_avg_sq(self, name):
         return self.banks[self.cur]["v_" + name][:self.P]
 
+    def _grad_offsets(self):
+        """{group: float offset} in grad_flat for the current P (each group
+        256-byte aligned) and the end of the last group."""
+        out, off = {}, 0
+        for n, w in self._grad_widths().items():
+            out[n] = off
+            off += (self.P * w + 63) // 64 * 64
+        return out, off
+
     def grad(self, name):
-        return self.single["grad_" + name][:self.P]
+        offs, _ = self._grad_offsets()
+        n = self.P * self._grad_widths()[name]
+        return self.single["grad_flat"][offs[name]:offs[name] + n].view(self._shape(name, self.P))
+
+    def grad_flat(self):
+        """Every group's gradient rows [:P] as one contiguous range
+        (grad() views into it; the < 64-float alignment gaps between groups
+        are never read)."""
+        return self.single["grad_flat"][:self._grad_offsets()[1]]
 
     def stat(self, name):
         return self.single[name][:self.P]
