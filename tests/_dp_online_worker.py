@@ -83,6 +83,10 @@ def main(out_path):
         rel[n] = {"max_abs": float((dp[n] - ref).abs().max()), "moved_l1": moved,
                   "rel_l1_of_update": float((dp[n] - ref).abs().sum()) / max(moved, 1e-30)}
     graphs = graph_phase(kfs, rank)
+    with open(f"{out_path}.rank{rank}.graphs.json", "w") as f:
+        json.dump(graphs, f)
+    if "error" in graphs:
+        raise RuntimeError(f"graph phase on rank {rank}: {graphs}")
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump({"world": world, "digest": digest.tolist(), "events": kinds, "psnr": psnr, "P": int(ms.P),
@@ -103,8 +107,14 @@ def graph_phase(kfs, rank):
            "gaussian_update_every": 100_000, "gaussian_update_offset": 99_999, "gaussian_reset": 100_001,
            "window_size": 4}
 
-    def run(graphs):
+    def run(graphs, holder=None):
+        # (fresh keyframes per run: a mapper's bank adopts a keyframe's CURRENT
+        # fields, and the previous run's bank would hand over its exposures)
+        from test_gpu_online import _keyframes
+        kfs = _keyframes(4)
         m = DPOnlineMapper(sh_degree=0, device=DEV, config=cfg, seed=3)
+        if holder is not None:
+            holder["m"] = m
         if not graphs:
             m.graphs = None
         m.initialize(kfs[:2])
@@ -122,7 +132,13 @@ def graph_phase(kfs, rank):
         return out
     eager = run(False)
     a = state(eager)
-    mg = run(True)
+    holder = {}
+    try:
+        mg = run(True, holder)
+    except Exception as e:  # (the capacity history and the error, for the test's message)
+        g = holder["m"].graphs
+        return {"error": f"{type(e).__name__}: {e}", "cap_log": g.stats.get("cap_log"), "stats": {
+            k: v for k, v in g.stats.items() if k != "cap_log"}}
     b = state(mg)
     rel = {k: float((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-12)) if a[k].shape == b[k].shape else None
            for k in a}
@@ -130,8 +146,18 @@ def graph_phase(kfs, rank):
     return {"digest_graphs": mg.replica_digest().cpu().tolist(), "digest_eager": eager.replica_digest().cpu().tolist(),
             "replays": st["replays"], "captures": st["captures"], "overflows": st["overflows"],
             "allreduce_ms_per_replay": 1e3 * st["allreduce_s"] / max(1, st["replays"]),
-            "rel_vs_eager": rel, "disabled": mg.graphs.disabled}
+            "rel_vs_eager": rel, "disabled": mg.graphs.disabled, "cap_log": st.get("cap_log"),
+            "exposure_eager": a["exposure"].tolist(), "exposure_graphs": b["exposure"].tolist(),
+            "kopt_steps": [eager.kopt_steps, mg.kopt_steps], "iterations": [eager.iteration_count, mg.iteration_count]}
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    try:
+        main(sys.argv[1])
+    except BaseException:
+        # every rank's own traceback next to the result file (the launcher
+        # keeps only the tail of the interleaved stderr)
+        import traceback
+        with open(f"{sys.argv[1]}.rank{os.environ.get('RANK', '?')}.err", "w") as f:
+            traceback.print_exc(file=f)
+        raise

@@ -42,7 +42,10 @@ def test_dp_online_mapper_two_ranks(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "_dp_online_worker.py"), str(out)]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert r.returncode == 0, r.stderr[-4000:]
+    if r.returncode != 0:
+        errs = "".join(f"--- rank {k} ---\n" + open(f"{out}.rank{k}.err").read()[-3000:]
+                       for k in range(2) if os.path.exists(f"{out}.rank{k}.err"))
+        raise AssertionError(errs or r.stderr[-4000:])
     res = json.loads(out.read_text())
     assert res["world"] == 2
     d = res["digest"]
@@ -60,5 +63,6 @@ def test_dp_online_mapper_two_ranks(tmp_path):
     assert g["digest_graphs"][0] == g["digest_graphs"][1], g["digest_graphs"]
     assert g["digest_eager"][0] == g["digest_eager"][1], g["digest_eager"]
     assert g["replays"] > 100 and g["captures"] >= 2 and g["overflows"] == 0, g
-    for k, r in g["rel_vs_eager"].items():
-        assert r is not None and r <= 2e-3, (k, r)
+    bad = {k: r for k, r in g["rel_vs_eager"].items() if r is None or r > 2e-3}
+    assert not bad, (g["rel_vs_eager"], g.get("exposure_eager"), g.get("exposure_graphs"), g.get("kopt_steps"),
+                     g.get("iterations"))

@@ -665,10 +665,11 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
     call_alloc(geom_alloc, ctx, 0);
     call_alloc(binning_alloc, ctx, 0);
     call_alloc(image_alloc, ctx, 0);
-    HIPCHK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), s));
-    HIPCHK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), s));
-    HIPCHK(hipMemsetAsync(out_opacity, 0, HW * sizeof(float), s));
-    HIPCHK(hipMemsetAsync(counts, 0, 5 * sizeof(uint32_t), s));
+    // (kernel nodes, not memset nodes: see launch_zero_u32)
+    HIPCHK(launch_zero_u32(reinterpret_cast<uint32_t*>(out_color), 3 * HW, s));
+    HIPCHK(launch_zero_u32(reinterpret_cast<uint32_t*>(out_depth), HW, s));
+    HIPCHK(launch_zero_u32(reinterpret_cast<uint32_t*>(out_opacity), HW, s));
+    HIPCHK(launch_zero_u32(counts, 5, s));
     return WGSR_OK;
   }
   const Grid grid(a);
@@ -696,7 +697,9 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   void* bds_scratch = at<char>(binning, BL.total + lists_bytes);
   uint32_t* counter = at<uint32_t>(geom, GL.counter);
   uint32_t* meta = at<uint32_t>(image, IL.meta);
-  HIPCHK(hipMemsetAsync(counter, 0, kCounterBytes, s));
+  // the counter block zeroed by a kernel node (a captured memset node did not
+  // reliably zero it: launch_zero_u32)
+  HIPCHK(launch_zero_u32(counter, kCounterBytes / 4, s));
   ZeroJob zj{};
   const bool scan_sup = true;
   if (scan_sup) {

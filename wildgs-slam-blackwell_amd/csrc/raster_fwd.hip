@@ -276,10 +276,13 @@ __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lan
 // loads queued AFTER the parameter loads: vmcnt retires in issue order, and
 // with the slab queued first (or a run-time trip count) the first parameter
 // use waited for the whole slab, so nothing overlapped it.
-// WGSR_PRE_LATE_SH: the SH slab loaded after the geometry, by the visible
-// rows only (A/B build switch)
+// WGSR_PRE_LATE_SH (default 1): the SH slab is loaded after the geometry, by
+// the visible rows only -- culled rows read no SH (17 % of the bench scene's
+// rows; 1M / 1080p / SH3: 103.6 -> 102.3 us over two A/B pairs).  0: the slab
+// is issued with the parameter loads, for every row, in flight during the
+// geometry.
 #ifndef WGSR_PRE_LATE_SH
-#define WGSR_PRE_LATE_SH 0
+#define WGSR_PRE_LATE_SH 1
 #endif
 template <int kCh, int kD>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2(
@@ -724,12 +727,11 @@ __global__ __launch_bounds__(kExpThreads) void k_expand_bins(const uint32_t* __r
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (blockIdx.x == 0 && t == 0) meta[0] = 1u;  // the lists are the sort-bin region
   const int B = 1 << bshift;
-  // (work item = xcd_remap(block): the 2^s row workgroups of a bin run on one
-  // XCD, so the bin's entries come from HBM once and from that XCD's L2 for
-  // the other rows -- round-robin dispatch would put every row on another XCD)
-  const uint32_t wi = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t bin = wi >> bshift;
-  const int r = (int)(wi & (uint32_t)(B - 1));
+  // (an XCD-aware mapping -- the 2^s row workgroups of a bin on one XCD, so
+  // that the bin comes from HBM once -- measured 31.5 vs 30.8 us: the rows'
+  // re-reads already hit the last-level cache)
+  const uint32_t bin = blockIdx.x >> bshift;
+  const int r = (int)(blockIdx.x & (uint32_t)(B - 1));
   const int bx = (int)(bin % (uint32_t)gbx), by = (int)(bin / (uint32_t)gbx);
   const int ty = (by << bshift) + r;
   if (ty >= gy) return;  // block-uniform
@@ -1264,9 +1266,7 @@ __global__ __launch_bounds__(kBdsThreads) void k_bin_depth_sort(
     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ogid, uint2* scratch, BdsEmit emit) {
   __shared__ BdsLds L;
   const int t = threadIdx.x;
-  // (bins in contiguous chunks per XCD, as k_expand_bins takes them: a bin's
-  // sorted entries are read back from the L2 they were written through)
-  const uint32_t bin = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t bin = blockIdx.x;
   const uint2 bb = bounds[bin];
   const uint32_t lo = bb.x, n = bb.y - bb.x;
   // (a flag, not a pointer to the by-value argument: that would put it in scratch)
@@ -2021,6 +2021,28 @@ __global__ __launch_bounds__(64) void k_check_tile_lists(const uint2* __restrict
   }
   if (nb) atomicAdd(&bad[1], nb);
   if (np) atomicAdd(&bad[2], np);
+}
+
+// p[0..n) = 0 by a kernel: the capacity-mode forward zeroes its buffers with
+// kernel nodes, not memset nodes.  A hipMemsetAsync captured into a HIP graph
+// (a memset node) was measured NOT to have zeroed the counter block before
+// k_preprocess accumulated into it on some replays -- the two-rank
+// data-parallel loop on one GPU: a replayed forward of an unchanged map and
+// camera reported N_rect >= 2^32 while the eager forward of the same state
+// gave 8561, deterministically, and the kernel zeroing below fixed it.  Garbage
+// counts make the bin sort take `cap` keys of which only the written ones are
+// valid, so the per-bin sort then gathers depth keys through unwritten
+// Gaussian ids: the out-of-bounds reads behind round 5's SIGABRT in the
+// overflow-recovery test are consistent with it.
+__global__ __launch_bounds__(256) void k_zero_u32(uint32_t* __restrict__ p, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) p[i] = 0u;
+}
+
+hipError_t launch_zero_u32(uint32_t* p, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_zero_u32, dim3((uint32_t)blocks), dim3(256), 0, s, p, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_check_tile_lists(const wgsr_raster_args& a, int bshift, uint64_t num_rendered, const void* binning,

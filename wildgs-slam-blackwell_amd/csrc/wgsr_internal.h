@@ -113,6 +113,8 @@ hipError_t launch_render_fwd(const wgsr_raster_args& a, const uint2* ranges, con
                              const void* geom, float* out_color, float* out_depth,
                              float* out_opacity, float* final_T, uint32_t* n_contrib, int32_t* n_touched,
                              uint32_t* tile_m4, hipStream_t s);
+// p[0..n) = 0 by a kernel (graph-capturable without a memset node)
+hipError_t launch_zero_u32(uint32_t* p, size_t n, hipStream_t s);
 // wgsr_check_tile_lists' kernel (lists region sizes from num_rendered and the bin shift)
 hipError_t launch_check_tile_lists(const wgsr_raster_args& a, int bshift, uint64_t num_rendered, const void* binning,
                                    const void* image, uint32_t* bad, hipStream_t s);

@@ -105,9 +105,8 @@ const float* fp(const at::Tensor& t) { return t.defined() ? t.data_ptr<float>() 
 // library reports WGSR_EALLOC through its own error path, and check() then
 // rethrows the original exception.
 // A second call for the same buffer within one library call (the forward's
-// predicted binning buffer, then its exact size) narrows the first
-// allocation when it is large enough (wgsr.h: the library uses the pointer of
-// the last call).
+// predicted binning buffer was too small for the exact size) replaces the
+// first allocation (wgsr.h: the library uses the pointer of the last call).
 struct Alloc {
   at::Device dev;
   at::Tensor geom, binning, image, scratch;

@@ -49,7 +49,7 @@ collective here is an all-reduce (RCCL, and gloo on CPU or CUDA tensors).
 """
 from __future__ import annotations
 
-import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -199,34 +199,66 @@ class DPIterationGraphs(IterationGraphs):
         self.rollback = False
         self.tail = None
         self.skip_dp = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.one = torch.ones(1, dtype=torch.int32, device=self.dev)
+        self.debug = os.environ.get("WGSR_DP_DEBUG", "0") == "1"
         self.stats.update(allreduce_s=0.0)
 
     def _capture_body(self, nbc: int, refine: bool):
         m = self.m
         world, rank = m.world, m.rank
-        nG = sum(p.numel() for p in self.S.mlp_params)
-        self.nG = nG
+
+        box = {}
 
         def body_a():
             G, gex, skip = self._body_grads(nbc, refine)
-            self.nparts = int(gex.shape[0])
+            box["nparts"] = int(gex.shape[0])
+            box["nG"] = int(G.numel())  # (wgsr_mlp_grad_floats: may exceed the parameters' count)
             # the tail: MLP gradient | overflow (float) | [world, nparts, 2]
-            # exposure partials, this rank's row filled (a gather by SUM)
-            ex = torch.zeros(world, self.nparts * 2, device=self.dev)
+            # exposure partials, this rank's row filled (a gather by SUM);
+            # allocated in the graphs' pool, one per captured pair
+            ex = torch.zeros(world, box["nparts"] * 2, device=self.dev)
             ex[rank].copy_(gex.reshape(-1))
-            self.tail = torch.cat([G.reshape(-1), skip.to(torch.float32), ex.reshape(-1)])
-            # this rank's overflow bookkeeping (the capacity is per rank)
-            self.sticky[0:1].add_(self.counts[3:4].to(torch.int64))
-            torch.maximum(self.sticky[1:2], self.counts[0:1].to(torch.int64), out=self.sticky[1:2])
+            box["tail"] = torch.cat([G.reshape(-1), skip.to(torch.float32), ex.reshape(-1)])
+            # this rank's overflow bookkeeping (the capacity is per rank): the
+            # exposure-step kernel with its own skip word set does only that
+            # (sticky[0] += overflow, sticky[1] = max N_rect)
+            L = _lib.load()
+            p = _lib.ptr
+            with torch.cuda.device(self.dev):
+                _lib.check(L.wgsr_exposure_step(p(self.m.bank.ex), p(self.i64), p(gex), int(gex.shape[0]),
+                                                p(self.f32[self.F_EXPO:self.F_EXPO + 2]), p(skip), p(self.one),
+                                                0.9, 0.999, 1e-8, p(self.sticky), p(self.counts), None,
+                                                _lib.stream_handle(self.dev)))
             self.sticky_host.copy_(self.sticky, non_blocking=True)
 
         def body_b():
-            self.skip_dp.copy_((self.tail[nG:nG + 1] > 0).to(torch.int32))
-            self._body_adam(self.tail[:nG], self.skip_dp)
+            tail, nG = box["tail"], box["nG"]
+            self.skip_dp.copy_((tail[nG:nG + 1] > 0).to(torch.int32))
+            self._body_adam(tail[:nG], self.skip_dp)
 
         ga = self._capture_one(body_a)
         gb = self._capture_one(body_b)
-        return ga, gb
+        self.tail = box["tail"]  # (the latest; bench_online reports its size)
+        return ga, gb, box["tail"], box["nparts"], box["nG"]
+
+    def _check(self, where, tail):
+        """WGSR_DP_DEBUG=1: synchronise and check the step's state (the
+        forward's counts, the tail, the store's gradients and parameters,
+        the exposure bank); raise with the iteration on the first bad one."""
+        m = self.m
+        torch.cuda.synchronize(self.dev)
+        c = self.counts.tolist()
+        st = m.ms.store
+        bad = [f"counts {c}"] if (c[0] < 0 or c[0] > (1 << 28)) else []
+        bad += [] if bool(torch.isfinite(tail).all()) else ["tail not finite"]
+        for n in m.ms.GROUPS:
+            bad += [] if bool(torch.isfinite(st.grad(n)).all()) else [f"grad {n} not finite"]
+            bad += [] if bool(torch.isfinite(st.param(n)).all()) else [f"param {n} not finite"]
+        bad += [] if bool(torch.isfinite(m.bank.ex).all()) else ["exposure bank not finite"]
+        if bad:
+            raise RuntimeError(f"DPIterationGraphs {where} (iteration {m.iteration_count}, replay "
+                               f"{self.stats['replays']}, cap {self.cap}, P {m.ms.P}, slots {self.i64.tolist()}): "
+                               f"{'; '.join(bad)}")
 
     def _capture(self, nbc: int, refine: bool):
         g = super()._capture(nbc, refine)
@@ -239,19 +271,24 @@ class DPIterationGraphs(IterationGraphs):
 
     def _replay(self, g, kf):
         m = self.m
-        ga, gb = g
+        ga, gb, tail, nparts, nG = g
         ga.replay()
+        dbg = self.debug
+        if dbg:
+            self._check("after graph A", tail)
         t0 = _time()
         _all_reduce(m.ms.store.grad_flat(), dist.ReduceOp.SUM, m.group)
-        _all_reduce(self.tail, dist.ReduceOp.SUM, m.group)
+        _all_reduce(tail, dist.ReduceOp.SUM, m.group)
         self.stats["allreduce_s"] += _time() - t0
+        if dbg:
+            self._check("after the all-reduces", tail)
         gb.replay()
+        if dbg:
+            self._check("after graph B", tail)
         # the exposure steps: every keyframe the ranks drew (every rank knows
         # the draws), one step on the sum of its ranks' partials
         uids = [m.stack[c] for c in m.picks]
-        ex = self.tail[self.nG + 1:].view(m.world, self.nparts, 2)
-        L = _lib.load()
-        p = _lib.ptr
+        ex = tail[nG + 1:].view(m.world, nparts, 2)
         lr = m.cfg["exposure_lr"]
         done = set()
         for r, uid in enumerate(uids):
@@ -261,15 +298,7 @@ class DPIterationGraphs(IterationGraphs):
             rows = [q for q, v in enumerate(uids) if v == uid]
             g_ex = ex[r] if len(rows) == 1 else ex[rows].reshape(-1, 2)
             m.kopt_steps[uid] += 1
-            n = m.kopt_steps[uid]
-            hs = torch.tensor([lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)], dtype=torch.float32)
-            idx = torch.tensor([m.bank.slots[uid]], dtype=torch.int64)
-            dv = torch.cat([hs, idx.view(torch.float32), torch.zeros(2)]).to(self.dev, non_blocking=True)
-            zero = dv[4:5].view(torch.int32)
-            with torch.cuda.device(self.dev):
-                _lib.check(L.wgsr_exposure_step(p(m.bank.ex), p(dv[2:4].view(torch.int64)), p(g_ex),
-                                                int(g_ex.shape[0]), p(dv[0:2]), p(self.skip_dp), p(zero), 0.9,
-                                                0.999, 1e-8, None, None, None, _lib.stream_handle(self.dev)))
+            m._exposure_apply(uid, g_ex, m.kopt_steps[uid], lr, skip=self.skip_dp)
 
 
 def _time():

@@ -440,7 +440,7 @@ class OnlineMapper:
         perm = self._perm(buf.shape[0], ns)
         s2 = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         sf = buf[perm].contiguous()
-        seeds = torch.tensor([s1, s2], dtype=torch.int32).to(self.dev, non_blocking=True)
+        seeds = torch.tensor([s1, s2], dtype=torch.int32).to(self.dev)  # (blocking: a pageable source)
         u_all, sv = forward_raw2(self.net, kf.features.reshape(h * w, C), sf, seeds[0:1], seeds[1:2])
         out = fb(u_all[:h * w].view(h, w))
         _, gu = dino_reg_raw(u_all[h * w:], sf, want_loss=False)
@@ -539,21 +539,23 @@ class OnlineMapper:
         with torch.cuda.device(self.dev):
             _lib.check(L.wgsr_adam_step((_lib.AdamTensor * 1)(t), 1, 0.9, 0.999, 1e-8, _lib.stream_handle(self.dev)))
 
-    def _exposure_apply(self, uid, g, n, lr):
+    def _exposure_apply(self, uid, g, n, lr, skip=None):
         """Adam step n of keyframe ``uid``'s exposure row from the loss
         backward's per-block (a, b) partials ``g`` [rows, 2] (summed in the
-        step kernel)."""
+        step kernel).  ``skip``: an optional device word; set, nothing moves."""
         from . import _lib
         L = _lib.load()
         p = _lib.ptr
         hs = np.zeros(6, dtype=np.float32)
         hs[0], hs[1] = lr / (1.0 - 0.9 ** n), math.sqrt(1.0 - 0.999 ** n)
         hs[2:4].view(np.int64)[0] = self.bank.slots[uid]
-        dv = torch.from_numpy(hs).to(self.dev, non_blocking=True)
+        # (a blocking copy: hs is pageable and dies with this call -- an
+        # asynchronous copy from it may read the memory after it was reused)
+        dv = torch.from_numpy(hs).to(self.dev)
         with torch.cuda.device(self.dev):
             _lib.check(L.wgsr_exposure_step(p(self.bank.ex), p(dv[2:4]), p(g), int(g.shape[0]), p(dv[0:2]),
-                                            p(dv[4:5]), p(dv[4:5]), 0.9, 0.999, 1e-8, None, None, None,
-                                            _lib.stream_handle(self.dev)))
+                                            p(dv[4:5]) if skip is None else p(skip), p(dv[4:5]), 0.9, 0.999, 1e-8,
+                                            None, None, None, _lib.stream_handle(self.dev)))
 
     # ---- hooks of the keyframe-view data-parallel mapper (wgsr.dp_online) ----
     def _pick(self, draw):

@@ -552,6 +552,10 @@ class IterationGraphs:
         if self.cap is None or ovf or mx > 0.75 * self.cap or want > self.cap or 2 * want < self.cap:
             if self.cap is not None and want != self.cap:
                 self.invalidate()
+            if want != self.cap:  # (the capacity's history: iteration, old, new, overflows, max N_rect)
+                log = self.stats.setdefault("cap_log", [])
+                if len(log) < 64:
+                    log.append((self.m.iteration_count, self.cap, want, ovf, mx, int(self.m._max_nr)))
             self.cap = want
         self.m._max_nr = 0
 
