@@ -26,7 +26,8 @@ def main():
     fn = lib.wgsr_debug_gbc_times
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
     dev = torch.device("cuda:0")
-    W, H, P, deg = 1920, 1080, 1_000_000, 3
+    W, H, deg = 1920, 1080, 3
+    P = int(os.environ.get("GBC_P", "1000000"))
     sc = make_scene(P, W, H, deg, seed=0)
     gc, gd = make_upstream_grads(W, H, seed=1)
     f = synthetic_camera(W, H, 0).raster_fields()
@@ -54,7 +55,7 @@ def main():
     fn(buf)
     v = list(buf)
     wg = max(v[8], 1)
-    out = {"workgroups_launched_per_call": v[15] / n, "workgroups_with_work_per_call": v[8] / n,
+    out = {"P": P, "workgroups_launched_per_call": v[15] / n, "workgroups_with_work_per_call": v[8] / n,
            "listed_per_wg": v[9] / wg, "slots_per_wg": v[10] / wg, "max_slots_one_wg": v[12],
            "max_slots_one_gaussian": v[14], "slowest_wg_clocks_to_record_sums_end": v[11],
            "slowest_wg_clocks_to_end": v[13],

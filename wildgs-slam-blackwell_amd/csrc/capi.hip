@@ -558,7 +558,8 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (bshift) {
       // (the backward's record flags live on the exact slots: zeroed here too)
       STAGE(a, s, launch_duplicate_bins(a, geom, depth_order, bshift, at<uint8_t>(binning, BL.flag),
-                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s));
+                                        at<uint32_t>(binning, BL.key), vin, scan_sup, zb,
+                                        at<uint32_t>(image, IL.meta), s));
     } else {
       STAGE(a, s, launch_duplicate(a, geom, depth_order, (uint32_t)a.P, at<uint32_t>(binning, BL.key), vin,
                                    at<uint8_t>(binning, BL.flag), s));
@@ -727,7 +728,8 @@ int wgsr_rasterize_forward_cap(const wgsr_raster_args* args, int64_t cap, wgsr_a
   }
   { StageTimer T(3, s);  // (pairs past the capacity are not written; exact-slot flags likewise)
   STAGE(a, s, launch_duplicate_bins(a, geom, nullptr, bshift, at<uint8_t>(binning, BL.flag),
-                                    at<uint32_t>(binning, BL.key), vin, scan_sup, zb, s, (uint32_t)C, (uint32_t)C)); }
+                                    at<uint32_t>(binning, BL.key), vin, scan_sup, zb, at<uint32_t>(image, IL.meta), s,
+                                    (uint32_t)C, (uint32_t)C)); }
   bool talt = false, bounds_done = false;
   uint2* bin_bounds = at<uint2>(image, IL.tile_m);
   { StageTimer T(4, s);
@@ -837,7 +839,7 @@ int wgsr_rasterize_backward(const wgsr_raster_args* args, const int32_t* radii, 
                                     zero, s, &partial, &pflag))
     return e;
   StageTimer T(8, s);
-  STAGE(a, s, launch_gauss_bwd(a, geom, partial, pflag, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+  STAGE(a, s, launch_gauss_bwd(a, geom, partial, pflag, at<uint32_t>(image, ImageLayout(a.W, a.H).meta), dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
                                dL_dsh, dL_dscales, dL_drotations, dL_dtau, s));
   return WGSR_OK;
 }

@@ -1045,6 +1045,14 @@ constexpr int kGbWave = 64;
 // group pass, 75 us; parameters loaded ahead of the record sums, 68-70 us.)
 constexpr int kGbcThreads = 256;
 constexpr int kRecChunk = 512;  // flattened record slots staged in LDS at a time
+// ... with 256 / 512 Gaussians per workgroup, whose smaller lists leave room
+// for 768 slots at four workgroups per CU: fewer chunk round trips
+#ifndef WGSR_GBC_IDX
+#define WGSR_GBC_IDX 1
+#endif
+#ifndef WGSR_GBC_CHUNK_SMALL
+#define WGSR_GBC_CHUNK_SMALL 768
+#endif
 template <int kR>
 __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     int P, int D, int M, const uint8_t* __restrict__ gflag, const uint32_t* __restrict__ slot_start,
@@ -1052,10 +1060,12 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
     const uint8_t* __restrict__ pflag, const float* __restrict__ means, const float* __restrict__ scales,
     const float* __restrict__ rots, const float* __restrict__ cov_pre, const float* __restrict__ shs, float scale_mod,
     const float* __restrict__ viewm, const float* __restrict__ projm, const float* __restrict__ praw,
-    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, float* __restrict__ o_m2d,
-    float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d, float* __restrict__ o_cov,
-    float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot, float* __restrict__ o_tau) {
+    const float* __restrict__ campos_p, int W, int H, float tanx, float tany, const uint32_t* __restrict__ meta,
+    float* __restrict__ o_m2d, float* __restrict__ o_col, float* __restrict__ o_opac, float* __restrict__ o_m3d,
+    float* __restrict__ o_cov, float* __restrict__ o_sh, float* __restrict__ o_sc, float* __restrict__ o_rot,
+    float* __restrict__ o_tau) {
   constexpr int NW = kGbcThreads / 64;
+  constexpr int kRecChunk = kR == 4 ? wgsr::kRecChunk : WGSR_GBC_CHUNK_SMALL;
   __shared__ uint32_t s_list[(kGbcThreads * kR)];
   __shared__ uint32_t s_s0[(kGbcThreads * kR)], s_n[(kGbcThreads * kR)], s_off[(kGbcThreads * kR) + 1];
   __shared__ uint2 s_tmp4[4];
@@ -1075,6 +1085,23 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   uint8_t gf[kR];
 #pragma unroll
   for (int r = 0; r < kR; ++r) gf[r] = gflag[min(i0 + r * kGbcThreads + t, P - 1)];
+  // record slots in index order (ImageLayout::meta[2], the default sort-bin
+  // forward): each row's slot range from two coalesced slot_start words,
+  // loaded with the flags -- no dependent gather of the live rows' ranges
+  // (the last row's end from its list length)
+  const bool idx = WGSR_GBC_IDX && meta[2] != 0u;  // (uniform)
+  uint32_t ss[kR], se[kR];
+  if (idx) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int i = min(i0 + r * kGbcThreads + t, P - 1);
+      ss[r] = slot_start[i];
+      se[r] = slot_start[min(i + 1, P - 1)];
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+      if (i0 + r * kGbcThreads + t == P - 1) se[r] = ss[r] + lrec[P - 1].w.w;
+  }
 #pragma unroll
   for (int r = 0; r < kR; ++r) live[r] = i0 + r * kGbcThreads + t < P && gf[r] != 0;
 #pragma unroll
@@ -1092,7 +1119,14 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
       base += k < w ? s_wc[r][k] : 0u;
       nlive += s_wc[r][k];
     }
-    if (live[r]) s_list[base + lanes_below(bal[r])] = (uint32_t)(i0 + r * kGbcThreads + t);
+    if (live[r]) {
+      const uint32_t c = base + lanes_below(bal[r]);
+      s_list[c] = (uint32_t)(i0 + r * kGbcThreads + t);
+      if (idx) {
+        s_s0[c] = ss[r];
+        s_n[c] = se[r] - ss[r];
+      }
+    }
   }
   if (nlive == 0) return;  // block-uniform
   __syncthreads();
@@ -1110,7 +1144,7 @@ __global__ __launch_bounds__(kGbcThreads) void k_gauss_bwd_compact(
   // -8 % (WGSR_GBC_TIMES) but the kernel 58.3 vs 57.8 us -- its time is the
   // slowest workgroups', the ones with the most record slots; loading every
   // row's range instead reads all of the 32-byte list records: 62 us)
-  for (uint32_t c = t; c < nlive; c += kGbcThreads) {
+  for (uint32_t c = idx ? nlive : t; c < nlive; c += kGbcThreads) {
     const uint32_t gi = s_list[c];
     s_s0[c] = slot_start[gi];
     s_n[c] = lrec[gi].w.w;
@@ -1438,9 +1472,9 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
 }
 
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const void* geom, const float4* partial, const uint8_t* pflag,
-                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
-                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau,
-                            hipStream_t s) {
+                            const uint32_t* meta, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot,
+                            float* dL_dtau, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   // (no pair listed: gflag is all zero and nothing is written)
@@ -1464,7 +1498,7 @@ hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const void* geom, const f
                      a.D, a.M, at<uint8_t>(geom, L.gflag), at<uint32_t>(geom, L.slot_start),
                      at<ListRec>(geom, L.lrec), at<uint32_t>(geom, L.clamped), partial, pflag, a.means3D, a.scales,
                      a.rotations, a.cov3D_precomp, a.shs, a.scale_modifier, a.viewmatrix, a.projmatrix,
-                     a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, dL_dmeans2D, dL_dcolors,
+                     a.projmatrix_raw, a.campos, a.W, a.H, a.tan_fovx, a.tan_fovy, meta, dL_dmeans2D, dL_dcolors,
                      dL_dopacity, dL_dmeans3D, dL_dcov3D, a.shs ? dL_dsh : nullptr, dL_dscales, dL_drot, dL_dtau);
   return hipGetLastError();
 }

@@ -372,7 +372,10 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   }
   wave_pair_counts(ac, khi, knlo, rect_pairs, list_pairs, bin_pairs, drange);
   zero_share(zero, blockIdx.x, gridDim.x, lane, kPreWave);
-  if (blockIdx.x == 0 && lane == 0) meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
+  if (blockIdx.x == 0 && lane == 0) {
+    meta[1] = 0u;  // no capacity overflow (ImageLayout::meta)
+    meta[2] = 0u;  // slots not (yet) known to follow the index order (k_duplicate_bins)
+  }
 }
 
 // Expand the exact tile lists (row_span) of depth ranks [r0, r0 + 64) (one
@@ -538,7 +541,8 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
     uint32_t P, int gbx, const ListRec* __restrict__ lrec, const uint32_t* __restrict__ sorted_g,
     const uint2* __restrict__ bsum, const uint2* __restrict__ bsup, const float4* __restrict__ splat,
     uint32_t* __restrict__ slot_start, uint8_t* __restrict__ pflag, uint32_t* __restrict__ keys,
-    uint32_t* __restrict__ vals, const ZeroJob zero, uint32_t cap_slots, uint32_t cap_pairs) {
+    uint32_t* __restrict__ vals, const ZeroJob zero, uint32_t* __restrict__ meta, uint32_t cap_slots,
+    uint32_t cap_pairs) {
   // (cap_slots / cap_pairs: the capacity-mode forward's buffer sizes -- writes
   // past them are dropped and the forward flags the overflow; ~0 otherwise)
   constexpr int NW = kDupScanThreads / 64;
@@ -551,6 +555,8 @@ __global__ __launch_bounds__(kDupScanThreads) void k_duplicate_bins(
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const uint32_t r = blockIdx.x * kDupScanThreads + t;
   const bool in = r < P;
+  // ranks in index order: Gaussian g's slots are [slot_start[g], slot_start[g + 1]) (ImageLayout::meta[2])
+  if (blockIdx.x == 0 && t == 0) meta[2] = sorted_g ? 0u : 1u;
   // (unconditional loads of a clamped rank, the selects after: a load under
   // `in` would be waited for at its join.)
   const uint32_t rc = min(r, P - 1u);
@@ -1870,7 +1876,7 @@ hipError_t launch_preprocess(const wgsr_raster_args& a, void* geom, int32_t* rad
 
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t cap_slots, uint32_t cap_pairs) {
+                                 uint32_t* meta, hipStream_t s, uint32_t cap_slots, uint32_t cap_pairs) {
   if (a.P == 0) return hipSuccess;
   const GeomLayout L(a.P);
   const Bins B((a.W + kTile - 1) / kTile, (a.H + kTile - 1) / kTile, bshift);
@@ -1880,7 +1886,7 @@ hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const ui
                      s, (uint32_t)a.P, B.bx, at<ListRec>(geom, L.lrec), depth_order, at<uint2>(geom, L.bsum),
                      bsup ? at<uint2>(geom, L.bsup) : nullptr,
                      at<float4>(geom, L.splat),
-                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, cap_slots, cap_pairs);
+                     at<uint32_t>(geom, L.slot_start), pflag, keys, vals, zero, meta, cap_slots, cap_pairs);
   return hipGetLastError();
 }
 

@@ -953,7 +953,8 @@ struct ImageLayout {
     order_bwd = take(4 * nt);  // the backward's launch order (heaviest first per XCD chunk)
     meta = take(16);           // [0]: where the forward left the tile lists (1: sort-bin region
                                // after the binning layout, 0: point_g) -- read by the backward;
-                               // [1]: capacity-mode overflow (the backward leaves no gradient)
+                               // [1]: capacity-mode overflow (the backward leaves no gradient);
+                               // [2]: the record slots follow the Gaussian index order
     final_T = take(4 * (size_t)W * H);
     n_contrib = take(4 * (size_t)W * H);
     total = o;

@@ -77,10 +77,12 @@ hipError_t launch_cap_counts(const unsigned long long* partial, uint64_t cap_rec
                              uint32_t* meta, hipStream_t s);
 // Sort bins: after packed_scan_blocks, the scan's down-sweep (slot_start[g],
 // the slot flags zeroed) fused with the (bin | exact tile mask << 16,
-// Gaussian) pair expansion.
+// Gaussian) pair expansion.  Sets ImageLayout::meta[2] when the slots follow
+// the Gaussian index order (depth_order null), which k_gauss_bwd_compact
+// reads: then Gaussian g's slots are [slot_start[g], slot_start[g + 1]).
 hipError_t launch_duplicate_bins(const wgsr_raster_args& a, void* geom, const uint32_t* depth_order, int bshift,
                                  uint8_t* pflag, uint32_t* keys, uint32_t* vals, bool bsup, const ZeroJob& zero,
-                                 hipStream_t s, uint32_t cap_slots = 0xFFFFFFFFu,
+                                 uint32_t* meta, hipStream_t s, uint32_t cap_slots = 0xFFFFFFFFu,
                                  uint32_t cap_pairs = 0xFFFFFFFFu);
 hipError_t launch_duplicate(const wgsr_raster_args& a, const void* geom, const uint32_t* sorted_g, uint32_t P,
                             uint32_t* keys, uint32_t* slot_g, uint8_t* pflag, hipStream_t s);
@@ -131,9 +133,9 @@ hipError_t launch_render_bwd(const wgsr_raster_args& a, const uint2* ranges, con
 // Per-Gaussian backward (k_gauss_bwd_compact): the rows of the Gaussians the
 // render backward marked in gflag; the render backward zero-filled the outputs.
 hipError_t launch_gauss_bwd(const wgsr_raster_args& a, const void* geom, const float4* partial, const uint8_t* pflag,
-                            float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
-                            float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot, float* dL_dtau,
-                            hipStream_t s);
+                            const uint32_t* meta, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                            float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot,
+                            float* dL_dtau, hipStream_t s);
 // view-sharded backward (raster_bwd.hip, wgsr/dp.py)
 hipError_t launch_view_records(const wgsr_raster_args& a, const int32_t* radii, const void* geom, const float4* partial,
                                const uint8_t* pflag, int P_pad, float* records, hipStream_t s);
