@@ -200,3 +200,49 @@ def test_bins_too_full_fall_back_to_the_gaussian_sort(monkeypatch):
     assert o_fb is not None
     np.testing.assert_array_equal(o_fb, o_glob)
     _same_outputs(r_glob, r_fb, "fallback vs global")
+
+
+def _forward_backward(scene, deg, w, h):
+    from diff_gaussian_rasterization import _C
+    from wgsr.camera import synthetic_camera
+    f = synthetic_camera(w, h, 0).raster_fields()
+    d = lambda x: x.to(DEV).contiguous()  # noqa: E731
+    means, scales, q, opac, shs = (d(x) for x in scene)
+    e = torch.empty(0, device=DEV)
+    bg = d(torch.zeros(3))
+    cam = [d(f["viewmatrix"]), d(f["projmatrix"]), d(f["projmatrix_raw"])]
+    nr, color, radii, geom, binning, img, depth, opac_o, nt = _C.rasterize_gaussians(
+        bg, means, e, opac, scales, q, 1.0, e, *cam, f["tanfovx"], f["tanfovy"], h, w, shs, deg,
+        d(f["campos"]), False, False)
+    g = torch.Generator().manual_seed(5)
+    gc = d(torch.randn(3, h, w, generator=g))
+    gd = d(torch.randn(1, h, w, generator=g))
+    grads = _C.rasterize_gaussians_backward(bg, means, radii, e, scales, q, 1.0, e, *cam, f["tanfovx"], f["tanfovy"],
+                                            gc, gd, shs, deg, d(f["campos"]), geom, nr, binning, img, False)
+    torch.cuda.synchronize()
+    return nr, [x.cpu().numpy() for x in grads]
+
+
+@pytest.mark.parametrize("w,h", [(512, 384), (1920, 1080)])
+def test_backward_identical_across_depth_schedules(w, h, monkeypatch):
+    """The per-Gaussian backward finds a Gaussian's record slots two ways: from
+    two index-ordered slot_start words (the per-bin schedule flags that its
+    slots follow the index order, ImageLayout::meta[2]) or by gathering
+    slot_start and the list length of each live row (the depth-ordered
+    schedules).  Same tile lists, same slots within each Gaussian, same sums:
+    every gradient is bit-identical."""
+    means, scales, q, opac, shs = _scene(80_000, 0.4, 9.0, behind=800, ties=4_000, log_z=True)
+    g = torch.Generator().manual_seed(7)
+    shs = torch.cat([shs, 0.1 * torch.randn(shs.shape[0], 15, 3, generator=g)], dim=1)  # SH3
+    scene = (means, scales, q, opac, shs)
+    monkeypatch.setenv("WGSR_BIN_DEPTH_MAX_AVG", str(1 << 40))
+    out = {}
+    for mode in ("global", "bins"):
+        monkeypatch.setenv("WGSR_DEPTH_SORT", mode)
+        out[mode] = _forward_backward(scene, 3, w, h)
+    (n_g, g_g), (n_b, g_b) = out["global"], out["bins"]
+    assert n_g == n_b and n_g > 0
+    names = ("means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations", "tau")
+    assert any(np.abs(x).max() > 0 for x in g_b)
+    for name, a, b in zip(names, g_g, g_b):
+        np.testing.assert_array_equal(b, a, err_msg=name)
