@@ -10,6 +10,8 @@
 #include <cstring>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "wgsr.h"
 #include "wgsr_common.h"
 #include "wgsr_internal.h"
@@ -31,6 +33,13 @@ struct HostCounters {
   // depth sort runs, which the copy then overlaps)
   hipStream_t side = nullptr;
   hipEvent_t pre = nullptr;
+  // per-bin default: k_publish_counts writes the block into `mbox` (coherent
+  // pinned memory, kCounterBytes) and then `seq` into mbox_seq; the host
+  // spins on that word instead of an event behind a blit-kernel copy (the
+  // copy and its completion signal left the GPU idle ~6 us before the scan
+  // and the host woke up later; measured in DESIGN.md section 8, round 6)
+  uint4* mbox = nullptr;  // {seq << 8 | flags | 0x80 if > 32 bits, N_rect, N, N_bin}
+  uint32_t seq = 0;
 };
 // one pinned block + event per (host thread, device): an event recorded on a
 // stream must belong to that stream's device
@@ -53,6 +62,15 @@ BinningGuess& binning_guess() {
   return g[dev];
 }
 
+// WGSR_PUBLISH_COUNTS=0: the blit-kernel copy + event wait for every forward
+bool publish_counts() {
+  static const bool on = [] {
+    const char* e = getenv("WGSR_PUBLISH_COUNTS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 HostCounters& host_counters() {
   thread_local HostCounters per_dev[kMaxDevices];
   int dev = 0;
@@ -66,6 +84,12 @@ HostCounters& host_counters() {
     if (hipStreamCreateWithFlags(&hc.side, hipStreamNonBlocking) != hipSuccess) hc.side = nullptr;
     if (hc.side && hipEventCreateWithFlags(&hc.pre, hipEventDisableTiming) != hipSuccess) hc.pre = nullptr;
     if (!hc.pre) hc.side = nullptr;
+    void* m = nullptr;
+    if (publish_counts() &&
+        hipHostMalloc(&m, 256, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
+      hc.mbox = static_cast<uint4*>(m);
+      *hc.mbox = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
   return hc;
 }
@@ -399,7 +423,19 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   if (!hc.buf || !hc.ev) return set_error(WGSR_EHIP, "pinned counter buffer / event allocation failed");
   // (with the per-bin depth sort nothing would overlap the copy on the side
   // stream, whose start waits out an event round trip: copy in stream order)
-  if (hc.side && !bin_depth) {
+  // per-bin default: the scan's first wave publishes the counts (PublishJob)
+  const bool mailbox = bin_depth && bshift && hc.mbox;
+  // (24-bit sequence numbers, never 0: the record's initial value)
+  const uint32_t want = mailbox ? (hc.seq = (hc.seq % 0xFFFFFFu) + 1u) : 0u;
+  PublishJob pub{};
+  if (mailbox) {
+    // (no event behind it: an event record makes the runtime end the kernel
+    // with a system-scope release, ~6 us before the next kernel starts; the
+    // wait below checks the stream itself instead)
+    pub.counter = counter;
+    pub.host = hc.mbox;
+    pub.seq = want;
+  } else if (hc.side && !bin_depth) {
     HIPCHK(hipEventRecord(hc.pre, s));
     HIPCHK(hipStreamWaitEvent(hc.side, hc.pre, 0));
     HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, hc.side));
@@ -429,11 +465,12 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
   // backward's record slots; Gaussian -> first slot), and with sort bins the
   // bin-pair offsets -- their down-sweep writes the pairs, after the binning
   // buffer exists
-  auto queue_scan = [&]() -> int {
+  auto queue_scan = [&](const PublishJob& pj) -> int {
     StageTimer T(2, s);
     if (bshift) {  // block sums of (list length, bins) in depth order; k_duplicate_bins finishes the scan
       STAGE(a, s, packed_scan_blocks(at<uint32_t>(geom, GL.tb), 1, depth_order, (size_t)a.P,
-                                     at<uint32_t>(geom, GL.bsum), s, scan_sup ? at<uint2>(geom, GL.bsup) : nullptr));
+                                     at<uint32_t>(geom, GL.bsum), s, scan_sup ? at<uint2>(geom, GL.bsup) : nullptr,
+                                     pj));
     } else {
       STAGE(a, s, exclusive_scan_gather(&at<ListRec>(geom, GL.lrec)->w.w, depth_order, (size_t)a.P,
                                         at<uint32_t>(geom, GL.offs), at<uint32_t>(geom, GL.slot_start),
@@ -442,7 +479,7 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     }
     return WGSR_OK;
   };
-  if (int e = queue_scan()) return e;
+  if (int e = queue_scan(pub)) return e;
   // the predicted binning buffer, allocated while the GPU works
   BinningGuess& bg = binning_guess();
   void* binning = nullptr;
@@ -452,16 +489,58 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     binning = call_alloc(binning_alloc, ctx, binning_have);
     if (!binning) binning_have = 0;
   }
-  HIPCHK(hipEventSynchronize(hc.ev));
-  sync_on_error.armed = false;
   const uint32_t* host_counter = hc.buf;
-  const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
+  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+  bool published_ok = true;
+  if (mailbox) {
+    // spin on the published word; every 1024 polls the stream is checked,
+    // so a failed stream ends the wait (and a publish that never became
+    // visible falls back to a copy)
+    // (one aligned 16-byte load: the record is written by one 16-byte store)
+    auto poll = [&]() {
+      asm volatile("" ::: "memory");  // (a fresh load every poll: the GPU writes the record)
+      const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(const_cast<const uint4*>(hc.mbox)));
+      _mm_storeu_si128(reinterpret_cast<__m128i*>(&rec), v);
+      return (rec.x >> 8) == want;
+    };
+    uint32_t polls = 0;
+    while (!poll()) {
+      _mm_pause();
+      if ((++polls & 1023u) == 0) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipErrorNotReady) continue;
+        HIPCHK(q);
+        if (poll()) break;
+        hc.mbox = nullptr;  // (not visible on this system: copies from now on)
+        break;
+      }
+    }
+    if (hc.mbox && (rec.x & 0x80u)) published_ok = false;  // a count beyond 32 bits: the block itself
+    if (!hc.mbox || !published_ok) {
+      HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+  } else {
+    HIPCHK(hipEventSynchronize(hc.ev));
+  }
+  sync_on_error.armed = false;
   // upstream num_rendered, exact (Gaussian, tile) pairs (<= N_rect), (Gaussian, bin) pairs
   size_t N_rect = 0, N = 0, N_bin = 0;
-  for (int i = 0; i < kRectPairLanes; ++i) {
-    N_rect += partial[i];
-    N += partial[kRectPairLanes + i];
-    N_bin += partial[2 * kRectPairLanes + i];
+  uint32_t host_flags = 0;
+  const bool published = mailbox && hc.mbox && published_ok;
+  if (published) {
+    host_flags = rec.x & 0x7Fu;
+    N_rect = rec.y;
+    N = rec.z;
+    N_bin = rec.w;
+  } else {
+    const uint64_t* partial = reinterpret_cast<const uint64_t*>(host_counter + 4);
+    for (int i = 0; i < kRectPairLanes; ++i) {
+      N_rect += partial[i];
+      N += partial[kRectPairLanes + i];
+      N_bin += partial[2 * kRectPairLanes + i];
+    }
+    host_flags = host_counter[1];
   }
   if (bin_depth && N_bin > bin_depth_max_avg() * (size_t)bins.n) {
     // bins too full for one LDS-resident sort each: the Gaussian-level depth
@@ -478,11 +557,17 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
     if (scan_sup)
       HIPCHK(hipMemsetAsync(at<uint2>(geom, GL.bsup), 0,
                             sizeof(uint2) * kScanSupStride * packed_scan_supers((size_t)a.P), s));
-    if (int e = queue_scan()) return e;
+    if (int e = queue_scan(PublishJob{})) return e;
   }
   if (!full_depth && !bin_depth) {
     // depths spanning more than the three passes' bits: one more stable pass
     // over the bits above them, then the scan again in the final order
+    // (the published counts carry no key range: the bins-too-full switch
+    // above reads the block, rarely)
+    if (published) {
+      HIPCHK(hipMemcpyAsync(hc.buf, counter, kCounterBytes, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     const uint32_t* rw = host_counter + kDepthRangeOffset / 4;
     uint32_t hi = 0, nlo = 0;
     for (int i = 0; i < kRectPairLanes; ++i) {
@@ -501,13 +586,13 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
       if (scan_sup)
         HIPCHK(hipMemsetAsync(at<uint2>(geom, GL.bsup), 0,
                               sizeof(uint2) * kScanSupStride * packed_scan_supers((size_t)a.P), s));
-      if (int e = queue_scan()) return e;
+      if (int e = queue_scan(PublishJob{})) return e;
     }
   }
   g_depth_order_off = depth_order ? (int64_t)(reinterpret_cast<const uint8_t*>(depth_order) -
                                               static_cast<const uint8_t*>(geom))
                                   : (int64_t)-1;
-  if (host_counter[1] && a.prefiltered)
+  if (host_flags && a.prefiltered)
     return set_error(WGSR_EINVAL, "Error: a prefiltered Gaussian lies behind the near plane");
   if (N > N_rect) return set_error(WGSR_EHIP, "internal: exact tile lists exceed the rectangles");
   if (N_bin > N_rect) return set_error(WGSR_EHIP, "internal: bin pairs exceed the rectangles");

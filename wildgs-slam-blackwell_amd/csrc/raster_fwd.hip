@@ -1815,6 +1815,7 @@ __global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __rest
 // (saturating u32), the bin-pair count clamped to the buffers (counts[4], what
 // the sort reads as its key count) and the overflow flag (counts[3] and the
 // image buffer's meta[1], which makes the render backward a no-op).
+
 __global__ __launch_bounds__(64) void k_cap_counts(const unsigned long long* __restrict__ partial,
                                                    uint64_t cap_rect, uint64_t cap_bin, uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ meta) {

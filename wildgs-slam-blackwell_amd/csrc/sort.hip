@@ -706,9 +706,11 @@ __global__ __launch_bounds__(256) void k_scan_down(const uint32_t* __restrict__ 
 template <int PER>
 __global__ __launch_bounds__(256) void k_scan2_reduce(const uint32_t* __restrict__ packed, uint32_t stride,
                                                       const uint32_t* __restrict__ idx, uint32_t n,
-                                                      uint2* __restrict__ bsum, uint2* __restrict__ bsup) {
+                                                      uint2* __restrict__ bsum, uint2* __restrict__ bsup,
+                                                      const PublishJob pub) {
   __shared__ uint2 s_tmp[4];
   const int t = threadIdx.x;
+  if (pub.counter && blockIdx.x == 0 && t < 64) publish_counts(pub, t);  // (the forward's counts to the host)
   const size_t b0 = (size_t)blockIdx.x * (256 * PER) + (size_t)t * PER;
   uint2 acc = make_uint2(0u, 0u);
 #pragma unroll
@@ -946,12 +948,12 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
 }
 
 hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
-                              hipStream_t stream, void* bsup) {
+                              hipStream_t stream, void* bsup, const PublishJob& pub) {
   const uint32_t nbs = (uint32_t)((n + kPackedScanTile - 1) / kPackedScanTile);
   if (n == 0) return hipMemsetAsync(bsum, 0, sizeof(uint2), stream);
   uint2* bs = static_cast<uint2*>(bsum);
   hipLaunchKernelGGL(k_scan2_reduce<kPackedScanTile / 256>, dim3(nbs), dim3(256), 0, stream, packed, stride, idx,
-                     (uint32_t)n, bs, static_cast<uint2*>(bsup));
+                     (uint32_t)n, bs, static_cast<uint2*>(bsup), pub);
   if (!bsup) hipLaunchKernelGGL(k_scan2_bsum, dim3(1), dim3(1024), 0, stream, bs, nbs);
   return hipGetLastError();
 }

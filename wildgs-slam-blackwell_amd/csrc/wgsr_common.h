@@ -775,6 +775,36 @@ constexpr int kRectPairLanes = 64;
 constexpr size_t kDepthRangeOffset = 16 + 3 * 8 * kRectPairLanes;
 constexpr size_t kCounterBytes = kDepthRangeOffset + 2 * 4 * kRectPairLanes;
 
+// The forward's one host wait without a copy-engine round trip: the first
+// wave of the scan that follows k_preprocess sums the counter block's three
+// sets of 64 u64 partials (upstream's num_rendered, the exact list pairs, the
+// bin pairs) and lane 0 writes ONE aligned 16-byte record into fine-grained
+// (coherent) pinned host memory: {seq << 8 | error flags | 0x80 if a count
+// needs more than 32 bits, N_rect, N, N_bin}.  One store carries the sequence
+// number and the counts together, so no fence orders them (a system-scope
+// release would write the whole L2 back); the host polls the record.
+struct PublishJob {
+  const uint32_t* counter = nullptr;  // null: no publish
+  uint4* host = nullptr;
+  uint32_t seq = 0;
+};
+__device__ __forceinline__ void publish_counts(const PublishJob& pj, int lane) {
+  const unsigned long long* partial = reinterpret_cast<const unsigned long long*>(pj.counter + 4);
+  unsigned long long v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v[k] = partial[k * kRectPairLanes + lane];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v[k] += (unsigned long long)__shfl_xor((long long)v[k], off, 64);
+  }
+  if (lane == 0) {
+    const bool big = ((v[0] | v[1] | v[2]) >> 32) != 0;
+    *pj.host = make_uint4((pj.seq << 8) | (pj.counter[1] & 0x7Fu) | (big ? 0x80u : 0u), (uint32_t)v[0],
+                          (uint32_t)v[1], (uint32_t)v[2]);
+  }
+}
+static_assert(kRectPairLanes == 64, "publish_counts: one lane per partial");
+
 // ---- depth sort over the visible key range -------------------------------------
 // Depth keys are the float bits of view-space depth (> 0.2 for a visible
 // Gaussian, so the bits order like the floats; culled Gaussians carry

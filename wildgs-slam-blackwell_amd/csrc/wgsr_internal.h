@@ -53,7 +53,7 @@ hipError_t exclusive_scan_gather(const uint32_t* vals, const uint32_t* idx, size
 // packed[idx[i] * stride]: (lo 16 | hi 16 bits) pairs gathered through idx
 hipError_t packed_scan_blocks(const uint32_t* packed, uint32_t stride, const uint32_t* idx, size_t n, void* bsum,
                               hipStream_t stream,
-                              void* bsup = nullptr);
+                              void* bsup = nullptr, const PublishJob& pub = PublishJob{});
 
 int num_bits(uint32_t n);  // bits needed to represent values in [0, n)
 
