@@ -510,7 +510,11 @@ int wgsr_rasterize_forward(const wgsr_raster_args* args, wgsr_alloc_fn geom_allo
         const hipError_t q = hipStreamQuery(s);
         if (q == hipErrorNotReady) continue;
         HIPCHK(q);
-        if (poll()) break;
+        // the stream is done: the record may still be in flight to host
+        // memory (a posted write) -- a few more polls before giving up on it
+        bool seen = false;
+        for (int k = 0; k < (1 << 16) && !(seen = poll()); ++k) _mm_pause();
+        if (seen) break;
         hc.mbox = nullptr;  // (not visible on this system: copies from now on)
         break;
       }
