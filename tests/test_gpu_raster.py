@@ -20,6 +20,7 @@ Tolerances (written here, SURVEY.md 8(c), north_star "<= 1e-4 rel L1"):
   distCUDA2                            bit-exact vs the CPU restatement
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -332,6 +333,40 @@ def test_radix_sorts_against_numpy(monkeypatch):
         np.testing.assert_array_equal(np.asarray(b[k]), np.asarray(v), err_msg=k)
     pts = make_points(300_000, seed=9)
     np.testing.assert_array_equal(distCUDA2(pts.to(DEV)).cpu().numpy(), cpu_oracle.dist_knn(pts.numpy()))
+
+
+_COPY_PATH_SCRIPT = r"""
+import os, sys
+import numpy as np
+root, out = sys.argv[1], sys.argv[2]
+for p in (os.path.join(root, "wildgs-slam-blackwell_amd", "python"), root, os.path.join(root, "tests")):
+    sys.path.insert(0, p)
+from test_gpu_raster import _synthetic, run_c
+res = run_c(*_synthetic(60_000, 640, 480, 3, view=1))
+np.savez(out, **{k: np.asarray(v) for k, v in res.items()})
+"""
+
+
+def test_published_counts_match_the_copy_path(tmp_path):
+    """The forward's pair counts reach the host either as the 16-byte record
+    the offsets scan publishes into coherent pinned memory (default) or by a
+    D->H copy + event (WGSR_PUBLISH_COUNTS=0, read once per process): a second
+    process runs the copy path on the same scene, and every output and
+    gradient is bit-identical."""
+    import subprocess
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    out = run_c(*_synthetic(60_000, 640, 480, 3, view=1))
+    path = tmp_path / "copy_path.npz"
+    env = dict(os.environ, WGSR_PUBLISH_COUNTS="0")
+    r = subprocess.run([sys.executable, "-c", _COPY_PATH_SCRIPT, root, str(path)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ref = np.load(path)
+    assert int(ref["num_rendered"]) == out["num_rendered"] > 0
+    for k, v in out.items():
+        if k != "num_rendered":
+            np.testing.assert_array_equal(v, ref[k], err_msg=k)
 
 
 def test_repeated_backward_of_one_forward_is_identical():
