@@ -98,7 +98,7 @@ __device__ __forceinline__ uint3 preprocess_one(
     ListRec* __restrict__ lrec, uint32_t* __restrict__ clamped,
     uint32_t* __restrict__ err_flag, int bshift,
     int i, const Cam& c, const f3 p, const f3 sc, const float4 q, const float o, const f3 sh_rgb,
-    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true) {
+    uint32_t sh_cbits, uint4& w, uint2& rcw, bool write_color = true, float4* ab = nullptr) {
 #pragma clang fp contract(off)
   w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);  // culled: radius 0, no list, key sorts last
   rcw = make_uint2(0u, 0u);
@@ -156,8 +156,13 @@ __device__ __forceinline__ uint3 preprocess_one(
   // lim, 0), C = (r, g, b, depth) -- pairs laid out for packed math
   const float4 A = make_float4(px, py, kConicSq * (cc * det_inv), kConicSq * (a * det_inv));
   const float4 B = make_float4(kConicXY * (-b * det_inv), o, lim, 0.f);
-  splat[3 * (size_t)i + 0] = A;
-  splat[3 * (size_t)i + 1] = B;
+  if (ab) {  // (the caller writes the whole record with its colour)
+    ab[0] = A;
+    ab[1] = B;
+  } else {
+    splat[3 * (size_t)i + 0] = A;
+    splat[3 * (size_t)i + 1] = B;
+  }
   if (write_color) splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
   rcw = make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
   // exact tile list length (row_span); upstream's num_rendered counts the rect
@@ -284,6 +289,14 @@ __device__ __forceinline__ f3 sh_rgb_lds(const float* __restrict__ s_sh, int lan
 #ifndef WGSR_PRE_LATE_SH
 #define WGSR_PRE_LATE_SH 1
 #endif
+// WGSR_PRE_AB_LATE (default 1): with SH colours, a visible row's whole 48-byte
+// splat record is stored after its colour, in three back-to-back stores.  The
+// geometry half used to be stored before the slab wait and the colour after
+// it: by then many of the record's lines had left the L2, so they were
+// written to HBM twice (write counters ~40 MB above the model at 1M).
+#ifndef WGSR_PRE_AB_LATE
+#define WGSR_PRE_AB_LATE 1
+#endif
 template <int kCh, int kD>
 __global__ __launch_bounds__(kPreWave) void k_preprocess2(
     int P, int D, int M, const float* __restrict__ means, const float* __restrict__ scales,
@@ -337,11 +350,13 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
   uint3 ac = make_uint3(0u, 0u, 0u);
   uint32_t khi = 0u, knlo = 0u;
   uint4 w = make_uint4(0u, 0u, 0u, 0xFFFFFFFFu);
+  constexpr bool ab_late = sh_on && WGSR_PRE_AB_LATE;
+  float4 ab[2];
   if (i < P) {
     uint2 rcw;
     ac = preprocess_one(P, D, M, means, scales, rots, opac, shs, colors, cov_pre, scale_mod, viewm, projm, campos_p,
                         W, H, tanx, tany, gx, gy, prefiltered, splat, lrec, clamped, err_flag, bshift, i, c, p,
-                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, !sh_on);
+                        sc, q, o, mk3(0.f, 0.f, 0.f), 0u, w, rcw, !sh_on, ab_late ? ab : nullptr);
     radii[i] = (int32_t)w.x;
     lrec[i].w = make_uint4(rcw.x, rcw.y, w.z, w.y);
     if (bshift) tb[i] = w.z;
@@ -366,6 +381,10 @@ __global__ __launch_bounds__(kPreWave) void k_preprocess2(
       dir = mk3(dir.x / len, dir.y / len, dir.z / len);
       uint32_t cbits = 0;
       const f3 rgb = sh_rgb_lds<(kD < 0 ? 0 : kD), kCh>(s_sh, lane, dir, cbits);
+      if constexpr (ab_late) {
+        splat[3 * (size_t)i + 0] = ab[0];
+        splat[3 * (size_t)i + 1] = ab[1];
+      }
       splat[3 * (size_t)i + 2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(w.w));
       clamped[i] = cbits;
     }
