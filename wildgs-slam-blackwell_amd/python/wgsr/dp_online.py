@@ -229,7 +229,6 @@ class DPIterationGraphs(IterationGraphs):
                                                 p(self.f32[self.F_EXPO:self.F_EXPO + 2]), p(skip), p(self.one),
                                                 0.9, 0.999, 1e-8, p(self.sticky), p(self.counts), None,
                                                 _lib.stream_handle(self.dev)))
-            self.sticky_host.copy_(self.sticky, non_blocking=True)
 
         def body_b():
             tail, nG = box["tail"], box["nG"]
